@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ by importing the REFERENCE
+implementation (read-only at /root/reference) on CPU.
+
+This script is the only thing in the repo that touches /root/reference, and it
+runs only in the build container (never on the GPU box).  It writes DATA
+(inputs + the reference's outputs) as small .npz / .json fixtures; no
+reference source is copied.
+
+Module stubs (the reference imports packages that are absent here; none of
+them is on the arithmetic path of the functions we capture):
+  * open3d, nibabel  -> empty modules (used only for I/O / eval metrics)
+  * MinkowskiEngine  -> SparseTensor/MinkowskiNetwork shells (FCGF is NOT run)
+  * np.float/np.int  -> builtins (removed in numpy>=1.24, used in lib/utils.py)
+  * Soft_NN device   -> 'cpu' (lib/layers.py:21 hard-codes 'cuda')
+
+Usage:  python tests/golden/make_golden.py [--ref /root/reference]
+"""
+import argparse
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from synth import synth_state, synth_correspondences, unit_features  # noqa: E402
+
+
+def install_stubs():
+    import torch
+    for name in ("open3d", "nibabel", "nibabel.quaternions", "coloredlogs"):
+        sys.modules.setdefault(name, types.ModuleType(name))
+    me = types.ModuleType("MinkowskiEngine")
+    me.__path__ = []
+
+    class SparseTensor:
+        def __init__(self, feats=None, coords=None, **kw):
+            self.F = feats
+            self.C = coords
+
+        def to(self, dev):
+            return self
+
+    class MinkowskiNetwork(torch.nn.Module):
+        def __init__(self, D):
+            super().__init__()
+            self.D = D
+
+    me.SparseTensor = SparseTensor
+    me.MinkowskiNetwork = MinkowskiNetwork
+    mef = types.ModuleType("MinkowskiEngine.MinkowskiFunctional")
+    me.MinkowskiFunctional = mef
+    sys.modules["MinkowskiEngine"] = me
+    sys.modules["MinkowskiEngine.MinkowskiFunctional"] = mef
+    np.float = float  # noqa
+    np.int = int  # noqa
+
+
+def small_cfg(net_channel=32, clusters=16, use_mutuals=0):
+    return {"misc": {"net_depth": 12, "clusters": clusters, "iter_num": 1, "net_channel": net_channel,
+                     "use_gpu": False, "normalize_weights": True},
+            "data": {"use_mutuals": use_mutuals, "max_num_points": 5000},
+            "method": {"task": "pairwise", "descriptor_module": None, "filter_module": "oanet"},
+            "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
+
+
+def load_state(module, seed, overrides=None):
+    import torch
+    shapes = {k: tuple(v.shape) for k, v in module.state_dict().items()}
+    st = synth_state(shapes, seed=seed, overrides=overrides)
+    module.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    return shapes
+
+
+def oanet_outputs(out):
+    d = {}
+    for i in range(len(out["logits"])):
+        d["logits%d" % i] = out["logits"][i].numpy()
+        d["scores%d" % i] = out["scores"][i].numpy()
+        d["R%d" % i] = out["rot_est"][i].numpy()
+        d["t%d" % i] = out["trans_est"][i].numpy()
+    d["latent"] = out["latent features"].numpy()
+    d["gradient_flag"] = np.asarray(bool(out["gradient_flag"]))
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--out", default=HERE)
+    args = ap.parse_args()
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, args.ref)
+    install_stubs()
+    import torch
+    torch.set_num_threads(8)
+    import lib.utils as U
+    import lib.layers as L
+    from lib.filtering import oanet as O
+
+    out = args.out
+    meta = {"generator": "tests/golden/make_golden.py", "reference": "zgojcic/3D_multiview_reg @ /root/reference",
+            "torch": torch.__version__, "numpy": np.__version__, "fixtures": {}}
+
+    # ---------------------------------------------------------------- Kabsch
+    # lib/utils.py:164-237 (+ transformation_residuals :240-256)
+    xs, Rg, tg = synth_correspondences(4, 5000, seed=11)
+    r = np.random.RandomState(12)
+    w = r.rand(4, 5000).astype(np.float32)
+    w[1] = 0.0                                    # all-zero weight row
+    w[2, r.rand(5000) < 0.7] = 0.0                # sparse weights
+    fx = {"x1": xs[..., :3], "x2": xs[..., 3:], "w": w}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        R, t, res, flag = U.kabsch_transformation_estimation(
+            torch.from_numpy(xs[..., :3]).to(dt), torch.from_numpy(xs[..., 3:]).to(dt), torch.from_numpy(w).to(dt))
+        fx["R_" + tag] = R.numpy()
+        fx["t_" + tag] = t.numpy()
+        fx["res_" + tag] = res.numpy()
+        fx["flag_" + tag] = np.asarray(bool(flag))
+    # unweighted call (weights=None)
+    R, t, res, flag = U.kabsch_transformation_estimation(torch.from_numpy(xs[..., :3]), torch.from_numpy(xs[..., 3:]))
+    fx["R_none"], fx["t_none"], fx["res_none"] = R.numpy(), t.numpy(), res.numpy()
+    np.savez_compressed(os.path.join(out, "kabsch.npz"), **fx)
+    meta["fixtures"]["kabsch.npz"] = "lib/utils.py:164-256 kabsch_transformation_estimation, fp32+fp64, zero row"
+
+    # ---------------------------------------------------------------- OANet
+    # lib/filtering/oanet.py:18-265
+    def run_oanet(cfg, xs, seed, train=False, overrides=None):
+        torch.manual_seed(0)
+        net = O.OANet(cfg)
+        shapes = load_state(net, seed, overrides)
+        net.train(train)
+        with torch.no_grad():
+            o = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
+        return shapes, oanet_outputs(o)
+
+    keys = {}
+    cfg = small_cfg()
+    xs_s, _, _ = synth_correspondences(3, 300, seed=21)
+    shapes, o = run_oanet(cfg, xs_s, seed=5)
+    keys["small"] = {k: list(v) for k, v in shapes.items()}
+    np.savez_compressed(os.path.join(out, "oanet_small_eval.npz"), xs=xs_s, **o)
+    _, o = run_oanet(cfg, xs_s, seed=5, train=True)
+    np.savez_compressed(os.path.join(out, "oanet_small_train.npz"), xs=xs_s, **o)
+    _, o = run_oanet(cfg, xs_s, seed=5, overrides={"reg_init.output.bias": [-50.0]})
+    assert o["scores0"].min() > 0, "guard should have fired"
+    np.savez_compressed(os.path.join(out, "oanet_small_guard.npz"), xs=xs_s, **o)
+    # NOTE: the side channel (use_mutuals == 2 -> 7 input channels, oanet.py:205) crashes in the
+    # reference: OANBlock slices x2 = xs[..., 3:] (oanet.py:180) which is 4 wide for 7-channel input,
+    # and kabsch's bmm then fails.  No fixture can be produced for it (reference defects).
+    cfgF = small_cfg(net_channel=128, clusters=500)
+    xs_f, _, _ = synth_correspondences(2, 5000, seed=31)
+    shapesF, o = run_oanet(cfgF, xs_f, seed=7)
+    keys["full"] = {k: list(v) for k, v in shapesF.items()}
+    o.pop("latent")   # 5 MB; not needed at full size
+    np.savez_compressed(os.path.join(out, "oanet_full_eval.npz"), xs=xs_f, **o)
+    meta["fixtures"]["oanet_*.npz"] = ("lib/filtering/oanet.py:218-265; weights = synth_state(seed) by key; "
+                                       "small: C=32,K=16,N=300,B=3 (eval / train-mode BN / zero-row guard / side channel); "
+                                       "full: C=128,K=500,N=5000,B=2 eval")
+    with open(os.path.join(out, "oanet_keys.json"), "w") as f:
+        json.dump(keys, f, indent=0, sort_keys=True)
+
+    # ---------------------------------------------------------------- Soft_NN
+    # lib/layers.py:10-88 + lib/utils.py:968-992
+    fs = unit_features(2, 1024, 32, seed=41)
+    ft = unit_features(2, 1024, 32, seed=42)
+    yc = np.random.RandomState(43).uniform(-2, 2, (2, 1024, 3)).astype(np.float32)
+    fx = {"fs": fs, "ft": ft, "yc": yc}
+    for mode, st in (("soft", False), ("soft", True), ("hard", False)):
+        nn = L.Soft_NN(corr_type=mode, st=st, device="cpu")
+        with torch.no_grad():
+            x = nn(torch.from_numpy(fs), torch.from_numpy(ft), torch.from_numpy(yc))
+        fx["x_%s%s" % (mode, "_st" if st else "")] = x.numpy()
+    # a temperature below the floor (min_temp 1e-4 clamps tau^2)
+    nn = L.Soft_NN(corr_type="soft", st=False, temp=0.005, device="cpu")
+    with torch.no_grad():
+        fx["x_soft_cold"] = nn(torch.from_numpy(fs), torch.from_numpy(ft), torch.from_numpy(yc)).numpy()
+    np.savez_compressed(os.path.join(out, "softnn.npz"), **fx)
+    meta["fixtures"]["softnn.npz"] = "lib/layers.py:44-88 soft / soft+st / hard, tau=0.3 and tau=0.005 (clamped)"
+
+    # ---------------------------------------------------------------- Sampler
+    # lib/layers.py:108-154 (host numpy RNG)
+    fx = {}
+    for tag, pts in (("demo", [18977, 19082]), ("short", [3000, 4500, 6000])):
+        np.random.seed(41)
+        tot = int(sum(pts))
+        C = torch.zeros(tot, 3)
+        C[:, 0] = torch.arange(tot, dtype=torch.float32)
+        F = torch.zeros(tot, 4)
+        s = L.Sampler(samp_type="rand", targeted_num_points=5000)
+        sc, sf = s(C, F, torch.tensor(pts))
+        fx["idx_" + tag] = sc[..., 0].numpy().astype(np.int64)
+        fx["pts_" + tag] = np.asarray(pts)
+    np.savez_compressed(os.path.join(out, "sampler.npz"), **fx)
+    meta["fixtures"]["sampler.npz"] = "lib/layers.py:108-154 rand sampling indices after np.random.seed(41)"
+
+    # ------------------------------------------- pairs + filtering input
+    # lib/utils.py:850-932
+    xyz = torch.from_numpy(np.random.RandomState(51).rand(5, 7, 3).astype(np.float32))
+    ft_ = torch.from_numpy(np.random.RandomState(52).rand(5, 7, 4).astype(np.float32))
+    xs_, xt_, fs_, ft2_ = U.extract_overlaping_pairs(xyz, ft_, None)
+    fd = U.construct_filtering_input_data(xs_, xt_, {}, None)
+    np.savez_compressed(os.path.join(out, "pairs.npz"), xyz=xyz.numpy(), feat=ft_.numpy(), xyz_s=xs_.numpy(),
+                        xyz_t=xt_.numpy(), f_s=fs_.numpy(), f_t=ft2_.numpy(), xs=fd["xs"].numpy(),
+                        ys=fd["ys"].numpy(), Rs=fd["Rs"].numpy(), ts=fd["ts"].numpy())
+    meta["fixtures"]["pairs.npz"] = "lib/utils.py:850-932 extract_overlaping_pairs + construct_filtering_input_data"
+
+    # --------------------------- PairwiseReg composition with a fake descriptor
+    # lib/pairwise/__init__.py:62-142 (compute_descriptors -> filter_correspondences)
+    import functools
+    L.Soft_NN.__init__ = functools.partialmethod(L.Soft_NN.__init__, device="cpu")
+    import lib.pairwise as PW
+
+    class FakeDesc(torch.nn.Module):
+        """Stands in for FCGFNet: returns a fixed unit-norm feature per input row."""
+        def __init__(self, table):
+            super().__init__()
+            self.table = table
+
+        def forward(self, st):
+            class R:
+                pass
+            r_ = R()
+            r_.F = self.table[: st.F.shape[0]]
+            return r_
+
+    pts = [1500, 1800, 1200]
+    tot = sum(pts)
+    table = torch.from_numpy(unit_features(1, tot, 32, seed=61)[0])
+    pcd = torch.from_numpy(np.random.RandomState(62).uniform(-1, 1, (tot, 3)).astype(np.float32))
+    filt = O.OANet(cfg)
+    load_state(filt, seed=9)
+    filt.eval()
+    model = PW.PairwiseReg(FakeDesc(table), filt, torch.device("cpu"), samp_type="rand", corr_type="soft",
+                           tgt_num_points=1000, straight_through_gradient=False)
+    with torch.no_grad():
+        np.random.seed(41)
+        fin, F0, F1, reg = model({"pcd0": pcd, "sinput0_C": torch.zeros(tot, 4, dtype=torch.int32),
+                                  "sinput0_F": torch.ones(tot, 1), "pts_list": torch.tensor(pts)})
+    o = oanet_outputs(reg)
+    np.savez_compressed(os.path.join(out, "pairwise_fake_desc.npz"), pcd=pcd.numpy(), table=table.numpy(),
+                        pts=np.asarray(pts), xs=fin["xs"].numpy(), **o)
+    meta["fixtures"]["pairwise_fake_desc.npz"] = ("lib/pairwise/__init__.py:62-142 with a fixed feature table in place "
+                                                  "of FCGF; np.random.seed(41); 3 fragments -> 3 pairs; small OANet seed 9")
+
+    with open(os.path.join(out, "GOLDEN_META.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote golden fixtures to", out)
+
+
+if __name__ == "__main__":
+    main()

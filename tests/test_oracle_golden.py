@@ -1,0 +1,115 @@
+"""Pin the CPU oracle against the golden vectors produced by the reference's own
+code (tests/golden/make_golden.py).  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden, GOLDEN
+from synth import synth_state
+
+from oracle.kabsch import kabsch
+from oracle.oanet import oanet_forward
+from oracle.soft_nn import soft_nn, sample_rand, pair_index, filtering_input
+
+
+def test_kabsch_matches_reference_f32_f64():
+    g = golden("kabsch.npz")
+    for tag, dt in (("f32", np.float32), ("f64", np.float64)):
+        R, t, res, flag = kabsch(g["x1"].astype(dt), g["x2"].astype(dt), g["w"].astype(dt))
+        tol = 2e-5 if dt == np.float32 else 1e-10
+        np.testing.assert_allclose(R, g["R_" + tag], atol=tol)
+        np.testing.assert_allclose(t, g["t_" + tag], atol=tol * 10)
+        np.testing.assert_allclose(res, g["res_" + tag], atol=tol * 10)
+        assert bool(flag) == bool(g["flag_" + tag])
+    R, t, res, _ = kabsch(g["x1"], g["x2"], None)
+    np.testing.assert_allclose(R, g["R_none"], atol=2e-5)
+    np.testing.assert_allclose(t, g["t_none"], atol=2e-4)
+
+
+def test_kabsch_diag_embed_variant_equal():
+    g = golden("kabsch.npz")
+    a = kabsch(g["x1"][:2, :800], g["x2"][:2, :800], g["w"][:2, :800])
+    b = kabsch(g["x1"][:2, :800], g["x2"][:2, :800], g["w"][:2, :800], diag_embed=True)
+    np.testing.assert_allclose(a[0], b[0], atol=1e-5)
+
+
+def _shapes(which):
+    with open(os.path.join(GOLDEN, "oanet_keys.json")) as f:
+        return json.load(f)[which]
+
+
+def _check_oanet(o, g, tol_logit, n_blocks=2):
+    for i in range(n_blocks):
+        np.testing.assert_allclose(o["logits"][i], g["logits%d" % i], atol=tol_logit, rtol=1e-4)
+        np.testing.assert_allclose(o["scores"][i], g["scores%d" % i], atol=tol_logit)
+        np.testing.assert_allclose(o["rot_est"][i], g["R%d" % i], atol=1e-4)
+        np.testing.assert_allclose(o["trans_est"][i], g["t%d" % i], atol=1e-4)
+
+
+@pytest.mark.parametrize("fx,train,seed,ovr", [
+    ("oanet_small_eval.npz", False, 5, None),
+    ("oanet_small_train.npz", True, 5, None),
+    ("oanet_small_guard.npz", False, 5, {"reg_init.output.bias": [-50.0]}),
+])
+def test_oanet_small_matches_reference(fx, train, seed, ovr):
+    g = golden(fx)
+    st = synth_state(_shapes("small"), seed=seed, overrides=ovr)
+    o = oanet_forward(st, g["xs"], train=train)
+    _check_oanet(o, g, 2e-4)
+    np.testing.assert_allclose(o["latent features"], g["latent"][..., 0], atol=5e-4, rtol=1e-4)
+
+
+def test_oanet_full_matches_reference():
+    g = golden("oanet_full_eval.npz")
+    st = synth_state(_shapes("full"), seed=7)
+    o = oanet_forward(st, g["xs"])
+    _check_oanet(o, g, 5e-4)
+    # identical inlier masks except for near-threshold scores
+    for i in range(2):
+        near = np.abs(g["scores%d" % i] - 0.5) < 1e-4
+        assert np.array_equal((o["scores"][i] > 0.5)[~near], (g["scores%d" % i] > 0.5)[~near])
+
+
+def test_soft_nn_matches_reference():
+    g = golden("softnn.npz")
+    np.testing.assert_allclose(soft_nn(g["fs"], g["ft"], g["yc"], "soft"), g["x_soft"], atol=2e-5)
+    np.testing.assert_allclose(soft_nn(g["fs"], g["ft"], g["yc"], "soft", st=True), g["x_soft_st"], atol=1e-6)
+    np.testing.assert_allclose(soft_nn(g["fs"], g["ft"], g["yc"], "hard"), g["x_hard"], atol=1e-6)
+    np.testing.assert_allclose(soft_nn(g["fs"], g["ft"], g["yc"], "soft", temp=0.005), g["x_soft_cold"], atol=2e-3)  # tau^2 clamped to 1e-4: d rounding x 1e4
+
+
+def test_sampler_indices_match_reference():
+    g = golden("sampler.npz")
+    for tag in ("demo", "short"):
+        np.random.seed(41)
+        idx = sample_rand(g["pts_" + tag], 5000)
+        assert np.array_equal(idx, g["idx_" + tag])
+
+
+def test_pairs_and_filtering_input_match_reference():
+    g = golden("pairs.npz")
+    pi = pair_index(g["xyz"].shape[0])
+    assert np.array_equal(g["xyz"][pi[:, 0]], g["xyz_s"])
+    assert np.array_equal(g["feat"][pi[:, 1]], g["f_t"])
+    fi = filtering_input(g["xyz_s"], g["xyz_t"])
+    for k in ("xs", "ys", "Rs", "ts"):
+        assert np.array_equal(fi[k], g[k])
+
+
+def test_pairwise_composition_matches_reference():
+    """compute_descriptors -> filter_correspondences with a fixed feature table."""
+    g = golden("pairwise_fake_desc.npz")
+    pts = g["pts"]
+    np.random.seed(41)
+    idx = sample_rand(pts, 1000)
+    xyz = g["pcd"][idx]
+    f = g["table"][idx]
+    pi = pair_index(len(pts))
+    xc = soft_nn(f[pi[:, 0]], f[pi[:, 1]], xyz[pi[:, 1]], "soft")
+    xs = filtering_input(xyz[pi[:, 0]], xc)["xs"]
+    np.testing.assert_allclose(xs, g["xs"], atol=2e-5)
+    st = synth_state(_shapes("small"), seed=9)
+    o = oanet_forward(st, g["xs"][:, 0])
+    _check_oanet(o, g, 2e-4)
