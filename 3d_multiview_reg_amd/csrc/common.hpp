@@ -1,0 +1,56 @@
+// Shared device helpers for the mvreg HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MVR_OK 0
+#define MVR_EINVAL -1
+#define MVR_ELAUNCH -2
+
+#define MVR_CHECK_LAUNCH()                                  \
+  do {                                                      \
+    hipError_t _e = hipGetLastError();                      \
+    if (_e != hipSuccess) return MVR_ELAUNCH;               \
+  } while (0)
+
+namespace mvr {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum of NV doubles; result valid in every thread.  `red` must hold
+// NV * (blockDim/64) doubles of LDS.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+  if (l == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) red[w * NV + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < nw; ++j) s += red[j * NV + i];
+    v[i] = s;
+  }
+  __syncthreads();
+}
+
+}  // namespace mvr

@@ -1,0 +1,387 @@
+// OANet inlier-weight block (lib/filtering/oanet.py:132-185) on MI355X.
+//
+// The host orchestrator below issues, per block, ~70 stream-ordered launches of
+// the fused fp32-MFMA GEMM (gemm.hip) plus small finalize kernels.  Every
+// InstanceNorm / BatchNorm / ReLU / softmax / residual of the reference is fused
+// into a GEMM prologue or epilogue; only per-(pair,channel) statistics travel
+// between launches (a few KB).  Activations are [P][C][L] (pair, channel,
+// point/cluster), i.e. the reference's NCHW with W=1.
+#include <math.h>
+#include <string.h>
+
+#include "common.hpp"
+#include "gemm.hpp"
+#include "mvreg.h"
+
+namespace mvr {
+
+// ----------------------------------------------------------------------------
+// InstanceNorm statistics -> folded IN+BN scale/shift for the consumer GEMM.
+//   y = (x-mu)/sqrt(var+eps_in);  z = (y-rm)/sqrt(rv+1e-5)*g + b   (eval)
+//   => z = x*sc + sh
+// train=1: BatchNorm uses batch statistics of y instead (mean 0, var =
+// mean_b var_b/(var_b+eps_in)) — written as per-(p,c) (mu, r_in) into `mv`,
+// finished by in_bn_train_kernel.
+// ----------------------------------------------------------------------------
+__global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld, int st_off, int T, int C, int L,
+                                   float eps_in, mvr_bn_p bn, int train, float* sc, float* sh, int64_t out_ld,
+                                   float2* mv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int t = 0; t < T; ++t) {
+    const float2 v = st[((int64_t)p * T + t) * st_ld + st_off + c];
+    s += v.x;
+    q += v.y;
+  }
+  const double mean = s / L;
+  const double var = fmax(q / L - mean * mean, 0.0);
+  const float rin = (float)(1.0 / sqrt(var + (double)eps_in));
+  if (train) {
+    mv[(int64_t)p * C + c] = make_float2((float)mean, (float)var);
+    return;
+  }
+  float g = 1.f, b = 0.f, rm = 0.f, rs = 1.f;
+  if (bn.gamma) {
+    g = bn.gamma[c];
+    b = bn.beta[c];
+    rm = bn.mean[c];
+    rs = 1.f / sqrtf(bn.var[c] + 1e-5f);
+  }
+  const float gs = g * rs;
+  sc[(int64_t)p * out_ld + c] = rin * gs;
+  sh[(int64_t)p * out_ld + c] = b - ((float)mean * rin + rm) * gs;
+}
+
+__global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int C, float eps_in, mvr_bn_p bn, float* sc,
+                                   float* sh, int64_t out_ld) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double bv = 0.0;
+  for (int p = 0; p < P; ++p) {
+    const double var = mv[(int64_t)p * C + c].y;
+    bv += var / (var + eps_in);
+  }
+  bv /= P;
+  const float g = bn.gamma ? bn.gamma[c] : 1.f, b = bn.gamma ? bn.beta[c] : 0.f;
+  const float gs = g / sqrtf((float)bv + 1e-5f);
+  for (int p = 0; p < P; ++p) {
+    const float2 m = mv[(int64_t)p * C + c];
+    const float rin = (float)(1.0 / sqrt((double)m.y + (double)eps_in));
+    sc[(int64_t)p * out_ld + c] = rin * gs;
+    sh[(int64_t)p * out_ld + c] = b - m.x * rin * gs;
+  }
+}
+
+// BatchNorm(points) of OAFilter.conv2 (oanet.py:72-76): per-cluster affine.
+__global__ void bn_fold_eval_kernel(mvr_bn_p bn, int C, float* sc, float* sh) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float s = bn.gamma[c] / sqrtf(bn.var[c] + 1e-5f);
+  sc[c] = s;
+  sh[c] = bn.beta[c] - bn.mean[c] * s;
+}
+
+// train-mode BN(points): batch stats over (pairs, channels) from ST_COL partials [P][MT][Kc].
+__global__ void bn_col_train_kernel(const float2* __restrict__ st, int P, int MT, int Kc, int rows, mvr_bn_p bn,
+                                    float* sc, float* sh) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= Kc) return;
+  double s = 0.0, q = 0.0;
+  for (int i = 0; i < P * MT; ++i) {
+    const float2 v = st[(int64_t)i * Kc + k];
+    s += v.x;
+    q += v.y;
+  }
+  const double n = (double)P * rows;
+  const double mean = s / n, var = fmax(q / n - mean * mean, 0.0);
+  const float g = bn.gamma[k] / sqrtf((float)var + 1e-5f);
+  sc[k] = g;
+  sh[k] = bn.beta[k] - (float)mean * g;
+}
+
+// softmax partials (max, sumexp) [P][T][L] -> mx[P][L], rs = 1/sum
+__global__ void smx_finalize_kernel(const float2* __restrict__ st, int T, int L, float* mx, float* rs) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (c >= L) return;
+  float m = -3.0e38f, s = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float2 v = st[((int64_t)p * T + t) * L + c];
+    const float M = fmaxf(m, v.x);
+    s = s * expf(m - M) + v.y * expf(v.x - M);
+    m = M;
+  }
+  mx[(int64_t)p * L + c] = m;
+  rs[(int64_t)p * L + c] = 1.f / s;
+}
+
+// Output head (oanet.py:163,174-175): logits = w.x + b; weights = relu(tanh(logits));
+// guard_pos[p] += #positive weights (the batch-coupled zero-row guard reads it).
+__global__ void head_kernel(const float* __restrict__ X, int64_t ps, int C, int N, const float* __restrict__ w,
+                            const float* __restrict__ bias, float* logits, float* scores, int32_t* pos) {
+  __shared__ int cnt;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  if (n < N) {
+    const float* x = X + (int64_t)p * ps + n;
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc = fmaf(w[c], x[(int64_t)c * N], acc);
+    const float lg = acc + bias[0];
+    const float wt = fmaxf(tanhf(lg), 0.f);
+    logits[(int64_t)p * N + n] = lg;
+    scores[(int64_t)p * N + n] = wt;
+    if (wt > 0.f) atomicAdd(&cnt, 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && cnt) atomicAdd(&pos[p], cnt);
+}
+
+// ----------------------------------------------------------------------------
+// Host orchestration
+// ----------------------------------------------------------------------------
+namespace {
+
+struct Act {
+  float* p;      // base
+  int64_t ps;    // pair stride
+  int64_t ld;    // channel (row) stride
+  int C, L;      // channels, length
+  float2* st;    // row statistics partials [P][T][st_ld] (+st_off)
+  int64_t st_ld;
+  int st_off;
+};
+
+struct Ws {
+  char* base;
+  size_t off, cap;
+  template <typename T>
+  T* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T* r = reinterpret_cast<T*>(base + off);
+    off += n * sizeof(T);
+    return r;
+  }
+};
+
+struct Plan {
+  int P, N, C, Kc, Cin;
+  size_t bytes;
+  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *mx, *rs;
+  float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
+};
+
+Plan plan(int C, int Kc, int P, int N, void* base) {
+  Plan pl{};
+  pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc;
+  Ws w{reinterpret_cast<char*>(base), 0, 0};
+  const size_t PN = (size_t)P * N, PK = (size_t)P * Kc;
+  const int TN = gemm_ntiles(N), TK = gemm_ntiles(Kc), MK = gemm_mtiles(Kc), MC = gemm_mtiles(C);
+  pl.X11 = w.take<float>(PN * 2 * C);
+  pl.XA = w.take<float>(PN * C);
+  pl.T1 = w.take<float>(PN * C);
+  pl.E = w.take<float>(PN * Kc);
+  pl.XD = w.take<float>(PK * C);
+  pl.O1 = w.take<float>(PK * C);
+  pl.O2 = w.take<float>(PK * C);
+  pl.sc = w.take<float>((size_t)P * 2 * C);
+  pl.sh = w.take<float>((size_t)P * 2 * C);
+  pl.scK = w.take<float>(Kc);
+  pl.shK = w.take<float>(Kc);
+  const size_t L = (size_t)(N > Kc ? N : Kc);
+  pl.mx = w.take<float>((size_t)P * L);
+  pl.rs = w.take<float>((size_t)P * L);
+  pl.st11 = w.take<float2>((size_t)P * TN * 2 * C);
+  pl.stA = w.take<float2>((size_t)P * TN * C);
+  pl.stT = w.take<float2>((size_t)P * TN * C);
+  pl.stD = w.take<float2>((size_t)P * TK * C);
+  pl.stO = w.take<float2>((size_t)P * TK * C);
+  size_t smx = (size_t)P * TN * Kc;
+  if ((size_t)P * MK * N > smx) smx = (size_t)P * MK * N;
+  pl.smx = w.take<float2>(smx);
+  pl.mv = w.take<float2>((size_t)P * 2 * C);
+  pl.stcol = w.take<float2>((size_t)P * MC * Kc);
+  pl.bytes = w.off + 256;
+  return pl;
+}
+
+struct Ctx {
+  const Plan& pl;
+  hipStream_t s;
+  int train;
+  int err = 0;
+  void chk(int e) {
+    if (e && !err) err = e;
+  }
+  void chk_launch() {
+    if (hipGetLastError() != hipSuccess && !err) err = MVR_ELAUNCH;
+  }
+
+  // IN(eps)+BN fold of activation `a` -> pl.sc / pl.sh ([P][a.C])
+  void finalize_in(const Act& a, float eps, const mvr_bn_p& bn) {
+    const int T = gemm_ntiles(a.L);
+    dim3 grid((a.C + 255) / 256, pl.P);
+    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(256), 0, s, a.st, a.st_ld, a.st_off, T, a.C, a.L, eps, bn, train,
+                       pl.sc, pl.sh, (int64_t)a.C, pl.mv);
+    chk_launch();
+    if (train) {
+      hipLaunchKernelGGL(in_bn_train_kernel, dim3((a.C + 255) / 256), dim3(256), 0, s, pl.mv, pl.P, a.C, eps, bn,
+                         pl.sc, pl.sh, (int64_t)a.C);
+      chk_launch();
+    }
+  }
+
+  // 1x1 conv: out = W . pro(in) + b (+res); stats into out.st when `stats`
+  void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode) {
+    GemmArgs g{};
+    g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
+    g.A = cv.weight; g.sAb = 0; g.lda = in.C;
+    g.B = in.p; g.sBb = in.ps; g.ldb = in.ld; g.bkc = 0;
+    g.C = out.p; g.sCb = out.ps; g.ldc = out.ld;
+    if (res) { g.R = res->p; g.sRb = res->ps; g.has_res = 1; }
+    g.bias = cv.bias; g.bias_mode = cv.bias ? BIAS_M : BIAS_NONE;
+    if (pro) { g.pro = PRO_B_K; g.psc = pl.sc; g.psh = pl.sh; g.sPb = in.C; }
+    g.stats_mode = stats_mode;
+    g.stats = out.st; g.st_ld = out.st_ld; g.st_off = out.st_off;
+    chk(launch_gemm(g, s));
+  }
+
+  void pointcn(const mvr_pointcn_p& pc, const Act& x, const Act& y) {
+    finalize_in(x, 1e-5f, pc.bn1);
+    Act t{pl.T1, (int64_t)y.C * pl.N, pl.N, y.C, pl.N, pl.stT, y.C, 0};
+    const bool sc = pc.shortcut.weight != nullptr;
+    if (sc) conv(pc.shortcut, x, false, y, nullptr, ST_NONE);
+    conv(pc.conv3, x, true, t, nullptr, ST_ROW);
+    finalize_in(t, 1e-5f, pc.bn5);
+    conv(pc.conv7, t, true, y, sc ? &y : &x, ST_ROW);
+  }
+
+  void oafilter(const mvr_oafilter_p& f, const Act& xd) {
+    const int C = pl.C, Kc = pl.Kc;
+    finalize_in(xd, 1e-3f, f.bn1);
+    Act o1{pl.O1, (int64_t)C * Kc, Kc, C, Kc, pl.stcol, Kc, 0};
+    conv(f.conv1, xd, true, o1, nullptr, train ? ST_COL : ST_NONE);
+    if (train) {
+      hipLaunchKernelGGL(bn_col_train_kernel, dim3((Kc + 255) / 256), dim3(256), 0, s, pl.stcol, pl.P,
+                         gemm_mtiles(C), Kc, C, f.bn2, pl.scK, pl.shK);
+    } else {
+      hipLaunchKernelGGL(bn_fold_eval_kernel, dim3((Kc + 255) / 256), dim3(256), 0, s, f.bn2, Kc, pl.scK, pl.shK);
+    }
+    chk_launch();
+    // out2(c,k') = sum_k relu(bn2_k(o1(c,k))) W2[k'][k] + b2[k'] + o1(c,k')   (conv on the transpose)
+    Act o2{pl.O2, (int64_t)C * Kc, Kc, C, Kc, pl.stO, C, 0};
+    GemmArgs g{};
+    g.M = C; g.N = Kc; g.K = Kc; g.batch = pl.P;
+    g.A = pl.O1; g.sAb = (int64_t)C * Kc; g.lda = Kc;
+    g.B = f.conv2.weight; g.sBb = 0; g.ldb = Kc; g.bkc = 1;
+    g.C = o2.p; g.sCb = o2.ps; g.ldc = Kc;
+    g.R = pl.O1; g.sRb = (int64_t)C * Kc; g.has_res = 1;
+    g.bias = f.conv2.bias; g.bias_mode = BIAS_N;
+    g.pro = PRO_A_K; g.psc = pl.scK; g.psh = pl.shK; g.sPb = 0;
+    g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
+    chk(launch_gemm(g, s));
+    finalize_in(o2, 1e-3f, f.bn3);
+    conv(f.conv3, o2, true, xd, &xd, ST_ROW);  // in place: out = conv3(...) + x
+  }
+
+  void smx_finalize(int T, int L) {
+    dim3 grid((L + 255) / 256, pl.P);
+    hipLaunchKernelGGL(smx_finalize_kernel, grid, dim3(256), 0, s, pl.smx, T, L, pl.mx, pl.rs);
+    chk_launch();
+  }
+};
+
+}  // namespace
+}  // namespace mvr
+
+using namespace mvr;
+
+extern "C" size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int P, int N) {
+  return plan(channels, clusters, P, N, nullptr).bytes;
+}
+
+extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride,
+                                     const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N,
+                                     int bn_train, float* logits, float* scores, float* R, float* t, float* res,
+                                     float* latent, float* res_row, float* score_row, int64_t row_pstride,
+                                     int32_t* guard_pos, int32_t* status, void* workspace, size_t workspace_bytes,
+                                     hipStream_t s) {
+  if (!blk || !input || !xs || !logits || !scores || !R || !t || !res || !guard_pos || !workspace) return MVR_EINVAL;
+  const int C = blk->channels, Kc = blk->clusters, H = blk->half_layers;
+  if (P <= 0 || N <= 0 || C <= 0 || Kc <= 0 || H <= 0 || H > MVR_OAN_MAX_HALF || blk->in_channels <= 0)
+    return MVR_EINVAL;
+  if (!blk->l1_2[0].shortcut.weight) return MVR_EINVAL;
+  const Plan pl = plan(C, Kc, P, N, workspace);
+  if (workspace_bytes < pl.bytes) return MVR_EINVAL;
+  Ctx cx{pl, s, bn_train};
+  const int64_t CN = (int64_t)C * N;
+  const int TN = gemm_ntiles(N);
+
+  // conv1: input (Cin ch) -> XA
+  Act in{const_cast<float*>(input), in_pstride, N, blk->in_channels, N, nullptr, 0, 0};
+  Act xa{pl.XA, CN, N, C, N, pl.stA, C, 0};
+  cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW);
+  // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C))
+  Act x11top{pl.X11, 2 * CN, N, C, N, pl.st11, 2 * C, 0};
+  for (int i = 0; i < H; ++i) cx.pointcn(blk->l1_1[i], xa, (i == H - 1) ? x11top : xa);
+
+  // diff_pool (oanet.py:96-110)
+  cx.finalize_in(x11top, 1e-3f, blk->down_bn);
+  Act e{pl.E, (int64_t)Kc * N, N, Kc, N, pl.smx, Kc, 0};
+  cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);
+  cx.smx_finalize(TN, Kc);
+  Act xd{pl.XD, (int64_t)C * Kc, Kc, C, Kc, pl.stD, C, 0};
+  {
+    GemmArgs g{};
+    g.M = C; g.N = Kc; g.K = N; g.batch = P;
+    g.A = pl.X11; g.sAb = 2 * CN; g.lda = N;
+    g.B = pl.E; g.sBb = (int64_t)Kc * N; g.ldb = N; g.bkc = 1;
+    g.C = pl.XD; g.sCb = (int64_t)C * Kc; g.ldc = Kc;
+    g.pro = PRO_B_SMX; g.psc = pl.mx; g.psh = pl.rs; g.sPb = Kc;
+    g.stats_mode = ST_ROW; g.stats = pl.stD; g.st_ld = C; g.st_off = 0;
+    cx.chk(launch_gemm(g, s));
+  }
+  // l2: OAFilter x H (in place on XD)
+  for (int i = 0; i < H; ++i) cx.oafilter(blk->l2[i], xd);
+
+  // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C)
+  cx.finalize_in(x11top, 1e-3f, blk->up_bn);
+  Act e2{pl.E, (int64_t)Kc * N, N, Kc, N, pl.smx, N, 0};
+  cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX);
+  cx.smx_finalize(gemm_mtiles(Kc), N);
+  {
+    GemmArgs g{};
+    g.M = C; g.N = N; g.K = Kc; g.batch = P;
+    g.A = pl.XD; g.sAb = (int64_t)C * Kc; g.lda = Kc;
+    g.B = pl.E; g.sBb = (int64_t)Kc * N; g.ldb = N; g.bkc = 0;
+    g.C = pl.X11 + CN; g.sCb = 2 * CN; g.ldc = N;
+    g.pro = PRO_B_SMX; g.psc = pl.mx; g.psh = pl.rs; g.sPb = N;
+    g.stats_mode = ST_ROW; g.stats = pl.st11; g.st_ld = 2 * C; g.st_off = C;
+    cx.chk(launch_gemm(g, s));
+  }
+  // l1_2: PointCN(2C -> C, shortcut) + (H-1) PointCN(C)
+  Act x11{pl.X11, 2 * CN, N, 2 * C, N, pl.st11, 2 * C, 0};
+  Act out{latent ? latent : pl.XA, CN, N, C, N, pl.stA, C, 0};
+  cx.pointcn(blk->l1_2[0], x11, out);
+  for (int i = 1; i < H; ++i) cx.pointcn(blk->l1_2[i], out, out);
+
+  // head + guard + Kabsch
+  (void)hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s);
+  hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, CN, C, N, blk->output.weight,
+                     blk->output.bias, logits, scores, guard_pos);
+  cx.chk_launch();
+  if (cx.err) return cx.err;
+  // weights = relu(tanh(logits)) already in `scores`; the guard (oanet.py:177-178) and
+  // Kabsch (oanet.py:180-183, normalize_w=True, eps=1e-7)
+  int e3 = mvr_procrustes(xs, xs + 3, xs_pstride, xs_nstride, scores, N, guard_pos, nullptr, 0, P, N, 1, 1e-7f, R,
+                          t, res, N, res_row, row_pstride, status, s);
+  if (e3) return e3;
+  if (score_row) {  // next block's input row 7 = (guarded) scores (oanet.py:247-248)
+    (void)hipMemcpy2DAsync(score_row, row_pstride * sizeof(float), scores, N * sizeof(float), N * sizeof(float), P,
+                     hipMemcpyDeviceToDevice, s);
+  }
+  return hipGetLastError() == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+}

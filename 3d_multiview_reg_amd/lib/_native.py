@@ -1,0 +1,116 @@
+"""ctypes binding of libmvreg_hip.so (the C ABI declared in include/mvreg.h).
+
+The product path has NO CPU fallback: if the HIP library or a HIP device is
+missing, every op raises.  torch is imported first so that the library binds
+to the HIP runtime torch already loaded (one runtime, shared streams).
+"""
+import ctypes
+import os
+
+import torch
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "libmvreg_hip.so")
+_lib = None
+
+c_i64 = ctypes.c_int64
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_vp = ctypes.c_void_p
+c_size = ctypes.c_size_t
+
+
+class ConvP(ctypes.Structure):
+    _fields_ = [("weight", c_vp), ("bias", c_vp)]
+
+
+class BnP(ctypes.Structure):
+    _fields_ = [("gamma", c_vp), ("beta", c_vp), ("mean", c_vp), ("var", c_vp)]
+
+
+class PointCNP(ctypes.Structure):
+    _fields_ = [("bn1", BnP), ("conv3", ConvP), ("bn5", BnP), ("conv7", ConvP), ("shortcut", ConvP)]
+
+
+class OAFilterP(ctypes.Structure):
+    _fields_ = [("bn1", BnP), ("conv1", ConvP), ("bn2", BnP), ("conv2", ConvP), ("bn3", BnP), ("conv3", ConvP)]
+
+
+MAX_HALF = 8
+
+
+class OanBlockP(ctypes.Structure):
+    _fields_ = [("in_channels", c_int), ("channels", c_int), ("clusters", c_int), ("half_layers", c_int),
+                ("conv1", ConvP), ("l1_1", PointCNP * MAX_HALF), ("down_bn", BnP), ("down_conv", ConvP),
+                ("l2", OAFilterP * MAX_HALF), ("up_bn", BnP), ("up_conv", ConvP), ("l1_2", PointCNP * MAX_HALF),
+                ("output", ConvP)]
+
+
+_SIGS = {
+    "mvr_procrustes": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_float,
+                               c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "mvr_procrustes_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int,
+                                   ctypes.c_double, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
+                             c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_int,
+                             c_vp]),
+    "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int]),
+    "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_size,
+                                      c_vp]),
+    "mvr_xs_to_channels": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp]),
+}
+
+# every symbol include/mvreg.h declares (checked by tests/test_native_abi.py)
+EXPORTS = tuple(_SIGS)
+
+
+def lib():
+    """Load libmvreg_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("libmvreg_hip.so not found at %s — run __graft_entry__.build() "
+                               "(there is no CPU fallback for the HIP path)" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def require_hip(t=None):
+    if not torch.cuda.is_available():
+        raise RuntimeError("mvreg HIP path: no HIP device available (no CPU fallback)")
+    if t is not None and t.device.type != "cuda":
+        raise RuntimeError("mvreg HIP path: tensor on %s, expected a HIP device" % t.device)
+
+
+def stream():
+    return c_vp(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return c_vp(t.data_ptr())
+
+
+def check(rc, name):
+    if rc != 0:
+        raise RuntimeError("%s failed with code %d" % (name, rc))
+
+
+_ws_cache = {}
+
+
+def workspace(nbytes, device):
+    """Reusable per-device scratch buffer (grown on demand)."""
+    key = (device.index if device.index is not None else torch.cuda.current_device())
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf

@@ -1,0 +1,195 @@
+"""OANet correspondence filter — MI355X implementation behind the reference's
+module surface (lib/filtering/oanet.py: OANet(cfg), forward(dict) -> dict).
+
+The parameter tree reproduces the reference's state-dict keys exactly
+(e.g. 'reg_init.l1_1.0.conv.3.weight', 'reg_iter.0.l2.2.conv2.0.running_var'),
+so reference checkpoints load unchanged (lib/checkpoints.py).  The forward
+pass is ONE native call per block (mvr_oan_block_forward in
+libmvreg_hip.so: fused fp32-MFMA GEMMs + InstanceNorm/softmax statistics +
+output head + zero-weight guard + weighted Procrustes).  There is no torch
+fallback: a CPU module raises.
+"""
+import ctypes
+import logging
+
+import torch
+import torch.nn as nn
+
+from lib import _native as N
+
+
+class _Slots(nn.Module):
+    """Numbered children (the parametric positions of the reference's
+    nn.Sequential stacks), so state-dict keys match index for index."""
+
+    def __init__(self, slots):
+        super().__init__()
+        for k in sorted(slots, key=int):
+            self.add_module(str(k), slots[k])
+
+    def __getitem__(self, i):
+        return self._modules[str(i)]
+
+    def __len__(self):
+        return len(self._modules)
+
+
+def _bn(c):
+    return nn.BatchNorm2d(c)
+
+
+def _conv(cin, cout):
+    return nn.Conv2d(cin, cout, kernel_size=1)
+
+
+class PointCN(nn.Module):
+    """oanet.py:18-43 — IN BN ReLU Conv IN BN ReLU Conv (+ shot_cut conv if cin != cout)."""
+
+    def __init__(self, channels, out_channels=None):
+        super().__init__()
+        out_channels = out_channels or channels
+        self.shot_cut = _conv(channels, out_channels) if out_channels != channels else None
+        self.conv = _Slots({1: _bn(channels), 3: _conv(channels, out_channels), 5: _bn(out_channels),
+                            7: _conv(out_channels, out_channels)})
+
+
+class OAFilter(nn.Module):
+    """oanet.py:56-93 — order-aware filtering over the clusters."""
+
+    def __init__(self, channels, points):
+        super().__init__()
+        self.conv1 = _Slots({1: _bn(channels), 3: _conv(channels, channels)})
+        self.conv2 = _Slots({0: _bn(points), 2: _conv(points, points)})
+        self.conv3 = _Slots({2: _bn(channels), 4: _conv(channels, channels)})
+
+
+class _Pool(nn.Module):
+    """diff_pool / diff_unpool parameters (oanet.py:96-129): IN BN ReLU Conv(C -> clusters)."""
+
+    def __init__(self, channels, clusters):
+        super().__init__()
+        self.output_points = clusters
+        self.conv = _Slots({1: _bn(channels), 3: _conv(channels, clusters)})
+
+
+class OANBlock(nn.Module):
+    """oanet.py:132-185."""
+
+    def __init__(self, net_channels, input_channel, depth, clusters, normalize_w=True):
+        super().__init__()
+        self.layer_num = depth
+        self.in_channels = input_channel
+        self.channels = net_channels
+        self.clusters = clusters
+        half = depth // 2
+        if half > N.MAX_HALF:
+            raise ValueError("net_depth too large for the native block (max %d layers per stage)" % (2 * N.MAX_HALF))
+        logging.info("OANET: channels:%d, layer_num:%d", net_channels, depth)
+        self.conv1 = _conv(input_channel, net_channels)
+        self.l1_1 = _Slots({i: PointCN(net_channels) for i in range(half)})
+        self.down1 = _Pool(net_channels, clusters)
+        self.l2 = _Slots({i: OAFilter(net_channels, clusters) for i in range(half)})
+        self.up1 = _Pool(net_channels, clusters)
+        self.l1_2 = _Slots({i: (PointCN(2 * net_channels, net_channels) if i == 0 else PointCN(net_channels))
+                            for i in range(half)})
+        self.output = _conv(net_channels, 1)
+
+    # ---- native parameter table (pointers into this module's device tensors)
+    @staticmethod
+    def _cp(conv):
+        if conv is None:
+            return N.ConvP(None, None)
+        return N.ConvP(conv.weight.data_ptr(), conv.bias.data_ptr() if conv.bias is not None else None)
+
+    @staticmethod
+    def _bp(bn):
+        return N.BnP(bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr())
+
+    def _pcn(self, m):
+        c = m.conv
+        return N.PointCNP(self._bp(c[1]), self._cp(c[3]), self._bp(c[5]), self._cp(c[7]), self._cp(m.shot_cut))
+
+    def native_params(self):
+        for t in list(self.parameters()) + list(self.buffers()):
+            if t.dtype.is_floating_point:
+                if t.dtype != torch.float32 or not t.is_contiguous() or t.device.type != "cuda":
+                    raise RuntimeError("OANBlock parameters must be contiguous float32 on a HIP device")
+        p = N.OanBlockP()
+        p.in_channels, p.channels, p.clusters, p.half_layers = (self.in_channels, self.channels, self.clusters,
+                                                                self.layer_num // 2)
+        p.conv1 = self._cp(self.conv1)
+        for i in range(self.layer_num // 2):
+            p.l1_1[i] = self._pcn(self.l1_1[i])
+            f = self.l2[i]
+            p.l2[i] = N.OAFilterP(self._bp(f.conv1[1]), self._cp(f.conv1[3]), self._bp(f.conv2[0]),
+                                  self._cp(f.conv2[2]), self._bp(f.conv3[2]), self._cp(f.conv3[4]))
+            p.l1_2[i] = self._pcn(self.l1_2[i])
+        p.down_bn, p.down_conv = self._bp(self.down1.conv[1]), self._cp(self.down1.conv[3])
+        p.up_bn, p.up_conv = self._bp(self.up1.conv[1]), self._cp(self.up1.conv[3])
+        p.output = self._cp(self.output)
+        return p
+
+
+class OANet(nn.Module):
+    """OANet filtering network (oanet.py:188-265): reg_init + iter_num reg_iter blocks,
+    each ending in a weighted Kabsch."""
+
+    def __init__(self, cfg):
+        super().__init__()
+        self.iter_num = cfg["misc"]["iter_num"]
+        depth_each_stage = cfg["misc"]["net_depth"] // (cfg["misc"]["iter_num"] + 1)
+        self.side_channel = (cfg["data"]["use_mutuals"] == 2)
+        C, K = cfg["misc"]["net_channel"], cfg["misc"]["clusters"]
+        nrm = cfg["misc"]["normalize_weights"]
+        self.reg_init = OANBlock(C, 6 + self.side_channel, depth_each_stage, K, nrm)
+        self.reg_iter = _Slots({i: OANBlock(C, 8 + self.side_channel, depth_each_stage, K, nrm)
+                                for i in range(self.iter_num)})
+        self.device = torch.device("cuda" if (torch.cuda.is_available() and cfg["misc"]["use_gpu"]) else "cpu")
+
+    def forward(self, data):
+        xs_in = data["xs"]
+        assert xs_in.dim() == 4 and xs_in.shape[1] == 1
+        N.require_hip()
+        dev = self.reg_init.conv1.weight.device
+        N.require_hip(self.reg_init.conv1.weight)
+        xs = xs_in.to(dev, torch.float32)[:, 0].contiguous()           # [P, N, Cxs]
+        P, Np, Cxs = xs.shape
+        if Cxs < 6:
+            raise ValueError("xs must have at least 6 channels (x1 | x2)")
+        L = N.lib()
+        st = N.stream()
+        rows = Cxs + 2
+        inp = torch.empty(P, rows, Np, device=dev, dtype=torch.float32)
+        N.check(L.mvr_xs_to_channels(N.ptr(xs), Np * Cxs, Cxs, Cxs, P, Np, N.ptr(inp), rows * Np, st),
+                "mvr_xs_to_channels")
+        blocks = [self.reg_init] + [self.reg_iter[i] for i in range(self.iter_num)]
+        C = self.reg_init.channels
+        ws_bytes = L.mvr_oan_block_workspace_bytes(C, self.reg_init.clusters, P, Np)
+        ws = N.workspace(ws_bytes, dev)
+        guard = torch.empty(P, dtype=torch.int32, device=dev)
+        status = torch.zeros(len(blocks), P, dtype=torch.int32, device=dev)
+        latent = torch.empty(P, C, Np, device=dev, dtype=torch.float32)
+        out = {"logits": [], "scores": [], "rot_est": [], "trans_est": []}
+        for bi, blk in enumerate(blocks):
+            params = blk.native_params()
+            logits = torch.empty(P, Np, device=dev)
+            scores = torch.empty(P, Np, device=dev)
+            R = torch.empty(P, 3, 3, device=dev)
+            t = torch.empty(P, 3, 1, device=dev)
+            res = torch.empty(P, Np, device=dev)
+            last = bi == len(blocks) - 1
+            rc = L.mvr_oan_block_forward(
+                ctypes.byref(params), N.ptr(inp), rows * Np, N.ptr(xs), Np * Cxs, Cxs, P, Np, int(self.training),
+                N.ptr(logits), N.ptr(scores), N.ptr(R), N.ptr(t), N.ptr(res), N.ptr(latent) if last else None,
+                None if last else N.ptr(inp[:, Cxs]), None if last else N.ptr(inp[:, Cxs + 1]), rows * Np,
+                N.ptr(guard), N.ptr(status[bi]), N.ptr(ws), ws.numel(), st)
+            N.check(rc, "mvr_oan_block_forward")
+            if bi == 0 and not last:
+                blk_in_ch = blocks[1].in_channels
+                if blk_in_ch != rows:
+                    raise ValueError("reg_iter input channels %d != %d" % (blk_in_ch, rows))
+            for k, v in zip(("logits", "scores", "rot_est", "trans_est"), (logits, scores, R, t)):
+                out[k].append(v)
+        out["latent features"] = latent.unsqueeze(3)
+        out["gradient_flag"] = bool(status.any().item())
+        return out

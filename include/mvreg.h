@@ -1,0 +1,117 @@
+/*
+ * mvreg — MI355X-native pairwise registration hot path of LMPCR
+ * (zgojcic/3D_multiview_reg).  C ABI of libmvreg_hip.so.
+ *
+ * Conventions (every entry point):
+ *   - returns 0 (MVR_OK) or a negative error code; never throws across the ABI;
+ *   - all pointers are DEVICE pointers allocated by the caller (no hidden
+ *     allocation); workspaces are sized by the paired *_workspace_bytes() query;
+ *   - calls are stream-ordered on `stream` (a hipStream_t; 0 = legacy default),
+ *     re-entrant, and thread-safe across distinct streams/devices;
+ *   - strides are in ELEMENTS.
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the reference repo).
+ */
+#ifndef MVREG_H
+#define MVREG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mvr_stream_t; /* == hipStream_t */
+
+#define MVR_OK 0
+#define MVR_EINVAL -1
+#define MVR_ELAUNCH -2
+
+/* ------------------------------------------------------------------------
+ * Weighted Procrustes / Kabsch.
+ * Replaces lib/utils.py:164-237 kabsch_transformation_estimation (+ residuals
+ * lib/utils.py:240-256), and — when guard_pos != NULL — the batch-coupled
+ * zero-weight guard of lib/filtering/oanet.py:177-178 (if any pair q has
+ * guard_pos[q]==0, every pair's weights get +1/N; w and w_copy are rewritten).
+ *   x1(p,n,:) = x1[p*x_pstride + n*x_nstride + 0..2], x2 likewise.
+ *   w may be NULL (all ones).  R [P,3,3] row-major, t [P,3], res [P, res_pstride],
+ *   status[P]: 0 ok, 1 non-finite covariance (reference's SVD-exception branch:
+ *   R=I, t=0).  res/res_copy/w_copy/status may be NULL.
+ * ---------------------------------------------------------------------- */
+int mvr_procrustes(const float* x1, const float* x2, int64_t x_pstride, int64_t x_nstride, float* w,
+                   int64_t w_pstride, const int32_t* guard_pos, float* w_copy, int64_t wc_pstride, int P, int N,
+                   int normalize, float eps, float* R, float* t, float* res, int64_t res_pstride, float* res_copy,
+                   int64_t rc_pstride, int32_t* status, mvr_stream_t stream);
+/* fp64 variant (fp64 inputs compute in fp64 in the reference, utils.py:164). */
+int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_pstride, int64_t x_nstride, double* w,
+                       int64_t w_pstride, const int32_t* guard_pos, double* w_copy, int64_t wc_pstride, int P, int N,
+                       int normalize, double eps, double* R, double* t, double* res, int64_t res_pstride,
+                       double* res_copy, int64_t rc_pstride, int32_t* status, mvr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * One fused fp32-MFMA batched GEMM of the OANet schedule (exposed for tests):
+ *   C[b](m,n) = sum_k pro_A(A(m,k)) pro_B(B(k,n)) + bias + R[b](m,n)
+ * pro: 0 none, 1 relu(A*sc[k]+sh[k]), 2 relu(B*sc[k]+sh[k]), 3 exp(B-sc[n])*sh[n]
+ * bias_mode: 0 none, 1 per m, 2 per n.  stats_mode: 0 none, 1 row sum/sumsq,
+ * 2 row max/sumexp, 3 column max/sumexp (float2 partials, see csrc/gemm.hpp).
+ * Replaces the nn.Conv2d(k=1) / torch.matmul calls of lib/filtering/oanet.py.
+ * ---------------------------------------------------------------------- */
+int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
+                 int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
+                 int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
+                 int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, mvr_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters
+ * are the reference module's tensors (conv weights [Cout][Cin] row-major =
+ * the Conv2d weight with its 1x1 tail dropped).
+ * ---------------------------------------------------------------------- */
+typedef struct { const float* weight; const float* bias; } mvr_conv_p;
+typedef struct { const float* gamma; const float* beta; const float* mean; const float* var; } mvr_bn_p;
+typedef struct { mvr_bn_p bn1; mvr_conv_p conv3; mvr_bn_p bn5; mvr_conv_p conv7; mvr_conv_p shortcut; } mvr_pointcn_p;
+typedef struct {
+  mvr_bn_p bn1; mvr_conv_p conv1; /* conv1: IN(1e-3) BN ReLU Conv          (oanet.py:64-69) */
+  mvr_bn_p bn2; mvr_conv_p conv2; /* conv2: BN(points) ReLU Conv(points)  (oanet.py:72-76) */
+  mvr_bn_p bn3; mvr_conv_p conv3; /* conv3: IN(1e-3) BN ReLU Conv          (oanet.py:77-83) */
+} mvr_oafilter_p;
+
+#define MVR_OAN_MAX_HALF 8
+typedef struct {
+  int in_channels;  /* 6 (reg_init) or 8 (reg_iter) */
+  int channels;     /* net_channel (128) */
+  int clusters;     /* clusters (500) */
+  int half_layers;  /* (net_depth / (iter_num+1)) / 2  (3) */
+  mvr_conv_p conv1;
+  mvr_pointcn_p l1_1[MVR_OAN_MAX_HALF];
+  mvr_bn_p down_bn; mvr_conv_p down_conv;
+  mvr_oafilter_p l2[MVR_OAN_MAX_HALF];
+  mvr_bn_p up_bn; mvr_conv_p up_conv;
+  mvr_pointcn_p l1_2[MVR_OAN_MAX_HALF]; /* l1_2[0] has a shortcut conv (2C -> C) */
+  mvr_conv_p output;
+} mvr_oan_block_p;
+
+size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int P, int N);
+
+/* input(p,c,n) = input[p*in_pstride + c*N + n]  (Cin = blk->in_channels)
+ * xs(p,n,0..5) = xs[p*xs_pstride + n*xs_nstride + 0..5]  (x1 | x2 for Kabsch)
+ * Outputs: logits/scores [P,N] (contiguous), R [P,3,3], t [P,3], res [P,N];
+ * latent [P,C,N] (may be NULL); res_row/score_row: optional copies written at
+ * row pointers with pair stride row_pstride (the next block's input rows 6,7).
+ * guard_pos: int32 [P] scratch (zeroed here).  status: int32 [P] (may be NULL).
+ * bn_train: BatchNorm layers normalise with batch statistics (module.train()). */
+int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride, const float* xs,
+                          int64_t xs_pstride, int64_t xs_nstride, int P, int N, int bn_train, float* logits,
+                          float* scores, float* R, float* t, float* res, float* latent, float* res_row,
+                          float* score_row, int64_t row_pstride, int32_t* guard_pos, int32_t* status, void* workspace,
+                          size_t workspace_bytes, mvr_stream_t stream);
+
+/* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*N + n]
+ * (the transpose of lib/filtering/oanet.py:234). */
+int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N, float* out,
+                       int64_t out_pstride, mvr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

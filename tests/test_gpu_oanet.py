@@ -1,0 +1,122 @@
+"""HIP path (libmvreg_hip.so) vs the reference's golden vectors and the CPU
+oracle: weighted Kabsch (lib/utils.py:164-237) and the OANet filter
+(lib/filtering/oanet.py), eval / train-mode BN / zero-row guard, full size.
+
+Tolerances (BASELINE.json north_star): R, t within 1e-4; identical inlier masks
+(scores > 0.5) except points whose reference score lies within 1e-4 of 0.5
+(fp32 summation-order noise, reported)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden, GOLDEN
+from synth import synth_state, synth_correspondences
+
+pytestmark = pytest.mark.gpu
+
+
+def _shapes(which):
+    with open(os.path.join(GOLDEN, "oanet_keys.json")) as f:
+        return json.load(f)[which]
+
+
+def test_kabsch_golden_f32_f64(gpu):
+    import torch
+    from lib.utils import kabsch_transformation_estimation as kabsch
+    g = golden("kabsch.npz")
+    for tag, dt in (("f32", torch.float32), ("f64", torch.float64)):
+        x1 = torch.from_numpy(g["x1"]).to(gpu, dt)
+        x2 = torch.from_numpy(g["x2"]).to(gpu, dt)
+        w = torch.from_numpy(g["w"]).to(gpu, dt)
+        R, t, res, flag = kabsch(x1, x2, w)
+        tol = 1e-5 if dt == torch.float32 else 1e-9
+        np.testing.assert_allclose(R.cpu().numpy(), g["R_" + tag], atol=tol)
+        np.testing.assert_allclose(t.cpu().numpy(), g["t_" + tag], atol=10 * tol)
+        np.testing.assert_allclose(res.cpu().numpy(), g["res_" + tag], atol=10 * tol)
+        assert flag == bool(g["flag_" + tag])
+    R, t, res, _ = kabsch(torch.from_numpy(g["x1"]).to(gpu), torch.from_numpy(g["x2"]).to(gpu))
+    np.testing.assert_allclose(R.cpu().numpy(), g["R_none"], atol=1e-5)
+    np.testing.assert_allclose(t.cpu().numpy(), g["t_none"], atol=1e-4)
+
+
+def test_kabsch_recovers_known_motion_large_batch(gpu):
+    """size-independent property at benchmark scale: exact correspondences -> exact motion."""
+    import torch
+    from lib.utils import kabsch_transformation_estimation as kabsch
+    xs, Rg, tg = synth_correspondences(64, 5000, seed=3, inlier_lo=1.0, inlier_hi=1.0)
+    x1 = torch.from_numpy(xs[..., :3]).to(gpu, torch.float64)
+    x2 = (x1 @ torch.from_numpy(Rg).to(gpu, torch.float64).transpose(1, 2)) + torch.from_numpy(tg).to(gpu, torch.float64)[:, None]
+    R, t, res, _ = kabsch(x1, x2)
+    np.testing.assert_allclose(R.cpu().numpy(), Rg, atol=1e-7)  # Rg is fp32-rounded (not exactly orthogonal)
+    assert float(res.max()) < 1e-6
+
+
+def _oanet(cfg_c, cfg_k, seed, gpu, train=False, overrides=None, which="small"):
+    import torch
+    from lib.filtering.oanet import OANet
+    cfg = {"misc": {"net_depth": 12, "clusters": cfg_k, "iter_num": 1, "net_channel": cfg_c, "use_gpu": True,
+                    "normalize_weights": True}, "data": {"use_mutuals": 0}}
+    net = OANet(cfg)
+    st = synth_state(_shapes(which), seed=seed, overrides=overrides)
+    sd = net.state_dict()
+    assert set(sd) == set(st), "state-dict keys differ from the reference"
+    for k in sd:
+        assert tuple(sd[k].shape) == tuple(np.asarray(st[k]).shape), k
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    net = net.to(gpu)
+    net.train(train)
+    return net
+
+
+def _check(out, g, atol_logit=5e-4):
+    for i in range(2):
+        sc = out["scores"][i].cpu().numpy()
+        np.testing.assert_allclose(out["logits"][i].cpu().numpy(), g["logits%d" % i], atol=atol_logit, rtol=1e-4)
+        np.testing.assert_allclose(sc, g["scores%d" % i], atol=atol_logit)
+        np.testing.assert_allclose(out["rot_est"][i].cpu().numpy(), g["R%d" % i], atol=1e-4)
+        np.testing.assert_allclose(out["trans_est"][i].cpu().numpy(), g["t%d" % i], atol=1e-4)
+        ref = g["scores%d" % i]
+        near = np.abs(ref - 0.5) < 1e-4
+        assert np.array_equal((sc > 0.5)[~near], (ref > 0.5)[~near])
+
+
+@pytest.mark.parametrize("fx,train,ovr", [("oanet_small_eval.npz", False, None),
+                                          ("oanet_small_train.npz", True, None),
+                                          ("oanet_small_guard.npz", False, {"reg_init.output.bias": [-50.0]})])
+def test_oanet_small_golden(gpu, fx, train, ovr):
+    import torch
+    g = golden(fx)
+    net = _oanet(32, 16, 5, gpu, train=train, overrides=ovr)
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(g["xs"]).unsqueeze(1)})
+    _check(out, g)
+    np.testing.assert_allclose(out["latent features"].cpu().numpy(), g["latent"], atol=2e-3, rtol=1e-3)
+    assert out["gradient_flag"] == bool(g["gradient_flag"])
+
+
+def test_oanet_full_golden(gpu):
+    import torch
+    g = golden("oanet_full_eval.npz")
+    net = _oanet(128, 500, 7, gpu, which="full")
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(g["xs"]).unsqueeze(1)})
+    _check(out, g, atol_logit=2e-3)
+
+
+def test_oanet_matches_oracle_batch_and_ragged_n(gpu):
+    """B=5 pairs, N=1234 (not a tile multiple) against the numpy oracle."""
+    import torch
+    from oracle.oanet import oanet_forward
+    xs, _, _ = synth_correspondences(5, 1234, seed=77)
+    net = _oanet(128, 500, 7, gpu, which="full")
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
+    st = synth_state(_shapes("full"), seed=7)
+    o = oanet_forward(st, xs)
+    g = {}
+    for i in range(2):
+        g["logits%d" % i], g["scores%d" % i] = o["logits"][i], o["scores"][i]
+        g["R%d" % i], g["t%d" % i] = o["rot_est"][i], o["trans_est"][i]
+    _check(out, g, atol_logit=2e-3)
