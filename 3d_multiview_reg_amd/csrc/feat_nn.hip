@@ -18,6 +18,7 @@
 // FLOPs per pair ~ 2*N*M*C (MFMA) + N*M*(exp + 5 FMA); HBM: features/coords of
 // the two fragments (L2/MALL-resident across the pairs that share them).
 #include "common.hpp"
+#include "prof.hpp"
 
 namespace mvr {
 
@@ -28,13 +29,15 @@ constexpr int NN_FLD = 32 + 4;     // padded LDS row (floats) for 32-dim feature
 constexpr float NN_NEG = -3.0e38f;
 
 struct NNArgs {
-  const float* F; int64_t f_fs;     // features [B][*][32], fragment stride (elements)
-  const float* X; int64_t x_fs;     // coords [B][*][3]
-  const int64_t* pairs;             // [P][2] (src, tgt)
+  const float* Fq; int64_t fq_fs;    // query features [*][Nq][32], fragment stride (elements)
+  const float* Ft; int64_t ft_fs;    // target features [*][Mt][32]
+  const float* Xq; int64_t xq_fs;    // query coords (optional: output then holds [x_q | x_corr])
+  const float* Xt; int64_t xt_fs;    // target coords [*][Mt][3]
+  const int64_t* pairs;              // [P][2] (query fragment, target fragment)
   int P, Nq, Mt;
   float k2;                          // log2(e) / tau^2
   int mode;                          // 0 soft, 1 argmax (soft+st / hard)
-  float* xs; int64_t xs_ps, xs_ns;   // output xs(p,n,0..5) = [x_src | x_corr]
+  float* out; int64_t o_ps, o_ns;    // out(p,n,:) = [x_q(0..2) |] x_corr(0..2)
   int32_t* idx;                      // optional argmax index [P][Nq]
 };
 
@@ -45,9 +48,9 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(NNArgs a) {
   const int l32 = lane & 31, kh = lane >> 5;
   const int p = blockIdx.y;
   const int64_t src = a.pairs[2 * p], tgt = a.pairs[2 * p + 1];
-  const float* Fq = a.F + src * a.f_fs;
-  const float* Ft = a.F + tgt * a.f_fs;
-  const float* Xt = a.X + tgt * a.x_fs;
+  const float* Fq = a.Fq + src * a.fq_fs;
+  const float* Ft = a.Ft + tgt * a.ft_fs;
+  const float* Xt = a.Xt + tgt * a.xt_fs;
   const int j = blockIdx.x * 128 + wid * 32 + l32;  // this lane's query
   const bool jok = j < a.Nq;
 
@@ -174,10 +177,13 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(NNArgs a) {
     ox = xp[0]; oy = xp[1]; oz = xp[2];
   }
   if (jok && kh == 0) {
-    const float* xs = a.X + src * a.x_fs + (int64_t)j * 3;
-    float* o = a.xs + (int64_t)p * a.xs_ps + (int64_t)j * a.xs_ns;
-    o[0] = xs[0]; o[1] = xs[1]; o[2] = xs[2];
-    o[3] = ox; o[4] = oy; o[5] = oz;
+    float* o = a.out + (int64_t)p * a.o_ps + (int64_t)j * a.o_ns;
+    if (a.Xq) {
+      const float* xq = a.Xq + src * a.xq_fs + (int64_t)j * 3;
+      o[0] = xq[0]; o[1] = xq[1]; o[2] = xq[2];
+      o += 3;
+    }
+    o[0] = ox; o[1] = oy; o[2] = oz;
     if (a.idx && a.mode == 1) a.idx[(int64_t)p * a.Nq + j] = besti;
   }
 }
@@ -193,16 +199,21 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int C, const i
 
 }  // namespace mvr
 
-extern "C" int mvr_feat_nn(const float* F, int64_t f_fstride, const float* X, int64_t x_fstride,
-                           const int64_t* pairs, int P, int Nq, int Mt, int C, float inv_tau2, int mode, float* xs_out,
-                           int64_t xs_pstride, int64_t xs_nstride, int32_t* idx_out, hipStream_t stream) {
-  if (!F || !X || !pairs || !xs_out || P < 0 || Nq < 0 || Mt <= 0) return MVR_EINVAL;
+extern "C" int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride, const float* Xq,
+                           int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P,
+                           int Nq, int Mt, int C, float inv_tau2, int mode, float* out, int64_t out_pstride,
+                           int64_t out_nstride, int32_t* idx_out, hipStream_t stream) {
+  if (!Fq || !Ft || !Xt || !pairs || !out || P < 0 || Nq < 0 || Mt <= 0) return MVR_EINVAL;
   if (C != 32) return MVR_EINVAL;  // FCGF descriptor width (fcgf.py:108 out_channels=32)
-  if ((reinterpret_cast<uintptr_t>(F) & 15) || (f_fstride & 3)) return MVR_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(Fq) & 15) || (reinterpret_cast<uintptr_t>(Ft) & 15) || (fq_fstride & 3) ||
+      (ft_fstride & 3))
+    return MVR_EINVAL;
   if (mode != 0 && mode != 1) return MVR_EINVAL;
   if (P == 0 || Nq == 0) return MVR_OK;
-  mvr::NNArgs a{F, f_fstride, X, x_fstride, pairs, P, Nq, Mt, inv_tau2 * 1.4426950408889634f, mode,
-                xs_out, xs_pstride, xs_nstride, idx_out};
+  mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt,
+                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out};
+  mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * (C + 3) * 4 + P * Nq * 24.0,
+                      stream);
   hipLaunchKernelGGL(mvr::feat_nn_kernel, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;

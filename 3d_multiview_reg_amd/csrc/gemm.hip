@@ -18,6 +18,7 @@
 // Roofline: 2*M*N*K flops per GEMM against the 157.3 TF/s fp32 MFMA peak.
 #include "common.hpp"
 #include "gemm.hpp"
+#include "prof.hpp"
 
 namespace mvr {
 
@@ -324,6 +325,10 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   ka.vecB = al16(g.B) && (g.ldb % 4 == 0) && (g.sBb % 4 == 0);
   dim3 grid(gemm_ntiles(g.N), gemm_mtiles(g.M), g.batch);
   if (grid.y > 65535 || grid.z > 65535) return MVR_EINVAL;
+  const double fl = 2.0 * g.M * g.N * (double)g.K * g.batch;
+  const double by = 4.0 * ((double)g.M * g.K * (g.sAb ? g.batch : 1) + (double)g.K * g.N * (g.sBb ? g.batch : 1) +
+                           (double)g.M * g.N * g.batch * (g.has_res ? 2 : 1));
+  ProfScope prof(g.prof_kind, fl, by, s);
   // Dispatch only the combinations the OANet schedule uses (oanet.hip).
 #define MVR_CASE(P, BKC_, BI, ST, RS)                                                                     \
   if (g.pro == P && g.bkc == BKC_ && g.bias_mode == BI && g.stats_mode == ST && (g.has_res != 0) == RS) { \

@@ -34,6 +34,7 @@ struct GemmArgs {
   const float* psc; const float* psh; int64_t sPb;     // prologue vectors (batch stride sPb, may be 0)
   float2* stats; int64_t st_ld; int st_off;            // partial statistics (see Stats)
   int pro, bias_mode, stats_mode, has_res;
+  int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
 };
 
 // Launch on `stream`; returns 0 or a negative error.

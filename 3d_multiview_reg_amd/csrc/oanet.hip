@@ -11,6 +11,7 @@
 
 #include "common.hpp"
 #include "gemm.hpp"
+#include "prof.hpp"
 #include "mvreg.h"
 
 namespace mvr {
@@ -246,6 +247,7 @@ struct Ctx {
     if (pro) { g.pro = PRO_B_K; g.psc = pl.sc; g.psh = pl.sh; g.sPb = in.C; }
     g.stats_mode = stats_mode;
     g.stats = out.st; g.st_ld = out.st_ld; g.st_off = out.st_off;
+    g.prof_kind = (in.L == pl.Kc && out.L == pl.Kc) ? PK_OAFILTER : (out.C == pl.Kc ? PK_EMBED : PK_CONV_PTS);
     chk(launch_gemm(g, s));
   }
 
@@ -282,6 +284,7 @@ struct Ctx {
     g.bias = f.conv2.bias; g.bias_mode = BIAS_N;
     g.pro = PRO_A_K; g.psc = pl.scK; g.psh = pl.shK; g.sPb = 0;
     g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
+    g.prof_kind = PK_OAFILTER;
     chk(launch_gemm(g, s));
     finalize_in(o2, 1e-3f, f.bn3);
     conv(f.conv3, o2, true, xd, &xd, ST_ROW);  // in place: out = conv3(...) + x
@@ -342,6 +345,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.C = pl.XD; g.sCb = (int64_t)C * Kc; g.ldc = Kc;
     g.pro = PRO_B_SMX; g.psc = pl.mx; g.psh = pl.rs; g.sPb = Kc;
     g.stats_mode = ST_ROW; g.stats = pl.stD; g.st_ld = C; g.st_off = 0;
+    g.prof_kind = PK_POOL;
     cx.chk(launch_gemm(g, s));
   }
   // l2: OAFilter x H (in place on XD)
@@ -360,6 +364,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.C = pl.X11 + CN; g.sCb = 2 * CN; g.ldc = N;
     g.pro = PRO_B_SMX; g.psc = pl.mx; g.psh = pl.rs; g.sPb = N;
     g.stats_mode = ST_ROW; g.stats = pl.st11; g.st_ld = 2 * C; g.st_off = C;
+    g.prof_kind = PK_UNPOOL;
     cx.chk(launch_gemm(g, s));
   }
   // l1_2: PointCN(2C -> C, shortcut) + (H-1) PointCN(C)

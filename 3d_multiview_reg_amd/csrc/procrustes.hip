@@ -13,6 +13,7 @@
 // HBM bytes per pair (algorithmic): N*(24 read xyz pairs + 4 read w + 4 write res)
 // (+4+4 when the guard rewrites w and its copy).
 #include "common.hpp"
+#include "prof.hpp"
 #include <math.h>
 
 namespace mvr {
@@ -219,6 +220,7 @@ static int procrustes_launch(const T* x1, const T* x2, int64_t x_pstride, int64_
   if (P == 0) return MVR_OK;
   mvr::ProcrustesArgs<T> a{x1, x2, x_pstride, x_nstride, w, w_pstride, guard_pos, w_copy, wc_pstride,
                            P, N, normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status};
+  mvr::ProfScope prof(mvr::PK_PROCRUSTES, 40.0 * P * N, (double)P * N * sizeof(T) * 8, stream);
   hipLaunchKernelGGL(mvr::procrustes_kernel<T>, dim3(P), dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;

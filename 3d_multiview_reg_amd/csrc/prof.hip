@@ -1,0 +1,77 @@
+#include "prof.hpp"
+
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mvr {
+namespace {
+struct Rec { int kind; hipEvent_t a, b; double flops, bytes; };
+std::mutex mu;
+bool enabled = false;
+std::vector<Rec> recs;
+std::vector<hipEvent_t> pool;
+std::vector<int> open_idx;  // stack of records awaiting their end event
+hipEvent_t get_ev() {
+  if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+  hipEvent_t e;
+  (void)hipEventCreate(&e);
+  return e;
+}
+double tot_ms[PK_COUNT], tot_fl[PK_COUNT], tot_by[PK_COUNT];
+long long tot_n[PK_COUNT];
+void drain() {
+  for (auto& r : recs) {
+    if (!r.b) continue;
+    float ms = 0.f;
+    (void)hipEventSynchronize(r.b);
+    (void)hipEventElapsedTime(&ms, r.a, r.b);
+    tot_ms[r.kind] += ms; tot_fl[r.kind] += r.flops; tot_by[r.kind] += r.bytes; tot_n[r.kind] += 1;
+    pool.push_back(r.a); pool.push_back(r.b);
+  }
+  recs.clear();
+  open_idx.clear();
+}
+}  // namespace
+
+bool prof_on() { return enabled; }
+void prof_begin(int kind, double flops, double bytes, hipStream_t s) {
+  std::lock_guard<std::mutex> g(mu);
+  Rec r{kind, get_ev(), nullptr, flops, bytes};
+  (void)hipEventRecord(r.a, s);
+  recs.push_back(r);
+  open_idx.push_back((int)recs.size() - 1);
+}
+void prof_end(int kind, hipStream_t s) {
+  std::lock_guard<std::mutex> g(mu);
+  if (open_idx.empty()) return;
+  Rec& r = recs[open_idx.back()];
+  open_idx.pop_back();
+  r.b = get_ev();
+  (void)hipEventRecord(r.b, s);
+  (void)kind;
+}
+}  // namespace mvr
+
+using namespace mvr;
+
+extern "C" int mvr_prof_set(int on) {
+  std::lock_guard<std::mutex> g(mu);
+  drain();
+  for (int k = 0; k < PK_COUNT; ++k) { tot_ms[k] = tot_fl[k] = tot_by[k] = 0; tot_n[k] = 0; }
+  enabled = on != 0;
+  return MVR_OK;
+}
+
+// Per-kind totals since mvr_prof_set: device milliseconds, launches, algorithmic flops and bytes.
+extern "C" int mvr_prof_get(int kind, double* ms, long long* launches, double* flops, double* bytes) {
+  if (kind < 0 || kind >= PK_COUNT) return MVR_EINVAL;
+  std::lock_guard<std::mutex> g(mu);
+  drain();
+  if (ms) *ms = tot_ms[kind];
+  if (launches) *launches = tot_n[kind];
+  if (flops) *flops = tot_fl[kind];
+  if (bytes) *bytes = tot_by[kind];
+  return MVR_OK;
+}

@@ -58,6 +58,12 @@ _SIGS = {
     "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),
+    "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
+                            c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "mvr_prof_set": (c_int, [c_int]),
+    "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "mvr_xs_to_channels": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp]),
 }
 
@@ -101,6 +107,23 @@ def ptr(t):
 def check(rc, name):
     if rc != 0:
         raise RuntimeError("%s failed with code %d" % (name, rc))
+
+
+PROF_KINDS = {"conv_pts": 0, "embed": 1, "pool": 2, "unpool": 3, "oafilter": 4, "small": 5, "procrustes": 6,
+              "feat_nn": 7, "spconv": 8, "sparse_misc": 9}
+
+
+def prof_set(on):
+    check(lib().mvr_prof_set(int(on)), "mvr_prof_set")
+
+
+def prof_get(kind):
+    """(device ms, launches, algorithmic flops, algorithmic bytes) since prof_set(1)."""
+    ms, n, fl, by = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double(), ctypes.c_double()
+    k = PROF_KINDS[kind] if isinstance(kind, str) else int(kind)
+    check(lib().mvr_prof_get(k, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl), ctypes.byref(by)),
+          "mvr_prof_get")
+    return ms.value, n.value, fl.value, by.value
 
 
 _ws_cache = {}

@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the MI355X pairwise-registration hot path.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload scene|precomputed]
+
+One process per GPU (torchrun for N>1, RCCL over xGMI).  A *step* is one pass
+of the hot path over one batch of synthetic input resident in HBM:
+
+  scene        (default, BASELINE configs[2]: one 3DMatch-scale scene per GPU)
+               30 fragments of ~20k voxels -> FCGF descriptors -> rand sampling
+               (5000 pts) -> feature NN for all 435 pairs -> OANet -> Procrustes
+               -> RCCL all-gather of the per-pair (R, t, conf) records.
+  precomputed  (BASELINE configs[3] shape: the benchmark's precomputed
+               correspondences) 435 pairs x 5000 correspondences -> OANet ->
+               Procrustes -> all-gather.
+
+Weak scaling: every rank processes its own scene / pair batch (different seed).
+Rank 0 prints ONE JSON line (the driver contract); the roofline object prices
+the dominant kernel class from per-launch hipEvent timings taken inside the
+timed region; cpu_baseline times the numpy oracle (oracle/) on a bounded
+sample of the same workload on this host's cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "3d_multiview_reg_amd"), ROOT, os.path.join(ROOT, "tests", "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "point-cloud pairs/s (feat+match+filter+SVD), 3DMatch 20k-pt, 1/2/4/8 GPU"
+PEAK_FP32_TFLOPS = 157.3    # MI355X dense fp32 (vector == MFMA), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def oanet_cfg():
+    # configs/pairwise_registration/eval/RegBlock.yaml
+    return {"misc": {"net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128, "use_gpu": True,
+                     "normalize_weights": True}, "data": {"use_mutuals": 0, "max_num_points": 5000},
+            "method": {"task": "pairwise", "descriptor_module": None, "filter_module": "oanet"},
+            "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
+
+
+def synth_module(mod, seed):
+    from synth import synth_state
+    shapes = {k: tuple(v.shape) for k, v in mod.state_dict().items()}
+    st = synth_state(shapes, seed=seed)
+    mod.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    return st
+
+
+class PrecomputedWorkload:
+    name = "precomputed"
+
+    def __init__(self, dev, rank, pairs, npts):
+        from lib.filtering.oanet import OANet
+        from synth import synth_correspondences
+        self.net = OANet(oanet_cfg())
+        self.state = synth_module(self.net, seed=7)
+        self.net = self.net.to(dev).eval()
+        xs, _, _ = synth_correspondences(pairs, npts, seed=1000 + rank)
+        self.xs_host = xs
+        self.xs = torch.from_numpy(xs).to(dev).unsqueeze(1)
+        self.pairs = pairs
+        self.npts = npts
+
+    def step(self):
+        out = self.net({"xs": self.xs})
+        R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
+        conf = (s > 0.5).float().mean(dim=1, keepdim=True)
+        return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)   # [P, 13] records
+
+    def config(self):
+        return {"workload": "precomputed correspondences (configs[3] shape): OANet(128ch,500 clusters,depth 12,"
+                            "2 blocks)+Procrustes", "pairs_per_gpu": self.pairs, "correspondences": self.npts}
+
+    def cpu_baseline(self, budget_s=20.0):
+        """oracle OANet + diag_embed Kabsch (the reference op sequence) on a bounded sample."""
+        from oracle.oanet import oanet_forward
+        import oracle.kabsch as K
+        orig = K.kabsch
+        import oracle.oanet as O
+        O.kabsch = lambda x1, x2, w: orig(x1, x2, w, diag_embed=True)
+        n, t0 = 0, time.time()
+        while time.time() - t0 < budget_s and n < self.pairs:
+            oanet_forward(self.state, self.xs_host[n:n + 1])
+            n += 1
+        O.kabsch = orig
+        dt = time.time() - t0
+        return n / dt, "%d pair(s) of the same workload, batch 1, numpy oracle incl. N x N diag_embed Kabsch" % n
+
+
+def records_allgather(rec, world):
+    if world == 1:
+        return rec
+    import torch.distributed as dist
+    out = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device)
+    dist.all_gather_into_tensor(out, rec.contiguous())
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default=os.environ.get("MVR_BENCH_WORKLOAD", "scene"),
+                    choices=["scene", "precomputed"])
+    ap.add_argument("--pairs", type=int, default=435)
+    ap.add_argument("--npts", type=int, default=5000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    from lib import _native
+    _native.lib()
+    if args.workload == "scene":
+        from lib.scene_bench import SceneWorkload
+        wl = SceneWorkload(dev, rank, npts=args.npts)
+    else:
+        wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            records_allgather(wl.step(), world)
+        torch.cuda.synchronize()
+        _native.prof_set(1)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rec = records_allgather(wl.step(), world)
+        torch.cuda.synchronize()
+        barrier()
+        t1 = time.perf_counter()
+        dt = t1 - t0
+        prof = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
+        _native.prof_set(0)
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    pairs_per_step = int(rec.shape[-2]) * world
+    value = pairs_per_step * args.steps / dt
+
+    # dominant kernel class by device time inside the timed region
+    dom = max(prof, key=lambda k: prof[k][0])
+    ms, nl, fl, by = prof[dom]
+    bound = "hbm" if dom in ("procrustes", "small", "sparse_misc") else "mfma"
+    if bound == "mfma":
+        achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        peak, unit = PEAK_FP32_TFLOPS, "TFLOP/s"
+    else:
+        achieved = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        peak, unit = PEAK_HBM_GBS, "GB/s"
+    traffic = os.environ.get("MVR_PMC_TRAFFIC_BYTES")
+    roof = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": (float(traffic) if traffic else None),
+            "kernel": dom, "launches_per_step": nl / max(args.steps, 1),
+            "avg_launch_ms": round(ms / max(nl, 1), 4), "share_of_step": round(ms / (dt * 1e3), 3),
+            "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in prof.items() if v[1]}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the box's CPU share per GPU (OMP_NUM_THREADS is set to it there; affinity shows the whole host)
+        cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+        torch.set_num_threads(cores)
+        v, sample = wl.cpu_baseline(args.cpu_budget)
+        cpu = {"value": round(v, 4), "unit": "pairs/s", "cores": cores, "kind": "port", "sample": sample}
+    line = {"metric": METRIC if args.workload == "scene" else METRIC + " [filter+SVD only: precomputed corr.]",
+            "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world),
+            "roofline": roof, "cpu_baseline": cpu}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -111,6 +111,33 @@ int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_
 int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N, float* out,
                        int64_t out_pstride, mvr_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * Feature-space (soft) nearest neighbour for a batch of fragment pairs.
+ * Replaces lib/layers.py:44-88 Soft_NN.forward (+ pairwise_distance
+ * lib/utils.py:968-992, the pair gather lib/utils.py:850-885 and the xs
+ * assembly lib/utils.py:915).  For pair p = (s, t) = pairs[2p], pairs[2p+1]:
+ *   queries Fq[s*fq_fstride + n*32 + c], targets Ft[t*ft_fstride + m*32 + c],
+ *   target coords Xt[t*xt_fstride + m*3 + k]  (n < Nq, m < Mt, C must be 32);
+ * mode 0: x_corr = softmax_m((2 fq.ft - |ft|^2) * inv_tau2) . Xt   ('soft')
+ * mode 1: x_corr = Xt[argmax_m(fq.ft*2 - |ft|^2)]                   ('soft'+st, 'hard')
+ * out(p,n,:) = [Xq(s,n,0..2) (if Xq != NULL) | x_corr(0..2)] at
+ * out[p*out_pstride + n*out_nstride]; idx_out [P][Nq] argmax (mode 1, may be NULL).
+ * ---------------------------------------------------------------------- */
+int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride, const float* Xq,
+                int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P, int Nq, int Mt,
+                int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
+                int32_t* idx_out, mvr_stream_t stream);
+
+/* Row gather dst[i][:] = src[idx[i]][:] (C floats per row): the Sampler's
+ * index_select (lib/layers.py:151-152) with host-drawn (np.random) indices. */
+int mvr_gather_rows(const float* src, int C, const int64_t* idx, int n, float* dst, mvr_stream_t stream);
+
+/* Opt-in per-kernel-class device timing (hipEvents on the launching stream).
+ * mvr_prof_set(1) resets and enables; mvr_prof_get(kind, ...) synchronises the
+ * recorded events and returns totals since then (kinds: csrc/prof.hpp ProfKind). */
+int mvr_prof_set(int on);
+int mvr_prof_get(int kind, double* ms, long long* launches, double* flops, double* bytes);
+
 #ifdef __cplusplus
 }
 #endif
