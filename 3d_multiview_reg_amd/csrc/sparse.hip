@@ -1,0 +1,409 @@
+// Sparse-voxel machinery of the FCGF descriptor (the MinkowskiEngine 0.4
+// primitives used by lib/descriptor/fcgf.py), written for MI355X:
+//
+//   * voxelisation  floor(xyz / voxel) + first-occurrence dedup  (ME.utils.sparse_quantize,
+//                   scripts/pairwise_demo.py:79, scripts/utils.py:108-113)
+//   * coordinate hash: open addressing on 64-bit (batch, x, y, z) keys, linear probing,
+//                   inserts by 64-bit CAS + atomicMin of the first source row
+//   * strided coordinate sets  floor(c / s) * s, first-occurrence order
+//   * kernel maps as output-stationary neighbour tables nbr[o][k] (-1 = absent)
+//                   for the 3^3 / 7^3 stencils, strided and transposed
+//   * the sparse convolution itself (gather -> fp32 MFMA -> fused BN/residual/ReLU
+//                   epilogue), csrc/spconv.hip
+//
+// Conventions the reference never pins (MinkowskiEngine is not vendored):
+//   offset index k = (dx+r) + ks*(dy+r) + ks^2*(dz+r) (x fastest); strided output
+//   coordinates floor(c/s)*s; transposed conv: in = out - off*s_out; output rows of
+//   every dedup in first-occurrence order of the input rows.
+#include "common.hpp"
+#include "prof.hpp"
+#include "sparse.hpp"
+
+namespace mvr {
+
+// ------------------------------------------------------------------ hashing
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ uint64_t pack_key(int b, int x, int y, int z) {
+  return ((uint64_t)(uint32_t)b << 51) | ((uint64_t)((uint32_t)(x + KEY_BIAS) & KEY_MASK) << 34) |
+         ((uint64_t)((uint32_t)(y + KEY_BIAS) & KEY_MASK) << 17) | (uint64_t)((uint32_t)(z + KEY_BIAS) & KEY_MASK);
+}
+
+__device__ __forceinline__ int64_t hash_find(const HashView& h, uint64_t key) {
+  uint64_t s = mix64(key) & (h.cap - 1);
+  for (uint64_t probe = 0; probe < h.cap; ++probe) {
+    const uint64_t k = h.keys[s];
+    if (k == key) return h.vals[s];
+    if (k == EMPTY_KEY) return -1;
+    s = (s + 1) & (h.cap - 1);
+  }
+  return -1;
+}
+
+// insert `key` with value candidate v; keeps the minimum v per key
+__device__ __forceinline__ void hash_insert_min(HashView h, uint64_t key, int32_t v) {
+  uint64_t s = mix64(key) & (h.cap - 1);
+  for (uint64_t probe = 0; probe < h.cap; ++probe) {
+    unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(&h.keys[s]),
+                                        (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+    if (prev == EMPTY_KEY || prev == key) {
+      atomicMin(&h.vals[s], v);
+      return;
+    }
+    s = (s + 1) & (h.cap - 1);
+  }
+}
+
+__device__ __forceinline__ int64_t hash_slot(const HashView& h, uint64_t key) {
+  uint64_t s = mix64(key) & (h.cap - 1);
+  for (uint64_t probe = 0; probe < h.cap; ++probe) {
+    const uint64_t k = h.keys[s];
+    if (k == key) return (int64_t)s;
+    if (k == EMPTY_KEY) return -1;
+    s = (s + 1) & (h.cap - 1);
+  }
+  return -1;
+}
+
+__global__ void hash_clear_kernel(HashView h) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < h.cap) {
+    h.keys[i] = EMPTY_KEY;
+    h.vals[i] = 0x7fffffff;
+  }
+}
+
+// ------------------------------------------------------------------ key generation
+__device__ __forceinline__ int floor_div(int a, int s) { return (a >= 0) ? a / s : -((-a + s - 1) / s); }
+
+// voxel keys of raw points: coords = floor(xyz / voxel) in double (the reference floors the
+// float64 Open3D points, scripts/utils.py:108), batch index from the fragment offsets
+__global__ void vox_keys_kernel(const float* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
+                                double inv_voxel, uint64_t* keys, int4* vcoords) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {  // last fragment with off[b] <= i
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const int x = (int)floor((double)xyz[3 * i] * inv_voxel);
+  const int y = (int)floor((double)xyz[3 * i + 1] * inv_voxel);
+  const int z = (int)floor((double)xyz[3 * i + 2] * inv_voxel);
+  keys[i] = pack_key(lo, x, y, z);
+  vcoords[i] = make_int4(lo, x, y, z);
+}
+
+// coarse keys of a level: (b, floor(c/s)*s)
+__global__ void coarse_keys_kernel(const int4* __restrict__ c, int64_t M, int s, uint64_t* keys, int4* cc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const int4 v = c[i];
+  const int4 o = make_int4(v.x, floor_div(v.y, s) * s, floor_div(v.z, s) * s, floor_div(v.w, s) * s);
+  keys[i] = pack_key(o.x, o.y, o.z, o.w);
+  cc[i] = o;
+}
+
+__global__ void insert_min_kernel(const uint64_t* __restrict__ keys, int64_t n, HashView h) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) hash_insert_min(h, keys[i], (int32_t)i);
+}
+
+__global__ void first_flag_kernel(const uint64_t* __restrict__ keys, int64_t n, HashView h, int32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t s = hash_slot(h, keys[i]);
+  flags[i] = (s >= 0 && h.vals[s] == (int32_t)i) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ exclusive scan (int32 flags)
+constexpr int SCAN_B = 1024;
+
+__global__ void scan_block_kernel(const int32_t* __restrict__ in, int64_t n, int32_t* out, int32_t* bsum) {
+  __shared__ int32_t s[SCAN_B];
+  const int64_t i = (int64_t)blockIdx.x * SCAN_B + threadIdx.x;
+  const int v = (i < n) ? in[i] : 0;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < SCAN_B; o <<= 1) {  // Hillis-Steele inclusive
+    const int t = (threadIdx.x >= o) ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (i < n) out[i] = s[threadIdx.x] - v;  // exclusive
+  if (threadIdx.x == SCAN_B - 1) bsum[blockIdx.x] = s[SCAN_B - 1];
+}
+
+__global__ void scan_sums_kernel(int32_t* bsum, int nb, int64_t* total) {
+  // single block: exclusive scan of nb block sums (serial chunks per thread)
+  __shared__ int32_t part[SCAN_B];
+  const int per = (nb + SCAN_B - 1) / SCAN_B;
+  const int b0 = threadIdx.x * per;
+  int acc = 0;
+  for (int k = 0; k < per && b0 + k < nb; ++k) acc += bsum[b0 + k];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int t = 0; t < SCAN_B; ++t) { const int v = part[t]; part[t] = run; run += v; }
+    *total = run;
+  }
+  __syncthreads();
+  int run = part[threadIdx.x];
+  for (int k = 0; k < per && b0 + k < nb; ++k) { const int v = bsum[b0 + k]; bsum[b0 + k] = run; run += v; }
+}
+
+__global__ void scan_add_kernel(int32_t* out, int64_t n, const int32_t* __restrict__ bsum) {
+  const int64_t i = (int64_t)blockIdx.x * SCAN_B + threadIdx.x;
+  if (i < n) out[i] += bsum[blockIdx.x];
+}
+
+// compact selected rows (first occurrences) in source order
+__global__ void compact_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ pos, int64_t n,
+                               const int4* __restrict__ cc, int4* coords_out, int64_t* sel_out, int64_t* counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !flags[i]) return;
+  const int p = pos[i];
+  const int4 c = cc[i];
+  coords_out[p] = c;
+  if (sel_out) sel_out[p] = i;
+  if (counts) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[1 + c.x]), 1ULL);
+}
+
+__global__ void build_table_kernel(const int4* __restrict__ c, int64_t M, HashView h) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M) {
+    const int4 v = c[i];
+    hash_insert_min(h, pack_key(v.x, v.y, v.z, v.w), (int32_t)i);
+  }
+}
+
+// ------------------------------------------------------------------ kernel maps
+// nbr[o][k] = row of (coords[o] + sign*off_k*step) in the input table, or -1
+__global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h, int ks, int step, int sign,
+                                  int32_t* __restrict__ nbr) {
+  const int K = ks * ks * ks;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= Mo * K) return;
+  const int64_t o = e / K;
+  const int k = (int)(e - o * K);
+  const int r = ks / 2;
+  const int dx = k % ks - r, dy = (k / ks) % ks - r, dz = k / (ks * ks) - r;
+  const int4 c = oc[o];
+  const int64_t v = hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step, c.w + sign * dz * step));
+  nbr[e] = (int32_t)v;
+}
+
+// ------------------------------------------------------------------ conv1: Cin = 1, large stencil
+// out[o][c] = sum_k feat[nbr(o,k)] * W[k][0][c]   with hash probes inline (no 343-wide table),
+// epilogue BN (eval, folded per column) / ReLU.  One thread per output row, W in LDS.
+template <int CO>
+__global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h,
+                                                        const float* __restrict__ feat, int ks, int step,
+                                                        const float* __restrict__ W, mvr_bn_p bn, float bn_eps,
+                                                        int relu, float* __restrict__ out, int64_t ldout) {
+  extern __shared__ float sW[];  // [K][CO]
+  const int K = ks * ks * ks;
+  for (int e = threadIdx.x; e < K * CO; e += blockDim.x) sW[e] = W[e];
+  __syncthreads();
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= Mo) return;
+  float acc[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+  const int4 cc = oc[o];
+  const int r = ks / 2;
+  for (int k = 0; k < K; ++k) {
+    const int dx = k % ks - r, dy = (k / ks) % ks - r, dz = k / (ks * ks) - r;
+    const int64_t v = hash_find(h, pack_key(cc.x, cc.y + dx * step, cc.z + dy * step, cc.w + dz * step));
+    if (v >= 0) {
+      const float f = feat[v];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) acc[c] = fmaf(f, sW[k * CO + c], acc[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CO; ++c) {
+    float y = acc[c];
+    if (bn.gamma) {
+      const float s = bn.gamma[c] / sqrtf(bn.var[c] + bn_eps);
+      y = (y - bn.mean[c]) * s + bn.beta[c];
+    }
+    if (relu) y = fmaxf(y, 0.f);
+    out[o * ldout + c] = y;
+  }
+}
+
+__global__ void l2norm_rows_kernel(float* x, int64_t M, int C, int64_t ld) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= M) return;
+  float* r = x + o * ld;
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s = fmaf(r[c], r[c], s);
+  const float inv = 1.f / sqrtf(s);
+  for (int c = 0; c < C; ++c) r[c] *= inv;
+}
+
+// ------------------------------------------------------------------ host helpers
+static inline uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1024;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+size_t hash_table_bytes(int64_t M) { return 16 + next_pow2((uint64_t)(2 * (M > 0 ? M : 1))) * 12; }
+
+HashView hash_view(void* table, size_t bytes) {
+  HashView h{};
+  if (bytes < 16 + 1024 * 12) return h;
+  uint64_t cap = 1024;
+  while (16 + cap * 2 * 12 <= bytes) cap <<= 1;
+  char* base = reinterpret_cast<char*>(table);
+  h.cap = cap;
+  h.keys = reinterpret_cast<uint64_t*>(base + 16);
+  h.vals = reinterpret_cast<int32_t*>(base + 16 + cap * 8);
+  return h;
+}
+
+static inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+// dedup n keys (first occurrence, source order) -> coords_out [count], sel_out (optional), counts
+struct DedupWs {
+  uint64_t* keys; int4* cc; int32_t* flags; int32_t* pos; int32_t* bsum; void* table; size_t table_bytes;
+};
+
+static size_t dedup_ws_bytes(int64_t n) {
+  const int64_t nb = (n + SCAN_B - 1) / SCAN_B;
+  return (size_t)n * (8 + 16 + 4 + 4) + (size_t)nb * 4 + hash_table_bytes(n) + 8 * 256;
+}
+
+static DedupWs dedup_ws(void* ws, int64_t n) {
+  char* p = reinterpret_cast<char*>(ws);
+  auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
+  DedupWs d{};
+  const int64_t nb = (n + SCAN_B - 1) / SCAN_B;
+  d.keys = reinterpret_cast<uint64_t*>(take((size_t)n * 8));
+  d.cc = reinterpret_cast<int4*>(take((size_t)n * 16));
+  d.flags = reinterpret_cast<int32_t*>(take((size_t)n * 4));
+  d.pos = reinterpret_cast<int32_t*>(take((size_t)n * 4));
+  d.bsum = reinterpret_cast<int32_t*>(take((size_t)nb * 4 + 4));
+  d.table_bytes = hash_table_bytes(n);
+  d.table = take(d.table_bytes);
+  return d;
+}
+
+static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel_out, int64_t* counts, int B,
+                     hipStream_t s) {
+  HashView h = hash_view(d.table, d.table_bytes);
+  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)h.cap)), dim3(256), 0, s, h);
+  hipLaunchKernelGGL(insert_min_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h);
+  hipLaunchKernelGGL(first_flag_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h, d.flags);
+  const int nb = (int)((n + SCAN_B - 1) / SCAN_B);
+  (void)hipMemsetAsync(counts, 0, sizeof(int64_t) * (1 + B), s);
+  hipLaunchKernelGGL(scan_block_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.flags, n, d.pos, d.bsum);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SCAN_B), 0, s, d.bsum, nb, counts);
+  hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.pos, n, d.bsum);
+  hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, d.flags, d.pos, n, d.cc, coords_out, sel_out,
+                     counts);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+}  // namespace mvr
+
+using namespace mvr;
+
+extern "C" size_t mvr_hash_table_bytes(int64_t M) { return hash_table_bytes(M); }
+
+extern "C" size_t mvr_voxelize_workspace_bytes(int64_t n) { return dedup_ws_bytes(n); }
+
+extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel, void* ws,
+                            size_t ws_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
+                            hipStream_t s) {
+  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.f) || !ws || !coords_out || !counts_out)
+    return MVR_EINVAL;
+  if (ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
+  if (n == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
+  DedupWs d = dedup_ws(ws, n);
+  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, 1.0 / (double)voxel,
+                     d.keys, d.cc);
+  return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s);
+}
+
+extern "C" size_t mvr_coords_downsample_workspace_bytes(int64_t M) { return dedup_ws_bytes(M); }
+
+extern "C" int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, int stride_out, void* ws,
+                                     size_t ws_bytes, int32_t* coords_out, int64_t* counts_out, hipStream_t s) {
+  if (!coords || M < 0 || B <= 0 || B > MAX_BATCH || stride_out <= 0 || !ws || !coords_out || !counts_out)
+    return MVR_EINVAL;
+  if (ws_bytes < dedup_ws_bytes(M)) return MVR_EINVAL;
+  if (M == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)M * 40.0, s);
+  DedupWs d = dedup_ws(ws, M);
+  hipLaunchKernelGGL(coarse_keys_kernel, dim3(nblk(M)), dim3(256), 0, s, reinterpret_cast<const int4*>(coords), M,
+                     stride_out, d.keys, d.cc);
+  return dedup_run(d, M, reinterpret_cast<int4*>(coords_out), nullptr, counts_out, B, s);
+}
+
+extern "C" int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_bytes, hipStream_t s) {
+  if (!coords || M < 0 || !table) return MVR_EINVAL;
+  if (table_bytes < hash_table_bytes(M)) return MVR_EINVAL;
+  HashView h = hash_view(table, table_bytes);
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)h.cap * 12 + M * 28.0, s);
+  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)h.cap)), dim3(256), 0, s, h);
+  if (M > 0)
+    hipLaunchKernelGGL(build_table_kernel, dim3(nblk(M)), dim3(256), 0, s, reinterpret_cast<const int4*>(coords), M,
+                       h);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
+                              int ksize, int step, int transposed, int32_t* nbr, hipStream_t s) {
+  if (!out_coords || Mout < 0 || !in_table || ksize <= 0 || (ksize & 1) == 0 || step <= 0 || !nbr) return MVR_EINVAL;
+  HashView h = hash_view(const_cast<void*>(in_table), in_table_bytes);
+  if (!h.cap) return MVR_EINVAL;
+  const int64_t tot = Mout * (int64_t)ksize * ksize * ksize;
+  if (tot == 0) return MVR_OK;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)tot * 4.0, s);
+  hipLaunchKernelGGL(kernel_map_kernel, dim3(nblk(tot)), dim3(256), 0, s, reinterpret_cast<const int4*>(out_coords),
+                     Mout, h, ksize, step, transposed ? -1 : 1, nbr);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
+                             const float* feat, int ksize, int step, const float* W, int Cout, mvr_bn_p bn,
+                             float bn_eps, int relu, float* out, int64_t ldout, hipStream_t s) {
+  if (!out_coords || Mout < 0 || !in_table || !feat || !W || !out || (ksize & 1) == 0) return MVR_EINVAL;
+  if (Cout != 32) return MVR_EINVAL;  // FCGF conv1: 1 -> CHANNELS[1] = 32 (fcgf.py:118-125)
+  HashView h = hash_view(const_cast<void*>(in_table), in_table_bytes);
+  if (!h.cap) return MVR_EINVAL;
+  if (Mout == 0) return MVR_OK;
+  const int K = ksize * ksize * ksize;
+  const size_t lds = (size_t)K * Cout * sizeof(float);
+  if (lds > 160 * 1024) return MVR_EINVAL;
+  ProfScope prof(PK_SPCONV, 2.0 * Mout * K * Cout, (double)Mout * (16 + Cout * 4), s);
+  hipLaunchKernelGGL(spconv_c1_kernel<32>, dim3(nblk(Mout)), dim3(256), lds, s,
+                     reinterpret_cast<const int4*>(out_coords), Mout, h, feat, ksize, step, W, bn, bn_eps, relu, out,
+                     ldout);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, hipStream_t s) {
+  if (!x || M < 0 || C <= 0 || ld < C) return MVR_EINVAL;
+  if (M == 0) return MVR_OK;
+  hipLaunchKernelGGL(l2norm_rows_kernel, dim3(nblk(M)), dim3(256), 0, s, x, M, C, ld);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}

@@ -1,0 +1,203 @@
+// Sparse 3-D convolution (MinkowskiConvolution / MinkowskiConvolutionTranspose forward,
+// used throughout lib/descriptor/fcgf.py:118-227) as an output-stationary gather-GEMM:
+//
+//   out[o][c] = epi( sum_k sum_ci in[nbr[o][k]][ci] * W[k][ci][c] )
+//   epi = (+bias) -> BatchNorm (eval: running stats) -> (+residual) -> (ReLU)
+//
+// nbr is the kernel map as a neighbour table (csrc/sparse.hip); -1 entries contribute
+// nothing.  Per 64/128-row output tile the workgroup first lists the stencil offsets
+// that have at least one neighbour in the tile and skips the empty ones; each step
+// gathers 16 input channels of the tile's neighbour rows (16-byte row loads) and the
+// matching W[k] slice into LDS, then runs v_mfma_f32_32x32x2_f32.  No atomics: every
+// output row is owned by exactly one workgroup (deterministic results).
+#include "common.hpp"
+#include "prof.hpp"
+#include "sparse.hpp"
+
+namespace mvr {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct SpArgs {
+  const float* in; int64_t ldin; int Cin;
+  const int32_t* nbr; int K; int64_t Mout;
+  const float* W; int Cout;
+  const float* bias;
+  mvr_bn_p bn; float bn_eps;
+  const float* res; int64_t ldres;
+  int relu;
+  float* out; int64_t ldout;
+};
+
+constexpr int SP_BK = 16;
+constexpr int SP_KMAX = 32;
+
+template <int TM, int TN, int WM, int WN>
+__global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
+  constexpr int WTN = TN / WN;  // wave tile columns (32 or 64)
+  constexpr int NJ = WTN / 32;
+  static_assert(TM / WM == 32, "wave tile rows must be 32");
+  __shared__ float As[2][SP_BK][TM + 4];
+  __shared__ float Bs[2][SP_BK][TN + 4];
+  __shared__ int32_t nb[TM][SP_KMAX + 1];
+  __shared__ int kact[SP_KMAX];
+  __shared__ int klist[SP_KMAX];
+  __shared__ int nk;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int64_t o0 = (int64_t)blockIdx.x * TM;
+  const int c0 = blockIdx.y * TN;
+  const int K = a.K;
+
+  if (tid < SP_KMAX) kact[tid] = 0;
+  __syncthreads();
+  for (int e = tid; e < TM * K; e += 256) {
+    const int row = e / K, k = e - row * K;
+    const int64_t o = o0 + row;
+    int v = -1;
+    if (o < a.Mout) v = a.nbr ? a.nbr[o * K + k] : (int)o;
+    nb[row][k] = v;
+    if (v >= 0) kact[k] = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;
+    for (int k = 0; k < K; ++k)
+      if (kact[k]) klist[n++] = k;
+    nk = n;
+  }
+  __syncthreads();
+
+  const int nch = (a.Cin + SP_BK - 1) / SP_BK;
+  const int steps = nk * nch;
+
+  constexpr int AV = TM * SP_BK / 4 / 256;                       // float4 per thread for A (1 or 2)
+  constexpr int BV = (SP_BK * TN / 4 + 255) / 256;               // float4 per thread for B (1 or 2)
+  float4 ra[AV], rb[BV];
+
+  auto load = [&](int s) {
+    const int k = klist[s / nch];
+    const int ci0 = (s % nch) * SP_BK;
+#pragma unroll
+    for (int r = 0; r < AV; ++r) {
+      const int idx = tid + 256 * r;
+      const int row = idx >> 2, ciq = (idx & 3) * 4;
+      const int src = nb[row][k];
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (src >= 0 && ci0 + ciq < a.Cin) v = *reinterpret_cast<const float4*>(a.in + (int64_t)src * a.ldin + ci0 + ciq);
+      ra[r] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < BV; ++r) {
+      const int idx = tid + 256 * r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < SP_BK * TN / 4) {
+        const int kk = idx / (TN / 4), nq = (idx % (TN / 4)) * 4;
+        const int ci = ci0 + kk, c = c0 + nq;
+        if (ci < a.Cin && c < a.Cout)
+          v = *reinterpret_cast<const float4*>(a.W + ((int64_t)k * a.Cin + ci) * a.Cout + c);
+      }
+      rb[r] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < AV; ++r) {
+      const int idx = tid + 256 * r;
+      const int row = idx >> 2, ciq = (idx & 3) * 4;
+      As[buf][ciq + 0][row] = ra[r].x;
+      As[buf][ciq + 1][row] = ra[r].y;
+      As[buf][ciq + 2][row] = ra[r].z;
+      As[buf][ciq + 3][row] = ra[r].w;
+    }
+#pragma unroll
+    for (int r = 0; r < BV; ++r) {
+      const int idx = tid + 256 * r;
+      if (idx < SP_BK * TN / 4) {
+        const int kk = idx / (TN / 4), nq = (idx % (TN / 4)) * 4;
+        *reinterpret_cast<float4*>(&Bs[buf][kk][nq]) = rb[r];
+      }
+    }
+  };
+
+  floatx16 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  if (steps > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int s = 0; s < steps; ++s) {
+    if (s + 1 < steps) load(s + 1);
+#pragma unroll
+    for (int kk = 0; kk < SP_BK; kk += 2) {
+      const float av = As[cur][kk + kh][wm * 32 + l32];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float bv = Bs[cur][kk + kh][wn * WTN + j * 32 + l32];
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j], 0, 0, 0);
+      }
+    }
+    if (s + 1 < steps) store(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = c0 + wn * WTN + j * 32 + l32;
+    if (c >= a.Cout) continue;
+    float bsc = 1.f, bsh = 0.f;
+    if (a.bn.gamma) {
+      bsc = a.bn.gamma[c] / sqrtf(a.bn.var[c] + a.bn_eps);
+      bsh = a.bn.beta[c] - a.bn.mean[c] * bsc;
+    }
+    const float bias = a.bias ? a.bias[c] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t o = o0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (o >= a.Mout) continue;
+      float v = acc[j][r] + bias;
+      v = fmaf(v, bsc, bsh);
+      if (a.res) v += a.res[o * a.ldres + c];
+      if (a.relu) v = fmaxf(v, 0.f);
+      a.out[o * a.ldout + c] = v;
+    }
+  }
+}
+
+}  // namespace mvr
+
+using namespace mvr;
+
+extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, int K, int64_t Mout,
+                          const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
+                          int64_t ldres, int relu, float* out, int64_t ldout, hipStream_t s) {
+  if (!in || !W || !out || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
+  if (!nbr && K != 1) return MVR_EINVAL;
+  if ((Cin & 3) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
+      (reinterpret_cast<uintptr_t>(W) & 15))
+    return MVR_EINVAL;
+  if (Mout == 0) return MVR_OK;
+  SpArgs a{in, ldin, Cin, nbr, K, Mout, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout};
+  ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
+  if (Cout <= 32) {
+    hipLaunchKernelGGL((spconv_kernel<128, 32, 4, 1>), dim3((unsigned)((Mout + 127) / 128), (Cout + 31) / 32),
+                       dim3(256), 0, s, a);
+  } else if (Cout <= 64) {
+    hipLaunchKernelGGL((spconv_kernel<64, 64, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 63) / 64), dim3(256),
+                       0, s, a);
+  } else {
+    hipLaunchKernelGGL((spconv_kernel<64, 128, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 127) / 128),
+                       dim3(256), 0, s, a);
+  }
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}

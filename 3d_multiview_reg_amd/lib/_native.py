@@ -61,6 +61,18 @@ _SIGS = {
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "mvr_hash_table_bytes": (c_size, [c_i64]),
+    "mvr_voxelize_workspace_bytes": (c_size, [c_i64]),
+    "mvr_voxelize": (c_int, [c_vp, c_vp, c_int, c_i64, c_float, c_vp, c_size, c_vp, c_vp, c_vp, c_vp]),
+    "mvr_coords_downsample_workspace_bytes": (c_size, [c_i64]),
+    "mvr_coords_downsample": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_size, c_vp, c_vp, c_vp]),
+    "mvr_hash_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),
+    "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
+    "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
+                           c_int, c_vp, c_i64, c_vp]),
+    "mvr_spconv_c1": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp, c_int, c_int, c_vp, c_int, BnP, c_float, c_int, c_vp,
+                              c_i64, c_vp]),
+    "mvr_l2norm_rows": (c_int, [c_vp, c_i64, c_int, c_i64, c_vp]),
     "mvr_prof_set": (c_int, [c_int]),
     "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),

@@ -1,0 +1,123 @@
+"""Sparse tensors on MI355X: the subset of MinkowskiEngine 0.4 that the FCGF
+descriptor and the demo/extract pipelines use (ME.SparseTensor, the coordinate
+manager with its strided coordinate sets and kernel maps,
+ME.utils.sparse_quantize / sparse_collate), implemented on libmvreg_hip.so.
+
+Coordinates are int32 [M, 4] = (batch, x, y, z) — batch FIRST (our convention;
+ME 0.4 itself stored the batch index last).  Every coordinate set, hash table
+and kernel map lives in HBM and is cached on the CoordinateManager shared by all
+tensors of one forward pass.
+"""
+import numpy as np
+import torch
+
+from lib import _native as N
+
+
+class CoordinateManager:
+    """Per-batch cache: stride -> coords / hash table; (kind, stride) -> neighbour table."""
+
+    def __init__(self, coords, batch_size):
+        self.B = int(batch_size)
+        self.device = coords.device
+        self.coords = {1: coords.contiguous()}
+        self.tables = {}
+        self.maps = {}
+
+    def coords_at(self, s):
+        if s not in self.coords:
+            prev = self.coords_at(s // 2)
+            M = prev.shape[0]
+            L = N.lib()
+            ws = N.workspace(L.mvr_coords_downsample_workspace_bytes(M), self.device)
+            out = torch.empty(M, 4, dtype=torch.int32, device=self.device)
+            cnt = torch.empty(1 + self.B, dtype=torch.int64, device=self.device)
+            N.check(L.mvr_coords_downsample(N.ptr(prev), M, self.B, s, N.ptr(ws), ws.numel(), N.ptr(out), N.ptr(cnt),
+                                            N.stream()), "mvr_coords_downsample")
+            n = int(cnt[0].item())
+            self.coords[s] = out[:n]
+        return self.coords[s]
+
+    def table(self, s):
+        if s not in self.tables:
+            c = self.coords_at(s)
+            L = N.lib()
+            nb = L.mvr_hash_table_bytes(c.shape[0])
+            t = torch.empty(nb, dtype=torch.uint8, device=self.device)
+            N.check(L.mvr_hash_build(N.ptr(c), c.shape[0], N.ptr(t), nb, N.stream()), "mvr_hash_build")
+            self.tables[s] = t
+        return self.tables[s]
+
+    def kernel_map(self, kind, s, ks=3):
+        """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed)."""
+        key = (kind, s, ks)
+        if key not in self.maps:
+            if kind == "s1":
+                out_c, tab, tr = self.coords_at(s), self.table(s), 0
+            elif kind == "down":
+                out_c, tab, tr = self.coords_at(2 * s), self.table(s), 0
+            elif kind == "up":
+                out_c, tab, tr = self.coords_at(s), self.table(2 * s), 1
+            else:
+                raise ValueError(kind)
+            K = ks ** 3
+            nbr = torch.empty(out_c.shape[0], K, dtype=torch.int32, device=self.device)
+            N.check(N.lib().mvr_kernel_map(N.ptr(out_c), out_c.shape[0], N.ptr(tab), tab.numel(), ks, s, tr,
+                                           N.ptr(nbr), N.stream()), "mvr_kernel_map")
+            self.maps[key] = nbr
+        return self.maps[key]
+
+
+class SparseTensor:
+    """ME.SparseTensor(feats, coords=...) / (feats, coords_key=..., coords_manager=...)."""
+
+    def __init__(self, feats, coords=None, coords_key=None, coords_manager=None, tensor_stride=1):
+        self.F = feats
+        self.tensor_stride = tensor_stride
+        if coords_manager is not None:
+            self.coords_man = coords_manager
+            self.coords_key = coords_key if coords_key is not None else tensor_stride
+        else:
+            if coords is None:
+                raise ValueError("SparseTensor needs coords or a coords_manager")
+            c = torch.as_tensor(coords).to(torch.int32)
+            B = int(c[:, 0].max().item()) + 1 if c.numel() else 1
+            self._pending = (c, B)
+            self.coords_man = None
+            self.coords_key = 1
+
+    def to(self, device):
+        self.F = self.F.to(device)
+        if self.coords_man is None:
+            c, B = self._pending
+            self.coords_man = CoordinateManager(c.to(device).contiguous(), B)
+        return self
+
+    @property
+    def C(self):
+        return self.coords_man.coords_at(self.coords_key)
+
+
+def voxelize(points_list, voxel_size, device):
+    """Batched sparse_quantize of raw fragments (scripts/pairwise_demo.py:74-96).
+    points_list: list of float arrays/tensors [n_b, 3].  Returns (coords int32 [M,4],
+    sel int64 [M] (global point index), counts list, xyz_down float32 [M,3])."""
+    pts = [torch.as_tensor(np.asarray(p, dtype=np.float32)) if not torch.is_tensor(p) else p.float() for p in points_list]
+    B = len(pts)
+    n = [int(p.shape[0]) for p in pts]
+    xyz = torch.cat(pts, 0).to(device).contiguous()
+    off = torch.tensor(np.concatenate([[0], np.cumsum(n)]), dtype=torch.int64, device=device)
+    total = int(sum(n))
+    L = N.lib()
+    ws = N.workspace(L.mvr_voxelize_workspace_bytes(total), device)
+    coords = torch.empty(total, 4, dtype=torch.int32, device=device)
+    sel = torch.empty(total, dtype=torch.int64, device=device)
+    cnt = torch.empty(1 + B, dtype=torch.int64, device=device)
+    N.check(L.mvr_voxelize(N.ptr(xyz), N.ptr(off), B, total, float(voxel_size), N.ptr(ws), ws.numel(), N.ptr(coords),
+                           N.ptr(sel), N.ptr(cnt), N.stream()), "mvr_voxelize")
+    c = cnt.cpu().numpy()
+    M = int(c[0])
+    coords, sel = coords[:M], sel[:M]
+    xyz_down = torch.empty(M, 3, device=device)
+    N.check(L.mvr_gather_rows(N.ptr(xyz), 3, N.ptr(sel), M, N.ptr(xyz_down), N.stream()), "mvr_gather_rows")
+    return coords, sel, [int(v) for v in c[1:]], xyz_down

@@ -101,6 +101,80 @@ class PrecomputedWorkload:
         return n / dt, "%d pair(s) of the same workload, batch 1, numpy oracle incl. N x N diag_embed Kabsch" % n
 
 
+class SceneWorkload:
+    """configs[2]: one synthetic 3DMatch-scale scene per GPU (30 fragments, ~20k voxels each)."""
+    name = "scene"
+
+    def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025):
+        import lib.config
+        from synth import synth_scene_fragments
+        cfg = oanet_cfg()
+        cfg["method"]["descriptor_module"] = "fcgf"
+        cfg["data"]["max_num_points"] = npts
+        self.model = lib.config.get_model(cfg)
+        self.state = synth_module(self.model, seed=7)
+        self.model = self.model.to(dev).eval()
+        self.frags, self.poses = synth_scene_fragments(n_frag, seed=41 + 1000 * rank)
+        self.raw = [torch.from_numpy(f).to(dev) for f in self.frags]     # resident in HBM
+        self.dev, self.voxel, self.npts, self.n_frag = dev, voxel, npts, n_frag
+        self.rng_seed = 41 + rank
+        self.pairs = n_frag * (n_frag - 1) // 2
+        self.vox_counts = None
+
+    def step(self):
+        from lib.sparse import voxelize
+        coords, sel, counts, xyz_down = voxelize(self.raw, self.voxel, self.dev)   # prepare_data on the GPU
+        self.vox_counts = counts
+        data = {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
+                "pts_list": torch.tensor(counts)}
+        np.random.seed(self.rng_seed)
+        fin, _, _ = self.model.compute_descriptors(data)
+        out = self.model.filter_correspondences(fin)
+        R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
+        conf = (s > 0.5).float().mean(dim=1, keepdim=True)
+        return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)
+
+    def config(self):
+        return {"workload": "one synthetic 3DMatch-scale scene per GPU (configs[2]): %d fragments x ~%d voxels "
+                            "(0.025 m) -> FCGF -> rand %d samples -> soft feature-NN for all %d pairs -> OANet "
+                            "(128ch, 500 clusters, 2 blocks) -> weighted Procrustes -> all-gather of (R,t,conf)"
+                            % (self.n_frag, int(np.mean(self.vox_counts or [0])), self.npts, self.pairs),
+                "fragments_per_gpu": self.n_frag, "pairs_per_gpu": self.pairs, "samples": self.npts,
+                "voxels_mean": int(np.mean(self.vox_counts or [0]))}
+
+    def cpu_baseline(self, budget_s=20.0):
+        """numpy oracle, reference op sequence: FCGF on 2 fragments + for 1 pair both Soft_NN directions
+        + OANet + N x N diag_embed Kabsch; projected to the scene: 435 / (30 t_fcgf + 435 t_pair)."""
+        from oracle.fcgf import voxelize as ovox, fcgf_forward
+        from oracle.soft_nn import soft_nn, sample_rand
+        from oracle.oanet import oanet_forward
+        import oracle.kabsch as K
+        import oracle.oanet as O
+        st = {k: v.detach().cpu().numpy() for k, v in self.model.state_dict().items()}
+        dst = {k[len("descriptor_module."):]: v for k, v in st.items() if k.startswith("descriptor_module.")}
+        fst = {k[len("filtering_module."):]: v for k, v in st.items() if k.startswith("filtering_module.")}
+        t0 = time.time()
+        c, sel, cnt = ovox(self.frags[:2], self.voxel)
+        F, _ = fcgf_forward(dst, c, np.ones((len(c), 1), np.float32))
+        t_fcgf = (time.time() - t0) / 2
+        xyz = np.concatenate(self.frags[:2])[sel]
+        np.random.seed(0)
+        idx = sample_rand(cnt, self.npts)
+        fs, xs = F[idx], xyz[idx]
+        orig = K.kabsch
+        O.kabsch = lambda x1, x2, w: orig(x1, x2, w, diag_embed=True)
+        t1 = time.time()
+        xc = soft_nn(fs[:1], fs[1:], xs[1:], "soft")
+        soft_nn(fs[1:], fs[:1], xs[:1], "soft")                       # reverse direction, as the reference
+        oanet_forward(fst, np.concatenate([xs[:1], xc], -1))
+        t_pair = time.time() - t1
+        O.kabsch = orig
+        v = self.pairs / (self.n_frag * t_fcgf + self.pairs * t_pair)
+        return v, ("measured FCGF %.2fs/fragment (2 fragments) + %.2fs/pair (1 pair: 2x Soft_NN + OANet + "
+                   "diag_embed Kabsch); projected to %d fragments / %d pairs" % (t_fcgf, t_pair, self.n_frag,
+                                                                              self.pairs))
+
+
 def records_allgather(rec, world):
     if world == 1:
         return rec
@@ -141,7 +215,6 @@ def main():
     from lib import _native
     _native.lib()
     if args.workload == "scene":
-        from lib.scene_bench import SceneWorkload
         wl = SceneWorkload(dev, rank, npts=args.npts)
     else:
         wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)

@@ -132,6 +132,43 @@ int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft
  * index_select (lib/layers.py:151-152) with host-drawn (np.random) indices. */
 int mvr_gather_rows(const float* src, int C, const int64_t* idx, int n, float* dst, mvr_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * Sparse-voxel primitives of the FCGF descriptor (MinkowskiEngine 0.4 calls in
+ * lib/descriptor/fcgf.py, scripts/pairwise_demo.py:79-93, scripts/utils.py:102-120).
+ * coords are int32 [M][4] = (batch, x, y, z); hash tables are opaque device
+ * buffers of mvr_hash_table_bytes(M) bytes.
+ * ---------------------------------------------------------------------- */
+size_t mvr_hash_table_bytes(int64_t M);
+size_t mvr_voxelize_workspace_bytes(int64_t n);
+/* ME.utils.sparse_quantize(floor(xyz/voxel), return_index=True) per fragment, batched:
+ * fragment b owns points [frag_off[b], frag_off[b+1]).  Writes the unique voxels in
+ * first-occurrence order: coords_out [n][4] (first count rows valid), sel_out [n]
+ * (source point index), counts_out int64 [1+B] = {total, per-fragment}. */
+int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel, void* workspace,
+                 size_t workspace_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
+                 mvr_stream_t stream);
+size_t mvr_coords_downsample_workspace_bytes(int64_t M);
+/* strided coordinate set floor(c/s)*s (first-occurrence order); counts_out as above */
+int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, int stride_out, void* workspace,
+                          size_t workspace_bytes, int32_t* coords_out, int64_t* counts_out, mvr_stream_t stream);
+int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_bytes, mvr_stream_t stream);
+/* kernel map as a neighbour table nbr[o][k] (k = (dx+r) + ks(dy+r) + ks^2(dz+r)):
+ * row of out_coords[o] + sign*off_k*step in the input table (sign -1 if transposed), or -1 */
+int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
+                   int step, int transposed, int32_t* nbr, mvr_stream_t stream);
+/* MinkowskiConvolution forward, gather-GEMM over the neighbour table (nbr NULL & K==1:
+ * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
+ * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu. */
+int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, int K, int64_t Mout, const float* W,
+               int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res, int64_t ldres, int relu,
+               float* out, int64_t ldout, mvr_stream_t stream);
+/* single-input-channel conv with a large stencil (FCGF conv1, 7^3) probing the hash inline */
+int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
+                  const float* feat, int ksize, int step, const float* W, int Cout, mvr_bn_p bn, float bn_eps,
+                  int relu, float* out, int64_t ldout, mvr_stream_t stream);
+/* x[o][:C] /= ||x[o][:C]||  (fcgf.py:274-278) */
+int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, mvr_stream_t stream);
+
 /* Opt-in per-kernel-class device timing (hipEvents on the launching stream).
  * mvr_prof_set(1) resets and enables; mvr_prof_get(kind, ...) synchronises the
  * recorded events and returns totals since then (kinds: csrc/prof.hpp ProfKind). */

@@ -34,7 +34,10 @@ def synth_state(shapes, seed=0, overrides=None):
         base = name.rsplit(".", 1)[0]
         wshape = shapes.get(base + ".weight")
         is_conv = wshape is not None and len(wshape) >= 2
-        if name.endswith(".weight") and len(shape) >= 2:
+        if name.endswith(".kernel"):                      # MinkowskiEngine conv [K, Cin, Cout]
+            fan_in = int(shape[0] * shape[1])
+            out[name] = (r.standard_normal(shape) * np.sqrt(2.0 / fan_in)).astype(np.float32)
+        elif name.endswith(".weight") and len(shape) >= 2:
             fan_in = int(np.prod(shape[1:]))
             out[name] = (r.standard_normal(shape) / np.sqrt(fan_in)).astype(np.float32)
         elif name.endswith(".bias") and is_conv:
@@ -94,3 +97,68 @@ def unit_features(B, N, C, seed=0):
     f = r.standard_normal((B, N, C)).astype(np.float32)
     f /= np.linalg.norm(f, axis=-1, keepdims=True)
     return f.astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- synthetic scenes
+def _rect(o, u, v):
+    return (np.asarray(o, float), np.asarray(u, float), np.asarray(v, float))
+
+
+def synth_room(seed=41, n_boxes=12, size=(6.0, 6.0, 3.0)):
+    """Axis-aligned room (floor, ceiling, 4 walls) + boxes on the floor, as rectangles
+    (origin, edge u, edge v) (SURVEY §8d synthetic 3DMatch-like scene)."""
+    r = np.random.default_rng(seed)
+    X, Y, Z = size
+    rects = [_rect((0, 0, 0), (X, 0, 0), (0, Y, 0)), _rect((0, 0, Z), (X, 0, 0), (0, Y, 0)),
+             _rect((0, 0, 0), (X, 0, 0), (0, 0, Z)), _rect((0, Y, 0), (X, 0, 0), (0, 0, Z)),
+             _rect((0, 0, 0), (0, Y, 0), (0, 0, Z)), _rect((X, 0, 0), (0, Y, 0), (0, 0, Z))]
+    for _ in range(n_boxes):
+        w, d, h = r.uniform(0.3, 1.2, 3)
+        x0, y0 = r.uniform(0.2, X - 0.2 - w), r.uniform(0.2, Y - 0.2 - d)
+        rects += [_rect((x0, y0, h), (w, 0, 0), (0, d, 0)),
+                  _rect((x0, y0, 0), (w, 0, 0), (0, 0, h)), _rect((x0, y0 + d, 0), (w, 0, 0), (0, 0, h)),
+                  _rect((x0, y0, 0), (0, d, 0), (0, 0, h)), _rect((x0 + w, y0, 0), (0, d, 0), (0, 0, h))]
+    return rects
+
+
+def sample_rects(rects, density, rng):
+    pts = []
+    for o, u, v in rects:
+        n = int(np.linalg.norm(np.cross(u, v)) * density)
+        a = rng.random((n, 2))
+        pts.append(o + a[:, :1] * u + a[:, 1:] * v)
+    return np.concatenate(pts)
+
+
+def random_rotation(rng):
+    q = rng.standard_normal(4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def synth_scene_fragments(n_frag=30, seed=41, n_pts=250000, density=26000.0):
+    """n_frag raw fragments of one synthetic room: camera random walk (0.3 m steps), the
+    n_pts surface points nearest to the camera (at this density 250k points cover
+    ~20k 2.5 cm voxels, like the demo fragment's 258k points -> 19k voxels), each
+    moved by a random SE(3).
+    Returns (list of float32 [n,3], list of 4x4 GT poses mapping fragment -> world)."""
+    rng = np.random.default_rng(seed)
+    scene = sample_rects(synth_room(seed), density, rng)
+    cam = np.array([3.0, 3.0, 1.5])
+    frags, poses = [], []
+    for _ in range(n_frag):
+        cam = np.clip(cam + rng.normal(0, 0.3, 3) * np.array([1, 1, 0.3]), [1.0, 1.0, 1.2], [5.0, 5.0, 1.8])
+        d = np.linalg.norm(scene - cam, axis=1)
+        sel = np.argpartition(d, n_pts)[:n_pts] if len(d) > n_pts else np.arange(len(d))
+        R = random_rotation(rng)
+        t = rng.normal(0, 1.0, 3)
+        p = (scene[sel] - cam) @ R.T + t             # fragment frame
+        T = np.eye(4)                                  # fragment -> world: x_w = R^T (x_f - t) + cam
+        T[:3, :3] = R.T
+        T[:3, 3] = cam - R.T @ t
+        frags.append(p.astype(np.float32))
+        poses.append(T)
+    return frags, poses
