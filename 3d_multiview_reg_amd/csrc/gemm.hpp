@@ -35,6 +35,7 @@ struct GemmArgs {
   float2* stats; int64_t st_ld; int st_off;            // partial statistics (see Stats)
   int pro, bias_mode, stats_mode, has_res;
   int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
+  int use_v1;                                          // force the register-staged kernel (tests)
 };
 
 // Launch on `stream`; returns 0 or a negative error.

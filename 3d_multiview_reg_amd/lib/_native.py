@@ -54,6 +54,9 @@ _SIGS = {
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
                              c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_int,
                              c_vp]),
+    "mvr_gemm_f32_variant": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp,
+                                     c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_i64,
+                                     c_int, c_int, c_int, c_vp]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int]),
     "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_size,

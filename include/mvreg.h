@@ -61,6 +61,13 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
                  int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
                  int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
                  int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, mvr_stream_t stream);
+/* same, use_v1 = 1 forces the register-staged kernel (v2 = LDS-DMA staged is chosen whenever
+ * rows are 16-byte aligned and K % 4 == 0) — exposed so tests cover both kernels */
+int mvr_gemm_f32_variant(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
+                         int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
+                         int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh,
+                         int64_t sPb, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, int use_v1,
+                         mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters

@@ -8,7 +8,7 @@ pytestmark = pytest.mark.gpu
 BT = 128  # GEMM tile (csrc/gemm.hpp)
 
 
-def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0):
+def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, use_v1=0):
     import torch
     from lib import _native as NV
     r = np.random.RandomState(seed)
@@ -54,9 +54,10 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0):
     else:
         st, st_ld = None, 0
     L = NV.lib()
-    rc = L.mvr_gemm_f32(M, N, K, batch, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, (K if bkc else N), bkc,
-                        NV.ptr(C), M * N, N, NV.ptr(tR), M * N, NV.ptr(tb), bias_mode, NV.ptr(tsc), NV.ptr(tsh),
-                        (K if pro in (1, 2) else N), pro, NV.ptr(st), st_ld, 0, stats_mode, NV.stream())
+    rc = L.mvr_gemm_f32_variant(M, N, K, batch, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, (K if bkc else N), bkc,
+                                NV.ptr(C), M * N, N, NV.ptr(tR), M * N, NV.ptr(tb), bias_mode, NV.ptr(tsc),
+                                NV.ptr(tsh), (K if pro in (1, 2) else N), pro, NV.ptr(st), st_ld, 0, stats_mode,
+                                use_v1, NV.stream())
     assert rc == 0
     torch.cuda.synchronize()
     Cg = C.cpu().numpy().astype(np.float64)
@@ -94,11 +95,13 @@ COMBOS = [(0, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 0), (2, 0, 1, 0, 0), (2
 
 
 @pytest.mark.parametrize("combo", COMBOS)
-@pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 37, 3), (500, 300, 64, 1), (1, 40, 6, 2)])
-def test_gemm_modes(gpu, combo, shape):
+@pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 37, 3), (500, 300, 64, 1), (1, 40, 6, 2),
+                                   (130, 516, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1)])
+@pytest.mark.parametrize("use_v1", [0, 1])
+def test_gemm_modes(gpu, combo, shape, use_v1):
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo
-    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000)
+    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, use_v1=use_v1)
 
 
 def test_gemm_unaligned_ld_scalar_path(gpu):

@@ -1,0 +1,73 @@
+"""Micro-benchmark of the fused GEMM kernels at OANet shapes (timing with HIP events).
+usage: python tools/gemm_micro.py [--iters N] [--only NAME]"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d_multiview_reg_amd"))
+import torch  # noqa: E402
+from lib import _native as NV  # noqa: E402
+
+P, N, C, K = 435, 5000, 128, 500
+CASES = {
+    # name: (M, N, K, pro, bkc, bias, stats, res)
+    "conv_plain": (C, N, C, 0, 0, 0, 0, 0),
+    "conv_pro_stats": (C, N, C, 2, 0, 1, 1, 0),
+    "conv_res": (C, N, C, 2, 0, 1, 1, 1),
+    "embed_rowsmx": (K, N, C, 2, 0, 1, 2, 0),
+    "pool": (C, K, N, 3, 1, 0, 1, 0),
+    "unpool": (C, N, K, 3, 0, 0, 1, 0),
+}
+
+
+def run(name, iters, use_v1):
+    M, Nn, Kk, pro, bkc, bias, stats, res = CASES[name]
+    d = torch.device("cuda")
+    A = torch.randn(M, Kk, device=d) * 0.1 if name.startswith(("conv", "embed")) else torch.randn(P, M, Kk, device=d)
+    sAb = 0 if A.dim() == 2 else M * Kk
+    Bt = torch.randn(P, Nn, Kk, device=d) if bkc else torch.randn(P, Kk, Nn, device=d)
+    Cout = torch.empty(P, M, Nn, device=d)
+    R = torch.randn(P, M, Nn, device=d) if res else None
+    bvec = torch.randn(M if bias == 1 else Nn, device=d) if bias else None
+    vlen = Kk if pro in (1, 2) else Nn
+    sc = torch.rand(P, vlen, device=d) + 0.5 if pro else None
+    sh = torch.rand(P, vlen, device=d) if pro else None
+    nt = (Nn + 127) // 128
+    mt = (M + 127) // 128
+    st = torch.empty(P, max(nt, mt), max(M, Nn), 2, device=d) if stats else None
+    st_ld = M if stats in (1, 2) else Nn
+    L = NV.lib()
+
+    def go():
+        rc = L.mvr_gemm_f32_variant(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk, Kk if bkc else Nn, bkc,
+                                    NV.ptr(Cout), M * Nn, Nn, NV.ptr(R), M * Nn, NV.ptr(bvec), bias, NV.ptr(sc),
+                                    NV.ptr(sh), vlen, pro, NV.ptr(st), st_ld, 0, stats, use_v1, NV.stream())
+        assert rc == 0
+    for _ in range(2):
+        go()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        go()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    fl = 2.0 * M * Nn * Kk * P
+    by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
+    print("%-16s v%d  %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, 1 if use_v1 else 2, ms, fl / ms / 1e9,
+                                                          by / ms / 1e6), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--v", default="12")
+    a = ap.parse_args()
+    for n in CASES:
+        if a.only and n != a.only:
+            continue
+        for v in a.v:
+            run(n, a.iters, 1 if v == "1" else 0)
