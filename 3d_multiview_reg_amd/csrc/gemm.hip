@@ -5,16 +5,25 @@
 //   C[b](m,n) = sum_k  pro_A(A[b](m,k)) * pro_B(B[b](k,n))  (+ bias) (+ R[b](m,n))
 //
 // with the OANet elementwise work fused in:
-//   * prologue (applied while staging the tile global -> registers -> LDS):
-//       InstanceNorm+BatchNorm+ReLU folded to relu(x*sc[k]+sh[k]) on the reduction axis, or the
-//       column softmax exp(x-mx[n])*rs[n] of diff_pool / diff_unpool (oanet.py:106-128);
-//   * epilogue: bias, residual add (PointCN / OAFilter shortcuts, oanet.py:39-42,87-92),
-//       and the partial statistics the NEXT layer needs (InstanceNorm sum/sumsq per row,
-//       softmax max/sum-exp per row or per column), reduced across the 32-lane half by a
-//       register-transposing butterfly (16 shuffles for 16 rows instead of 80).
+//   * prologue, applied to the operand right after its LDS read: InstanceNorm+BatchNorm+ReLU
+//     folded to relu(x*sc[k]+sh[k]) on the reduction axis, or the per-tile softmax factor of
+//     diff_pool / diff_unpool (oanet.py:106-128, see ST_ROWSMX / PRO_B_SMX in gemm.hpp);
+//   * epilogue: bias, residual (PointCN / OAFilter shortcuts, oanet.py:39-42,87-92), the softmax
+//     exponentials (one exp per element, normalised later by the consumer's factor) and the
+//     partial statistics the NEXT layer needs.
 //
-// Tile: 128x128 per 256-thread workgroup (4 waves in 2x2, each 64x64 = 2x2 MFMA 32x32
-// blocks), BK=16, register-staged double-buffered LDS, one barrier per K step.
+// Schedule: persistent grid (2 workgroups per CU), 128x128 tile per 256-thread workgroup
+// (4 waves in 2x2, each 64x64 = 2x2 MFMA 32x32 blocks), BK = 32, operands staged by
+// global_load_lds_dwordx4 (no register staging) into a 2-stage LDS ring that runs across tile
+// boundaries, so the next tile's loads overlap the current tile's epilogue.
+//   * x-major tiles (k contiguous) land in LDS as [row][32] with the 16-byte chunks XOR-swizzled
+//     by (row & 7) through the per-lane SOURCE address (the LDS write stays lane-linear), read
+//     back with ds_read_b128 = 4 consecutive k.  The MFMA k order inside a stage is permuted
+//     (step s, lane half h -> k = 8*(s>>2) + 4h + (s&3)) identically for A and B, so a k-major B
+//     value is read at its permuted row with ds_read_b32.
+//   * epilogue: each 4x4 quad of an accumulator block is transposed across its 4 lanes (DPP) so a
+//     lane owns 4 consecutive columns of a row: float4 residual loads and stores, row statistics
+//     reduced with 3 swizzles, column statistics with 2 DPP moves and one cross-half shuffle.
 // Roofline: 2*M*N*K flops per GEMM against the 157.3 TF/s fp32 MFMA peak.
 #include "common.hpp"
 #include "gemm.hpp"
@@ -25,302 +34,17 @@ namespace mvr {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int BM = GEMM_BM, BN = GEMM_BN, BK = GEMM_BK;
-constexpr int LDA_S = BM + 4, LDB_S = BN + 4;
+constexpr int KV = 512;            // max K with a per-k prologue vector held in LDS
+constexpr int STAGE = 128 * BK;    // floats per operand per stage
 constexpr float NEG_BIG = -3.0e38f;
 
 struct KArgs {
   GemmArgs g;
-  int vecA, vecB;
-  long long persist;  // v2: number of persistent workgroups
+  int persist;  // number of persistent workgroups
 };
-
-__device__ __forceinline__ float4 ld4(const float* p, bool vec, int valid) {
-  // valid: number of in-range elements (0..4) starting at p
-  if (vec && valid == 4) return *reinterpret_cast<const float4*>(p);
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid > 0) r.x = p[0];
-  if (valid > 1) r.y = p[1];
-  if (valid > 2) r.z = p[2];
-  if (valid > 3) r.w = p[3];
-  return r;
-}
 
 __device__ __forceinline__ float& f4(float4& v, int i) { return reinterpret_cast<float*>(&v)[i]; }
 __device__ __forceinline__ float f4(const float4& v, int i) { return reinterpret_cast<const float*>(&v)[i]; }
-
-__device__ __forceinline__ void smx_combine(float& m, float& s, float m2, float s2) {
-  const float M = fmaxf(m, m2);
-  s = s * expf(m - M) + s2 * expf(m2 - M);
-  m = M;
-}
-
-// Butterfly over the 32 lanes of a half-wave for 16 per-lane values (one per MFMA row
-// register).  On return lane l holds in v[0] the reduction of register
-// rho(l) = 8*b4 + 4*b3 + 2*b2 + b1 (bits of l), lanes l and l^1 identical.
-template <bool SMX>
-__device__ __forceinline__ void butterfly16(float (&v)[16], float (&s)[16], int lane) {
-#pragma unroll
-  for (int step = 0; step < 4; ++step) {
-    const int half = 8 >> step;             // 8,4,2,1 registers kept
-    const int mask = 16 >> step;            // xor 16,8,4,2
-    const bool hi = (lane & mask) != 0;
-#pragma unroll
-    for (int r = 0; r < half; ++r) {
-      const float send_v = hi ? v[r] : v[r + half];
-      const float send_s = hi ? s[r] : s[r + half];
-      const float rv = __shfl_xor(send_v, mask, 64);
-      const float rs = __shfl_xor(send_s, mask, 64);
-      float kv = hi ? v[r + half] : v[r];
-      float ks = hi ? s[r + half] : s[r];
-      if (SMX) {
-        smx_combine(kv, ks, rv, rs);
-      } else {
-        kv += rv;
-        ks += rs;
-      }
-      v[r] = kv;
-      s[r] = ks;
-    }
-  }
-  const float rv = __shfl_xor(v[0], 1, 64);
-  const float rs = __shfl_xor(s[0], 1, 64);
-  if (SMX) {
-    smx_combine(v[0], s[0], rv, rs);
-  } else {
-    v[0] += rv;
-    s[0] += rs;
-  }
-}
-
-template <int PRO, int BKC, int BIAS, int STATS, int RES>
-__global__ __launch_bounds__(256) void gemm_kernel(KArgs ka) {
-  const GemmArgs& g = ka.g;
-  __shared__ float As[2][BK][LDA_S];
-  __shared__ float Bs[2][BK][LDB_S];
-  __shared__ float2 red[2][BM];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int b = blockIdx.z;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int M = g.M, N = g.N, K = g.K;
-
-  const float* A = g.A + (int64_t)b * g.sAb;
-  const float* B = g.B + (int64_t)b * g.sBb;
-  const float* psc = g.psc ? g.psc + (int64_t)b * g.sPb : nullptr;
-  const float* psh = g.psh ? g.psh + (int64_t)b * g.sPb : nullptr;
-  const bool vecA = ka.vecA, vecB = ka.vecB;
-
-  float4 ra[2], rb[2];
-
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
-      // ---- A tile: 128 (m) x 16 (k), k-contiguous in memory
-      {
-        const int m = (tid >> 2) + 64 * rep, kq = (tid & 3) * 4;
-        const int gm = m0 + m, gk = k0 + kq;
-        const int valid = (gm < M) ? min(4, max(0, K - gk)) : 0;
-        float4 v = ld4(A + (int64_t)gm * g.lda + gk, vecA, valid);
-        if (PRO == PRO_A_K) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            f4(v, i) = (gk + i < K) ? fmaxf(fmaf(f4(v, i), psc[gk + i], psh[gk + i]), 0.f) : 0.f;
-        }
-        ra[rep] = v;
-      }
-      // ---- B tile: 16 (k) x 128 (n)
-      if (!BKC) {
-        const int k = (tid >> 5) + 8 * rep, nq = (tid & 31) * 4;
-        const int gk = k0 + k, gn = n0 + nq;
-        const int valid = (gk < K) ? min(4, max(0, N - gn)) : 0;
-        float4 v = ld4(B + (int64_t)gk * g.ldb + gn, vecB, valid);
-        if (PRO == PRO_B_K) {
-          if (gk < K) {
-            const float sc = psc[gk], sh = psh[gk];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) f4(v, i) = fmaxf(fmaf(f4(v, i), sc, sh), 0.f);
-          }
-        } else if (PRO == PRO_B_SMX) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            f4(v, i) = (i < valid) ? expf(f4(v, i) - psc[gn + i]) * psh[gn + i] : 0.f;
-        }
-        rb[rep] = v;
-      } else {
-        const int n = (tid >> 2) + 64 * rep, kq = (tid & 3) * 4;
-        const int gn = n0 + n, gk = k0 + kq;
-        const int valid = (gn < N) ? min(4, max(0, K - gk)) : 0;
-        float4 v = ld4(B + (int64_t)gn * g.ldb + gk, vecB, valid);
-        if (PRO == PRO_B_K) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            f4(v, i) = (i < valid) ? fmaxf(fmaf(f4(v, i), psc[gk + i], psh[gk + i]), 0.f) : 0.f;
-        } else if (PRO == PRO_B_SMX) {
-          if (valid > 0) {
-            const float mx = psc[gn], rs = psh[gn];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) f4(v, i) = (i < valid) ? expf(f4(v, i) - mx) * rs : 0.f;
-          }
-        }
-        rb[rep] = v;
-      }
-    }
-  };
-
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int rep = 0; rep < 2; ++rep) {
-      {
-        const int m = (tid >> 2) + 64 * rep, kq = (tid & 3) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) As[buf][kq + i][m] = f4(ra[rep], i);
-      }
-      if (!BKC) {
-        const int k = (tid >> 5) + 8 * rep, nq = (tid & 31) * 4;
-        *reinterpret_cast<float4*>(&Bs[buf][k][nq]) = rb[rep];
-      } else {
-        const int n = (tid >> 2) + 64 * rep, kq = (tid & 3) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Bs[buf][kq + i][n] = f4(rb[rep], i);
-      }
-    }
-  };
-
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int nk = (K + BK - 1) / BK;
-  load(0);
-  store(0);
-  __syncthreads();
-  int cur = 0;
-  const int khalf = lane >> 5, l32 = lane & 31;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) load((kt + 1) * BK);
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      const float a0 = As[cur][kk + khalf][wm * 64 + l32];
-      const float a1 = As[cur][kk + khalf][wm * 64 + 32 + l32];
-      const float b0 = Bs[cur][kk + khalf][wn * 64 + l32];
-      const float b1 = Bs[cur][kk + khalf][wn * 64 + 32 + l32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (kt + 1 < nk) store(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
-  }
-
-  // ------------------------------------------------------------------ epilogue
-  float* C = g.C + (int64_t)b * g.sCb;
-  const float* Rr = RES ? g.R + (int64_t)b * g.sRb : nullptr;
-  float colm[2], cols[2];  // COLSMX running (max, sum) / COL (sum, sumsq) for this lane's two columns
-  colm[0] = colm[1] = (STATS == ST_COLSMX) ? NEG_BIG : 0.f;
-  cols[0] = cols[1] = 0.f;
-
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    float sv[16], ss[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sv[r] = (STATS == ST_ROWSMX) ? NEG_BIG : 0.f;
-      ss[r] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int gn = n0 + wn * 64 + j * 32 + l32;
-      const bool nok = gn < N;
-      float bn_ = 0.f;
-      if (BIAS == BIAS_N && nok) bn_ = g.bias[gn];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-        const bool ok = nok && gm < M;
-        float v = acc[i][j][r];
-        if (BIAS == BIAS_M) v += (gm < M) ? g.bias[gm] : 0.f;
-        if (BIAS == BIAS_N) v += bn_;
-        if (RES && ok) v += Rr[(int64_t)gm * g.ldc + gn];
-        if (ok) C[(int64_t)gm * g.ldc + gn] = v;
-        if (STATS == ST_ROW) {
-          if (ok) { sv[r] += v; ss[r] = fmaf(v, v, ss[r]); }
-        } else if (STATS == ST_ROWSMX) {
-          if (ok) smx_combine(sv[r], ss[r], v, 1.f);
-        } else if (STATS == ST_COLSMX) {
-          if (ok) smx_combine(colm[j], cols[j], v, 1.f);
-        } else if (STATS == ST_COL) {
-          if (ok) { colm[j] += v; cols[j] = fmaf(v, v, cols[j]); }
-        }
-      }
-    }
-    if (STATS == ST_ROW || STATS == ST_ROWSMX) {
-      butterfly16<STATS == ST_ROWSMX>(sv, ss, lane);
-      const int rho = ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
-      const int row = wm * 64 + i * 32 + (rho & 3) + 8 * (rho >> 2) + 4 * khalf;
-      if ((lane & 1) == 0) red[wn][row] = make_float2(sv[0], ss[0]);
-    }
-  }
-  if (STATS == ST_ROW || STATS == ST_ROWSMX) {
-    __syncthreads();
-    if (tid < BM && m0 + tid < M) {
-      float2 a = red[0][tid], c = red[1][tid];
-      if (STATS == ST_ROW) {
-        a.x += c.x;
-        a.y += c.y;
-      } else {
-        smx_combine(a.x, a.y, c.x, c.y);
-      }
-      g.stats[((int64_t)b * gridDim.x + blockIdx.x) * g.st_ld + g.st_off + m0 + tid] = a;
-    }
-  }
-  if (STATS == ST_COLSMX || STATS == ST_COL) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float om = __shfl_xor(colm[j], 32, 64), os = __shfl_xor(cols[j], 32, 64);
-      if (STATS == ST_COLSMX) {
-        smx_combine(colm[j], cols[j], om, os);
-      } else {
-        colm[j] += om;
-        cols[j] += os;
-      }
-      if (khalf == 0) red[wm][wn * 64 + j * 32 + l32] = make_float2(colm[j], cols[j]);
-    }
-    __syncthreads();
-    if (tid < BN && n0 + tid < N) {
-      float2 a = red[0][tid], c = red[1][tid];
-      if (STATS == ST_COLSMX) {
-        smx_combine(a.x, a.y, c.x, c.y);
-      } else {
-        a.x += c.x;
-        a.y += c.y;
-      }
-      g.stats[((int64_t)b * gridDim.y + blockIdx.y) * g.st_ld + g.st_off + n0 + tid] = a;
-    }
-  }
-}
-
-// ============================================================================================
-// v2: LDS-DMA staged variant (global_load_lds_dwordx4, no register staging), BK = 32.
-//   * A is always row-major [M][K] ("x-major": k contiguous); B is [K][N] (k-major) or [N][K].
-//   * x-major tiles land in LDS as [row][32] with the 16-byte chunks XOR-swizzled by (row & 7)
-//     through the per-lane SOURCE address (the LDS write stays lane-linear), read back with
-//     ds_read_b128 = 4 consecutive k.  The MFMA k order inside a BK step is permuted
-//     (step s, lane half h -> k = 8*(s>>2) + 4h + (s&3)) identically for A and B, so every
-//     k-major B value is read at its permuted row with ds_read_b32.
-//   * prologue transforms (IN/BN/ReLU, softmax) are applied to the operand right after the
-//     LDS read; the K tail is zeroed there (clamped loads keep every address in bounds).
-//   * 2-stage ring: stage t+1 is in flight while stage t is multiplied; one barrier per stage.
-// ============================================================================================
-constexpr int G2_BK = 32;
-constexpr int G2_KV = 512;  // max K with a per-k prologue vector held in LDS
-constexpr int G2_STAGE = 128 * G2_BK;  // floats per operand per stage
 
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_base + 16*l.
 // Inline asm so that hipcc does not track it: the compiler otherwise drains every LDS-DMA in flight
@@ -335,28 +59,63 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_base) {
                : "memory");
 }
 __device__ __forceinline__ void glds_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// workgroup barrier publishing LDS writes only (leaves LDS-DMA / global traffic in flight)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// cross-lane moves: DPP inside a quad of lanes, ds_swizzle (xor) inside a 32-lane half
+__device__ __forceinline__ float dpp_x1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float dpp_x2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));  // quad_perm 2,3,0,1
+}
+template <int X>
+__device__ __forceinline__ float swz(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (X << 10)));
+}
+
+// 4x4 transpose across the 4 lanes t of a quad: on return register u of lane t holds what
+// register t of lane u held.
+__device__ __forceinline__ void quad_transpose(float& a0, float& a1, float& a2, float& a3, bool h1, bool h2) {
+  {
+    const float r = dpp_x1(h1 ? a0 : a1);
+    if (h1) a0 = r; else a1 = r;
+  }
+  {
+    const float r = dpp_x1(h1 ? a2 : a3);
+    if (h1) a2 = r; else a3 = r;
+  }
+  {
+    const float r = dpp_x2(h2 ? a0 : a2);
+    if (h2) a0 = r; else a2 = r;
+  }
+  {
+    const float r = dpp_x2(h2 ? a1 : a3);
+    if (h2) a1 = r; else a3 = r;
+  }
+}
 
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
-__global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
-  // Persistent: workgroup w owns tiles w, w + grid, ...; the 2-stage LDS-DMA ring runs across
-  // tile boundaries, so the next tile's first stage (and its prologue vectors) is in flight while
-  // the current tile finishes and runs its epilogue.
+__global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
+  // Persistent: workgroup w owns tiles w, w + grid, ...
   const GemmArgs& g = ka.g;
-  constexpr int VEC = G2_KV + 32;
-  __shared__ __attribute__((aligned(16))) float smem[4 * G2_STAGE + 4 * VEC + 4 * BM];
-  float* Asm = smem;                         // [2][128][32]
-  float* Bsm = smem + 2 * G2_STAGE;          // [2][...]
-  float* vec = smem + 4 * G2_STAGE;          // [2 tile parities][2 (scale|max), (shift|1/sum)][VEC]
-  float2* red = reinterpret_cast<float2*>(vec + 4 * VEC);   // [2][128]
+  __shared__ __attribute__((aligned(16))) float smem[4 * STAGE + 4 * KV + 2 * BN + 4 * BM + 2 * BM];
+  float* Asm = smem;                          // [2][128][32]
+  float* Bsm = smem + 2 * STAGE;              // [2][...]
+  float* vec = smem + 4 * STAGE;              // [2 tile parities][scale | shift][KV]
+  float* fac = vec + 4 * KV;                  // [2 stages][128] softmax factors (PRO_B_SMX)
+  float2* red = reinterpret_cast<float2*>(fac + 2 * BN);    // [2][128] partial statistics
+  float* redm = fac + 2 * BN + 4 * BM;                      // [2][128] tile maxima (softmax)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int kh = lane >> 5, l32 = lane & 31;
   const int M = g.M, N = g.N, K = g.K;
+  const int N4 = (N + 3) & ~3, K4 = (K + 3) & ~3;
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
   const int ntiles = ntn * ntm * g.batch;
-  const int nk = (K + G2_BK - 1) / G2_BK;
+  const int nk = (K + BK - 1) / BK;
   const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   const int S = my_tiles * nk;
   if (S <= 0) return;
@@ -369,23 +128,16 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
     b = r / ntm;
   };
 
-  // per-tile prologue vectors -> LDS (wave 0, LDS-DMA): per-k scale/shift (IN/BN) or per-column
-  // softmax max / reciprocal sum
-  auto issue_vec = [&](int par, int b, int n0) {
+  // per-tile prologue vectors -> LDS (wave 0): per-k scale/shift (IN/BN)
+  auto issue_vec = [&](int par, int b) {
     if (wid != 0) return;
-    if (PRO == PRO_A_K || PRO == PRO_B_K) {
-      const float* ps = g.psc + (int64_t)b * g.sPb;
-      const float* ph = g.psh + (int64_t)b * g.sPb;
-      for (int c0 = 0; c0 < K / 4; c0 += 64) {
-        if (c0 + lane < K / 4) {
-          glds16(ps + 4 * (c0 + lane), vec + (2 * par) * VEC + 4 * c0);
-          glds16(ph + 4 * (c0 + lane), vec + (2 * par + 1) * VEC + 4 * c0);
-        }
+    const float* ps = g.psc + (int64_t)b * g.sPb;
+    const float* ph = g.psh + (int64_t)b * g.sPb;
+    for (int c0 = 0; c0 < K / 4; c0 += 64) {
+      if (c0 + lane < K / 4) {
+        glds16(ps + 4 * (c0 + lane), vec + (2 * par) * KV + 4 * c0);
+        glds16(ph + 4 * (c0 + lane), vec + (2 * par + 1) * KV + 4 * c0);
       }
-    } else if (PRO == PRO_B_SMX) {
-      const int n = min(n0 + 4 * l32, N - 4);
-      const float* src = (kh == 0 ? g.psc : g.psh) + (int64_t)b * g.sPb + n;
-      glds16(src, vec + (2 * par) * VEC);   // lanes 0-31 -> max[128], lanes 32-63 -> rsum[128]
     }
   };
 
@@ -393,10 +145,14 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
     const int i = gs / nk, ks = gs - (gs / nk) * nk;
     int b, tm, tn;
     tile_of(i, b, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN, k0 = ks * G2_BK;
-    if (ks == 0) issue_vec(i & 1, b, n0);
-    float* As = Asm + (gs & 1) * G2_STAGE;
-    float* Bs = Bsm + (gs & 1) * G2_STAGE;
+    const int m0 = tm * BM, n0 = tn * BN, k0 = ks * BK;
+    if ((PRO == PRO_A_K || PRO == PRO_B_K) && ks == 0) issue_vec(i & 1, b);
+    if (PRO == PRO_B_SMX && wid == 0 && lane < 32) {
+      const int n = min(n0 + 4 * lane, N4 - 4);
+      glds16(g.psc + (int64_t)b * g.sPb + (int64_t)(k0 / 128) * g.pld + n, fac + (gs & 1) * BN);
+    }
+    float* As = Asm + (gs & 1) * STAGE;
+    float* Bs = Bsm + (gs & 1) * STAGE;
     const float* A = g.A + (int64_t)b * g.sAb;
     const float* B = g.B + (int64_t)b * g.sBb;
 #pragma unroll
@@ -404,15 +160,15 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
       const int r = 32 * wid + 8 * ii + (lane >> 3);          // tile row
       const int c = (lane & 7) ^ (r & 7);                      // logical chunk held by this lane
       const int gm = min(m0 + r, M - 1);
-      const int gk = min(k0 + 4 * c, K - 4);
-      glds16(A + (int64_t)gm * g.lda + gk, As + (32 * wid + 8 * ii) * G2_BK);
+      const int gk = min(k0 + 4 * c, K4 - 4);
+      glds16(A + (int64_t)gm * g.lda + gk, As + (32 * wid + 8 * ii) * BK);
     }
     if (!BKC) {
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
         const int kr = 8 * wid + 2 * ii + (lane >> 5);
         const int gk = min(k0 + kr, K - 1);
-        const int gn = min(n0 + 4 * (lane & 31), N - 4);
+        const int gn = min(n0 + 4 * (lane & 31), N4 - 4);
         glds16(B + (int64_t)gk * g.ldb + gn, Bs + (8 * wid + 2 * ii) * BN);
       }
     } else {
@@ -421,14 +177,15 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
         const int r = 32 * wid + 8 * ii + (lane >> 3);
         const int c = (lane & 7) ^ (r & 7);
         const int gn = min(n0 + r, N - 1);
-        const int gk = min(k0 + 4 * c, K - 4);
-        glds16(B + (int64_t)gn * g.ldb + gk, Bs + (32 * wid + 8 * ii) * G2_BK);
+        const int gk = min(k0 + 4 * c, K4 - 4);
+        glds16(B + (int64_t)gn * g.ldb + gk, Bs + (32 * wid + 8 * ii) * BK);
       }
     }
   };
 
   floatx16 acc[2][2];
-  float cmx[2] = {0.f, 0.f}, crs[2] = {0.f, 0.f};   // per-column softmax constants (PRO_B_SMX)
+  const int t4 = lane & 3, p8 = l32 >> 2;   // epilogue: lane = (kh, p8, t4)
+  const bool h1 = (t4 & 1) != 0, h2 = (t4 & 2) != 0;
 
   issue(0);
   glds_wait_all();
@@ -437,8 +194,8 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
   for (int gs = 0; gs < S; ++gs) {
     const int i = gs / nk, ks = gs - (gs / nk) * nk;
     const int par = i & 1;
-    const float* vsc = vec + (2 * par) * VEC;
-    const float* vsh = vec + (2 * par + 1) * VEC;
+    const float* vsc = vec + (2 * par) * KV;
+    const float* vsh = vec + (2 * par + 1) * KV;
     if (ks == 0) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
@@ -446,18 +203,11 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
-      if (PRO == PRO_B_SMX) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          cmx[j] = vsc[wn * 64 + j * 32 + l32];
-          crs[j] = vsc[BN + wn * 64 + j * 32 + l32];
-        }
-      }
     }
-    const float* As = Asm + (gs & 1) * G2_STAGE;
-    const float* Bs = Bsm + (gs & 1) * G2_STAGE;
-    const int k0 = ks * G2_BK;
-    const bool tail = k0 + G2_BK > K;
+    const float* As = Asm + (gs & 1) * STAGE;
+    const float* Bs = Bsm + (gs & 1) * STAGE;
+    const int k0 = ks * BK;
+    const bool tail = k0 + BK > K;
     // all operands of the stage -> registers (one LDS wait), transforms, then 64 MFMAs back to back
     float4 a4[2][4], b4[2][4];
 #pragma unroll
@@ -466,18 +216,23 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         const int x = wm * 64 + ii * 32 + l32;
-        a4[ii][s4] = *reinterpret_cast<const float4*>(As + x * G2_BK + 4 * (q ^ (x & 7)));
+        a4[ii][s4] = *reinterpret_cast<const float4*>(As + x * BK + 4 * (q ^ (x & 7)));
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int x = wn * 64 + j * 32 + l32;
         if (BKC) {
-          b4[j][s4] = *reinterpret_cast<const float4*>(Bs + x * G2_BK + 4 * (q ^ (x & 7)));
+          b4[j][s4] = *reinterpret_cast<const float4*>(Bs + x * BK + 4 * (q ^ (x & 7)));
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) f4(b4[j][s4], e) = Bs[(4 * q + e) * BN + x];
         }
       }
+    }
+    float fm[2] = {1.f, 1.f};
+    if (PRO == PRO_B_SMX) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fm[j] = fac[(gs & 1) * BN + wn * 64 + j * 32 + l32];
     }
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
@@ -487,26 +242,30 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
         const float4 sh4 = *reinterpret_cast<const float4*>(vsh + kb);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const bool ok = kb + e < K;
           if (PRO == PRO_A_K) {
 #pragma unroll
             for (int ii = 0; ii < 2; ++ii)
-              f4(a4[ii][s4], e) = ok ? fmaxf(fmaf(f4(a4[ii][s4], e), f4(sc4, e), f4(sh4, e)), 0.f) : 0.f;
+              f4(a4[ii][s4], e) = fmaxf(fmaf(f4(a4[ii][s4], e), f4(sc4, e), f4(sh4, e)), 0.f);
           } else {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-              f4(b4[j][s4], e) = ok ? fmaxf(fmaf(f4(b4[j][s4], e), f4(sc4, e), f4(sh4, e)), 0.f) : 0.f;
+              f4(b4[j][s4], e) = fmaxf(fmaf(f4(b4[j][s4], e), f4(sc4, e), f4(sh4, e)), 0.f);
           }
         }
-      } else {
+      } else if (PRO == PRO_B_SMX) {
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float v = f4(b4[j][s4], e);
-            if (PRO == PRO_B_SMX) v = expf(v - cmx[j]) * crs[j];
-            if (tail && kb + e >= K) v = 0.f;
-            f4(b4[j][s4], e) = v;
+          for (int e = 0; e < 4; ++e) f4(b4[j][s4], e) *= fm[j];
+      }
+      if (tail) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (kb + e >= K) {
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii) f4(a4[ii][s4], e) = 0.f;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) f4(b4[j][s4], e) = 0.f;
           }
       }
     }
@@ -526,140 +285,316 @@ __global__ __launch_bounds__(256, 2) void gemm2_kernel(KArgs ka) {
     if (ks != nk - 1) continue;
 
     // -------------------------------------------------------------- epilogue of tile i
+    // after the quad transpose, value v[ii][j][q] (float4) of this lane is
+    //   C(m0 + 64wm + 32ii + 8q + 4kh + t4,  n0 + 64wn + 32j + 4p8 + u),  u = 0..3
     int b, tm, tn;
     tile_of(i, b, tm, tn);
     const int m0 = tm * BM, n0 = tn * BN;
     float* C = g.C + (int64_t)b * g.sCb;
-    const float* Rr = RES ? g.R + (int64_t)b * g.sRb : nullptr;
-    float colm[2], cols[2];
-    colm[0] = colm[1] = (STATS == ST_COLSMX) ? NEG_BIG : 0.f;
-    cols[0] = cols[1] = 0.f;
+    float4 v[2][2][4];
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii) {
-      float sv[16], ss[16];
+      asm volatile("" ::: "memory");   // keep each block's residual loads in its own iteration (VGPRs)
+      if (RES) {   // residual rows of this 32-row block (loads issued before the transposes)
+        const float* Rr = g.R + (int64_t)b * g.sRb;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sv[r] = (STATS == ST_ROWSMX) ? NEG_BIG : 0.f;
-        ss[r] = 0.f;
-      }
+        for (int q = 0; q < 4; ++q) {
+          const int gm = min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int gn = n0 + wn * 64 + j * 32 + l32;
-        const bool nok = gn < N;
-        float bn_ = 0.f;
-        if (BIAS == BIAS_N && nok) bn_ = g.bias[gn];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int gm = m0 + wm * 64 + ii * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-          const bool ok = nok && gm < M;
-          float v = acc[ii][j][r];
-          if (BIAS == BIAS_M) v += (gm < M) ? g.bias[gm] : 0.f;
-          if (BIAS == BIAS_N) v += bn_;
-          if (RES && ok) v += Rr[(int64_t)gm * g.ldc + gn];
-          if (ok) C[(int64_t)gm * g.ldc + gn] = v;
-          if (STATS == ST_ROW) {
-            if (ok) { sv[r] += v; ss[r] = fmaf(v, v, ss[r]); }
-          } else if (STATS == ST_ROWSMX) {
-            if (ok) smx_combine(sv[r], ss[r], v, 1.f);
-          } else if (STATS == ST_COLSMX) {
-            if (ok) smx_combine(colm[j], cols[j], v, 1.f);
-          } else if (STATS == ST_COL) {
-            if (ok) { colm[j] += v; cols[j] = fmaf(v, v, cols[j]); }
+          for (int j = 0; j < 2; ++j) {
+            const int gn = min(n0 + wn * 64 + j * 32 + 4 * p8, N4 - 4);
+            v[ii][j][q] = *reinterpret_cast<const float4*>(Rr + (int64_t)gm * g.ldc + gn);
           }
         }
       }
-      if (STATS == ST_ROW || STATS == ST_ROWSMX) {
-        butterfly16<STATS == ST_ROWSMX>(sv, ss, lane);
-        const int rho = ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
-        const int row = wm * 64 + ii * 32 + (rho & 3) + 8 * (rho >> 2) + 4 * kh;
-        if ((lane & 1) == 0) red[wn * BM + row] = make_float2(sv[0], ss[0]);
-      }
-    }
-    if (STATS == ST_ROW || STATS == ST_ROWSMX) {
-      __syncthreads();
-      if (tid < BM && m0 + tid < M) {
-        float2 a = red[tid], c = red[BM + tid];
-        if (STATS == ST_ROW) {
-          a.x += c.x;
-          a.y += c.y;
-        } else {
-          smx_combine(a.x, a.y, c.x, c.y);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float a0 = acc[ii][j][4 * q], a1 = acc[ii][j][4 * q + 1], a2 = acc[ii][j][4 * q + 2],
+                a3 = acc[ii][j][4 * q + 3];
+          quad_transpose(a0, a1, a2, a3, h1, h2);
+          if (RES) {
+            v[ii][j][q].x += a0; v[ii][j][q].y += a1; v[ii][j][q].z += a2; v[ii][j][q].w += a3;
+          } else {
+            v[ii][j][q] = make_float4(a0, a1, a2, a3);
+          }
         }
-        g.stats[((int64_t)b * ntn + tn) * g.st_ld + g.st_off + m0 + tid] = a;
-      }
-      __syncthreads();   // red reusable by the next tile
     }
-    if (STATS == ST_COLSMX || STATS == ST_COL) {
+    // validity: rows, columns (per component), float4 stores inside the padded row
+    bool rok[2][4];
+    bool cok[2][4];
+    bool sok[2];
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rok[ii][q] = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4 < M;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+      sok[j] = gn < N4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cok[j][u] = gn + u < N;
+    }
+    if (BIAS == BIAS_M) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float bm = g.bias[min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1)];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            v[ii][j][q].x += bm; v[ii][j][q].y += bm; v[ii][j][q].z += bm; v[ii][j][q].w += bm;
+          }
+        }
+    } else if (BIAS == BIAS_N) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const float om = __shfl_xor(colm[j], 32, 64), os = __shfl_xor(cols[j], 32, 64);
-        if (STATS == ST_COLSMX) {
-          smx_combine(colm[j], cols[j], om, os);
-        } else {
-          colm[j] += om;
-          cols[j] += os;
-        }
-        if (kh == 0) red[wm * BN + wn * 64 + j * 32 + l32] = make_float2(colm[j], cols[j]);
+        const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+        float bn[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bn[u] = cok[j][u] ? g.bias[gn + u] : 0.f;
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f4(v[ii][j][q], u) += bn[u];
       }
-      __syncthreads();
-      if (tid < BN && n0 + tid < N) {
-        float2 a = red[tid], c = red[BN + tid];
-        if (STATS == ST_COLSMX) {
-          smx_combine(a.x, a.y, c.x, c.y);
-        } else {
-          a.x += c.x;
-          a.y += c.y;
-        }
-        g.stats[((int64_t)b * ntm + tm) * g.st_ld + g.st_off + n0 + tid] = a;
-      }
-      __syncthreads();
     }
+
+    if (STATS == ST_ROWSMX) {
+      // tile row maxima -> exp(v - max) in place
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float mx = NEG_BIG;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (cok[j][u]) mx = fmaxf(mx, f4(v[ii][j][q], u));
+          mx = fmaxf(mx, swz<4>(mx));
+          mx = fmaxf(mx, swz<8>(mx));
+          mx = fmaxf(mx, swz<16>(mx));
+          if (p8 == 0) redm[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = mx;
+        }
+      lds_barrier();
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int rl = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+          const float mx = fmaxf(redm[rl], redm[BM + rl]);
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? expf(f4(v[ii][j][q], u) - mx) : 0.f;
+        }
+    } else if (STATS == ST_COLSMX) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float4 cm = make_float4(NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG);
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (rok[ii][q]) {
+#pragma unroll
+              for (int u = 0; u < 4; ++u) f4(cm, u) = fmaxf(f4(cm, u), f4(v[ii][j][q], u));
+            }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float x = f4(cm, u);
+          x = fmaxf(x, dpp_x1(x));
+          x = fmaxf(x, dpp_x2(x));
+          x = fmaxf(x, __shfl_xor(x, 32, 64));
+          f4(cm, u) = x;
+        }
+        const float mine = t4 == 0 ? cm.x : t4 == 1 ? cm.y : t4 == 2 ? cm.z : cm.w;
+        if (kh == 0) redm[wm * BN + wn * 64 + j * 32 + 4 * p8 + t4] = mine;
+      }
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = wn * 64 + j * 32 + 4 * p8;
+        const float4 c0 = *reinterpret_cast<const float4*>(redm + cl);
+        const float4 c1 = *reinterpret_cast<const float4*>(redm + BN + cl);
+        float mx[4] = {fmaxf(c0.x, c1.x), fmaxf(c0.y, c1.y), fmaxf(c0.z, c1.z), fmaxf(c0.w, c1.w)};
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? expf(f4(v[ii][j][q], u) - mx[u]) : 0.f;
+      }
+    }
+
+    // stores (full float4 inside the padded row)
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!rok[ii][q]) continue;
+        const int gm = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+          if (sok[j]) *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + gn) = v[ii][j][q];
+        }
+      }
+
+    // Statistics.  ST_ROW / ST_COL: per wave (64 columns / rows) the sum and the sum of squared
+    // deviations from the wave-local mean, merged across the two waves with Chan's formula — a
+    // two-pass variance per tile (sum-of-squares minus squared mean cancels catastrophically for
+    // InstanceNorm inputs whose mean is large against their spread).
+    if (STATS == ST_ROW || STATS == ST_ROWSMX) {
+      const int nw = min(max(N - (n0 + wn * 64), 0), 64);   // valid columns of this wave
+      const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float s = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s += cok[j][u] ? f4(v[ii][j][q], u) : 0.f;
+          s += swz<4>(s);
+          s += swz<8>(s);
+          s += swz<16>(s);
+          if (STATS == ST_ROW) {
+            const float mu = s * rnw;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const float d = cok[j][u] ? f4(v[ii][j][q], u) - mu : 0.f;
+                s2 = fmaf(d, d, s2);
+              }
+            s2 += swz<4>(s2);
+            s2 += swz<8>(s2);
+            s2 += swz<16>(s2);
+          }
+          if (p8 == 0) red[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(s, s2);
+        }
+      lds_barrier();
+      if (tid < BM && m0 + tid < M) {
+        const float2 a = red[tid], c = red[BM + tid];
+        float2 o;
+        if (STATS == ST_ROW) {
+          const int na = min(N - n0, 64), nb = min(max(N - n0 - 64, 0), 64);
+          o = a;
+          if (nb > 0) {
+            const float d = c.x / (float)nb - a.x / (float)na;
+            o = make_float2(a.x + c.x, a.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
+          }
+        } else {
+          o = make_float2(fmaxf(redm[tid], redm[BM + tid]), a.x + c.x);
+        }
+        g.stats[((int64_t)b * ntn + tn) * g.st_ld + g.st_off + m0 + tid] = o;
+      }
+    } else if (STATS == ST_COL || STATS == ST_COLSMX) {
+      const int nw = min(max(M - (m0 + wm * 64), 0), 64);   // valid rows of this wave
+      const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float s[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[u] += rok[ii][q] ? f4(v[ii][j][q], u) : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s[u] += dpp_x1(s[u]);
+          s[u] += dpp_x2(s[u]);
+          s[u] += __shfl_xor(s[u], 32, 64);
+        }
+        if (STATS == ST_COL) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float mu = s[u] * rnw;
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float d = rok[ii][q] ? f4(v[ii][j][q], u) - mu : 0.f;
+                s2[u] = fmaf(d, d, s2[u]);
+              }
+            s2[u] += dpp_x1(s2[u]);
+            s2[u] += dpp_x2(s2[u]);
+            s2[u] += __shfl_xor(s2[u], 32, 64);
+          }
+        }
+        const float ms = t4 == 0 ? s[0] : t4 == 1 ? s[1] : t4 == 2 ? s[2] : s[3];
+        const float ms2 = t4 == 0 ? s2[0] : t4 == 1 ? s2[1] : t4 == 2 ? s2[2] : s2[3];
+        if (kh == 0) red[wm * BN + wn * 64 + j * 32 + 4 * p8 + t4] = make_float2(ms, ms2);
+      }
+      lds_barrier();
+      if (tid < BN && n0 + tid < N) {
+        const float2 a = red[tid], c = red[BN + tid];
+        float2 o;
+        if (STATS == ST_COL) {
+          const int na = min(M - m0, 64), nb = min(max(M - m0 - 64, 0), 64);
+          o = a;
+          if (nb > 0) {
+            const float d = c.x / (float)nb - a.x / (float)na;
+            o = make_float2(a.x + c.x, a.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
+          }
+        } else {
+          o = make_float2(fmaxf(redm[tid], redm[BN + tid]), a.x + c.x);
+        }
+        g.stats[((int64_t)b * ntm + tm) * g.st_ld + g.st_off + n0 + tid] = o;
+      }
+    }
+    // (red / redm are next written in the next tile's epilogue, after at least one stage barrier)
   }
 }
 
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
-static void launch_t2(const KArgs& ka, dim3 grid, hipStream_t s) {
-  const long long tiles = (long long)grid.x * grid.y * grid.z;
+static void launch_t(const KArgs& ka, long long tiles, hipStream_t s) {
   const unsigned wgs = (unsigned)(tiles < ka.persist ? tiles : ka.persist);
-  hipLaunchKernelGGL((gemm2_kernel<PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
-}
-
-template <int PRO, int BKC, int BIAS, int STATS, int RES>
-static void launch_t(const KArgs& ka, dim3 grid, hipStream_t s) {
-  hipLaunchKernelGGL((gemm_kernel<PRO, BKC, BIAS, STATS, RES>), grid, dim3(256), 0, s, ka);
+  hipLaunchKernelGGL((gemm_kernel<PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
 }
 
 static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 int launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return MVR_OK;
-  if (!g.A || !g.B || !g.C) return MVR_EINVAL;
-  if (g.K < 0) return MVR_EINVAL;
-  if (g.pro != PRO_NONE && (!g.psc || !g.psh)) return MVR_EINVAL;
+  if (!g.A || !g.B || !g.C || g.K <= 0) return MVR_EINVAL;
+  if (g.pro != PRO_NONE && !g.psc) return MVR_EINVAL;
+  if ((g.pro == PRO_A_K || g.pro == PRO_B_K) && !g.psh) return MVR_EINVAL;
   if (g.stats_mode != ST_NONE && !g.stats) return MVR_EINVAL;
   if (g.bias_mode != BIAS_NONE && !g.bias) return MVR_EINVAL;
   if (g.has_res && !g.R) return MVR_EINVAL;
+  // layout contract (gemm.hpp)
+  const int64_t K4 = round4(g.K), N4 = round4(g.N);
+  bool ok = al16(g.A) && al16(g.B) && al16(g.C) && g.lda % 4 == 0 && g.ldb % 4 == 0 && g.ldc % 4 == 0 &&
+            g.sAb % 4 == 0 && g.sBb % 4 == 0 && g.sCb % 4 == 0 && g.lda >= K4 && g.ldc >= N4 &&
+            g.ldb >= (g.bkc ? K4 : N4);
+  if (g.has_res) ok = ok && al16(g.R) && g.sRb % 4 == 0;
+  if (g.pro == PRO_A_K || g.pro == PRO_B_K)
+    ok = ok && al16(g.psc) && al16(g.psh) && g.sPb % 4 == 0 && g.K % 4 == 0 && g.K <= KV;
+  if (g.pro == PRO_B_SMX) ok = ok && al16(g.psc) && g.sPb % 4 == 0 && g.pld % 4 == 0 && g.pld >= N4;
+  if (!ok) return MVR_EINVAL;
   KArgs ka;
   ka.g = g;
-  ka.vecA = al16(g.A) && (g.lda % 4 == 0) && (g.sAb % 4 == 0);
-  ka.vecB = al16(g.B) && (g.ldb % 4 == 0) && (g.sBb % 4 == 0);
   ka.persist = 2 * 256;  // 2 workgroups per CU (LDS-bound), 256 CUs
-  dim3 grid(gemm_ntiles(g.N), gemm_mtiles(g.M), g.batch);
-  if (grid.y > 65535 || grid.z > 65535) return MVR_EINVAL;
+  const long long tiles = (long long)gemm_ntiles(g.N) * gemm_mtiles(g.M) * g.batch;
+  if (tiles > 0x7fffffffLL) return MVR_EINVAL;
   const double fl = 2.0 * g.M * g.N * (double)g.K * g.batch;
   const double by = 4.0 * ((double)g.M * g.K * (g.sAb ? g.batch : 1) + (double)g.K * g.N * (g.sBb ? g.batch : 1) +
                            (double)g.M * g.N * g.batch * (g.has_res ? 2 : 1));
   ProfScope prof(g.prof_kind, fl, by, s);
-  // v2 (LDS-DMA) needs 16-byte aligned rows everywhere it loads and K >= 4
-  const bool vec_ok = (g.pro == PRO_NONE) ||
-                      (al16(g.psc) && al16(g.psh) && (g.sPb % 4 == 0) && (g.pro != PRO_B_SMX || g.N % 4 == 0));
-  const bool v2 = g.use_v1 == 0 && ka.vecA && ka.vecB && vec_ok && (g.K % 4 == 0) && g.K >= 4 &&
-                  (g.N % 4 == 0 || g.bkc) && g.N >= 4 && ((g.pro != PRO_A_K && g.pro != PRO_B_K) || g.K <= G2_KV);
   // Dispatch only the combinations the OANet schedule uses (oanet.hip).
 #define MVR_CASE(P, BKC_, BI, ST, RS)                                                                     \
   if (g.pro == P && g.bkc == BKC_ && g.bias_mode == BI && g.stats_mode == ST && (g.has_res != 0) == RS) { \
-    if (v2) launch_t2<P, BKC_, BI, ST, RS>(ka, grid, s);                                                \
-    else launch_t<P, BKC_, BI, ST, RS>(ka, grid, s);                                                    \
+    launch_t<P, BKC_, BI, ST, RS>(ka, tiles, s);                                                        \
     MVR_CHECK_LAUNCH();                                                                                  \
     return MVR_OK;                                                                                       \
   }
@@ -683,29 +618,19 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
 }  // namespace mvr
 
 // C-ABI: one fused GEMM (exposed for unit tests and host-side composition).
-extern "C" int mvr_gemm_f32_variant(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
+extern "C" int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
                             int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc,
                             const float* R, int64_t sRb, const float* bias, int bias_mode, const float* psc,
-                            const float* psh, int64_t sPb, int pro, float* stats, int64_t st_ld, int st_off,
-                            int stats_mode, int use_v1, hipStream_t stream) {
+                            const float* psh, int64_t sPb, int64_t pld, int pro, float* stats, int64_t st_ld,
+                            int st_off, int stats_mode, hipStream_t stream) {
   mvr::GemmArgs g{};
-  g.use_v1 = use_v1;
   g.M = M; g.N = N; g.K = K; g.batch = batch;
   g.A = A; g.sAb = sAb; g.lda = lda;
   g.B = B; g.sBb = sBb; g.ldb = ldb; g.bkc = b_kcontig;
   g.C = C; g.sCb = sCb; g.ldc = ldc;
   g.R = R; g.sRb = sRb; g.has_res = R != nullptr;
   g.bias = bias; g.bias_mode = bias_mode;
-  g.psc = psc; g.psh = psh; g.sPb = sPb; g.pro = pro;
+  g.psc = psc; g.psh = psh; g.sPb = sPb; g.pld = pld; g.pro = pro;
   g.stats = reinterpret_cast<float2*>(stats); g.st_ld = st_ld; g.st_off = st_off; g.stats_mode = stats_mode;
   return mvr::launch_gemm(g, stream);
-}
-
-extern "C" int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
-                            int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc,
-                            const float* R, int64_t sRb, const float* bias, int bias_mode, const float* psc,
-                            const float* psh, int64_t sPb, int pro, float* stats, int64_t st_ld, int st_off,
-                            int stats_mode, hipStream_t stream) {
-  return mvr_gemm_f32_variant(M, N, K, batch, A, sAb, lda, B, sBb, ldb, b_kcontig, C, sCb, ldc, R, sRb, bias,
-                              bias_mode, psc, psh, sPb, pro, stats, st_ld, st_off, stats_mode, 0, stream);
 }

@@ -11,18 +11,24 @@ enum Pro : int {
   PRO_NONE = 0,   // operands used as stored
   PRO_A_K = 1,    // A(m,k) <- relu(A*sc[k] + sh[k])           (BN+ReLU on the reduction axis of A)
   PRO_B_K = 2,    // B(k,n) <- relu(B*sc[k] + sh[k])           (IN+BN+ReLU folded, per input channel)
-  PRO_B_SMX = 3,  // B(k,n) <- exp(B - mx[n]) * rs[n]           (softmax normalised by column)
+  PRO_B_SMX = 3,  // B(k,n) <- B(k,n) * f[k/128][n]            (softmax: B holds exp(x - tile max) as
+                  //                                            written by an ST_*SMX epilogue, f the
+                  //                                            per-tile factor exp(tile max - max)/sum)
 };
 enum Bias : int { BIAS_NONE = 0, BIAS_M = 1, BIAS_N = 2 };
 enum Stats : int {
   ST_NONE = 0,
-  ST_ROW = 1,     // per (b, n-tile, m): (sum, sumsq) over the tile's columns  -> InstanceNorm stats
-  ST_ROWSMX = 2,  // per (b, n-tile, m): (max, sum exp(v-max))                 -> softmax over n
-  ST_COLSMX = 3,  // per (b, m-tile, n): (max, sum exp(v-max))                 -> softmax over m
-  ST_COL = 4,     // per (b, m-tile, n): (sum, sumsq) over the tile's rows     -> train-mode BN over m
+  ST_ROW = 1,     // per (b, n-tile, m): (sum, sum of squared deviations from the tile mean) over
+                  // the tile's columns                                          -> InstanceNorm stats
+  ST_ROWSMX = 2,  // C <- exp(v - mt), mt = max of row m over the tile's columns;
+                  // per (b, n-tile, m): (mt, sum exp(v - mt))                 -> softmax over n
+  ST_COLSMX = 3,  // C <- exp(v - mt), mt = max of column n over the tile's rows;
+                  // per (b, m-tile, n): (mt, sum exp(v - mt))                 -> softmax over m
+  ST_COL = 4,     // per (b, m-tile, n): (sum, squared deviations) over the tile's rows
+                  //                                                           -> train-mode BN over m
 };
 
-constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 16;
+constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 32;
 
 struct GemmArgs {
   int M, N, K, batch;
@@ -31,17 +37,25 @@ struct GemmArgs {
   float* C; int64_t sCb; int64_t ldc;                  // C(m,n) = C[b*sCb + m*ldc + n]
   const float* R; int64_t sRb;                         // residual, same ldc as C
   const float* bias;                                   // [M] (BIAS_M) or [N] (BIAS_N)
-  const float* psc; const float* psh; int64_t sPb;     // prologue vectors (batch stride sPb, may be 0)
+  const float* psc; const float* psh; int64_t sPb;     // PRO_A_K/PRO_B_K: per-k vectors psc/psh [b*sPb + k];
+  int64_t pld;                                         // PRO_B_SMX: factors psc[b*sPb + (k/128)*pld + n]
   float2* stats; int64_t st_ld; int st_off;            // partial statistics (see Stats)
   int pro, bias_mode, stats_mode, has_res;
   int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
-  int use_v1;                                          // force the register-staged kernel (tests)
 };
 
-// Launch on `stream`; returns 0 or a negative error.
+// Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the
+// padded rows, so: all pointers 16-byte aligned; lda, ldb, ldc, pld and every batch stride a
+// multiple of 4; A rows (and B rows when bkc) readable up to round_up(K, 4) floats, B rows
+// (bkc = 0), C/R rows and factor rows up to round_up(N, 4) floats, all of them finite there.
+// Padding columns of C in [N, round_up(N, 4)) are written (finite values: 0 after a softmax
+// epilogue) and never enter results, statistics or the K tail.  PRO_A_K / PRO_B_K need K % 4 == 0
+// and K <= 512.  Launch on `stream`; returns 0 or a negative error (MVR_EINVAL on a violated
+// contract).
 int launch_gemm(const GemmArgs& g, hipStream_t stream);
 
 inline int gemm_ntiles(int N) { return (N + GEMM_BN - 1) / GEMM_BN; }
 inline int gemm_mtiles(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }
+inline int64_t round4(int64_t x) { return (x + 3) & ~(int64_t)3; }
 
 }  // namespace mvr

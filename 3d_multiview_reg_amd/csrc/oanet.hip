@@ -30,14 +30,17 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
+  // tiles of 128 columns carry (sum, squared deviations from the tile mean): Chan's merge
+  double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int t = 0; t < T; ++t) {
     const float2 v = st[((int64_t)p * T + t) * st_ld + st_off + c];
-    s += v.x;
-    q += v.y;
+    const double nb = (double)min(128, L - 128 * t);
+    const double d = (double)v.x / nb - mean, tot = n + nb;
+    mean += d * nb / tot;
+    m2 += (double)v.y + d * d * n * nb / tot;
+    n = tot;
   }
-  const double mean = s / L;
-  const double var = fmax(q / L - mean * mean, 0.0);
+  const double var = fmax(m2 / L, 0.0);
   const float rin = (float)(1.0 / sqrt(var + (double)eps_in));
   if (train) {
     mv[(int64_t)p * C + c] = make_float2((float)mean, (float)var);
@@ -52,7 +55,7 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
   }
   const float gs = g * rs;
   sc[(int64_t)p * out_ld + c] = rin * gs;
-  sh[(int64_t)p * out_ld + c] = b - ((float)mean * rin + rm) * gs;
+  sh[(int64_t)p * out_ld + c] = (float)((double)b - (mean * (double)rin + (double)rm) * (double)gs);
 }
 
 __global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int C, float eps_in, mvr_bn_p bn, float* sc,
@@ -89,38 +92,57 @@ __global__ void bn_col_train_kernel(const float2* __restrict__ st, int P, int MT
                                     float* sc, float* sh) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= Kc) return;
-  double s = 0.0, q = 0.0;
+  double n = 0.0, mean = 0.0, m2 = 0.0;   // Chan's merge of (sum, squared deviations) per row tile
   for (int i = 0; i < P * MT; ++i) {
     const float2 v = st[(int64_t)i * Kc + k];
-    s += v.x;
-    q += v.y;
+    const double nb = (double)min(128, rows - 128 * (i % MT));
+    const double d = (double)v.x / nb - mean, tot = n + nb;
+    mean += d * nb / tot;
+    m2 += (double)v.y + d * d * n * nb / tot;
+    n = tot;
   }
-  const double n = (double)P * rows;
-  const double mean = s / n, var = fmax(q / n - mean * mean, 0.0);
+  const double var = fmax(m2 / n, 0.0);
   const float g = bn.gamma[k] / sqrtf((float)var + 1e-5f);
   sc[k] = g;
   sh[k] = bn.beta[k] - (float)mean * g;
 }
 
-// softmax partials (max, sumexp) [P][T][L] -> mx[P][L], rs = 1/sum
-__global__ void smx_finalize_kernel(const float2* __restrict__ st, int T, int L, float* mx, float* rs) {
+// softmax partials (tile max m_t, sum_t exp(v - m_t)) [P][T][L] -> per-tile factors
+// fac[p][t][c] = exp(m_t - M) / S with M = max_t m_t, S = sum_t s_t exp(m_t - M): the consumer GEMM
+// (PRO_B_SMX) multiplies the stored exp(v - m_t) by it, which is exp(v - M) / S, the softmax.
+// Columns [L, ld) of every factor row are zeroed (padding columns of the operand).
+__global__ void smx_factor_kernel(const float2* __restrict__ st, int T, int L, int64_t ld, float* fac) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
-  if (c >= L) return;
-  float m = -3.0e38f, s = 0.f;
-  for (int t = 0; t < T; ++t) {
-    const float2 v = st[((int64_t)p * T + t) * L + c];
-    const float M = fmaxf(m, v.x);
-    s = s * expf(m - M) + v.y * expf(v.x - M);
-    m = M;
+  if (c >= ld) return;
+  float* f = fac + (int64_t)p * T * ld + c;
+  if (c >= L) {
+    for (int t = 0; t < T; ++t) f[(int64_t)t * ld] = 0.f;
+    return;
   }
-  mx[(int64_t)p * L + c] = m;
-  rs[(int64_t)p * L + c] = 1.f / s;
+  const float2* sp = st + (int64_t)p * T * L + c;
+  float m = -3.0e38f;
+  for (int t = 0; t < T; ++t) m = fmaxf(m, sp[(int64_t)t * L].x);
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float2 v = sp[(int64_t)t * L];
+    s += v.y * expf(v.x - m);
+  }
+  const float r = 1.f / s;
+  for (int t = 0; t < T; ++t) f[(int64_t)t * ld] = expf(sp[(int64_t)t * L].x - m) * r;
+}
+
+// zero-padded copy of a [rows][cols] weight to [rows][ld] (ld = round_up(cols, 4))
+__global__ void pad_cols_kernel(const float* __restrict__ w, int rows, int cols, int ld, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * ld) return;
+  const int r = i / ld, c = i - r * ld;
+  out[i] = c < cols ? w[(int64_t)r * cols + c] : 0.f;
 }
 
 // Output head (oanet.py:163,174-175): logits = w.x + b; weights = relu(tanh(logits));
 // guard_pos[p] += #positive weights (the batch-coupled zero-row guard reads it).
-__global__ void head_kernel(const float* __restrict__ X, int64_t ps, int C, int N, const float* __restrict__ w,
+__global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld, int C, int N, const float* __restrict__ w,
                             const float* __restrict__ bias, float* logits, float* scores, int32_t* pos) {
   __shared__ int cnt;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -130,7 +152,7 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int C, int 
   if (n < N) {
     const float* x = X + (int64_t)p * ps + n;
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(w[c], x[(int64_t)c * N], acc);
+    for (int c = 0; c < C; ++c) acc = fmaf(w[c], x[(int64_t)c * ld], acc);
     const float lg = acc + bias[0];
     const float wt = fmaxf(tanhf(lg), 0.f);
     logits[(int64_t)p * N + n] = lg;
@@ -170,16 +192,20 @@ struct Ws {
 
 struct Plan {
   int P, N, C, Kc, Cin;
+  int64_t Np, Kp, Cinp;  // padded row lengths (points, clusters, conv1 input channels)
   size_t bytes;
-  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *mx, *rs;
+  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *fac, *W1;
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
 };
 
-Plan plan(int C, int Kc, int P, int N, void* base) {
+// Activations [P][C][Np] over points and [P][C][Kp] over clusters, rows padded to a multiple of 4
+// floats (16-byte rows for the LDS-DMA staging of gemm.hip).
+Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   Plan pl{};
-  pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc;
+  pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc; pl.Cin = Cin;
+  pl.Np = round4(N); pl.Kp = round4(Kc); pl.Cinp = round4(Cin);
   Ws w{reinterpret_cast<char*>(base), 0, 0};
-  const size_t PN = (size_t)P * N, PK = (size_t)P * Kc;
+  const size_t PN = (size_t)P * pl.Np, PK = (size_t)P * pl.Kp;
   const int TN = gemm_ntiles(N), TK = gemm_ntiles(Kc), MK = gemm_mtiles(Kc), MC = gemm_mtiles(C);
   pl.X11 = w.take<float>(PN * 2 * C);
   pl.XA = w.take<float>(PN * C);
@@ -190,11 +216,12 @@ Plan plan(int C, int Kc, int P, int N, void* base) {
   pl.O2 = w.take<float>(PK * C);
   pl.sc = w.take<float>((size_t)P * 2 * C);
   pl.sh = w.take<float>((size_t)P * 2 * C);
-  pl.scK = w.take<float>(Kc);
-  pl.shK = w.take<float>(Kc);
-  const size_t L = (size_t)(N > Kc ? N : Kc);
-  pl.mx = w.take<float>((size_t)P * L);
-  pl.rs = w.take<float>((size_t)P * L);
+  pl.scK = w.take<float>(pl.Kp);
+  pl.shK = w.take<float>(pl.Kp);
+  size_t nf = (size_t)P * TN * pl.Kp;
+  if ((size_t)P * MK * pl.Np > nf) nf = (size_t)P * MK * pl.Np;
+  pl.fac = w.take<float>(nf);
+  pl.W1 = w.take<float>((size_t)C * pl.Cinp);
   pl.st11 = w.take<float2>((size_t)P * TN * 2 * C);
   pl.stA = w.take<float2>((size_t)P * TN * C);
   pl.stT = w.take<float2>((size_t)P * TN * C);
@@ -236,10 +263,11 @@ struct Ctx {
   }
 
   // 1x1 conv: out = W . pro(in) + b (+res); stats into out.st when `stats`
-  void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode) {
+  void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
+            const float* w_padded = nullptr) {
     GemmArgs g{};
     g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
-    g.A = cv.weight; g.sAb = 0; g.lda = in.C;
+    g.A = w_padded ? w_padded : cv.weight; g.sAb = 0; g.lda = w_padded ? round4(in.C) : in.C;
     g.B = in.p; g.sBb = in.ps; g.ldb = in.ld; g.bkc = 0;
     g.C = out.p; g.sCb = out.ps; g.ldc = out.ld;
     if (res) { g.R = res->p; g.sRb = res->ps; g.has_res = 1; }
@@ -253,7 +281,7 @@ struct Ctx {
 
   void pointcn(const mvr_pointcn_p& pc, const Act& x, const Act& y) {
     finalize_in(x, 1e-5f, pc.bn1);
-    Act t{pl.T1, (int64_t)y.C * pl.N, pl.N, y.C, pl.N, pl.stT, y.C, 0};
+    Act t{pl.T1, (int64_t)y.C * pl.Np, pl.Np, y.C, pl.N, pl.stT, y.C, 0};
     const bool sc = pc.shortcut.weight != nullptr;
     if (sc) conv(pc.shortcut, x, false, y, nullptr, ST_NONE);
     conv(pc.conv3, x, true, t, nullptr, ST_ROW);
@@ -263,8 +291,9 @@ struct Ctx {
 
   void oafilter(const mvr_oafilter_p& f, const Act& xd) {
     const int C = pl.C, Kc = pl.Kc;
+    const int64_t Kp = pl.Kp;
     finalize_in(xd, 1e-3f, f.bn1);
-    Act o1{pl.O1, (int64_t)C * Kc, Kc, C, Kc, pl.stcol, Kc, 0};
+    Act o1{pl.O1, (int64_t)C * Kp, Kp, C, Kc, pl.stcol, Kc, 0};
     conv(f.conv1, xd, true, o1, nullptr, train ? ST_COL : ST_NONE);
     if (train) {
       hipLaunchKernelGGL(bn_col_train_kernel, dim3((Kc + 255) / 256), dim3(256), 0, s, pl.stcol, pl.P,
@@ -274,13 +303,13 @@ struct Ctx {
     }
     chk_launch();
     // out2(c,k') = sum_k relu(bn2_k(o1(c,k))) W2[k'][k] + b2[k'] + o1(c,k')   (conv on the transpose)
-    Act o2{pl.O2, (int64_t)C * Kc, Kc, C, Kc, pl.stO, C, 0};
+    Act o2{pl.O2, (int64_t)C * Kp, Kp, C, Kc, pl.stO, C, 0};
     GemmArgs g{};
     g.M = C; g.N = Kc; g.K = Kc; g.batch = pl.P;
-    g.A = pl.O1; g.sAb = (int64_t)C * Kc; g.lda = Kc;
+    g.A = pl.O1; g.sAb = (int64_t)C * Kp; g.lda = Kp;
     g.B = f.conv2.weight; g.sBb = 0; g.ldb = Kc; g.bkc = 1;
-    g.C = o2.p; g.sCb = o2.ps; g.ldc = Kc;
-    g.R = pl.O1; g.sRb = (int64_t)C * Kc; g.has_res = 1;
+    g.C = o2.p; g.sCb = o2.ps; g.ldc = Kp;
+    g.R = pl.O1; g.sRb = (int64_t)C * Kp; g.has_res = 1;
     g.bias = f.conv2.bias; g.bias_mode = BIAS_N;
     g.pro = PRO_A_K; g.psc = pl.scK; g.psh = pl.shK; g.sPb = 0;
     g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
@@ -290,9 +319,10 @@ struct Ctx {
     conv(f.conv3, o2, true, xd, &xd, ST_ROW);  // in place: out = conv3(...) + x
   }
 
-  void smx_finalize(int T, int L) {
-    dim3 grid((L + 255) / 256, pl.P);
-    hipLaunchKernelGGL(smx_finalize_kernel, grid, dim3(256), 0, s, pl.smx, T, L, pl.mx, pl.rs);
+  // softmax partials [P][T][L] -> factors pl.fac [P][T][ld]
+  void smx_factors(int T, int L, int64_t ld) {
+    dim3 grid((unsigned)((ld + 255) / 256), pl.P);
+    hipLaunchKernelGGL(smx_factor_kernel, grid, dim3(256), 0, s, pl.smx, T, L, ld, pl.fac);
     chk_launch();
   }
 };
@@ -302,48 +332,58 @@ struct Ctx {
 
 using namespace mvr;
 
-extern "C" size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int P, int N) {
-  return plan(channels, clusters, P, N, nullptr).bytes;
+extern "C" size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N) {
+  return plan(channels, clusters, in_channels, P, N, nullptr).bytes;
 }
 
-extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride,
+extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride, int64_t ld,
                                      const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N,
                                      int bn_train, float* logits, float* scores, float* R, float* t, float* res,
                                      float* latent, float* res_row, float* score_row, int64_t row_pstride,
                                      int32_t* guard_pos, int32_t* status, void* workspace, size_t workspace_bytes,
                                      hipStream_t s) {
   if (!blk || !input || !xs || !logits || !scores || !R || !t || !res || !guard_pos || !workspace) return MVR_EINVAL;
-  const int C = blk->channels, Kc = blk->clusters, H = blk->half_layers;
-  if (P <= 0 || N <= 0 || C <= 0 || Kc <= 0 || H <= 0 || H > MVR_OAN_MAX_HALF || blk->in_channels <= 0)
+  const int C = blk->channels, Kc = blk->clusters, H = blk->half_layers, Cin = blk->in_channels;
+  if (P <= 0 || N <= 0 || C <= 0 || Kc <= 0 || H <= 0 || H > MVR_OAN_MAX_HALF || Cin <= 0) return MVR_EINVAL;
+  if (C % 4 || ld < round4(N) || ld % 4 || in_pstride % 4 || (reinterpret_cast<uintptr_t>(input) & 15))
     return MVR_EINVAL;
   if (!blk->l1_2[0].shortcut.weight) return MVR_EINVAL;
-  const Plan pl = plan(C, Kc, P, N, workspace);
+  const Plan pl = plan(C, Kc, Cin, P, N, workspace);
   if (workspace_bytes < pl.bytes) return MVR_EINVAL;
   Ctx cx{pl, s, bn_train};
-  const int64_t CN = (int64_t)C * N;
+  const int64_t Np = pl.Np, Kp = pl.Kp;
+  const int64_t CN = (int64_t)C * Np;
   const int TN = gemm_ntiles(N);
 
-  // conv1: input (Cin ch) -> XA
-  Act in{const_cast<float*>(input), in_pstride, N, blk->in_channels, N, nullptr, 0, 0};
-  Act xa{pl.XA, CN, N, C, N, pl.stA, C, 0};
-  cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW);
+  // conv1: input (Cin ch) -> XA; a Cin % 4 != 0 weight is zero-padded to 16-byte rows first
+  const float* w1 = nullptr;
+  if (Cin % 4) {
+    const int n = (int)(C * pl.Cinp);
+    hipLaunchKernelGGL(pad_cols_kernel, dim3((n + 255) / 256), dim3(256), 0, s, blk->conv1.weight, C, Cin,
+                       (int)pl.Cinp, pl.W1);
+    cx.chk_launch();
+    w1 = pl.W1;
+  }
+  Act in{const_cast<float*>(input), in_pstride, ld, Cin, N, nullptr, 0, 0};
+  Act xa{pl.XA, CN, Np, C, N, pl.stA, C, 0};
+  cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW, w1);
   // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C))
-  Act x11top{pl.X11, 2 * CN, N, C, N, pl.st11, 2 * C, 0};
+  Act x11top{pl.X11, 2 * CN, Np, C, N, pl.st11, 2 * C, 0};
   for (int i = 0; i < H; ++i) cx.pointcn(blk->l1_1[i], xa, (i == H - 1) ? x11top : xa);
 
-  // diff_pool (oanet.py:96-110)
+  // diff_pool (oanet.py:96-110): E = exp(embed - tile max) over points, x_down = x . softmax(E)^T
   cx.finalize_in(x11top, 1e-3f, blk->down_bn);
-  Act e{pl.E, (int64_t)Kc * N, N, Kc, N, pl.smx, Kc, 0};
+  Act e{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, Kc, 0};
   cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);
-  cx.smx_finalize(TN, Kc);
-  Act xd{pl.XD, (int64_t)C * Kc, Kc, C, Kc, pl.stD, C, 0};
+  cx.smx_factors(TN, Kc, Kp);
+  Act xd{pl.XD, (int64_t)C * Kp, Kp, C, Kc, pl.stD, C, 0};
   {
     GemmArgs g{};
     g.M = C; g.N = Kc; g.K = N; g.batch = P;
-    g.A = pl.X11; g.sAb = 2 * CN; g.lda = N;
-    g.B = pl.E; g.sBb = (int64_t)Kc * N; g.ldb = N; g.bkc = 1;
-    g.C = pl.XD; g.sCb = (int64_t)C * Kc; g.ldc = Kc;
-    g.pro = PRO_B_SMX; g.psc = pl.mx; g.psh = pl.rs; g.sPb = Kc;
+    g.A = pl.X11; g.sAb = 2 * CN; g.lda = Np;
+    g.B = pl.E; g.sBb = (int64_t)Kc * Np; g.ldb = Np; g.bkc = 1;
+    g.C = pl.XD; g.sCb = (int64_t)C * Kp; g.ldc = Kp;
+    g.pro = PRO_B_SMX; g.psc = pl.fac; g.sPb = (int64_t)TN * Kp; g.pld = Kp;
     g.stats_mode = ST_ROW; g.stats = pl.stD; g.st_ld = C; g.st_off = 0;
     g.prof_kind = PK_POOL;
     cx.chk(launch_gemm(g, s));
@@ -351,32 +391,33 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   // l2: OAFilter x H (in place on XD)
   for (int i = 0; i < H; ++i) cx.oafilter(blk->l2[i], xd);
 
-  // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C)
+  // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C): softmax over clusters
   cx.finalize_in(x11top, 1e-3f, blk->up_bn);
-  Act e2{pl.E, (int64_t)Kc * N, N, Kc, N, pl.smx, N, 0};
+  Act e2{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, N, 0};
   cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX);
-  cx.smx_finalize(gemm_mtiles(Kc), N);
+  const int MK = gemm_mtiles(Kc);
+  cx.smx_factors(MK, N, Np);
   {
     GemmArgs g{};
     g.M = C; g.N = N; g.K = Kc; g.batch = P;
-    g.A = pl.XD; g.sAb = (int64_t)C * Kc; g.lda = Kc;
-    g.B = pl.E; g.sBb = (int64_t)Kc * N; g.ldb = N; g.bkc = 0;
-    g.C = pl.X11 + CN; g.sCb = 2 * CN; g.ldc = N;
-    g.pro = PRO_B_SMX; g.psc = pl.mx; g.psh = pl.rs; g.sPb = N;
+    g.A = pl.XD; g.sAb = (int64_t)C * Kp; g.lda = Kp;
+    g.B = pl.E; g.sBb = (int64_t)Kc * Np; g.ldb = Np; g.bkc = 0;
+    g.C = pl.X11 + CN; g.sCb = 2 * CN; g.ldc = Np;
+    g.pro = PRO_B_SMX; g.psc = pl.fac; g.sPb = (int64_t)MK * Np; g.pld = Np;
     g.stats_mode = ST_ROW; g.stats = pl.st11; g.st_ld = 2 * C; g.st_off = C;
     g.prof_kind = PK_UNPOOL;
     cx.chk(launch_gemm(g, s));
   }
   // l1_2: PointCN(2C -> C, shortcut) + (H-1) PointCN(C)
-  Act x11{pl.X11, 2 * CN, N, 2 * C, N, pl.st11, 2 * C, 0};
-  Act out{latent ? latent : pl.XA, CN, N, C, N, pl.stA, C, 0};
+  Act x11{pl.X11, 2 * CN, Np, 2 * C, N, pl.st11, 2 * C, 0};
+  Act out{latent ? latent : pl.XA, latent ? (int64_t)C * ld : CN, latent ? ld : Np, C, N, pl.stA, C, 0};
   cx.pointcn(blk->l1_2[0], x11, out);
   for (int i = 1; i < H; ++i) cx.pointcn(blk->l1_2[i], out, out);
 
   // head + guard + Kabsch
   (void)hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s);
-  hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, CN, C, N, blk->output.weight,
-                     blk->output.bias, logits, scores, guard_pos);
+  hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, out.ps, out.ld, C, N,
+                     blk->output.weight, blk->output.bias, logits, scores, guard_pos);
   cx.chk_launch();
   if (cx.err) return cx.err;
   // weights = relu(tanh(logits)) already in `scores`; the guard (oanet.py:177-178) and

@@ -52,13 +52,10 @@ _SIGS = {
     "mvr_procrustes_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int,
                                    ctypes.c_double, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
-                             c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_i64, c_int, c_int,
-                             c_vp]),
-    "mvr_gemm_f32_variant": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp,
-                                     c_i64, c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_int, c_vp, c_i64,
-                                     c_int, c_int, c_int, c_vp]),
-    "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int]),
-    "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
+                             c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int,
+                             c_int, c_vp]),
+    "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
+    "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_size,
                                       c_vp]),
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
@@ -79,7 +76,7 @@ _SIGS = {
     "mvr_prof_set": (c_int, [c_int]),
     "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
-    "mvr_xs_to_channels": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_vp]),
+    "mvr_xs_to_channels": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp]),
 }
 
 # every symbol include/mvreg.h declares (checked by tests/test_native_abi.py)

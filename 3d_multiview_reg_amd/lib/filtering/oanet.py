@@ -153,35 +153,37 @@ class OANet(nn.Module):
         dev = self.reg_init.conv1.weight.device
         N.require_hip(self.reg_init.conv1.weight)
         xs = xs_in.to(dev, torch.float32)[:, 0].contiguous()           # [P, N, Cxs]
-        P, Np, Cxs = xs.shape
+        P, Npts, Cxs = xs.shape
+        ld = (Npts + 3) // 4 * 4            # point rows padded to 16 bytes (csrc/gemm.hpp layout contract)
         if Cxs < 6:
             raise ValueError("xs must have at least 6 channels (x1 | x2)")
         L = N.lib()
         st = N.stream()
         rows = Cxs + 2
-        inp = torch.empty(P, rows, Np, device=dev, dtype=torch.float32)
-        N.check(L.mvr_xs_to_channels(N.ptr(xs), Np * Cxs, Cxs, Cxs, P, Np, N.ptr(inp), rows * Np, st),
+        inp = torch.zeros(P, rows, ld, device=dev, dtype=torch.float32)
+        N.check(L.mvr_xs_to_channels(N.ptr(xs), Npts * Cxs, Cxs, Cxs, P, Npts, N.ptr(inp), rows * ld, ld, st),
                 "mvr_xs_to_channels")
         blocks = [self.reg_init] + [self.reg_iter[i] for i in range(self.iter_num)]
         C = self.reg_init.channels
-        ws_bytes = L.mvr_oan_block_workspace_bytes(C, self.reg_init.clusters, P, Np)
+        ws_bytes = max(L.mvr_oan_block_workspace_bytes(C, self.reg_init.clusters, b.in_channels, P, Npts)
+                       for b in blocks)
         ws = N.workspace(ws_bytes, dev)
         guard = torch.empty(P, dtype=torch.int32, device=dev)
         status = torch.zeros(len(blocks), P, dtype=torch.int32, device=dev)
-        latent = torch.empty(P, C, Np, device=dev, dtype=torch.float32)
+        latent = torch.empty(P, C, ld, device=dev, dtype=torch.float32)
         out = {"logits": [], "scores": [], "rot_est": [], "trans_est": []}
         for bi, blk in enumerate(blocks):
             params = blk.native_params()
-            logits = torch.empty(P, Np, device=dev)
-            scores = torch.empty(P, Np, device=dev)
+            logits = torch.empty(P, Npts, device=dev)
+            scores = torch.empty(P, Npts, device=dev)
             R = torch.empty(P, 3, 3, device=dev)
             t = torch.empty(P, 3, 1, device=dev)
-            res = torch.empty(P, Np, device=dev)
+            res = torch.empty(P, Npts, device=dev)
             last = bi == len(blocks) - 1
             rc = L.mvr_oan_block_forward(
-                ctypes.byref(params), N.ptr(inp), rows * Np, N.ptr(xs), Np * Cxs, Cxs, P, Np, int(self.training),
+                ctypes.byref(params), N.ptr(inp), rows * ld, ld, N.ptr(xs), Npts * Cxs, Cxs, P, Npts, int(self.training),
                 N.ptr(logits), N.ptr(scores), N.ptr(R), N.ptr(t), N.ptr(res), N.ptr(latent) if last else None,
-                None if last else N.ptr(inp[:, Cxs]), None if last else N.ptr(inp[:, Cxs + 1]), rows * Np,
+                None if last else N.ptr(inp[:, Cxs]), None if last else N.ptr(inp[:, Cxs + 1]), rows * ld,
                 N.ptr(guard), N.ptr(status[bi]), N.ptr(ws), ws.numel(), st)
             N.check(rc, "mvr_oan_block_forward")
             if bi == 0 and not last:
@@ -190,6 +192,6 @@ class OANet(nn.Module):
                     raise ValueError("reg_iter input channels %d != %d" % (blk_in_ch, rows))
             for k, v in zip(("logits", "scores", "rot_est", "trans_est"), (logits, scores, R, t)):
                 out[k].append(v)
-        out["latent features"] = latent.unsqueeze(3)
+        out["latent features"] = latent[:, :, :Npts].unsqueeze(3)
         out["gradient_flag"] = bool(status.any().item())
         return out

@@ -52,22 +52,20 @@ int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_pstride, in
 /* ------------------------------------------------------------------------
  * One fused fp32-MFMA batched GEMM of the OANet schedule (exposed for tests):
  *   C[b](m,n) = sum_k pro_A(A(m,k)) pro_B(B(k,n)) + bias + R[b](m,n)
- * pro: 0 none, 1 relu(A*sc[k]+sh[k]), 2 relu(B*sc[k]+sh[k]), 3 exp(B-sc[n])*sh[n]
+ * pro: 0 none, 1 relu(A*sc[k]+sh[k]), 2 relu(B*sc[k]+sh[k]) (sc/sh at [b*sPb + k]),
+ *      3 B(k,n) * f[b*sPb + (k/128)*pld + n] (per-tile softmax factor).
  * bias_mode: 0 none, 1 per m, 2 per n.  stats_mode: 0 none, 1 row sum/sumsq,
- * 2 row max/sumexp, 3 column max/sumexp (float2 partials, see csrc/gemm.hpp).
+ * 2 row softmax (C <- exp(v - tile row max), partials (tile max, sum)), 3 the same per column,
+ * 4 column sum/sumsq (float2 partials, see csrc/gemm.hpp).
+ * Layout: 16-byte aligned pointers, all strides multiples of 4 floats, rows padded to
+ * round_up(K|N, 4) floats holding finite values (MVR_EINVAL otherwise).
  * Replaces the nn.Conv2d(k=1) / torch.matmul calls of lib/filtering/oanet.py.
  * ---------------------------------------------------------------------- */
 int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
                  int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
                  int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
-                 int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, mvr_stream_t stream);
-/* same, use_v1 = 1 forces the register-staged kernel (v2 = LDS-DMA staged is chosen whenever
- * rows are 16-byte aligned and K % 4 == 0) — exposed so tests cover both kernels */
-int mvr_gemm_f32_variant(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
-                         int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
-                         int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh,
-                         int64_t sPb, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, int use_v1,
-                         mvr_stream_t stream);
+                 int64_t pld, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode,
+                 mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters
@@ -98,25 +96,27 @@ typedef struct {
   mvr_conv_p output;
 } mvr_oan_block_p;
 
-size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int P, int N);
+size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N);
 
-/* input(p,c,n) = input[p*in_pstride + c*N + n]  (Cin = blk->in_channels)
+/* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
+ * a multiple of 4, input 16-byte aligned, padding columns [N, ld) finite (zero).
  * xs(p,n,0..5) = xs[p*xs_pstride + n*xs_nstride + 0..5]  (x1 | x2 for Kabsch)
  * Outputs: logits/scores [P,N] (contiguous), R [P,3,3], t [P,3], res [P,N];
- * latent [P,C,N] (may be NULL); res_row/score_row: optional copies written at
+ * latent(p,c,n) = latent[p*C*ld + c*ld + n] (may be NULL); res_row/score_row: optional copies written at
  * row pointers with pair stride row_pstride (the next block's input rows 6,7).
  * guard_pos: int32 [P] scratch (zeroed here).  status: int32 [P] (may be NULL).
  * bn_train: BatchNorm layers normalise with batch statistics (module.train()). */
-int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride, const float* xs,
-                          int64_t xs_pstride, int64_t xs_nstride, int P, int N, int bn_train, float* logits,
+int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride, int64_t ld,
+                          const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N, int bn_train,
+                          float* logits,
                           float* scores, float* R, float* t, float* res, float* latent, float* res_row,
                           float* score_row, int64_t row_pstride, int32_t* guard_pos, int32_t* status, void* workspace,
                           size_t workspace_bytes, mvr_stream_t stream);
 
-/* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*N + n]
+/* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*out_ld + n]
  * (the transpose of lib/filtering/oanet.py:234). */
 int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N, float* out,
-                       int64_t out_pstride, mvr_stream_t stream);
+                       int64_t out_pstride, int64_t out_ld, mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Feature-space (soft) nearest neighbour for a batch of fragment pairs.

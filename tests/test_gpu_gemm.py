@@ -1,5 +1,5 @@
 """Fused fp32-MFMA GEMM (csrc/gemm.hip) vs a float64 numpy reference, every
-prologue/epilogue combination the OANet schedule uses, ragged shapes."""
+prologue/epilogue combination the OANet schedule uses, ragged shapes, padded rows."""
 import numpy as np
 import pytest
 
@@ -8,22 +8,35 @@ pytestmark = pytest.mark.gpu
 BT = 128  # GEMM tile (csrc/gemm.hpp)
 
 
-def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, use_v1=0):
+def r4(x):
+    return (x + 3) // 4 * 4
+
+
+def _pad(a, width):
+    out = np.zeros(a.shape[:-1] + (width,), a.dtype)
+    out[..., :a.shape[-1]] = a
+    return out
+
+
+def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shared_a=False):
     import torch
     from lib import _native as NV
     r = np.random.RandomState(seed)
-    A = r.standard_normal((batch, M, K)).astype(np.float32)
+    K4, N4 = r4(K), r4(N)
+    A = r.standard_normal((1 if shared_a else batch, M, K)).astype(np.float32)
     Bm = r.standard_normal((batch, K, N)).astype(np.float32)       # logical B(k, n)
-    Bstore = np.ascontiguousarray(np.swapaxes(Bm, 1, 2)) if bkc else Bm
-    R = r.standard_normal((batch, M, N)).astype(np.float32) if res else None
+    if pro == 3:
+        Bm = np.abs(Bm)
+    Bstore = _pad(np.swapaxes(Bm, 1, 2), K4) if bkc else _pad(Bm, N4)
+    Rm = r.standard_normal((batch, M, N)).astype(np.float32) if res else None
     bias = r.standard_normal(M if bias_mode == 1 else N).astype(np.float32) if bias_mode else None
-    sc = sh = None
+    sc = sh = fac = None
+    KT = (K + BT - 1) // BT
     if pro in (1, 2):
         sc = r.uniform(0.5, 1.5, (batch, K)).astype(np.float32)
         sh = r.uniform(-0.5, 0.5, (batch, K)).astype(np.float32)
     elif pro == 3:
-        sc = r.uniform(0.0, 1.0, (batch, N)).astype(np.float32)     # "max"
-        sh = r.uniform(0.5, 1.5, (batch, N)).astype(np.float32)     # "1/sum"
+        fac = _pad(r.uniform(0.1, 1.5, (batch, KT, N)).astype(np.float32), N4)
     # reference in float64
     Ad, Bd = A.astype(np.float64), Bm.astype(np.float64)
     if pro == 1:
@@ -31,18 +44,19 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, use_
     elif pro == 2:
         Bd = np.maximum(Bd * sc[:, :, None] + sh[:, :, None], 0)
     elif pro == 3:
-        Bd = np.exp(Bd - sc[:, None, :]) * sh[:, None, :]
+        Bd = Bd * np.repeat(fac[:, :, :N].astype(np.float64), BT, axis=1)[:, :K]
     Cref = Ad @ Bd
     if bias_mode == 1:
         Cref += bias[None, :, None]
     elif bias_mode == 2:
         Cref += bias[None, None, :]
     if res:
-        Cref += R
+        Cref += Rm
     dev = gpu
     t = lambda x: None if x is None else torch.from_numpy(np.ascontiguousarray(x)).to(dev)
-    tA, tB, tR, tb, tsc, tsh = t(A), t(Bstore), t(R), t(bias), t(sc), t(sh)
-    C = torch.full((batch, M, N), float("nan"), device=dev)
+    tA, tB, tR, tb = t(_pad(A, K4)), t(Bstore), t(None if Rm is None else _pad(Rm, N4)), t(bias)
+    tsc, tsh, tf = t(sc), t(sh), t(fac)
+    C = torch.full((batch, M, N4), float("nan"), device=dev)
     nT = (N + BT - 1) // BT
     mT = (M + BT - 1) // BT
     if stats_mode in (1, 2):
@@ -53,39 +67,55 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, use_
         st_ld = N
     else:
         st, st_ld = None, 0
+    if pro in (1, 2):
+        pv, sPb, pld = (tsc, tsh), K, 0
+    elif pro == 3:
+        pv, sPb, pld = (tf, None), KT * N4, N4
+    else:
+        pv, sPb, pld = (None, None), 0, 0
     L = NV.lib()
-    rc = L.mvr_gemm_f32_variant(M, N, K, batch, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, (K if bkc else N), bkc,
-                                NV.ptr(C), M * N, N, NV.ptr(tR), M * N, NV.ptr(tb), bias_mode, NV.ptr(tsc),
-                                NV.ptr(tsh), (K if pro in (1, 2) else N), pro, NV.ptr(st), st_ld, 0, stats_mode,
-                                use_v1, NV.stream())
+    rc = L.mvr_gemm_f32(M, N, K, batch, NV.ptr(tA), 0 if shared_a else M * K4, K4, NV.ptr(tB),
+                        K * N4 if not bkc else N * K4, K4 if bkc else N4, bkc,
+                        NV.ptr(C), M * N4, N4, NV.ptr(tR), M * N4, NV.ptr(tb), bias_mode, NV.ptr(pv[0]),
+                        NV.ptr(pv[1]), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats_mode, NV.stream())
     assert rc == 0
     torch.cuda.synchronize()
     Cg = C.cpu().numpy().astype(np.float64)
+    assert np.all(np.isfinite(Cg)), "padding columns must be written with finite values"
+    Cg = Cg[..., :N]
     scale = np.abs(Ad) @ np.abs(Bd) + 1.0
-    assert np.all(np.abs(Cg - Cref) <= 1e-5 * scale), np.max(np.abs(Cg - Cref) / scale)
-    if st is None:
+    S = None if st is None else st.cpu().numpy().astype(np.float64)
+    if stats_mode in (2, 3):
+        # softmax epilogues store exp(v - tile max) and emit (tile max, sum)
+        ax = -1 if stats_mode == 2 else 1
+        nt = nT if stats_mode == 2 else mT
+        for tt in range(nt):
+            sl = (slice(None), slice(None), slice(tt * BT, (tt + 1) * BT)) if stats_mode == 2 else \
+                (slice(None), slice(tt * BT, (tt + 1) * BT), slice(None))
+            blk = Cref[sl]
+            mx = blk.max(ax, keepdims=True)
+            E = np.exp(blk - mx)
+            # |d exp(v - m)| <= E * (|dv| + |dm|)
+            tol = E * 4e-5 * scale[sl].max(ax, keepdims=True) + 1e-6
+            assert np.all(np.abs(Cg[sl] - E) <= tol), np.max(np.abs(Cg[sl] - E) - tol)
+            np.testing.assert_allclose(S[:, tt, :, 0], mx.squeeze(ax), rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(S[:, tt, :, 1], E.sum(ax), rtol=1e-4)
         return
-    S = st.cpu().numpy().astype(np.float64)
-    if stats_mode in (1, 2):
+    assert np.all(np.abs(Cg - Cref) <= 1e-5 * scale), np.max(np.abs(Cg - Cref) / scale)
+    if S is None:
+        return
+    if stats_mode == 1:
         for tt in range(nT):
             blk = Cref[:, :, tt * BT:(tt + 1) * BT]
-            if stats_mode == 1:
-                np.testing.assert_allclose(S[:, tt, :, 0], blk.sum(-1), rtol=1e-4, atol=1e-3)
-                np.testing.assert_allclose(S[:, tt, :, 1], (blk ** 2).sum(-1), rtol=1e-4, atol=1e-3)
-            else:
-                mx = blk.max(-1)
-                np.testing.assert_allclose(S[:, tt, :, 0], mx, rtol=1e-5, atol=1e-5)
-                np.testing.assert_allclose(S[:, tt, :, 1], np.exp(blk - mx[..., None]).sum(-1), rtol=1e-4)
+            np.testing.assert_allclose(S[:, tt, :, 0], blk.sum(-1), rtol=1e-4, atol=1e-3)
+            dev2 = ((blk - blk.mean(-1, keepdims=True)) ** 2).sum(-1)      # squared deviations
+            np.testing.assert_allclose(S[:, tt, :, 1], dev2, rtol=1e-4, atol=1e-3)
     else:
         for tt in range(mT):
             blk = Cref[:, tt * BT:(tt + 1) * BT, :]
-            if stats_mode == 4:
-                np.testing.assert_allclose(S[:, tt, :, 0], blk.sum(1), rtol=1e-4, atol=1e-3)
-                np.testing.assert_allclose(S[:, tt, :, 1], (blk ** 2).sum(1), rtol=1e-4, atol=1e-3)
-            else:
-                mx = blk.max(1)
-                np.testing.assert_allclose(S[:, tt, :, 0], mx, rtol=1e-5, atol=1e-5)
-                np.testing.assert_allclose(S[:, tt, :, 1], np.exp(blk - mx[:, None, :]).sum(1), rtol=1e-4)
+            np.testing.assert_allclose(S[:, tt, :, 0], blk.sum(1), rtol=1e-4, atol=1e-3)
+            dev2 = ((blk - blk.mean(1, keepdims=True)) ** 2).sum(1)
+            np.testing.assert_allclose(S[:, tt, :, 1], dev2, rtol=1e-4, atol=1e-3)
 
 
 # (pro, bkc, bias, stats, res) — the dispatch table of csrc/gemm.hip
@@ -95,16 +125,37 @@ COMBOS = [(0, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 0), (2, 0, 1, 0, 0), (2
 
 
 @pytest.mark.parametrize("combo", COMBOS)
-@pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 37, 3), (500, 300, 64, 1), (1, 40, 6, 2),
-                                   (130, 516, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1)])
-@pytest.mark.parametrize("use_v1", [0, 1])
-def test_gemm_modes(gpu, combo, shape, use_v1):
+@pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 36, 3), (500, 300, 64, 1), (1, 40, 8, 2),
+                                   (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2)])
+def test_gemm_modes(gpu, combo, shape):
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo
-    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, use_v1=use_v1)
+    if pro in (1, 2) and K % 4:
+        pytest.skip("per-k prologue needs K % 4 == 0")
+    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1))
 
 
-def test_gemm_unaligned_ld_scalar_path(gpu):
-    # K=6 rows (conv1 of reg_init) -> A rows not 16-byte aligned
-    _run(gpu, 128, 5000, 6, 2, 0, 0, 1, 1, 0)
-    _run(gpu, 128, 999, 8, 2, 0, 0, 1, 1, 0)
+def test_gemm_ragged_k(gpu):
+    # K = 6 (conv1 of reg_init, weight rows zero-padded to 8) and odd K for plain GEMMs
+    _run(gpu, 128, 5000, 6, 2, 0, 0, 1, 1, 0, shared_a=True)
+    _run(gpu, 128, 999, 7, 2, 0, 0, 1, 1, 0, shared_a=True)
+    _run(gpu, 70, 333, 45, 2, 0, 1, 0, 0, 0)
+    _run(gpu, 70, 333, 45, 2, 3, 1, 0, 1, 0)
+
+
+def test_gemm_rejects_bad_layout(gpu):
+    import torch
+    from lib import _native as NV
+    L = NV.lib()
+    A = torch.zeros(16, 8, device=gpu)
+    B = torch.zeros(8, 16, device=gpu)
+    C = torch.zeros(16, 16, device=gpu)
+    ok = L.mvr_gemm_f32(16, 16, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C), 0, 16, None, 0, None, 0,
+                        None, None, 0, 0, 0, None, 0, 0, 0, NV.stream())
+    assert ok == 0
+    # lda not a multiple of 4 / row shorter than round_up(K, 4)
+    assert L.mvr_gemm_f32(16, 16, 6, 1, NV.ptr(A), 0, 6, NV.ptr(B), 0, 16, 0, NV.ptr(C), 0, 16, None, 0, None, 0,
+                          None, None, 0, 0, 0, None, 0, 0, 0, NV.stream()) == -1
+    # misaligned C
+    assert L.mvr_gemm_f32(15, 12, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C[0, 1:]), 0, 16, None, 0,
+                          None, 0, None, None, 0, 0, 0, None, 0, 0, 0, NV.stream()) == -1

@@ -35,7 +35,7 @@ def test_python_binding_covers_header():
     from lib import _native
     assert set(header_symbols()) == set(_native.EXPORTS)
     L = _native.lib()
-    assert L.mvr_oan_block_workspace_bytes(128, 500, 2, 5000) > 2 * 5000 * 128 * 4
+    assert L.mvr_oan_block_workspace_bytes(128, 500, 6, 2, 5000) > 2 * 5000 * 128 * 4
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libmvreg_hip.so not built")

@@ -21,7 +21,7 @@ CASES = {
 }
 
 
-def run(name, iters, use_v1):
+def run(name, iters):
     M, Nn, Kk, pro, bkc, bias, stats, res = CASES[name]
     d = torch.device("cuda")
     A = torch.randn(M, Kk, device=d) * 0.1 if name.startswith(("conv", "embed")) else torch.randn(P, M, Kk, device=d)
@@ -30,9 +30,14 @@ def run(name, iters, use_v1):
     Cout = torch.empty(P, M, Nn, device=d)
     R = torch.randn(P, M, Nn, device=d) if res else None
     bvec = torch.randn(M if bias == 1 else Nn, device=d) if bias else None
-    vlen = Kk if pro in (1, 2) else Nn
-    sc = torch.rand(P, vlen, device=d) + 0.5 if pro else None
-    sh = torch.rand(P, vlen, device=d) if pro else None
+    kt = (Kk + 127) // 128
+    if pro in (1, 2):
+        sc, sh, sPb, pld = torch.rand(P, Kk, device=d) + 0.5, torch.rand(P, Kk, device=d), Kk, 0
+    elif pro == 3:
+        sc, sh, sPb, pld = torch.rand(P, kt, Nn, device=d), None, kt * Nn, Nn
+    else:
+        sc = sh = None
+        sPb = pld = 0
     nt = (Nn + 127) // 128
     mt = (M + 127) // 128
     st = torch.empty(P, max(nt, mt), max(M, Nn), 2, device=d) if stats else None
@@ -40,9 +45,9 @@ def run(name, iters, use_v1):
     L = NV.lib()
 
     def go():
-        rc = L.mvr_gemm_f32_variant(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk, Kk if bkc else Nn, bkc,
-                                    NV.ptr(Cout), M * Nn, Nn, NV.ptr(R), M * Nn, NV.ptr(bvec), bias, NV.ptr(sc),
-                                    NV.ptr(sh), vlen, pro, NV.ptr(st), st_ld, 0, stats, use_v1, NV.stream())
+        rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk, Kk if bkc else Nn, bkc,
+                            NV.ptr(Cout), M * Nn, Nn, NV.ptr(R), M * Nn, NV.ptr(bvec), bias, NV.ptr(sc),
+                            NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, NV.stream())
         assert rc == 0
     for _ in range(2):
         go()
@@ -56,18 +61,15 @@ def run(name, iters, use_v1):
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * M * Nn * Kk * P
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
-    print("%-16s v%d  %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, 1 if use_v1 else 2, ms, fl / ms / 1e9,
-                                                          by / ms / 1e6), flush=True)
+    print("%-16s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
-    ap.add_argument("--v", default="12")
     a = ap.parse_args()
     for n in CASES:
         if a.only and n != a.only:
             continue
-        for v in a.v:
-            run(n, a.iters, 1 if v == "1" else 0)
+        run(n, a.iters)
