@@ -31,10 +31,25 @@
 
 namespace mvr {
 
+int g_default_math = MATH_BF16X3;
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Which 16-byte chunk q (4 consecutive k of the 32-k stage) lane half h reads as its s4-th
+// register.  f32 MFMA 32x32x2: step (s4, e) takes k = 4(2 s4 + h) + e.  bf16 32x32x16: step st
+// takes k = 16 st + 8h + j, i.e. chunks 4st + 2h and 4st + 2h + 1 as registers 2st, 2st + 1.
+template <int MATH>
+__device__ __forceinline__ int chunk_of(int s4, int h) {
+  return MATH == MATH_F32 ? 2 * s4 + h : 4 * (s4 >> 1) + 2 * h + (s4 & 1);
+}
 
 constexpr int BM = GEMM_BM, BN = GEMM_BN, BK = GEMM_BK;
-constexpr int KV = 512;            // max K with a per-k prologue vector held in LDS
+constexpr int KV_MAX = 512;        // max K with a per-k prologue vector held in LDS
+constexpr int KV = KV_MAX + BK;    // vector slots: a stage may read up to 31 past K (zeros there)
 constexpr int STAGE = 128 * BK;    // floats per operand per stage
 constexpr float NEG_BIG = -3.0e38f;
 
@@ -59,6 +74,28 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_base) {
                : "memory");
 }
 __device__ __forceinline__ void glds_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+// two LDS floats 128 floats (one k-major tile row) apart.  Inline asm: the compiler pairs the
+// k-major reads across the wrong axis and shuffles registers; completion is awaited explicitly
+// (lds_wait_all) before the values are used.
+__device__ __forceinline__ f32x2 ds_read2_rows(uint32_t addr) {
+  f32x2 r;
+  asm volatile("ds_read2_b32 %0, %1 offset1:128" : "=v"(r) : "v"(addr) : "memory");
+  return r;
+}
+// lgkmcnt(0) with the 16 register pairs of the k-major reads as operands, so that the compiler
+// cannot schedule any use of them before the wait (an asm output is "ready" at the asm otherwise)
+__device__ __forceinline__ void lds_wait_regs(f32x2 (&r)[2][4][2]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(r[0][0][0]), "+v"(r[0][0][1]), "+v"(r[0][1][0]), "+v"(r[0][1][1]), "+v"(r[0][2][0]),
+                 "+v"(r[0][2][1]), "+v"(r[0][3][0]), "+v"(r[0][3][1]), "+v"(r[1][0][0]), "+v"(r[1][0][1]),
+                 "+v"(r[1][1][0]), "+v"(r[1][1][1]), "+v"(r[1][2][0]), "+v"(r[1][2][1]), "+v"(r[1][3][0]),
+                 "+v"(r[1][3][1])
+               :
+               : "memory");
+}
 // workgroup barrier publishing LDS writes only (leaves LDS-DMA / global traffic in flight)
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -95,7 +132,40 @@ __device__ __forceinline__ void quad_transpose(float& a0, float& a1, float& a2, 
   }
 }
 
-template <int PRO, int BKC, int BIAS, int STATS, int RES>
+// 3-way bf16 split of 8 fp32 values (two float4 = 8 consecutive k) into MFMA fragments:
+// x = h + m + l to 2^-25 |x| (RNE at each step; x - h and r - m are exact in fp32).  Works on
+// packed pairs: v_cvt_pk_bf16_f32, shift/and unpack, v_pk_add_f32 — 4.5 VALU ops per value.
+__device__ __forceinline__ unsigned cvt_pk_bf16(f32x2 x) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+}
+__device__ __forceinline__ f32x2 unpack_bf16(unsigned p) {
+  f32x2 r;
+  r.x = __uint_as_float(p << 16);
+  r.y = __uint_as_float(p & 0xffff0000u);
+  return r;
+}
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
+  u32x4 H, Mm, L;
+  const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned hp = cvt_pk_bf16(x[i]);
+    const f32x2 r = x[i] - unpack_bf16(hp);
+    const unsigned mp = cvt_pk_bf16(r);
+    H[i] = hp;
+    Mm[i] = mp;
+    L[i] = cvt_pk_bf16(r - unpack_bf16(mp));
+  }
+  h = __builtin_bit_cast(bf16x8, H);
+  m = __builtin_bit_cast(bf16x8, Mm);
+  l = __builtin_bit_cast(bf16x8, L);
+}
+
+// exp(x) for the softmax epilogues on v_exp_f32 (relative error ~1e-6 for |x| <= 20, against the
+// ~1e-4 tolerance of the scores; the argument is <= 0 here)
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+template <int MATH, int PRO, int BKC, int BIAS, int STATS, int RES>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   // Persistent: workgroup w owns tiles w, w + grid, ...
   const GemmArgs& g = ka.g;
@@ -141,44 +211,67 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     }
   };
 
+  // stage issue: stages run tile-major (tile i of this workgroup, k step ks), tracked incrementally
+  int is_i = 0, is_ks = 0, is_b = 0, is_m0 = 0, is_n0 = 0;
+  // per-tile int32 element offsets of this lane's LDS-DMA sources (k0 = 0); x-major tiles put
+  // logical 16-byte chunk lc of row (lane >> 3) into LDS slot (lane & 7)
+  const int lc = (lane & 7) ^ ((lane >> 3) & 7);
+  int a_off[4], b_off[4];
+  const float* Ab = g.A;
+  const float* Bb = g.B;
   auto issue = [&](int gs) {
-    const int i = gs / nk, ks = gs - (gs / nk) * nk;
-    int b, tm, tn;
-    tile_of(i, b, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN, k0 = ks * BK;
-    if ((PRO == PRO_A_K || PRO == PRO_B_K) && ks == 0) issue_vec(i & 1, b);
+    if (is_ks == 0) {
+      int tm, tn;
+      tile_of(is_i, is_b, tm, tn);
+      is_m0 = tm * BM;
+      is_n0 = tn * BN;
+      if (PRO == PRO_A_K || PRO == PRO_B_K) issue_vec(is_i & 1, is_b);
+      Ab = g.A + (int64_t)is_b * g.sAb;
+      Bb = g.B + (int64_t)is_b * g.sBb;
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int r = 32 * wid + 8 * ii + (lane >> 3);
+        a_off[ii] = min(is_m0 + r, M - 1) * (int)g.lda + 4 * lc;
+        if (!BKC)
+          b_off[ii] = (8 * wid + 2 * ii + (lane >> 5)) * (int)g.ldb + min(is_n0 + 4 * (lane & 31), N4 - 4);
+        else
+          b_off[ii] = min(is_n0 + r, N - 1) * (int)g.ldb + 4 * lc;
+      }
+    }
+    const int b = is_b, n0 = is_n0, k0 = is_ks * BK;
+    if (++is_ks == nk) {
+      is_ks = 0;
+      ++is_i;
+    }
     if (PRO == PRO_B_SMX && wid == 0 && lane < 32) {
       const int n = min(n0 + 4 * lane, N4 - 4);
       glds16(g.psc + (int64_t)b * g.sPb + (int64_t)(k0 / 128) * g.pld + n, fac + (gs & 1) * BN);
     }
     float* As = Asm + (gs & 1) * STAGE;
     float* Bs = Bsm + (gs & 1) * STAGE;
-    const float* A = g.A + (int64_t)b * g.sAb;
-    const float* B = g.B + (int64_t)b * g.sBb;
+    if (k0 + BK <= K) {   // full stage: no clamping
 #pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-      const int r = 32 * wid + 8 * ii + (lane >> 3);          // tile row
-      const int c = (lane & 7) ^ (r & 7);                      // logical chunk held by this lane
-      const int gm = min(m0 + r, M - 1);
-      const int gk = min(k0 + 4 * c, K4 - 4);
-      glds16(A + (int64_t)gm * g.lda + gk, As + (32 * wid + 8 * ii) * BK);
-    }
-    if (!BKC) {
+      for (int ii = 0; ii < 4; ++ii) glds16(Ab + a_off[ii] + k0, As + (32 * wid + 8 * ii) * BK);
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
-        const int kr = 8 * wid + 2 * ii + (lane >> 5);
-        const int gk = min(k0 + kr, K - 1);
-        const int gn = min(n0 + 4 * (lane & 31), N4 - 4);
-        glds16(B + (int64_t)gk * g.ldb + gn, Bs + (8 * wid + 2 * ii) * BN);
+        if (!BKC)
+          glds16(Bb + (b_off[ii] + (int64_t)k0 * g.ldb), Bs + (8 * wid + 2 * ii) * BN);
+        else
+          glds16(Bb + b_off[ii] + k0, Bs + (32 * wid + 8 * ii) * BK);
       }
-    } else {
+    } else {              // K tail: clamp every source into the padded rows
+      const int gk = min(k0 + 4 * lc, K4 - 4) - 4 * lc;
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) glds16(Ab + a_off[ii] + gk, As + (32 * wid + 8 * ii) * BK);
 #pragma unroll
       for (int ii = 0; ii < 4; ++ii) {
-        const int r = 32 * wid + 8 * ii + (lane >> 3);
-        const int c = (lane & 7) ^ (r & 7);
-        const int gn = min(n0 + r, N - 1);
-        const int gk = min(k0 + 4 * c, K4 - 4);
-        glds16(B + (int64_t)gn * g.ldb + gk, Bs + (32 * wid + 8 * ii) * BK);
+        if (!BKC) {
+          const int kr = 8 * wid + 2 * ii + (lane >> 5);
+          const int64_t o = b_off[ii] + (int64_t)(min(k0 + kr, K - 1) - kr) * g.ldb;
+          glds16(Bb + o, Bs + (8 * wid + 2 * ii) * BN);
+        } else {
+          glds16(Bb + b_off[ii] + gk, Bs + (32 * wid + 8 * ii) * BK);
+        }
       }
     }
   };
@@ -187,12 +280,20 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   const int t4 = lane & 3, p8 = l32 >> 2;   // epilogue: lane = (kh, p8, t4)
   const bool h1 = (t4 & 1) != 0, h2 = (t4 & 2) != 0;
 
+  if (PRO == PRO_A_K || PRO == PRO_B_K) {   // zero scale/shift past K (see the K-tail note below)
+    for (int e = tid; e < 4 * KV; e += 256) vec[e] = 0.f;
+    lds_barrier();
+  }
   issue(0);
   glds_wait_all();
   __syncthreads();
   if (S > 1) issue(1);
+  int i = 0, ks = -1;   // tile / k step of the stage being multiplied
   for (int gs = 0; gs < S; ++gs) {
-    const int i = gs / nk, ks = gs - (gs / nk) * nk;
+    if (++ks == nk) {
+      ks = 0;
+      ++i;
+    }
     const int par = i & 1;
     const float* vsc = vec + (2 * par) * KV;
     const float* vsh = vec + (2 * par + 1) * KV;
@@ -207,12 +308,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     const float* As = Asm + (gs & 1) * STAGE;
     const float* Bs = Bsm + (gs & 1) * STAGE;
     const int k0 = ks * BK;
-    const bool tail = k0 + BK > K;
+    // K tail: rows k >= K of the stage must contribute nothing.  Prologue transforms see zero
+    // scale/shift there (the vector area is zero-filled past K); untransformed / softmax-scaled
+    // B operands are zeroed in LDS.
+    if ((PRO == PRO_NONE || PRO == PRO_B_SMX) && k0 + BK > K) {
+      float* Bz = Bsm + (gs & 1) * STAGE;
+      const int kv = K - k0;   // valid k of this stage (1..31)
+      for (int e = tid; e < STAGE; e += 256) {
+        const int k = BKC ? 4 * ((e & 31) >> 2 ^ ((e >> 5) & 7)) + (e & 3) : e / BN;
+        if (k >= kv) Bz[e] = 0.f;
+      }
+      lds_barrier();
+    }
     // all operands of the stage -> registers (one LDS wait), transforms, then 64 MFMAs back to back
     float4 a4[2][4], b4[2][4];
+    f32x2 bkr[2][4][2];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      const int q = 2 * s4 + kh;   // 16-byte chunk (4 consecutive k) of this lane half
+      const int q = chunk_of<MATH>(s4, kh);   // 16-byte chunk (4 consecutive k) of this lane half
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         const int x = wm * 64 + ii * 32 + l32;
@@ -224,10 +337,20 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
         if (BKC) {
           b4[j][s4] = *reinterpret_cast<const float4*>(Bs + x * BK + 4 * (q ^ (x & 7)));
         } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) f4(b4[j][s4], e) = Bs[(4 * q + e) * BN + x];
+          // rows 4q..4q+3 of the k-major tile: two ds_read2_b32 (row pairs 128 floats apart)
+          const uint32_t la = lds_addr(Bs + (4 * q) * BN + x);
+          bkr[j][s4][0] = ds_read2_rows(la);
+          bkr[j][s4][1] = ds_read2_rows(la + 2 * BN * 4);
         }
       }
+    }
+    if (!BKC) {
+      lds_wait_regs(bkr);   // the asm reads' registers are tied to the wait: no use can move above it
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          b4[j][s4] = make_float4(bkr[j][s4][0].x, bkr[j][s4][0].y, bkr[j][s4][1].x, bkr[j][s4][1].y);
     }
     float fm[2] = {1.f, 1.f};
     if (PRO == PRO_B_SMX) {
@@ -236,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     }
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      const int kb = k0 + 4 * (2 * s4 + kh);
+      const int kb = k0 + 4 * chunk_of<MATH>(s4, kh);
       if (PRO == PRO_A_K || PRO == PRO_B_K) {
         const float4 sc4 = *reinterpret_cast<const float4*>(vsc + kb);
         const float4 sh4 = *reinterpret_cast<const float4*>(vsh + kb);
@@ -258,27 +381,41 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) f4(b4[j][s4], e) *= fm[j];
       }
-      if (tail) {
+    }
+    if (MATH == MATH_F32) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          if (kb + e >= K) {
 #pragma unroll
-            for (int ii = 0; ii < 2; ++ii) f4(a4[ii][s4], e) = 0.f;
+          for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) f4(b4[j][s4], e) = 0.f;
-          }
-      }
-    }
+            for (int j = 0; j < 2; ++j)
+              acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4(a4[ii][s4], e), f4(b4[j][s4], e), acc[ii][j], 0,
+                                                                0, 0);
+    } else {
+      // two k16 steps; lane half h holds k = 16s + 8h + (0..7) = chunks (2s, 2s+1) of its registers
 #pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+        for (int ii = 0; ii < 2; ++ii) split8(a4[ii][2 * st], a4[ii][2 * st + 1], ah[ii], am[ii], al[ii]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) split8(b4[j][2 * st], b4[j][2 * st + 1], bh[j], bm[j], bl[j]);
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4(a4[ii][s4], e), f4(b4[j][s4], e), acc[ii][j], 0, 0,
-                                                              0);
+          for (int j = 0; j < 2; ++j) {
+            // small terms first
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ii], bh[j], acc[ii][j], 0, 0, 0);
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bl[j], acc[ii][j], 0, 0, 0);
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ii], bm[j], acc[ii][j], 0, 0, 0);
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ii], bh[j], acc[ii][j], 0, 0, 0);
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bm[j], acc[ii][j], 0, 0, 0);
+            acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bh[j], acc[ii][j], 0, 0, 0);
+          }
+      }
+    }
     glds_wait_all();                                  // stage gs+1 (issued one stage ago) landed
     __syncthreads();                                  // ... for every wave; stage gs fully read
     if (gs + 2 < S) issue(gs + 2);
@@ -391,7 +528,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? expf(f4(v[ii][j][q], u) - mx) : 0.f;
+              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? fast_exp(f4(v[ii][j][q], u) - mx) : 0.f;
         }
     } else if (STATS == ST_COLSMX) {
 #pragma unroll
@@ -429,7 +566,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
           for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? expf(f4(v[ii][j][q], u) - mx[u]) : 0.f;
+              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? fast_exp(f4(v[ii][j][q], u) - mx[u]) : 0.f;
       }
     }
 
@@ -559,7 +696,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
 static void launch_t(const KArgs& ka, long long tiles, hipStream_t s) {
   const unsigned wgs = (unsigned)(tiles < ka.persist ? tiles : ka.persist);
-  hipLaunchKernelGGL((gemm_kernel<PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
+  if (ka.g.math == MATH_F32)
+    hipLaunchKernelGGL((gemm_kernel<MATH_F32, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
+  else
+    hipLaunchKernelGGL((gemm_kernel<MATH_BF16X3, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
 }
 
 static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -572,6 +712,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.stats_mode != ST_NONE && !g.stats) return MVR_EINVAL;
   if (g.bias_mode != BIAS_NONE && !g.bias) return MVR_EINVAL;
   if (g.has_res && !g.R) return MVR_EINVAL;
+  if (g.math != MATH_F32 && g.math != MATH_BF16X3) return MVR_EINVAL;
   // layout contract (gemm.hpp)
   const int64_t K4 = round4(g.K), N4 = round4(g.N);
   bool ok = al16(g.A) && al16(g.B) && al16(g.C) && g.lda % 4 == 0 && g.ldb % 4 == 0 && g.ldc % 4 == 0 &&
@@ -579,7 +720,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
             g.ldb >= (g.bkc ? K4 : N4);
   if (g.has_res) ok = ok && al16(g.R) && g.sRb % 4 == 0;
   if (g.pro == PRO_A_K || g.pro == PRO_B_K)
-    ok = ok && al16(g.psc) && al16(g.psh) && g.sPb % 4 == 0 && g.K % 4 == 0 && g.K <= KV;
+    ok = ok && al16(g.psc) && al16(g.psh) && g.sPb % 4 == 0 && g.K % 4 == 0 && g.K <= KV_MAX;
   if (g.pro == PRO_B_SMX) ok = ok && al16(g.psc) && g.sPb % 4 == 0 && g.pld % 4 == 0 && g.pld >= N4;
   if (!ok) return MVR_EINVAL;
   KArgs ka;
@@ -622,8 +763,9 @@ extern "C" int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int6
                             int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc,
                             const float* R, int64_t sRb, const float* bias, int bias_mode, const float* psc,
                             const float* psh, int64_t sPb, int64_t pld, int pro, float* stats, int64_t st_ld,
-                            int st_off, int stats_mode, hipStream_t stream) {
+                            int st_off, int stats_mode, int math, hipStream_t stream) {
   mvr::GemmArgs g{};
+  g.math = math;
   g.M = M; g.N = N; g.K = K; g.batch = batch;
   g.A = A; g.sAb = sAb; g.lda = lda;
   g.B = B; g.sBb = sBb; g.ldb = ldb; g.bkc = b_kcontig;
@@ -633,4 +775,10 @@ extern "C" int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int6
   g.psc = psc; g.psh = psh; g.sPb = sPb; g.pld = pld; g.pro = pro;
   g.stats = reinterpret_cast<float2*>(stats); g.st_ld = st_ld; g.st_off = st_off; g.stats_mode = stats_mode;
   return mvr::launch_gemm(g, stream);
+}
+
+extern "C" int mvr_set_gemm_math(int math) {
+  if (math != mvr::MATH_F32 && math != mvr::MATH_BF16X3) return MVR_EINVAL;
+  mvr::g_default_math = math;
+  return MVR_OK;
 }

@@ -28,6 +28,13 @@ enum Stats : int {
                   //                                                           -> train-mode BN over m
 };
 
+// Arithmetic of the MFMA main loop.  MATH_F32: v_mfma_f32_32x32x2_f32 (an exact fp32 fma chain).
+// MATH_BF16X3: each fp32 operand split into three bf16 terms (x = h + m + l to 2^-25 |x|) and the
+// six products hh, hm, mh, mm, hl, lh accumulated in fp32 by v_mfma_f32_32x32x16_bf16 — fp32-level
+// accuracy (the dropped ml, lm, ll terms are <= 2^-23 relative) at 6/16 of the fp32 MFMA cycles.
+enum Math : int { MATH_F32 = 0, MATH_BF16X3 = 1 };
+extern int g_default_math;   // used by the OANet orchestrator (mvr_set_gemm_math)
+
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 32;
 
 struct GemmArgs {
@@ -42,6 +49,7 @@ struct GemmArgs {
   float2* stats; int64_t st_ld; int st_off;            // partial statistics (see Stats)
   int pro, bias_mode, stats_mode, has_res;
   int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
+  int math;                                            // Math (MATH_F32 = 0 by default)
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the

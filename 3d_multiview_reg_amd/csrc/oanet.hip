@@ -266,6 +266,7 @@ struct Ctx {
   void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
             const float* w_padded = nullptr) {
     GemmArgs g{};
+    g.math = g_default_math;
     g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
     g.A = w_padded ? w_padded : cv.weight; g.sAb = 0; g.lda = w_padded ? round4(in.C) : in.C;
     g.B = in.p; g.sBb = in.ps; g.ldb = in.ld; g.bkc = 0;
@@ -305,6 +306,7 @@ struct Ctx {
     // out2(c,k') = sum_k relu(bn2_k(o1(c,k))) W2[k'][k] + b2[k'] + o1(c,k')   (conv on the transpose)
     Act o2{pl.O2, (int64_t)C * Kp, Kp, C, Kc, pl.stO, C, 0};
     GemmArgs g{};
+    g.math = g_default_math;
     g.M = C; g.N = Kc; g.K = Kc; g.batch = pl.P;
     g.A = pl.O1; g.sAb = (int64_t)C * Kp; g.lda = Kp;
     g.B = f.conv2.weight; g.sBb = 0; g.ldb = Kc; g.bkc = 1;
@@ -379,6 +381,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   Act xd{pl.XD, (int64_t)C * Kp, Kp, C, Kc, pl.stD, C, 0};
   {
     GemmArgs g{};
+    g.math = g_default_math;
     g.M = C; g.N = Kc; g.K = N; g.batch = P;
     g.A = pl.X11; g.sAb = 2 * CN; g.lda = Np;
     g.B = pl.E; g.sBb = (int64_t)Kc * Np; g.ldb = Np; g.bkc = 1;
@@ -399,6 +402,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   cx.smx_factors(MK, N, Np);
   {
     GemmArgs g{};
+    g.math = g_default_math;
     g.M = C; g.N = N; g.K = Kc; g.batch = P;
     g.A = pl.XD; g.sAb = (int64_t)C * Kp; g.lda = Kp;
     g.B = pl.E; g.sBb = (int64_t)Kc * Np; g.ldb = Np; g.bkc = 0;

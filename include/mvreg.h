@@ -59,13 +59,17 @@ int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_pstride, in
  * 4 column sum/sumsq (float2 partials, see csrc/gemm.hpp).
  * Layout: 16-byte aligned pointers, all strides multiples of 4 floats, rows padded to
  * round_up(K|N, 4) floats holding finite values (MVR_EINVAL otherwise).
+ * math: 0 exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 three-term bf16 split (x = h+m+l,
+ * products hh+hm+mh+mm+hl+lh on v_mfma_f32_32x32x16_bf16, fp32 accumulation: fp32-level accuracy).
  * Replaces the nn.Conv2d(k=1) / torch.matmul calls of lib/filtering/oanet.py.
  * ---------------------------------------------------------------------- */
 int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
                  int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
                  int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
-                 int64_t pld, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode,
+                 int64_t pld, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, int math,
                  mvr_stream_t stream);
+/* GEMM arithmetic used by mvr_oan_block_forward (process-wide; default 1 = bf16 split). */
+int mvr_set_gemm_math(int math);
 
 /* ------------------------------------------------------------------------
  * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters

@@ -18,7 +18,7 @@ def _pad(a, width):
     return out
 
 
-def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shared_a=False):
+def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shared_a=False, math=1):
     import torch
     from lib import _native as NV
     r = np.random.RandomState(seed)
@@ -77,7 +77,7 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shar
     rc = L.mvr_gemm_f32(M, N, K, batch, NV.ptr(tA), 0 if shared_a else M * K4, K4, NV.ptr(tB),
                         K * N4 if not bkc else N * K4, K4 if bkc else N4, bkc,
                         NV.ptr(C), M * N4, N4, NV.ptr(tR), M * N4, NV.ptr(tb), bias_mode, NV.ptr(pv[0]),
-                        NV.ptr(pv[1]), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats_mode, NV.stream())
+                        NV.ptr(pv[1]), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats_mode, math, NV.stream())
     assert rc == 0
     torch.cuda.synchronize()
     Cg = C.cpu().numpy().astype(np.float64)
@@ -124,23 +124,46 @@ COMBOS = [(0, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 0), (2, 0, 1, 0, 0), (2
           (0, 1, 0, 0, 0)]
 
 
+@pytest.mark.parametrize("math", [0, 1])       # exact fp32 MFMA / 3-term bf16 split
 @pytest.mark.parametrize("combo", COMBOS)
 @pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 36, 3), (500, 300, 64, 1), (1, 40, 8, 2),
                                    (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2)])
-def test_gemm_modes(gpu, combo, shape):
+def test_gemm_modes(gpu, combo, shape, math):
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo
     if pro in (1, 2) and K % 4:
         pytest.skip("per-k prologue needs K % 4 == 0")
-    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1))
+    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1),
+         math=math)
 
 
-def test_gemm_ragged_k(gpu):
+@pytest.mark.parametrize("math", [0, 1])
+def test_gemm_ragged_k(gpu, math):
     # K = 6 (conv1 of reg_init, weight rows zero-padded to 8) and odd K for plain GEMMs
-    _run(gpu, 128, 5000, 6, 2, 0, 0, 1, 1, 0, shared_a=True)
-    _run(gpu, 128, 999, 7, 2, 0, 0, 1, 1, 0, shared_a=True)
-    _run(gpu, 70, 333, 45, 2, 0, 1, 0, 0, 0)
-    _run(gpu, 70, 333, 45, 2, 3, 1, 0, 1, 0)
+    _run(gpu, 128, 5000, 6, 2, 0, 0, 1, 1, 0, shared_a=True, math=math)
+    _run(gpu, 128, 999, 7, 2, 0, 0, 1, 1, 0, shared_a=True, math=math)
+    _run(gpu, 70, 333, 45, 2, 0, 1, 0, 0, 0, math=math)
+    _run(gpu, 70, 333, 45, 2, 3, 1, 0, 1, 0, math=math)
+
+
+def test_gemm_bf16x3_accuracy_vs_fp32(gpu):
+    """The split path's error against float64 stays at the exact-fp32 path's level."""
+    import torch
+    from lib import _native as NV
+    r = np.random.RandomState(3)
+    M, N, K, b = 128, 2048, 512, 2
+    A = r.standard_normal((b, M, K)).astype(np.float32)
+    B = r.standard_normal((b, K, N)).astype(np.float32)
+    ref = A.astype(np.float64) @ B.astype(np.float64)
+    errs = []
+    for math in (0, 1):
+        C = torch.empty(b, M, N, device=gpu)
+        tA, tB = torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu)
+        L = NV.lib()
+        assert L.mvr_gemm_f32(M, N, K, b, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, N, 0, NV.ptr(C), M * N, N, None,
+                              0, None, 0, None, None, 0, 0, 0, None, 0, 0, 0, math, NV.stream()) == 0
+        errs.append(np.abs(C.cpu().numpy() - ref).max())
+    assert errs[1] < 3 * errs[0] + 1e-6, errs
 
 
 def test_gemm_rejects_bad_layout(gpu):
@@ -151,11 +174,11 @@ def test_gemm_rejects_bad_layout(gpu):
     B = torch.zeros(8, 16, device=gpu)
     C = torch.zeros(16, 16, device=gpu)
     ok = L.mvr_gemm_f32(16, 16, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C), 0, 16, None, 0, None, 0,
-                        None, None, 0, 0, 0, None, 0, 0, 0, NV.stream())
+                        None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.stream())
     assert ok == 0
     # lda not a multiple of 4 / row shorter than round_up(K, 4)
     assert L.mvr_gemm_f32(16, 16, 6, 1, NV.ptr(A), 0, 6, NV.ptr(B), 0, 16, 0, NV.ptr(C), 0, 16, None, 0, None, 0,
-                          None, None, 0, 0, 0, None, 0, 0, 0, NV.stream()) == -1
+                          None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.stream()) == -1
     # misaligned C
     assert L.mvr_gemm_f32(15, 12, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C[0, 1:]), 0, 16, None, 0,
-                          None, 0, None, None, 0, 0, 0, None, 0, 0, 0, NV.stream()) == -1
+                          None, 0, None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.stream()) == -1

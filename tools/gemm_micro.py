@@ -21,7 +21,7 @@ CASES = {
 }
 
 
-def run(name, iters):
+def run(name, iters, math):
     M, Nn, Kk, pro, bkc, bias, stats, res = CASES[name]
     d = torch.device("cuda")
     A = torch.randn(M, Kk, device=d) * 0.1 if name.startswith(("conv", "embed")) else torch.randn(P, M, Kk, device=d)
@@ -47,7 +47,7 @@ def run(name, iters):
     def go():
         rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk, Kk if bkc else Nn, bkc,
                             NV.ptr(Cout), M * Nn, Nn, NV.ptr(R), M * Nn, NV.ptr(bvec), bias, NV.ptr(sc),
-                            NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, NV.stream())
+                            NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, math, NV.stream())
         assert rc == 0
     for _ in range(2):
         go()
@@ -61,15 +61,17 @@ def run(name, iters):
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * M * Nn * Kk * P
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
-    print("%-16s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
+    print("%-16s m%d %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--math", default="01")
     a = ap.parse_args()
     for n in CASES:
         if a.only and n != a.only:
             continue
-        run(n, a.iters)
+        for m in a.math:
+            run(n, a.iters, int(m))
