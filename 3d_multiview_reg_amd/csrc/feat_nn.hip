@@ -5,27 +5,33 @@
 // assembly of lib/utils.py:915.  The reference materialises the [P,N,M]
 // distance and softmax matrices (100 MB per pair); here they never leave
 // registers:
-//   * S^T = Ft . Fs^T on v_mfma_f32_32x32x2_f32 (the QUERY index is the lane
-//     column, so each lane owns one query's running softmax state),
-//   * logits (2 fs.ft - |ft|^2) / tau^2 (|fs|^2 is constant per query and
-//     cancels in the softmax / argmax),
-//   * flash-style online softmax in base 2 over 32-target chunks, and the
-//     3-wide weighted coordinate sum accumulated in fp32 registers,
+//   * S^T = Ft . Fs^T on v_mfma_f32_32x32x16_bf16 with both operands split into three bf16
+//     terms (fp32-level accuracy, see gemm.hpp MATH_BF16X3); the QUERY index is the lane column,
+//     so each lane owns one query's running softmax state;
+//   * logits (2 fs.ft - |ft|^2) / tau^2 (|fs|^2 is constant per query and cancels in the
+//     softmax / argmax);
+//   * flash-style online softmax in base 2 over 32-target chunks, the 3-wide weighted
+//     coordinate sum accumulated in packed fp32 (v_pk_fma_f32) registers;
 //   * argmax tracking for the straight-through ('st') and 'hard' modes.
-// Targets stream through double-buffered LDS in 128-row stages shared by the
-// 4 waves (128 queries) of a workgroup.
+// Targets stream through double-buffered LDS in 128-row stages shared by the 4 waves (128
+// queries) of a workgroup: the next stage is loaded into registers during the current one, then
+// split into bf16 planes once per workgroup (not per wave) on its way into LDS.
 //
-// FLOPs per pair ~ 2*N*M*C (MFMA) + N*M*(exp + 5 FMA); HBM: features/coords of
-// the two fragments (L2/MALL-resident across the pairs that share them).
+// FLOPs per pair ~ 2*N*M*C (MFMA) + N*M*(exp + ~6 VALU); HBM: features/coords of the two
+// fragments (L2/MALL-resident across the pairs that share them).
 #include "common.hpp"
 #include "prof.hpp"
 
 namespace mvr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NN_STAGE = 128;      // targets per LDS stage
-constexpr int NN_FLD = 32 + 4;     // padded LDS row (floats) for 32-dim features
+constexpr int NN_ROW = 40;         // bf16 per LDS plane row (32 dims + 16 B pad: conflict-free b128 reads)
 constexpr float NN_NEG = -3.0e38f;
 
 struct NNArgs {
@@ -41,9 +47,34 @@ struct NNArgs {
   int32_t* idx;                      // optional argmax index [P][Nq]
 };
 
-__global__ __launch_bounds__(256) void feat_nn_kernel(NNArgs a) {
-  __shared__ float Fs[2][NN_STAGE][NN_FLD];
-  __shared__ float4 Xs[2][NN_STAGE];   // xyz + |f|^2
+__device__ __forceinline__ unsigned nn_cvt_pk(f32x2 x) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+}
+__device__ __forceinline__ f32x2 nn_unpack(unsigned p) {
+  f32x2 r;
+  r.x = __uint_as_float(p << 16);
+  r.y = __uint_as_float(p & 0xffff0000u);
+  return r;
+}
+// 8 fp32 -> three bf16x8 terms (x = h + m + l to 2^-25 |x|), as u32x4 (packed pairs)
+__device__ __forceinline__ void nn_split8(const float4& a, const float4& b, u32x4& H, u32x4& Mm, u32x4& L) {
+  const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned hp = nn_cvt_pk(x[i]);
+    const f32x2 r = x[i] - nn_unpack(hp);
+    const unsigned mp = nn_cvt_pk(r);
+    H[i] = hp;
+    Mm[i] = mp;
+    L[i] = nn_cvt_pk(r - nn_unpack(mp));
+  }
+}
+__device__ __forceinline__ float nn_max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Fp[2][3][NN_STAGE][NN_ROW];   // bf16 planes h, m, l
+  __shared__ __attribute__((aligned(16))) float Xs[2][4][NN_STAGE];                    // x, y, z, |ft|^2 k2
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l32 = lane & 31, kh = lane >> 5;
   const int p = blockIdx.y;
@@ -53,118 +84,158 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(NNArgs a) {
   const float* Xt = a.Xt + tgt * a.xt_fs;
   const int j = blockIdx.x * 128 + wid * 32 + l32;  // this lane's query
   const bool jok = j < a.Nq;
+  const int Mt = a.Mt;
 
-  // query operand: fs[j][16*kh + e], e = 0..15 (k-order permuted identically for A and B)
-  float q[16];
+  // query = B operand of k16 step s: lane half kh holds dims 16s + 8kh + (0..7)
+  bf16x8 qh[2], qm[2], ql[2];
   {
-    const float4* qp = reinterpret_cast<const float4*>(Fq + (int64_t)(jok ? j : 0) * 32 + 16 * kh);
+    const float4* qp = reinterpret_cast<const float4*>(Fq + (int64_t)(jok ? j : 0) * 32);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const float4 t = qp[v];
-      q[4 * v] = t.x; q[4 * v + 1] = t.y; q[4 * v + 2] = t.z; q[4 * v + 3] = t.w;
+    for (int s = 0; s < 2; ++s) {
+      u32x4 H, Mm, L;
+      nn_split8(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], H, Mm, L);
+      qh[s] = __builtin_bit_cast(bf16x8, H);
+      qm[s] = __builtin_bit_cast(bf16x8, Mm);
+      ql[s] = __builtin_bit_cast(bf16x8, L);
     }
   }
 
-  auto stage_load = [&](int buf, int t0) {
-    // 128 targets x 32 floats = 1024 float4, 4 per thread
+  // stage staging: thread -> target row (tid >> 1), dims 16 (tid & 1) .. +15; coords by tid < 128
+  const int srow = tid >> 1, shalf = tid & 1;
+  float4 fr[4];
+  float xr0 = 0.f, xr1 = 0.f, xr2 = 0.f;
+  auto load_regs = [&](int t0) {
+    const int gi = t0 + srow;
+    const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + 16 * shalf);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = tid + 256 * r;
-      const int row = e >> 3, c4 = e & 7;
-      const int gi = t0 + row;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gi < a.Mt) v = reinterpret_cast<const float4*>(Ft + (int64_t)gi * 32)[c4];
-      *reinterpret_cast<float4*>(&Fs[buf][row][4 * c4]) = v;
+    for (int v = 0; v < 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < NN_STAGE) {
+      const int gc = t0 + tid;
+      if (gc < Mt) {
+        const float* xp = Xt + (int64_t)gc * 3;
+        xr0 = xp[0]; xr1 = xp[1]; xr2 = xp[2];
+      }
     }
   };
-  auto stage_finish = [&](int buf, int t0) {
-    if (tid < NN_STAGE) {
-      const int gi = t0 + tid;
-      float n2 = 0.f;
+  auto store_lds = [&](int buf, int t0) {
 #pragma unroll
-      for (int c = 0; c < 32; ++c) n2 = fmaf(Fs[buf][tid][c], Fs[buf][tid][c], n2);
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gi < a.Mt) {
-        const float* xp = Xt + (int64_t)gi * 3;
-        x = make_float4(xp[0], xp[1], xp[2], n2);
-      }
-      Xs[buf][tid] = x;
+    for (int g = 0; g < 2; ++g) {   // dims 16 shalf + 8g .. +7
+      u32x4 H, Mm, L;
+      nn_split8(fr[2 * g], fr[2 * g + 1], H, Mm, L);
+      const int c = 16 * shalf + 8 * g;
+      *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = H;
+      *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = Mm;
+      *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
+    }
+    float n2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
+    n2 += __shfl_xor(n2, 1, 64);
+    // invalid targets: +inf -> logit -inf -> weight 0, never the argmax
+    if (shalf == 0) Xs[buf][3][srow] = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
+    if (tid < NN_STAGE) {
+      Xs[buf][0][tid] = xr0;
+      Xs[buf][1][tid] = xr1;
+      Xs[buf][2][tid] = xr2;
     }
   };
 
-  float run_m = NN_NEG, run_s = 0.f, ax = 0.f, ay = 0.f, az = 0.f;
+  float run_m = NN_NEG;
+  f32x2 s2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f}, az2 = {0.f, 0.f};
   float best = NN_NEG;
   int besti = 0x7fffffff;
+  const float kk2 = 2.f * a.k2;
 
-  const int nst = (a.Mt + NN_STAGE - 1) / NN_STAGE;
-  stage_load(0, 0);
-  __syncthreads();
-  stage_finish(0, 0);
+  const int nst = (Mt + NN_STAGE - 1) / NN_STAGE;
+  load_regs(0);
+  store_lds(0, 0);
   __syncthreads();
   int cur = 0;
   for (int st = 0; st < nst; ++st) {
     const int t0 = st * NN_STAGE;
-    if (st + 1 < nst) stage_load(cur ^ 1, t0 + NN_STAGE);
+    if (st + 1 < nst) load_regs(t0 + NN_STAGE);
 #pragma unroll 1
     for (int sub = 0; sub < NN_STAGE / 32; ++sub) {
       const int i0 = sub * 32;
-      if (t0 + i0 >= a.Mt) break;
+      if (t0 + i0 >= Mt) break;
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const float* frow = &Fs[cur][i0 + l32][16 * kh];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float4 f = *reinterpret_cast<const float4*>(frow + 4 * v);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.x, q[4 * v + 0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.y, q[4 * v + 1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.z, q[4 * v + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(f.w, q[4 * v + 3], acc, 0, 0, 0);
+      for (int s = 0; s < 2; ++s) {
+        const int c = 16 * s + 8 * kh;
+        const bf16x8 th = *reinterpret_cast<const bf16x8*>(&Fp[cur][0][i0 + l32][c]);
+        const bf16x8 tm = *reinterpret_cast<const bf16x8*>(&Fp[cur][1][i0 + l32][c]);
+        const bf16x8 tl = *reinterpret_cast<const bf16x8*>(&Fp[cur][2][i0 + l32][c]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh[s], acc, 0, 0, 0);
       }
-      // acc[r] = ft[i] . fs[j],  i = i0 + (r&3) + 8(r>>2) + 4kh
-      float z[16];
-      float cm = NN_NEG;
+      // acc[r] = ft[i] . fs[j],  i = i0 + 8 (r >> 2) + 4 kh + (r & 3)
+      f32x2 z[8];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int il = i0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        const float tn = Xs[cur][il].w;
-        float v = (2.f * acc[r] - tn) * a.k2;
-        if (t0 + il >= a.Mt) v = NN_NEG;
-        z[r] = v;
-        cm = fmaxf(cm, v);
-        if (a.mode == 1 && v > best) {  // strict '>' keeps the first maximum within a lane
-          best = v;
-          besti = t0 + il;
+      for (int g = 0; g < 4; ++g) {
+        const float4 T = *reinterpret_cast<const float4*>(&Xs[cur][3][i0 + 8 * g + 4 * kh]);
+        const f32x2 a0 = {acc[4 * g], acc[4 * g + 1]}, a1 = {acc[4 * g + 2], acc[4 * g + 3]};
+        const f32x2 t0v = {T.x, T.y}, t1v = {T.z, T.w};
+        z[2 * g] = a0 * kk2 - t0v;
+        z[2 * g + 1] = a1 * kk2 - t1v;
+      }
+      if (MODE == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {   // increasing r = increasing target index: '>' keeps the first
+          const float v = z[r >> 1][r & 1];
+          if (v > best) {
+            best = v;
+            besti = t0 + i0 + 8 * (r >> 2) + 4 * kh + (r & 3);
+          }
         }
-      }
-      if (a.mode == 0) {
-        cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-        const float nm = fmaxf(run_m, cm);
-        const float sc = __builtin_amdgcn_exp2f(run_m - nm);
-        run_s *= sc; ax *= sc; ay *= sc; az *= sc;
-        run_m = nm;
+      } else {
+        float cm = nn_max3(z[0].x, z[0].y, z[1].x);
+        cm = nn_max3(cm, z[1].y, z[2].x);
+        cm = nn_max3(cm, z[2].y, z[3].x);
+        cm = nn_max3(cm, z[3].y, z[4].x);
+        cm = nn_max3(cm, z[4].y, z[5].x);
+        cm = nn_max3(cm, z[5].y, z[6].x);
+        cm = nn_max3(cm, z[6].y, z[7].x);
+        cm = __builtin_fmaxf(cm, z[7].y);
+        cm = __builtin_fmaxf(cm, __shfl_xor(cm, 32, 64));
+        if (cm > run_m) {   // rescale (rare after the first chunks)
+          const float sc = __builtin_amdgcn_exp2f(run_m - cm);
+          s2 *= sc; ax2 *= sc; ay2 *= sc; az2 *= sc;
+          run_m = cm;
+        }
+        const f32x2 nm2 = {run_m, run_m};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int il = i0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-          const float4 xt = Xs[cur][il];
-          const float pr = __builtin_amdgcn_exp2f(z[r] - nm);
-          run_s += pr;
-          ax = fmaf(pr, xt.x, ax);
-          ay = fmaf(pr, xt.y, ay);
-          az = fmaf(pr, xt.z, az);
+        for (int g = 0; g < 4; ++g) {
+          const int il = i0 + 8 * g + 4 * kh;
+          const float4 X = *reinterpret_cast<const float4*>(&Xs[cur][0][il]);
+          const float4 Y = *reinterpret_cast<const float4*>(&Xs[cur][1][il]);
+          const float4 Z = *reinterpret_cast<const float4*>(&Xs[cur][2][il]);
+          const f32x2 d0 = z[2 * g] - nm2, d1 = z[2 * g + 1] - nm2;
+          const f32x2 p0 = {__builtin_amdgcn_exp2f(d0.x), __builtin_amdgcn_exp2f(d0.y)};
+          const f32x2 p1 = {__builtin_amdgcn_exp2f(d1.x), __builtin_amdgcn_exp2f(d1.y)};
+          s2 += p0 + p1;
+          ax2 = __builtin_elementwise_fma(p0, (f32x2){X.x, X.y}, ax2);
+          ax2 = __builtin_elementwise_fma(p1, (f32x2){X.z, X.w}, ax2);
+          ay2 = __builtin_elementwise_fma(p0, (f32x2){Y.x, Y.y}, ay2);
+          ay2 = __builtin_elementwise_fma(p1, (f32x2){Y.z, Y.w}, ay2);
+          az2 = __builtin_elementwise_fma(p0, (f32x2){Z.x, Z.y}, az2);
+          az2 = __builtin_elementwise_fma(p1, (f32x2){Z.z, Z.w}, az2);
         }
       }
     }
+    if (st + 1 < nst) store_lds(cur ^ 1, t0 + NN_STAGE);   // buffer last read in stage st-1
     __syncthreads();
-    if (st + 1 < nst) {
-      stage_finish(cur ^ 1, t0 + NN_STAGE);
-      __syncthreads();
-    }
     cur ^= 1;
   }
 
   float ox, oy, oz;
-  if (a.mode == 0) {
+  if (MODE == 0) {
+    const float run_s = s2.x + s2.y, ax = ax2.x + ax2.y, ay = ay2.x + ay2.y, az = az2.x + az2.y;
     const float s = run_s + __shfl_xor(run_s, 32, 64);
     ox = (ax + __shfl_xor(ax, 32, 64)) / s;
     oy = (ay + __shfl_xor(ay, 32, 64)) / s;
@@ -173,7 +244,7 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(NNArgs a) {
     const float ob = __shfl_xor(best, 32, 64);
     const int oi = __shfl_xor(besti, 32, 64);
     if (ob > best || (ob == best && oi < besti)) { best = ob; besti = oi; }
-    const float* xp = Xt + (int64_t)(besti < a.Mt ? besti : 0) * 3;
+    const float* xp = Xt + (int64_t)(besti < Mt ? besti : 0) * 3;
     ox = xp[0]; oy = xp[1]; oz = xp[2];
   }
   if (jok && kh == 0) {
@@ -184,7 +255,7 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(NNArgs a) {
       o += 3;
     }
     o[0] = ox; o[1] = oy; o[2] = oz;
-    if (a.idx && a.mode == 1) a.idx[(int64_t)p * a.Nq + j] = besti;
+    if (a.idx && MODE == 1) a.idx[(int64_t)p * a.Nq + j] = besti;
   }
 }
 
@@ -214,7 +285,10 @@ extern "C" int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft,
                 inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out};
   mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * (C + 3) * 4 + P * Nq * 24.0,
                       stream);
-  hipLaunchKernelGGL(mvr::feat_nn_kernel, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
+  if (mode == 0)
+    hipLaunchKernelGGL(mvr::feat_nn_kernel<0>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(mvr::feat_nn_kernel<1>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }

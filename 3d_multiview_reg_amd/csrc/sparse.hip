@@ -166,16 +166,30 @@ __global__ void scan_add_kernel(int32_t* out, int64_t n, const int32_t* __restri
   if (i < n) out[i] += bsum[blockIdx.x];
 }
 
-// compact selected rows (first occurrences) in source order
+// compact selected rows (first occurrences) in source order; per-batch counts aggregated per wave
+// (one atomic per distinct batch index in the wave — inputs are batch-major, so usually one)
 __global__ void compact_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ pos, int64_t n,
                                const int4* __restrict__ cc, int4* coords_out, int64_t* sel_out, int64_t* counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !flags[i]) return;
-  const int p = pos[i];
-  const int4 c = cc[i];
-  coords_out[p] = c;
-  if (sel_out) sel_out[p] = i;
-  if (counts) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[1 + c.x]), 1ULL);
+  const bool active = i < n && flags[i];
+  int bx = -1;
+  if (active) {
+    const int p = pos[i];
+    const int4 c = cc[i];
+    coords_out[p] = c;
+    if (sel_out) sel_out[p] = i;
+    bx = c.x;
+  }
+  if (!counts) return;
+  unsigned long long act = __ballot(active);
+  while (act) {
+    const int leader = __ffsll((long long)act) - 1;
+    const int bl = __shfl(bx, leader, 64);
+    const unsigned long long same = __ballot(active && bx == bl);
+    if ((int)(threadIdx.x & 63) == leader)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&counts[1 + bl]), (unsigned long long)__popcll(same));
+    act &= ~same;
+  }
 }
 
 __global__ void build_table_kernel(const int4* __restrict__ c, int64_t M, HashView h) {

@@ -258,7 +258,9 @@ def main():
             "frac": round(achieved / peak, 4), "traffic": (float(traffic) if traffic else None),
             "kernel": dom, "launches_per_step": nl / max(args.steps, 1),
             "avg_launch_ms": round(ms / max(nl, 1), 4), "share_of_step": round(ms / (dt * 1e3), 3),
-            "classes_ms_per_step": {k: round(v[0] / args.steps, 3) for k, v in prof.items() if v[1]}}
+            # per kernel class: [ms per step, algorithmic TFLOP/s, algorithmic GB/s]
+            "classes": {k: [round(v[0] / args.steps, 3), round(v[2] / (v[0] * 1e9), 1), round(v[3] / (v[0] * 1e6))]
+                        for k, v in prof.items() if v[1] and v[0] > 0}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
