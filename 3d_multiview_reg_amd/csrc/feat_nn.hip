@@ -31,7 +31,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int NN_STAGE = 128;      // targets per LDS stage
-constexpr int NN_ROW = 40;         // bf16 per LDS plane row (32 dims + 16 B pad: conflict-free b128 reads)
+constexpr int NN_ROW = 32;         // bf16 per LDS plane row; 16-byte chunk c of row r sits at slot
+                                   // c ^ ((r >> 2) & 3): conflict-free ds_read_b128 down 16 rows
 constexpr float NN_NEG = -3.0e38f;
 
 struct NNArgs {
@@ -72,7 +73,7 @@ __device__ __forceinline__ void nn_split8(const float4& a, const float4& b, u32x
 __device__ __forceinline__ float nn_max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
 template <int MODE>
-__global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
+__global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Fp[2][3][NN_STAGE][NN_ROW];   // bf16 planes h, m, l
   __shared__ __attribute__((aligned(16))) float Xs[2][4][NN_STAGE];                    // x, y, z, |ft|^2 k2
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -122,7 +123,7 @@ __global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
     for (int g = 0; g < 2; ++g) {   // dims 16 shalf + 8g .. +7
       u32x4 H, Mm, L;
       nn_split8(fr[2 * g], fr[2 * g + 1], H, Mm, L);
-      const int c = 16 * shalf + 8 * g;
+      const int c = 8 * ((2 * shalf + g) ^ ((srow >> 2) & 3));
       *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = H;
       *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = Mm;
       *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
@@ -154,19 +155,19 @@ __global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
   for (int st = 0; st < nst; ++st) {
     const int t0 = st * NN_STAGE;
     if (st + 1 < nst) load_regs(t0 + NN_STAGE);
-#pragma unroll 1
-    for (int sub = 0; sub < NN_STAGE / 32; ++sub) {
-      const int i0 = sub * 32;
-      if (t0 + i0 >= Mt) break;
+    // 4 chunks of 32 targets; the MFMAs of chunk c+1 are issued before the softmax of chunk c so
+    // the two streams interleave within the wave (invalid targets carry |ft|^2 k2 = +inf)
+    auto mfma_chunk = [&](int i0) {
       floatx16 acc;
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int row = i0 + l32;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int c = 16 * s + 8 * kh;
-        const bf16x8 th = *reinterpret_cast<const bf16x8*>(&Fp[cur][0][i0 + l32][c]);
-        const bf16x8 tm = *reinterpret_cast<const bf16x8*>(&Fp[cur][1][i0 + l32][c]);
-        const bf16x8 tl = *reinterpret_cast<const bf16x8*>(&Fp[cur][2][i0 + l32][c]);
+        const int c = 8 * ((2 * s + kh) ^ ((row >> 2) & 3));
+        const bf16x8 th = *reinterpret_cast<const bf16x8*>(&Fp[cur][0][row][c]);
+        const bf16x8 tm = *reinterpret_cast<const bf16x8*>(&Fp[cur][1][row][c]);
+        const bf16x8 tl = *reinterpret_cast<const bf16x8*>(&Fp[cur][2][row][c]);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tl, qh[s], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, ql[s], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tm, qm[s], acc, 0, 0, 0);
@@ -174,7 +175,10 @@ __global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qm[s], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(th, qh[s], acc, 0, 0, 0);
       }
-      // acc[r] = ft[i] . fs[j],  i = i0 + 8 (r >> 2) + 4 kh + (r & 3)
+      return acc;
+    };
+    // acc[r] = ft[i] . fs[j],  i = i0 + 8 (r >> 2) + 4 kh + (r & 3)
+    auto consume = [&](const floatx16& acc, int i0) {
       f32x2 z[8];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -203,12 +207,11 @@ __global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
         cm = nn_max3(cm, z[6].y, z[7].x);
         cm = __builtin_fmaxf(cm, z[7].y);
         cm = __builtin_fmaxf(cm, __shfl_xor(cm, 32, 64));
-        if (cm > run_m) {   // rescale (rare after the first chunks)
-          const float sc = __builtin_amdgcn_exp2f(run_m - cm);
-          s2 *= sc; ax2 *= sc; ay2 *= sc; az2 *= sc;
-          run_m = cm;
-        }
-        const f32x2 nm2 = {run_m, run_m};
+        const float nm = __builtin_fmaxf(run_m, cm);
+        const float sc = __builtin_amdgcn_exp2f(run_m - nm);   // 1 unless the maximum moved
+        s2 *= sc; ax2 *= sc; ay2 *= sc; az2 *= sc;
+        run_m = nm;
+        const f32x2 nm2 = {nm, nm};
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int il = i0 + 8 * g + 4 * kh;
@@ -227,7 +230,15 @@ __global__ __launch_bounds__(256, 2) void feat_nn_kernel(NNArgs a) {
           az2 = __builtin_elementwise_fma(p1, (f32x2){Z.z, Z.w}, az2);
         }
       }
+    };
+    floatx16 acc = mfma_chunk(0);
+#pragma unroll 1
+    for (int i0 = 0; i0 < NN_STAGE - 32; i0 += 32) {
+      const floatx16 nxt = mfma_chunk(i0 + 32);
+      consume(acc, i0);
+      acc = nxt;
     }
+    consume(acc, NN_STAGE - 32);
     if (st + 1 < nst) store_lds(cur ^ 1, t0 + NN_STAGE);   // buffer last read in stage st-1
     __syncthreads();
     cur ^= 1;
