@@ -144,8 +144,7 @@ __device__ __forceinline__ f32x2 unpack_bf16(unsigned p) {
   r.y = __uint_as_float(p & 0xffff0000u);
   return r;
 }
-__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
-  u32x4 H, Mm, L;
+__device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& H, u32x4& Mm, u32x4& L) {
   const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -156,6 +155,10 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8&
     Mm[i] = mp;
     L[i] = cvt_pk_bf16(r - unpack_bf16(mp));
   }
+}
+__device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
+  u32x4 H, Mm, L;
+  split8(a, b, H, Mm, L);
   h = __builtin_bit_cast(bf16x8, H);
   m = __builtin_bit_cast(bf16x8, Mm);
   l = __builtin_bit_cast(bf16x8, L);
@@ -164,6 +167,387 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8&
 // exp(x) for the softmax epilogues on v_exp_f32 (relative error ~1e-6 for |x| <= 20, against the
 // ~1e-4 tolerance of the scores; the argument is <= 0 here)
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+// Persistent-grid slot of this workgroup, XCD-aware: workgroups are dispatched round-robin over the
+// 8 XCDs (each with its own L2), so consecutive tile indices (which share an operand: the n-tiles
+// of one pair reuse its A rows, the m-tiles its B columns) are given to workgroups of one XCD.
+__device__ __forceinline__ int xcd_slot() {
+  const int G = gridDim.x, w = blockIdx.x;
+  return (G & 7) ? w : (w & 7) * (G >> 3) + (w >> 3);
+}
+
+// Epilogue of one 128x128 tile from the 2x2-wave accumulator layout (MFMA 32x32 C map): bias,
+// residual, softmax exponentials, stores and partial statistics (see gemm.hpp Stats).  After the
+// quad transpose, value v[ii][j][q] (float4) of this lane is
+//   C(m0 + 64wm + 32ii + 8q + 4kh + t4,  n0 + 64wn + 32j + 4p8 + u),  u = 0..3
+// red / redm: LDS scratch ([2][128] float2 / float); the caller guarantees a workgroup barrier
+// between two epilogues.
+template <int BIAS, int STATS, int RES>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx16 (&acc)[2][2], int b, int tm, int tn,
+                                              float2* red, float* redm) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int kh = lane >> 5, l32 = lane & 31;
+  const int t4 = lane & 3, p8 = l32 >> 2;
+  const bool h1 = (t4 & 1) != 0, h2 = (t4 & 2) != 0;
+  const int M = g.M, N = g.N;
+  const int N4 = (N + 3) & ~3;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int m0 = tm * BM, n0 = tn * BN;
+  float* C = g.C + (int64_t)b * g.sCb;
+  if (STATS == ST_NONE || STATS == ST_ROW) {
+    // row-local work: one 32-row block at a time (half the live registers of the general path)
+    const int nw = min(max(N - (n0 + wn * 64), 0), 64);   // valid columns of this wave
+    const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
+    bool cok[2][4], sok[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+      sok[j] = gn < N4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cok[j][u] = gn + u < N;
+    }
+    float bn[2][4];
+    if (BIAS == BIAS_N) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bn[j][u] = cok[j][u] ? g.bias[n0 + wn * 64 + j * 32 + 4 * p8 + u] : 0.f;
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
+      asm volatile("" ::: "memory");   // keep each block's loads in its own iteration (VGPRs)
+      float4 w[2][4];
+      if (RES) {
+        const float* Rr = g.R + (int64_t)b * g.sRb;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gm = min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int gn = min(n0 + wn * 64 + j * 32 + 4 * p8, N4 - 4);
+            w[j][q] = *reinterpret_cast<const float4*>(Rr + (int64_t)gm * g.ldc + gn);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gm = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+        const bool rok = gm < M;
+        const float bm = BIAS == BIAS_M ? g.bias[min(gm, M - 1)] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float a0 = acc[ii][j][4 * q], a1 = acc[ii][j][4 * q + 1], a2 = acc[ii][j][4 * q + 2],
+                a3 = acc[ii][j][4 * q + 3];
+          quad_transpose(a0, a1, a2, a3, h1, h2);
+          float4 x = make_float4(a0 + bm, a1 + bm, a2 + bm, a3 + bm);
+          if (BIAS == BIAS_N) { x.x += bn[j][0]; x.y += bn[j][1]; x.z += bn[j][2]; x.w += bn[j][3]; }
+          if (RES) { x.x += w[j][q].x; x.y += w[j][q].y; x.z += w[j][q].z; x.w += w[j][q].w; }
+          w[j][q] = x;
+          if (rok && sok[j]) *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + n0 + wn * 64 + j * 32 + 4 * p8) = x;
+        }
+        if (STATS == ST_ROW) {   // (sum, squared deviations from the wave-local mean) of this row
+          float sm = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sm += cok[j][u] ? f4(w[j][q], u) : 0.f;
+          sm += swz<4>(sm);
+          sm += swz<8>(sm);
+          sm += swz<16>(sm);
+          const float mu = sm * rnw;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float d = cok[j][u] ? f4(w[j][q], u) - mu : 0.f;
+              s2 = fmaf(d, d, s2);
+            }
+          s2 += swz<4>(s2);
+          s2 += swz<8>(s2);
+          s2 += swz<16>(s2);
+          if (p8 == 0) red[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(sm, s2);
+        }
+      }
+    }
+    if (STATS == ST_ROW) {
+      lds_barrier();
+      if (tid < BM && m0 + tid < M) {
+        const float2 x = red[tid], c = red[BM + tid];
+        const int na = min(N - n0, 64), nb = min(max(N - n0 - 64, 0), 64);
+        float2 o = x;
+        if (nb > 0) {
+          const float d = c.x / (float)nb - x.x / (float)na;
+          o = make_float2(x.x + c.x, x.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
+        }
+        g.stats[((int64_t)b * ntn + tn) * g.st_ld + g.st_off + m0 + tid] = o;
+      }
+    }
+    return;
+  }
+  float4 v[2][2][4];
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii) {
+    asm volatile("" ::: "memory");   // keep each block's residual loads in its own iteration (VGPRs)
+    if (RES) {   // residual rows of this 32-row block (loads issued before the transposes)
+      const float* Rr = g.R + (int64_t)b * g.sRb;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int gm = min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int gn = min(n0 + wn * 64 + j * 32 + 4 * p8, N4 - 4);
+          v[ii][j][q] = *reinterpret_cast<const float4*>(Rr + (int64_t)gm * g.ldc + gn);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float a0 = acc[ii][j][4 * q], a1 = acc[ii][j][4 * q + 1], a2 = acc[ii][j][4 * q + 2],
+              a3 = acc[ii][j][4 * q + 3];
+        quad_transpose(a0, a1, a2, a3, h1, h2);
+        if (RES) {
+          v[ii][j][q].x += a0; v[ii][j][q].y += a1; v[ii][j][q].z += a2; v[ii][j][q].w += a3;
+        } else {
+          v[ii][j][q] = make_float4(a0, a1, a2, a3);
+        }
+      }
+  }
+  // validity: rows, columns (per component), float4 stores inside the padded row
+  bool rok[2][4];
+  bool cok[2][4];
+  bool sok[2];
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rok[ii][q] = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4 < M;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+    sok[j] = gn < N4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cok[j][u] = gn + u < N;
+  }
+  if (BIAS == BIAS_M) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float bm = g.bias[min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          v[ii][j][q].x += bm; v[ii][j][q].y += bm; v[ii][j][q].z += bm; v[ii][j][q].w += bm;
+        }
+      }
+  } else if (BIAS == BIAS_N) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+      float bn[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) bn[u] = cok[j][u] ? g.bias[gn + u] : 0.f;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) f4(v[ii][j][q], u) += bn[u];
+    }
+  }
+
+  if (STATS == ST_ROWSMX) {
+    // tile row maxima -> exp(v - max) in place
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float mx = NEG_BIG;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (cok[j][u]) mx = fmaxf(mx, f4(v[ii][j][q], u));
+        mx = fmaxf(mx, swz<4>(mx));
+        mx = fmaxf(mx, swz<8>(mx));
+        mx = fmaxf(mx, swz<16>(mx));
+        if (p8 == 0) redm[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = mx;
+      }
+    lds_barrier();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rl = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+        const float mx = fmaxf(redm[rl], redm[BM + rl]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? fast_exp(f4(v[ii][j][q], u) - mx) : 0.f;
+      }
+  } else if (STATS == ST_COLSMX) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float4 cm = make_float4(NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG);
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (rok[ii][q]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) f4(cm, u) = fmaxf(f4(cm, u), f4(v[ii][j][q], u));
+          }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float x = f4(cm, u);
+        x = fmaxf(x, dpp_x1(x));
+        x = fmaxf(x, dpp_x2(x));
+        x = fmaxf(x, __shfl_xor(x, 32, 64));
+        f4(cm, u) = x;
+      }
+      const float mine = t4 == 0 ? cm.x : t4 == 1 ? cm.y : t4 == 2 ? cm.z : cm.w;
+      if (kh == 0) redm[wm * BN + wn * 64 + j * 32 + 4 * p8 + t4] = mine;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int cl = wn * 64 + j * 32 + 4 * p8;
+      const float4 c0 = *reinterpret_cast<const float4*>(redm + cl);
+      const float4 c1 = *reinterpret_cast<const float4*>(redm + BN + cl);
+      float mx[4] = {fmaxf(c0.x, c1.x), fmaxf(c0.y, c1.y), fmaxf(c0.z, c1.z), fmaxf(c0.w, c1.w)};
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? fast_exp(f4(v[ii][j][q], u) - mx[u]) : 0.f;
+    }
+  }
+
+  // stores (full float4 inside the padded row)
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!rok[ii][q]) continue;
+      const int gm = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
+        if (sok[j]) *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + gn) = v[ii][j][q];
+      }
+    }
+
+  // Statistics.  ST_ROW / ST_COL: per wave (64 columns / rows) the sum and the sum of squared
+  // deviations from the wave-local mean, merged across the two waves with Chan's formula — a
+  // two-pass variance per tile (sum-of-squares minus squared mean cancels catastrophically for
+  // InstanceNorm inputs whose mean is large against their spread).
+  if (STATS == ST_ROW || STATS == ST_ROWSMX) {
+    const int nw = min(max(N - (n0 + wn * 64), 0), 64);   // valid columns of this wave
+    const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float s = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) s += cok[j][u] ? f4(v[ii][j][q], u) : 0.f;
+        s += swz<4>(s);
+        s += swz<8>(s);
+        s += swz<16>(s);
+        if (STATS == ST_ROW) {
+          const float mu = s * rnw;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float d = cok[j][u] ? f4(v[ii][j][q], u) - mu : 0.f;
+              s2 = fmaf(d, d, s2);
+            }
+          s2 += swz<4>(s2);
+          s2 += swz<8>(s2);
+          s2 += swz<16>(s2);
+        }
+        if (p8 == 0) red[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(s, s2);
+      }
+    lds_barrier();
+    if (tid < BM && m0 + tid < M) {
+      const float2 a = red[tid], c = red[BM + tid];
+      float2 o;
+      if (STATS == ST_ROW) {
+        const int na = min(N - n0, 64), nb = min(max(N - n0 - 64, 0), 64);
+        o = a;
+        if (nb > 0) {
+          const float d = c.x / (float)nb - a.x / (float)na;
+          o = make_float2(a.x + c.x, a.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
+        }
+      } else {
+        o = make_float2(fmaxf(redm[tid], redm[BM + tid]), a.x + c.x);
+      }
+      g.stats[((int64_t)b * ntn + tn) * g.st_ld + g.st_off + m0 + tid] = o;
+    }
+  } else if (STATS == ST_COL || STATS == ST_COLSMX) {
+    const int nw = min(max(M - (m0 + wm * 64), 0), 64);   // valid rows of this wave
+    const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float s[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) s[u] += rok[ii][q] ? f4(v[ii][j][q], u) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s[u] += dpp_x1(s[u]);
+        s[u] += dpp_x2(s[u]);
+        s[u] += __shfl_xor(s[u], 32, 64);
+      }
+      if (STATS == ST_COL) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float mu = s[u] * rnw;
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const float d = rok[ii][q] ? f4(v[ii][j][q], u) - mu : 0.f;
+              s2[u] = fmaf(d, d, s2[u]);
+            }
+          s2[u] += dpp_x1(s2[u]);
+          s2[u] += dpp_x2(s2[u]);
+          s2[u] += __shfl_xor(s2[u], 32, 64);
+        }
+      }
+      const float ms = t4 == 0 ? s[0] : t4 == 1 ? s[1] : t4 == 2 ? s[2] : s[3];
+      const float ms2 = t4 == 0 ? s2[0] : t4 == 1 ? s2[1] : t4 == 2 ? s2[2] : s2[3];
+      if (kh == 0) red[wm * BN + wn * 64 + j * 32 + 4 * p8 + t4] = make_float2(ms, ms2);
+    }
+    lds_barrier();
+    if (tid < BN && n0 + tid < N) {
+      const float2 a = red[tid], c = red[BN + tid];
+      float2 o;
+      if (STATS == ST_COL) {
+        const int na = min(M - m0, 64), nb = min(max(M - m0 - 64, 0), 64);
+        o = a;
+        if (nb > 0) {
+          const float d = c.x / (float)nb - a.x / (float)na;
+          o = make_float2(a.x + c.x, a.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
+        }
+      } else {
+        o = make_float2(fmaxf(redm[tid], redm[BN + tid]), a.x + c.x);
+      }
+      g.stats[((int64_t)b * ntm + tm) * g.st_ld + g.st_off + n0 + tid] = o;
+    }
+  }
+}
 
 template <int MATH, int PRO, int BKC, int BIAS, int STATS, int RES>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
@@ -186,12 +570,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
   const int ntiles = ntn * ntm * g.batch;
   const int nk = (K + BK - 1) / BK;
-  const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int my_tiles = (ntiles - xcd_slot() + (int)gridDim.x - 1) / (int)gridDim.x;
   const int S = my_tiles * nk;
   if (S <= 0) return;
 
   auto tile_of = [&](int i, int& b, int& tm, int& tn) {
-    const int t = blockIdx.x + i * gridDim.x;
+    const int t = xcd_slot() + i * gridDim.x;
     tn = t % ntn;
     const int r = t / ntn;
     tm = r % ntm;
@@ -277,8 +661,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   };
 
   floatx16 acc[2][2];
-  const int t4 = lane & 3, p8 = l32 >> 2;   // epilogue: lane = (kh, p8, t4)
-  const bool h1 = (t4 & 1) != 0, h2 = (t4 & 2) != 0;
 
   if (PRO == PRO_A_K || PRO == PRO_B_K) {   // zero scale/shift past K (see the K-tail note below)
     for (int e = tid; e < 4 * KV; e += 256) vec[e] = 0.f;
@@ -426,269 +808,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     //   C(m0 + 64wm + 32ii + 8q + 4kh + t4,  n0 + 64wn + 32j + 4p8 + u),  u = 0..3
     int b, tm, tn;
     tile_of(i, b, tm, tn);
-    const int m0 = tm * BM, n0 = tn * BN;
-    float* C = g.C + (int64_t)b * g.sCb;
-    float4 v[2][2][4];
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      asm volatile("" ::: "memory");   // keep each block's residual loads in its own iteration (VGPRs)
-      if (RES) {   // residual rows of this 32-row block (loads issued before the transposes)
-        const float* Rr = g.R + (int64_t)b * g.sRb;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int gm = min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int gn = min(n0 + wn * 64 + j * 32 + 4 * p8, N4 - 4);
-            v[ii][j][q] = *reinterpret_cast<const float4*>(Rr + (int64_t)gm * g.ldc + gn);
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float a0 = acc[ii][j][4 * q], a1 = acc[ii][j][4 * q + 1], a2 = acc[ii][j][4 * q + 2],
-                a3 = acc[ii][j][4 * q + 3];
-          quad_transpose(a0, a1, a2, a3, h1, h2);
-          if (RES) {
-            v[ii][j][q].x += a0; v[ii][j][q].y += a1; v[ii][j][q].z += a2; v[ii][j][q].w += a3;
-          } else {
-            v[ii][j][q] = make_float4(a0, a1, a2, a3);
-          }
-        }
-    }
-    // validity: rows, columns (per component), float4 stores inside the padded row
-    bool rok[2][4];
-    bool cok[2][4];
-    bool sok[2];
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) rok[ii][q] = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4 < M;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
-      sok[j] = gn < N4;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) cok[j][u] = gn + u < N;
-    }
-    if (BIAS == BIAS_M) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float bm = g.bias[min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1)];
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            v[ii][j][q].x += bm; v[ii][j][q].y += bm; v[ii][j][q].z += bm; v[ii][j][q].w += bm;
-          }
-        }
-    } else if (BIAS == BIAS_N) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
-        float bn[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) bn[u] = cok[j][u] ? g.bias[gn + u] : 0.f;
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) f4(v[ii][j][q], u) += bn[u];
-      }
-    }
-
-    if (STATS == ST_ROWSMX) {
-      // tile row maxima -> exp(v - max) in place
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float mx = NEG_BIG;
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              if (cok[j][u]) mx = fmaxf(mx, f4(v[ii][j][q], u));
-          mx = fmaxf(mx, swz<4>(mx));
-          mx = fmaxf(mx, swz<8>(mx));
-          mx = fmaxf(mx, swz<16>(mx));
-          if (p8 == 0) redm[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = mx;
-        }
-      lds_barrier();
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int rl = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
-          const float mx = fmaxf(redm[rl], redm[BM + rl]);
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? fast_exp(f4(v[ii][j][q], u) - mx) : 0.f;
-        }
-    } else if (STATS == ST_COLSMX) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float4 cm = make_float4(NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG);
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (rok[ii][q]) {
-#pragma unroll
-              for (int u = 0; u < 4; ++u) f4(cm, u) = fmaxf(f4(cm, u), f4(v[ii][j][q], u));
-            }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          float x = f4(cm, u);
-          x = fmaxf(x, dpp_x1(x));
-          x = fmaxf(x, dpp_x2(x));
-          x = fmaxf(x, __shfl_xor(x, 32, 64));
-          f4(cm, u) = x;
-        }
-        const float mine = t4 == 0 ? cm.x : t4 == 1 ? cm.y : t4 == 2 ? cm.z : cm.w;
-        if (kh == 0) redm[wm * BN + wn * 64 + j * 32 + 4 * p8 + t4] = mine;
-      }
-      lds_barrier();
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int cl = wn * 64 + j * 32 + 4 * p8;
-        const float4 c0 = *reinterpret_cast<const float4*>(redm + cl);
-        const float4 c1 = *reinterpret_cast<const float4*>(redm + BN + cl);
-        float mx[4] = {fmaxf(c0.x, c1.x), fmaxf(c0.y, c1.y), fmaxf(c0.z, c1.z), fmaxf(c0.w, c1.w)};
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-              f4(v[ii][j][q], u) = (rok[ii][q] && cok[j][u]) ? fast_exp(f4(v[ii][j][q], u) - mx[u]) : 0.f;
-      }
-    }
-
-    // stores (full float4 inside the padded row)
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!rok[ii][q]) continue;
-        const int gm = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int gn = n0 + wn * 64 + j * 32 + 4 * p8;
-          if (sok[j]) *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + gn) = v[ii][j][q];
-        }
-      }
-
-    // Statistics.  ST_ROW / ST_COL: per wave (64 columns / rows) the sum and the sum of squared
-    // deviations from the wave-local mean, merged across the two waves with Chan's formula — a
-    // two-pass variance per tile (sum-of-squares minus squared mean cancels catastrophically for
-    // InstanceNorm inputs whose mean is large against their spread).
-    if (STATS == ST_ROW || STATS == ST_ROWSMX) {
-      const int nw = min(max(N - (n0 + wn * 64), 0), 64);   // valid columns of this wave
-      const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float s = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) s += cok[j][u] ? f4(v[ii][j][q], u) : 0.f;
-          s += swz<4>(s);
-          s += swz<8>(s);
-          s += swz<16>(s);
-          if (STATS == ST_ROW) {
-            const float mu = s * rnw;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-#pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                const float d = cok[j][u] ? f4(v[ii][j][q], u) - mu : 0.f;
-                s2 = fmaf(d, d, s2);
-              }
-            s2 += swz<4>(s2);
-            s2 += swz<8>(s2);
-            s2 += swz<16>(s2);
-          }
-          if (p8 == 0) red[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(s, s2);
-        }
-      lds_barrier();
-      if (tid < BM && m0 + tid < M) {
-        const float2 a = red[tid], c = red[BM + tid];
-        float2 o;
-        if (STATS == ST_ROW) {
-          const int na = min(N - n0, 64), nb = min(max(N - n0 - 64, 0), 64);
-          o = a;
-          if (nb > 0) {
-            const float d = c.x / (float)nb - a.x / (float)na;
-            o = make_float2(a.x + c.x, a.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
-          }
-        } else {
-          o = make_float2(fmaxf(redm[tid], redm[BM + tid]), a.x + c.x);
-        }
-        g.stats[((int64_t)b * ntn + tn) * g.st_ld + g.st_off + m0 + tid] = o;
-      }
-    } else if (STATS == ST_COL || STATS == ST_COLSMX) {
-      const int nw = min(max(M - (m0 + wm * 64), 0), 64);   // valid rows of this wave
-      const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float s[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) s[u] += rok[ii][q] ? f4(v[ii][j][q], u) : 0.f;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          s[u] += dpp_x1(s[u]);
-          s[u] += dpp_x2(s[u]);
-          s[u] += __shfl_xor(s[u], 32, 64);
-        }
-        if (STATS == ST_COL) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float mu = s[u] * rnw;
-#pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const float d = rok[ii][q] ? f4(v[ii][j][q], u) - mu : 0.f;
-                s2[u] = fmaf(d, d, s2[u]);
-              }
-            s2[u] += dpp_x1(s2[u]);
-            s2[u] += dpp_x2(s2[u]);
-            s2[u] += __shfl_xor(s2[u], 32, 64);
-          }
-        }
-        const float ms = t4 == 0 ? s[0] : t4 == 1 ? s[1] : t4 == 2 ? s[2] : s[3];
-        const float ms2 = t4 == 0 ? s2[0] : t4 == 1 ? s2[1] : t4 == 2 ? s2[2] : s2[3];
-        if (kh == 0) red[wm * BN + wn * 64 + j * 32 + 4 * p8 + t4] = make_float2(ms, ms2);
-      }
-      lds_barrier();
-      if (tid < BN && n0 + tid < N) {
-        const float2 a = red[tid], c = red[BN + tid];
-        float2 o;
-        if (STATS == ST_COL) {
-          const int na = min(M - m0, 64), nb = min(max(M - m0 - 64, 0), 64);
-          o = a;
-          if (nb > 0) {
-            const float d = c.x / (float)nb - a.x / (float)na;
-            o = make_float2(a.x + c.x, a.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
-          }
-        } else {
-          o = make_float2(fmaxf(redm[tid], redm[BN + tid]), a.x + c.x);
-        }
-        g.stats[((int64_t)b * ntm + tm) * g.st_ld + g.st_off + n0 + tid] = o;
-      }
-    }
+    tile_epilogue<BIAS, STATS, RES>(g, acc, b, tm, tn, red, redm);
     // (red / redm are next written in the next tile's epilogue, after at least one stage barrier)
   }
 }

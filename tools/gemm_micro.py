@@ -64,12 +64,30 @@ def run(name, iters, math):
     print("%-16s m%d %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
 
 
+def copy_bw(iters):
+    d = torch.device("cuda")
+    x = torch.randn(P, C, N, device=d)
+    y = torch.empty_like(x)
+    for _ in range(2):
+        y.copy_(x)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    print("%-16s    %8.3f ms  %7.0f GB/s (read+write of the conv activation)" % ("copy", ms, 2 * x.numel() * 4 / ms / 1e6))
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
     ap.add_argument("--math", default="01")
     a = ap.parse_args()
+    copy_bw(a.iters)
     for n in CASES:
         if a.only and n != a.only:
             continue
