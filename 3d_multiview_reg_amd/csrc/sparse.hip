@@ -216,11 +216,63 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
   nbr[e] = (int32_t)v;
 }
 
+// ------------------------------------------------------------------ brick map
+// Coordinates grouped in 4x4x4 bricks: a hash (batch, x>>2, y>>2, z>>2) -> brick id and a pool
+// of 64 row indices per brick (-1 = empty cell).  A large stencil (FCGF conv1, 7^3) then costs
+// <= 8 hash probes per output instead of 343, and neighbouring outputs read the same bricks
+// (L1/L2 locality the per-voxel hash scatters away).
+//   workspace: [16 B header: int32 brick counter] [keys u64 x cap] [rep/ids i32 x cap] [rows i32 x 64 x M]
+struct BrickView {
+  HashView h;      // vals: representative row during the build, then the brick id
+  int32_t* count;  // number of bricks
+  int32_t* rows;   // [bricks][64]
+};
+
+__device__ __forceinline__ int brick_cell(int x, int y, int z) { return (x & 3) | ((y & 3) << 2) | ((z & 3) << 4); }
+
+__global__ void brick_insert_kernel(const int4* __restrict__ c, int64_t M, HashView h) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M) {
+    const int4 v = c[i];
+    hash_insert_min(h, pack_key(v.x, v.y >> 2, v.z >> 2, v.w >> 2), (int32_t)i);
+  }
+}
+
+// representatives (the minimum row of each brick) draw brick ids; wave-aggregated counter
+__global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView h, int32_t* count,
+                                 int32_t* slot_of) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t sl = -1;
+  bool rep = false;
+  if (i < M) {
+    const int4 v = c[i];
+    sl = hash_slot(h, pack_key(v.x, v.y >> 2, v.z >> 2, v.w >> 2));
+    rep = sl >= 0 && h.vals[sl] == (int32_t)i;
+    slot_of[i] = (int32_t)sl;
+  }
+  const unsigned long long m = __ballot(rep);
+  const int lane = threadIdx.x & 63;
+  int base = 0;
+  if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
+  base = __shfl(base, 0, 64);
+  if (rep) h.vals[sl] = base + __popcll(m & ((1ULL << lane) - 1));
+}
+
+__global__ void brick_fill_kernel(const int4* __restrict__ c, int64_t M, HashView h, const int32_t* __restrict__ slot_of,
+                                  int32_t* rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  const int4 v = c[i];
+  const int sl = slot_of[i];
+  if (sl < 0) return;
+  rows[(int64_t)h.vals[sl] * 64 + brick_cell(v.y, v.z, v.w)] = (int32_t)i;
+}
+
 // ------------------------------------------------------------------ conv1: Cin = 1, large stencil
-// out[o][c] = sum_k feat[nbr(o,k)] * W[k][0][c]   with hash probes inline (no 343-wide table),
+// out[o][c] = sum_k feat[nbr(o,k)] * W[k][0][c] over the ks^3 window, gathered brick by brick;
 // epilogue BN (eval, folded per column) / ReLU.  One thread per output row, W in LDS.
 template <int CO>
-__global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h,
+__global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__ oc, int64_t Mo, BrickView bv,
                                                         const float* __restrict__ feat, int ks, int step,
                                                         const float* __restrict__ W, mvr_bn_p bn, float bn_eps,
                                                         int relu, float* __restrict__ out, int64_t ldout) {
@@ -235,24 +287,37 @@ __global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__
   for (int c = 0; c < CO; ++c) acc[c] = 0.f;
   const int4 cc = oc[o];
   const int r = ks / 2;
-  for (int k = 0; k < K; ++k) {
-    const int dx = k % ks - r, dy = (k / ks) % ks - r, dz = k / (ks * ks) - r;
-    const int64_t v = hash_find(h, pack_key(cc.x, cc.y + dx * step, cc.z + dy * step, cc.w + dz * step));
-    if (v >= 0) {
-      const float f = feat[v];
+  // the input set lives at tensor stride `step`: cell coordinates are c / step
+  const int x = cc.y / step, y = cc.z / step, z = cc.w / step;
+  for (int bz = (z - r) >> 2; bz <= (z + r) >> 2; ++bz)
+    for (int by = (y - r) >> 2; by <= (y + r) >> 2; ++by)
+      for (int bx = (x - r) >> 2; bx <= (x + r) >> 2; ++bx) {
+        const int64_t sl = hash_slot(bv.h, pack_key(cc.x, bx, by, bz));
+        if (sl < 0) continue;
+        const int32_t* br = bv.rows + (int64_t)bv.h.vals[sl] * 64;
+        const int x0 = max(x - r, 4 * bx), x1 = min(x + r, 4 * bx + 3);
+        const int y0 = max(y - r, 4 * by), y1 = min(y + r, 4 * by + 3);
+        const int z0 = max(z - r, 4 * bz), z1 = min(z + r, 4 * bz + 3);
+        for (int cz = z0; cz <= z1; ++cz)
+          for (int cy = y0; cy <= y1; ++cy)
+            for (int cx = x0; cx <= x1; ++cx) {
+              const int row = br[brick_cell(cx, cy, cz)];
+              if (row < 0) continue;
+              const float f = feat[row];
+              const float* w = sW + ((cx - x + r) + ks * (cy - y + r) + ks * ks * (cz - z + r)) * CO;
 #pragma unroll
-      for (int c = 0; c < CO; ++c) acc[c] = fmaf(f, sW[k * CO + c], acc[c]);
-    }
-  }
+              for (int c = 0; c < CO; ++c) acc[c] = fmaf(f, w[c], acc[c]);
+            }
+      }
 #pragma unroll
   for (int c = 0; c < CO; ++c) {
-    float y = acc[c];
+    float v = acc[c];
     if (bn.gamma) {
-      const float s = bn.gamma[c] / sqrtf(bn.var[c] + bn_eps);
-      y = (y - bn.mean[c]) * s + bn.beta[c];
+      const float sc = bn.gamma[c] / sqrtf(bn.var[c] + bn_eps);
+      v = (v - bn.mean[c]) * sc + bn.beta[c];
     }
-    if (relu) y = fmaxf(y, 0.f);
-    out[o * ldout + c] = y;
+    if (relu) v = fmaxf(v, 0.f);
+    out[o * ldout + c] = v;
   }
 }
 
@@ -395,20 +460,57 @@ extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const voi
   return MVR_OK;
 }
 
-extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
-                             const float* feat, int ksize, int step, const float* W, int Cout, mvr_bn_p bn,
-                             float bn_eps, int relu, float* out, int64_t ldout, hipStream_t s) {
-  if (!out_coords || Mout < 0 || !in_table || !feat || !W || !out || (ksize & 1) == 0) return MVR_EINVAL;
+static size_t brick_map_bytes(int64_t M) {
+  const uint64_t cap = next_pow2((uint64_t)(2 * (M > 0 ? M : 1)));
+  return 16 + cap * 12 + (size_t)(M > 0 ? M : 1) * 64 * 4 + (size_t)(M > 0 ? M : 1) * 4;
+}
+static BrickView brick_view(void* ws, int64_t M) {
+  BrickView v{};
+  const uint64_t cap = next_pow2((uint64_t)(2 * (M > 0 ? M : 1)));
+  char* base = reinterpret_cast<char*>(ws);
+  v.count = reinterpret_cast<int32_t*>(base);
+  v.h.cap = cap;
+  v.h.keys = reinterpret_cast<uint64_t*>(base + 16);
+  v.h.vals = reinterpret_cast<int32_t*>(base + 16 + cap * 8);
+  v.rows = reinterpret_cast<int32_t*>(base + 16 + cap * 12);
+  return v;
+}
+
+extern "C" size_t mvr_brick_map_bytes(int64_t M) { return brick_map_bytes(M); }
+
+extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (!coords || M < 0 || !ws || ws_bytes < brick_map_bytes(M)) return MVR_EINVAL;
+  BrickView v = brick_view(ws, M);
+  int32_t* slot_of = v.rows + (M > 0 ? M : 1) * 64;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)v.h.cap * 12 + M * 300.0, s);
+  (void)hipMemsetAsync(v.count, 0, 16, s);
+  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)v.h.cap)), dim3(256), 0, s, v.h);
+  if (M > 0) {
+    (void)hipMemsetAsync(v.rows, 0xff, (size_t)M * 64 * 4, s);
+    const int4* c = reinterpret_cast<const int4*>(coords);
+    hipLaunchKernelGGL(brick_insert_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h);
+    hipLaunchKernelGGL(brick_ids_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, v.count, slot_of);
+    hipLaunchKernelGGL(brick_fill_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, slot_of, v.rows);
+  }
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
+                             size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
+                             mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, hipStream_t s) {
+  if (!out_coords || Mout < 0 || !in_bricks || !feat || !W || !out || (ksize & 1) == 0 || step <= 0 || Min < 0)
+    return MVR_EINVAL;
   if (Cout != 32) return MVR_EINVAL;  // FCGF conv1: 1 -> CHANNELS[1] = 32 (fcgf.py:118-125)
-  HashView h = hash_view(const_cast<void*>(in_table), in_table_bytes);
-  if (!h.cap) return MVR_EINVAL;
+  if (in_bricks_bytes < brick_map_bytes(Min)) return MVR_EINVAL;
   if (Mout == 0) return MVR_OK;
+  BrickView v = brick_view(const_cast<void*>(in_bricks), Min);
   const int K = ksize * ksize * ksize;
   const size_t lds = (size_t)K * Cout * sizeof(float);
   if (lds > 160 * 1024) return MVR_EINVAL;
   ProfScope prof(PK_SPCONV, 2.0 * Mout * K * Cout, (double)Mout * (16 + Cout * 4), s);
   hipLaunchKernelGGL(spconv_c1_kernel<32>, dim3(nblk(Mout)), dim3(256), lds, s,
-                     reinterpret_cast<const int4*>(out_coords), Mout, h, feat, ksize, step, W, bn, bn_eps, relu, out,
+                     reinterpret_cast<const int4*>(out_coords), Mout, v, feat, ksize, step, W, bn, bn_eps, relu, out,
                      ldout);
   MVR_CHECK_LAUNCH();
   return MVR_OK;

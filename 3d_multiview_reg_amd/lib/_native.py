@@ -71,8 +71,10 @@ _SIGS = {
     "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
                            c_int, c_vp, c_i64, c_vp]),
-    "mvr_spconv_c1": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp, c_int, c_int, c_vp, c_int, BnP, c_float, c_int, c_vp,
-                              c_i64, c_vp]),
+    "mvr_brick_map_bytes": (c_size, [c_i64]),
+    "mvr_brick_map_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),
+    "mvr_spconv_c1": (c_int, [c_vp, c_i64, c_vp, c_i64, c_size, c_vp, c_int, c_int, c_vp, c_int, BnP, c_float, c_int,
+                              c_vp, c_i64, c_vp]),
     "mvr_l2norm_rows": (c_int, [c_vp, c_i64, c_int, c_i64, c_vp]),
     "mvr_prof_set": (c_int, [c_int]),
     "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),

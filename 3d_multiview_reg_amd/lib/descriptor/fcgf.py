@@ -126,8 +126,8 @@ class FCGFNet(nn.Module):
         # conv1 (7^3, 1 -> 32) + norm1
         s1 = torch.empty(M[0], C[1], device=dev)
         bnp, eps = _bn(self.norm1)
-        tab = cm.table(1)
-        N.check(L.mvr_spconv_c1(N.ptr(cm.coords_at(1)), M[0], N.ptr(tab), tab.numel(), N.ptr(feat),
+        bricks = cm.brick_map(1)
+        N.check(L.mvr_spconv_c1(N.ptr(cm.coords_at(1)), M[0], N.ptr(bricks), M[0], bricks.numel(), N.ptr(feat),
                                 self.conv1_kernel_size, 1, N.ptr(self.conv1.kernel), C[1], bnp, eps, 0, N.ptr(s1),
                                 C[1], N.stream()), "mvr_spconv_c1")
         # concatenation buffers: [tr-branch | skip]

@@ -22,6 +22,7 @@ class CoordinateManager:
         self.device = coords.device
         self.coords = {1: coords.contiguous()}
         self.tables = {}
+        self.bricks = {}
         self.maps = {}
 
     def coords_at(self, s):
@@ -47,6 +48,17 @@ class CoordinateManager:
             N.check(L.mvr_hash_build(N.ptr(c), c.shape[0], N.ptr(t), nb, N.stream()), "mvr_hash_build")
             self.tables[s] = t
         return self.tables[s]
+
+    def brick_map(self, s):
+        """4x4x4 brick map of the stride-s set (large-stencil neighbourhoods, csrc/sparse.hip)."""
+        if s not in self.bricks:
+            c = self.coords_at(s)
+            L = N.lib()
+            nb = L.mvr_brick_map_bytes(c.shape[0])
+            t = torch.empty(nb, dtype=torch.uint8, device=self.device)
+            N.check(L.mvr_brick_map_build(N.ptr(c), c.shape[0], N.ptr(t), nb, N.stream()), "mvr_brick_map_build")
+            self.bricks[s] = t
+        return self.bricks[s]
 
     def kernel_map(self, kind, s, ks=3):
         """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed)."""

@@ -173,8 +173,14 @@ int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table
 int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, int K, int64_t Mout, const float* W,
                int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res, int64_t ldres, int relu,
                float* out, int64_t ldout, mvr_stream_t stream);
-/* single-input-channel conv with a large stencil (FCGF conv1, 7^3) probing the hash inline */
-int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
+/* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
+ * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
+size_t mvr_brick_map_bytes(int64_t M);
+int mvr_brick_map_build(const int32_t* coords, int64_t M, void* workspace, size_t workspace_bytes,
+                        mvr_stream_t stream);
+/* single-input-channel conv with a large stencil (FCGF conv1, 7^3) over the input set's brick map
+ * (in_bricks built from the Min input coordinates; input cell = coordinate / step) */
+int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min, size_t in_bricks_bytes,
                   const float* feat, int ksize, int step, const float* W, int Cout, mvr_bn_p bn, float bn_eps,
                   int relu, float* out, int64_t ldout, mvr_stream_t stream);
 /* x[o][:C] /= ||x[o][:C]||  (fcgf.py:274-278) */
