@@ -15,6 +15,8 @@
 //   offset index k = (dx+r) + ks*(dy+r) + ks^2*(dz+r) (x fastest); strided output
 //   coordinates floor(c/s)*s; transposed conv: in = out - off*s_out; output rows of
 //   every dedup in first-occurrence order of the input rows.
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 #include "prof.hpp"
 #include "sparse.hpp"
@@ -396,6 +398,16 @@ static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel
   return MVR_OK;
 }
 
+// ------------------------------------------------------------------ kernel-map row order
+__global__ void offset_mask_kernel(const int32_t* __restrict__ nbr, int64_t Mo, int K, uint32_t* keys, int32_t* rows) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= Mo) return;
+  uint32_t m = 0;
+  for (int k = 0; k < K; ++k) m |= (nbr[o * K + k] >= 0 ? 1u : 0u) << k;
+  keys[o] = m;
+  rows[o] = (int32_t)o;
+}
+
 }  // namespace mvr
 
 using namespace mvr;
@@ -520,6 +532,39 @@ extern "C" int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, hipStream
   if (!x || M < 0 || C <= 0 || ld < C) return MVR_EINVAL;
   if (M == 0) return MVR_OK;
   hipLaunchKernelGGL(l2norm_rows_kernel, dim3(nblk(M)), dim3(256), 0, s, x, M, C, ld);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+// Order the output rows of a kernel map by their active-offset mask (LSD radix sort, stable):
+// perm[i] = i-th row.  Workspace: mvr_kernel_map_order_bytes(Mo).
+static size_t order_sort_bytes(int64_t Mo) {
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)(Mo > 0 ? Mo : 1), 0, 32);
+  return tmp;
+}
+extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) {
+  const size_t n = (size_t)(Mo > 0 ? Mo : 1);
+  return order_sort_bytes(Mo) + n * 12 + 3 * 256;
+}
+extern "C" int mvr_kernel_map_order(const int32_t* nbr, int64_t Mo, int K, int32_t* perm, void* ws, size_t ws_bytes,
+                                    hipStream_t s) {
+  if (!nbr || !perm || Mo < 0 || K <= 0 || K > 32 || !ws || ws_bytes < mvr_kernel_map_order_bytes(Mo) ||
+      Mo > 0x7fffffff)
+    return MVR_EINVAL;
+  if (Mo == 0) return MVR_OK;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mo * (4.0 * K + 32), s);
+  char* p = reinterpret_cast<char*>(ws);
+  auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
+  uint32_t* kin = reinterpret_cast<uint32_t*>(take((size_t)Mo * 4));
+  uint32_t* kout = reinterpret_cast<uint32_t*>(take((size_t)Mo * 4));
+  int32_t* vin = reinterpret_cast<int32_t*>(take((size_t)Mo * 4));
+  size_t tmp = order_sort_bytes(Mo);
+  void* tbuf = take(tmp);
+  hipLaunchKernelGGL(offset_mask_kernel, dim3(nblk(Mo)), dim3(256), 0, s, nbr, Mo, K, kin, vin);
+  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, kin, kout, vin, perm, (int)Mo, 0, K, s) != hipSuccess)
+    return MVR_ELAUNCH;
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }

@@ -5,7 +5,9 @@
 //   epi = (+bias) -> BatchNorm (eval: running stats) -> (+residual) -> (ReLU)
 //
 // nbr is the kernel map as a neighbour table (csrc/sparse.hip); -1 entries contribute
-// nothing.  Per 64/128-row output tile the workgroup first lists the stencil offsets
+// nothing.  Output rows are visited in the order `perm` (mvr_kernel_map_order: rows sorted by
+// their active-offset mask), so a tile's rows share their active offsets and the union the tile
+// iterates stays small (a transposed stride-2 conv has <= 8 of 27 per row, by coordinate parity).  Per 64/128-row output tile the workgroup first lists the stencil offsets
 // that have at least one neighbour in the tile and skips the empty ones; each step
 // gathers 16 input channels of the tile's neighbour rows (16-byte row loads) and the
 // matching W[k] slice into LDS, then runs v_mfma_f32_32x32x2_f32.  No atomics: every
@@ -21,6 +23,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 struct SpArgs {
   const float* in; int64_t ldin; int Cin;
   const int32_t* nbr; int K; int64_t Mout;
+  const int32_t* perm;   // optional output row order (tile t covers rows perm[64t .. 64t+63])
   const float* W; int Cout;
   const float* bias;
   mvr_bn_p bn; float bn_eps;
@@ -57,7 +60,10 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
     const int row = e / K, k = e - row * K;
     const int64_t o = o0 + row;
     int v = -1;
-    if (o < a.Mout) v = a.nbr ? a.nbr[o * K + k] : (int)o;
+    if (o < a.Mout) {
+      const int64_t orow = a.perm ? a.perm[o] : o;
+      v = a.nbr ? a.nbr[orow * K + k] : (int)orow;
+    }
     nb[row][k] = v;
     if (v >= 0) kact[k] = 1;
   }
@@ -162,8 +168,9 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
     const float bias = a.bias ? a.bias[c] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t o = o0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (o >= a.Mout) continue;
+      const int64_t ot = o0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (ot >= a.Mout) continue;
+      const int64_t o = a.perm ? a.perm[ot] : ot;
       float v = acc[j][r] + bias;
       v = fmaf(v, bsc, bsh);
       if (a.res) v += a.res[o * a.ldres + c];
@@ -177,16 +184,16 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
 
 using namespace mvr;
 
-extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, int K, int64_t Mout,
-                          const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
-                          int64_t ldres, int relu, float* out, int64_t ldout, hipStream_t s) {
+extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K,
+                          int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
+                          const float* res, int64_t ldres, int relu, float* out, int64_t ldout, hipStream_t s) {
   if (!in || !W || !out || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
   if (!nbr && K != 1) return MVR_EINVAL;
   if ((Cin & 3) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
       (reinterpret_cast<uintptr_t>(W) & 15))
     return MVR_EINVAL;
   if (Mout == 0) return MVR_OK;
-  SpArgs a{in, ldin, Cin, nbr, K, Mout, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout};
+  SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout};
   ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
   if (Cout <= 32) {
     hipLaunchKernelGGL((spconv_kernel<128, 32, 4, 1>), dim3((unsigned)((Mout + 127) / 128), (Cout + 31) / 32),

@@ -69,7 +69,9 @@ _SIGS = {
     "mvr_coords_downsample": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_size, c_vp, c_vp, c_vp]),
     "mvr_hash_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),
     "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
-    "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
+    "mvr_kernel_map_order_bytes": (c_size, [c_i64]),
+    "mvr_kernel_map_order": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
+    "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
                            c_int, c_vp, c_i64, c_vp]),
     "mvr_brick_map_bytes": (c_size, [c_i64]),
     "mvr_brick_map_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),

@@ -92,19 +92,22 @@ class FCGFNet(nn.Module):
         self.final = _MEConv(T[1], out_channels, 1, has_bias=True)
 
     # ------------------------------------------------------------------ native helpers
-    def _conv(self, x, ldx, conv, nbr, M, out, ldout, norm=None, res=None, ldres=0, relu=False, bias=None):
+    def _conv(self, x, ldx, conv, km, M, out, ldout, norm=None, res=None, ldres=0, relu=False, bias=None):
+        """km: (neighbour table, row order) of lib.sparse.CoordinateManager, or None for a 1x1x1 conv."""
         bnp, eps = _bn(norm)
         K, cin, cout = conv.kernel.shape
-        N.check(N.lib().mvr_spconv(N.ptr(x), ldx, cin, N.ptr(nbr), K, M, N.ptr(conv.kernel), cout, N.ptr(bias), bnp,
-                                   eps, N.ptr(res), ldres, int(relu), N.ptr(out), ldout, N.stream()), "mvr_spconv")
+        nbr, perm = km if km is not None else (None, None)
+        N.check(N.lib().mvr_spconv(N.ptr(x), ldx, cin, N.ptr(nbr), N.ptr(perm), K, M, N.ptr(conv.kernel), cout,
+                                   N.ptr(bias), bnp, eps, N.ptr(res), ldres, int(relu), N.ptr(out), ldout, N.stream()),
+                "mvr_spconv")
         return out
 
-    def _block(self, blk, x, ldx, nbr, M, out, ldout):
+    def _block(self, blk, x, ldx, km, M, out, ldout):
         """BasicBlockBN at one stride; x may live inside a wider buffer (ldx)."""
         c = blk.conv1.kernel.shape[2]
         t = torch.empty(M, c, device=x.device)
-        self._conv(x, ldx, blk.conv1, nbr, M, t, c, blk.norm1, relu=True)
-        self._conv(t, c, blk.conv2, nbr, M, out, ldout, blk.norm2, res=x, ldres=ldx, relu=True)
+        self._conv(x, ldx, blk.conv1, km, M, t, c, blk.norm1, relu=True)
+        self._conv(t, c, blk.conv2, km, M, out, ldout, blk.norm2, res=x, ldres=ldx, relu=True)
         return out
 
     def forward(self, x):
@@ -116,6 +119,9 @@ class FCGFNet(nn.Module):
         if self.training:
             raise NotImplementedError("FCGFNet on the HIP path runs in eval mode (BatchNorm running statistics)")
         cm = x.coords_man
+
+        def km(kind, s):
+            return cm.kernel_map(kind, s), cm.kernel_map_order(kind, s)
         dev = x.F.device
         C, T = self.CHANNELS, self.TR_CHANNELS
         M = [cm.coords_at(s).shape[0] for s in (1, 2, 4, 8)]
@@ -137,27 +143,27 @@ class FCGFNet(nn.Module):
         w1, w2, w3 = cat1.shape[1], cat2.shape[1], cat3.shape[1]
         skip1, skip2, skip3 = cat1[:, T[2]:], cat2[:, T[3]:], cat3[:, T[4]:]
         # encoder
-        self._block(self.block1, s1, C[1], cm.kernel_map("s1", 1), M[0], skip1, w1)        # out_s1 (relu'd)
+        self._block(self.block1, s1, C[1], km("s1", 1), M[0], skip1, w1)        # out_s1 (relu'd)
         t2 = torch.empty(M[1], C[2], device=dev)
-        self._conv(skip1, w1, self.conv2, cm.kernel_map("down", 1), M[1], t2, C[2], self.norm2)
-        self._block(self.block2, t2, C[2], cm.kernel_map("s1", 2), M[1], skip2, w2)        # out_s2
+        self._conv(skip1, w1, self.conv2, km("down", 1), M[1], t2, C[2], self.norm2)
+        self._block(self.block2, t2, C[2], km("s1", 2), M[1], skip2, w2)        # out_s2
         t3 = torch.empty(M[2], C[3], device=dev)
-        self._conv(skip2, w2, self.conv3, cm.kernel_map("down", 2), M[2], t3, C[3], self.norm3)
-        self._block(self.block3, t3, C[3], cm.kernel_map("s1", 4), M[2], skip3, w3)        # out_s4
+        self._conv(skip2, w2, self.conv3, km("down", 2), M[2], t3, C[3], self.norm3)
+        self._block(self.block3, t3, C[3], km("s1", 4), M[2], skip3, w3)        # out_s4
         t4 = torch.empty(M[3], C[4], device=dev)
-        self._conv(skip3, w3, self.conv4, cm.kernel_map("down", 4), M[3], t4, C[4], self.norm4)
+        self._conv(skip3, w3, self.conv4, km("down", 4), M[3], t4, C[4], self.norm4)
         s8 = torch.empty(M[3], C[4], device=dev)
-        self._block(self.block4, t4, C[4], cm.kernel_map("s1", 8), M[3], s8, C[4])         # out_s8
+        self._block(self.block4, t4, C[4], km("s1", 8), M[3], s8, C[4])         # out_s8
         # decoder
         u = torch.empty(M[2], T[4], device=dev)
-        self._conv(s8, C[4], self.conv4_tr, cm.kernel_map("up", 4), M[2], u, T[4], self.norm4_tr)
-        self._block(self.block4_tr, u, T[4], cm.kernel_map("s1", 4), M[2], cat3, w3)       # out_s4_tr
+        self._conv(s8, C[4], self.conv4_tr, km("up", 4), M[2], u, T[4], self.norm4_tr)
+        self._block(self.block4_tr, u, T[4], km("s1", 4), M[2], cat3, w3)       # out_s4_tr
         u = torch.empty(M[1], T[3], device=dev)
-        self._conv(cat3, w3, self.conv3_tr, cm.kernel_map("up", 2), M[1], u, T[3], self.norm3_tr)
-        self._block(self.block3_tr, u, T[3], cm.kernel_map("s1", 2), M[1], cat2, w2)       # out_s2_tr
+        self._conv(cat3, w3, self.conv3_tr, km("up", 2), M[1], u, T[3], self.norm3_tr)
+        self._block(self.block3_tr, u, T[3], km("s1", 2), M[1], cat2, w2)       # out_s2_tr
         u = torch.empty(M[0], T[2], device=dev)
-        self._conv(cat2, w2, self.conv2_tr, cm.kernel_map("up", 1), M[0], u, T[2], self.norm2_tr)
-        self._block(self.block2_tr, u, T[2], cm.kernel_map("s1", 1), M[0], cat1, w1)       # out_s1_tr
+        self._conv(cat2, w2, self.conv2_tr, km("up", 1), M[0], u, T[2], self.norm2_tr)
+        self._block(self.block2_tr, u, T[2], km("s1", 1), M[0], cat1, w1)       # out_s1_tr
         h = torch.empty(M[0], T[1], device=dev)
         self._conv(cat1, w1, self.conv1_tr, None, M[0], h, T[1], relu=True)
         cout = self.final.kernel.shape[2]

@@ -24,6 +24,7 @@ class CoordinateManager:
         self.tables = {}
         self.bricks = {}
         self.maps = {}
+        self.orders = {}
 
     def coords_at(self, s):
         if s not in self.coords:
@@ -78,6 +79,20 @@ class CoordinateManager:
                                            N.ptr(nbr), N.stream()), "mvr_kernel_map")
             self.maps[key] = nbr
         return self.maps[key]
+
+
+    def kernel_map_order(self, kind, s, ks=3):
+        """Rows of kernel_map(kind, s) sorted by their active-offset mask (tiling order of mvr_spconv)."""
+        key = (kind, s, ks)
+        if key not in self.orders:
+            nbr = self.kernel_map(kind, s, ks)
+            L = N.lib()
+            ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr.shape[0]), self.device)
+            perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.device)
+            N.check(L.mvr_kernel_map_order(N.ptr(nbr), nbr.shape[0], nbr.shape[1], N.ptr(perm), N.ptr(ws), ws.numel(),
+                                           N.stream()), "mvr_kernel_map_order")
+            self.orders[key] = perm
+        return self.orders[key]
 
 
 class SparseTensor:

@@ -167,12 +167,19 @@ int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_b
  * row of out_coords[o] + sign*off_k*step in the input table (sign -1 if transposed), or -1 */
 int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
                    int step, int transposed, int32_t* nbr, mvr_stream_t stream);
+/* Row order of a kernel map: output rows sorted by their active-offset mask (K <= 32), so that a
+ * tile of consecutive rows shares its active offsets.  Workspace: mvr_kernel_map_order_bytes(Mout). */
+size_t mvr_kernel_map_order_bytes(int64_t Mout);
+int mvr_kernel_map_order(const int32_t* nbr, int64_t Mout, int K, int32_t* perm, void* workspace,
+                         size_t workspace_bytes, mvr_stream_t stream);
 /* MinkowskiConvolution forward, gather-GEMM over the neighbour table (nbr NULL & K==1:
  * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
- * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu. */
-int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, int K, int64_t Mout, const float* W,
-               int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res, int64_t ldres, int relu,
-               float* out, int64_t ldout, mvr_stream_t stream);
+ * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
+ * perm (optional): order in which output rows are tiled (mvr_kernel_map_order); results are
+ * written to their own rows either way. */
+int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K, int64_t Mout,
+               const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
+               int64_t ldres, int relu, float* out, int64_t ldout, mvr_stream_t stream);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
 size_t mvr_brick_map_bytes(int64_t M);
