@@ -342,8 +342,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
                                      const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N,
                                      int bn_train, float* logits, float* scores, float* R, float* t, float* res,
                                      float* latent, float* res_row, float* score_row, int64_t row_pstride,
-                                     int32_t* guard_pos, int32_t* status, void* workspace, size_t workspace_bytes,
-                                     hipStream_t s) {
+                                     int32_t* guard_pos, int32_t* status, int guard_group, void* workspace,
+                                     size_t workspace_bytes, hipStream_t s) {
   if (!blk || !input || !xs || !logits || !scores || !R || !t || !res || !guard_pos || !workspace) return MVR_EINVAL;
   const int C = blk->channels, Kc = blk->clusters, H = blk->half_layers, Cin = blk->in_channels;
   if (P <= 0 || N <= 0 || C <= 0 || Kc <= 0 || H <= 0 || H > MVR_OAN_MAX_HALF || Cin <= 0) return MVR_EINVAL;
@@ -427,7 +427,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   // weights = relu(tanh(logits)) already in `scores`; the guard (oanet.py:177-178) and
   // Kabsch (oanet.py:180-183, normalize_w=True, eps=1e-7)
   int e3 = mvr_procrustes(xs, xs + 3, xs_pstride, xs_nstride, scores, N, guard_pos, nullptr, 0, P, N, 1, 1e-7f, R,
-                          t, res, N, res_row, row_pstride, status, s);
+                          t, res, N, res_row, row_pstride, status, guard_group, s);
   if (e3) return e3;
   if (score_row) {  // next block's input row 7 = (guarded) scores (oanet.py:247-248)
     (void)hipMemcpy2DAsync(score_row, row_pstride * sizeof(float), scores, N * sizeof(float), N * sizeof(float), P,

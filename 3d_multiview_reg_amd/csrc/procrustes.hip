@@ -91,6 +91,7 @@ struct ProcrustesArgs {
   T* w; int64_t w_ps;
   const int32_t* guard_pos; T* w_copy; int64_t wc_ps;
   int P, N, normalize; T eps;
+  int guard_group;   // pairs [g*G, (g+1)*G) share the guard; 0 = the whole batch
   T* R; T* t; T* res; int64_t res_ps;
   T* res_copy; int64_t rc_ps;
   int32_t* status;
@@ -108,12 +109,15 @@ __global__ __launch_bounds__(256) void procrustes_kernel(ProcrustesArgs<T> a) {
   const T* x2 = a.x2 + (int64_t)p * a.x_ps;
   T* w = a.w ? a.w + (int64_t)p * a.w_ps : nullptr;
 
-  // ---- zero-weight guard (oanet.py:177-178): any pair of the batch with sum(w)==0
+  // ---- zero-weight guard (oanet.py:177-178): any pair of the batch (or of this pair's guard
+  // group, see ProcrustesArgs::guard_group) with sum(w)==0
   if (tid == 0) sflag = 0;
   __syncthreads();
   if (a.guard_pos) {
+    const int q0 = a.guard_group > 0 ? (p / a.guard_group) * a.guard_group : 0;
+    const int q1 = a.guard_group > 0 ? min(q0 + a.guard_group, a.P) : a.P;
     int any = 0;
-    for (int q = tid; q < a.P; q += blockDim.x) any |= (a.guard_pos[q] == 0);
+    for (int q = q0 + tid; q < q1; q += blockDim.x) any |= (a.guard_pos[q] == 0);
     if (any) atomicOr(&sflag, 1);
   }
   __syncthreads();
@@ -214,12 +218,12 @@ template <typename T>
 static int procrustes_launch(const T* x1, const T* x2, int64_t x_pstride, int64_t x_nstride, T* w, int64_t w_pstride,
                              const int32_t* guard_pos, T* w_copy, int64_t wc_pstride, int P, int N, int normalize,
                              T eps, T* R, T* t, T* res, int64_t res_pstride, T* res_copy, int64_t rc_pstride,
-                             int32_t* status, hipStream_t stream) {
-  if (P < 0 || N < 0 || !x1 || !x2 || !R || !t) return MVR_EINVAL;
+                             int32_t* status, int guard_group, hipStream_t stream) {
+  if (P < 0 || N < 0 || !x1 || !x2 || !R || !t || guard_group < 0) return MVR_EINVAL;
   if (guard_pos && !w) return MVR_EINVAL;
   if (P == 0) return MVR_OK;
   mvr::ProcrustesArgs<T> a{x1, x2, x_pstride, x_nstride, w, w_pstride, guard_pos, w_copy, wc_pstride,
-                           P, N, normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status};
+                           P, N, normalize, eps, guard_group, R, t, res, res_pstride, res_copy, rc_pstride, status};
   mvr::ProfScope prof(mvr::PK_PROCRUSTES, 40.0 * P * N, (double)P * N * sizeof(T) * 8, stream);
   hipLaunchKernelGGL(mvr::procrustes_kernel<T>, dim3(P), dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
@@ -229,16 +233,19 @@ static int procrustes_launch(const T* x1, const T* x2, int64_t x_pstride, int64_
 extern "C" int mvr_procrustes(const float* x1, const float* x2, int64_t x_pstride, int64_t x_nstride, float* w,
                               int64_t w_pstride, const int32_t* guard_pos, float* w_copy, int64_t wc_pstride, int P,
                               int N, int normalize, float eps, float* R, float* t, float* res, int64_t res_pstride,
-                              float* res_copy, int64_t rc_pstride, int32_t* status, hipStream_t stream) {
+                              float* res_copy, int64_t rc_pstride, int32_t* status, int guard_group,
+                              hipStream_t stream) {
   return procrustes_launch<float>(x1, x2, x_pstride, x_nstride, w, w_pstride, guard_pos, w_copy, wc_pstride, P, N,
-                                  normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status, stream);
+                                  normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status, guard_group,
+                                  stream);
 }
 
 extern "C" int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_pstride, int64_t x_nstride, double* w,
                                   int64_t w_pstride, const int32_t* guard_pos, double* w_copy, int64_t wc_pstride,
                                   int P, int N, int normalize, double eps, double* R, double* t, double* res,
                                   int64_t res_pstride, double* res_copy, int64_t rc_pstride, int32_t* status,
-                                  hipStream_t stream) {
+                                  int guard_group, hipStream_t stream) {
   return procrustes_launch<double>(x1, x2, x_pstride, x_nstride, w, w_pstride, guard_pos, w_copy, wc_pstride, P, N,
-                                   normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status, stream);
+                                   normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status, guard_group,
+                                   stream);
 }

@@ -48,17 +48,17 @@ class OanBlockP(ctypes.Structure):
 
 _SIGS = {
     "mvr_procrustes": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int, c_float,
-                               c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+                               c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_vp]),
     "mvr_procrustes_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int,
-                                   ctypes.c_double, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+                                   ctypes.c_double, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_vp]),
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
                              c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int,
                              c_int, c_int, c_vp]),
     "mvr_set_gemm_math": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
-                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_size,
-                                      c_vp]),
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_vp,
+                                      c_size, c_vp]),
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),

@@ -1,0 +1,108 @@
+"""Multi-GPU sharding of the pair batch.
+
+One process per GPU (torchrun; backend "nccl" = RCCL over xGMI on MI355X, "gloo" for the CPU
+tests).  Pairs are independent given the fragment descriptors, so the only exchange is one
+all-gather of fixed-size per-pair records at the end:
+
+  * every rank computes the FCGF descriptors and samples of all fragments of the scene
+    (cheap, and identical on every rank: same seeds), or receives them precomputed;
+  * the lexicographic pair list (lib/utils.py:873 ``itertools.combinations``) is split into
+    contiguous blocks of whole 32-pair groups (the reference evaluation batch,
+    scripts/benchmark_pairwise_registration.py:363-367), so the batch-coupled zero-row guard of
+    OANBlock (lib/filtering/oanet.py:177-178) sees exactly the reference's groups;
+  * each rank runs Soft_NN -> OANet -> Procrustes on its block and packs one record per pair;
+  * ``gather_records`` all-gathers the blocks (one collective, ~64 B per pair) into pair order.
+"""
+import math
+
+import numpy as np
+import torch
+
+GROUP = 32          # reference evaluation batch: the zero-row guard is evaluated per group
+REC = 16            # floats per record: idx | R (9) | t (3) | conf | flag | pad
+
+
+def shard_pairs(P, world, rank, group=GROUP):
+    """Contiguous [start, end) block of the P pairs for `rank`, made of whole `group`-sized groups.
+    Blocks are as equal as the grouping allows; trailing ranks may get an empty block."""
+    if not 0 <= rank < world:
+        raise ValueError("rank %d outside world %d" % (rank, world))
+    n_groups = math.ceil(P / group)
+    per = math.ceil(n_groups / world) if n_groups else 0
+    g0 = min(rank * per, n_groups)
+    g1 = min(g0 + per, n_groups)
+    return min(g0 * group, P), min(g1 * group, P)
+
+
+def block_capacity(P, world, group=GROUP):
+    """Rows of the (equal-size, padded) per-rank block exchanged by gather_records."""
+    n_groups = math.ceil(P / group)
+    return (math.ceil(n_groups / world) if n_groups else 0) * group
+
+
+def pack_records(first_pair, R, t, scores, flag=None):
+    """Per-pair records [n, 16] float32: pair index, R row-major, t, conf = mean(scores > 0.5)
+    (not a reference quantity), SVD-fallback flag."""
+    n = R.shape[0]
+    rec = torch.zeros(n, REC, dtype=torch.float32, device=R.device)
+    rec[:, 0] = torch.arange(first_pair, first_pair + n, device=R.device, dtype=torch.float32)
+    rec[:, 1:10] = R.reshape(n, 9).float()
+    rec[:, 10:13] = t.reshape(n, 3).float()
+    rec[:, 13] = (scores > 0.5).float().mean(dim=1)
+    if flag is not None:
+        rec[:, 14] = torch.as_tensor(flag, device=R.device).float().reshape(-1).expand(n)
+    return rec
+
+
+def gather_records(rec, P, world, group=GROUP):
+    """All-gather every rank's block of records (padded to block_capacity rows) and return the
+    [P, 16] records of all pairs in pair order, on every rank."""
+    if world == 1:
+        return rec
+    import torch.distributed as dist
+    cap = block_capacity(P, world, group)
+    buf = torch.zeros(cap, REC, dtype=rec.dtype, device=rec.device)
+    buf[:rec.shape[0]] = rec
+    if dist.get_backend() == "gloo":
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf)
+        out = torch.cat(parts)
+    else:
+        out = torch.empty(world * cap, REC, dtype=rec.dtype, device=rec.device)
+        dist.all_gather_into_tensor(out, buf)
+    rows = []
+    for r in range(world):
+        s, e = shard_pairs(P, world, r, group)
+        rows.append(out[r * cap:r * cap + (e - s)])
+    return torch.cat(rows)
+
+
+def unpack_records(rec):
+    """-> (pair_idx int64 [P], R [P,3,3], t [P,3,1], conf [P], flag bool [P]) on the host."""
+    a = rec.detach().cpu().numpy()
+    return (a[:, 0].astype(np.int64), a[:, 1:10].reshape(-1, 3, 3), a[:, 10:13].reshape(-1, 3, 1), a[:, 13],
+            a[:, 14] > 0)
+
+
+def register_pairs_sharded(model, filtering_input, world, rank, group=GROUP):
+    """Run model.filter_correspondences on this rank's block of the pair batch (one call, the
+    zero-row guard evaluated per `group` pairs as in the reference's batch-32 evaluation) and
+    all-gather the records.  `filtering_input` is the dict of
+    lib/utils.py:construct_filtering_input_data over ALL pairs (every rank holds it)."""
+    xs = filtering_input["xs"]
+    P = xs.shape[0]
+    s, e = shard_pairs(P, world, rank, group)
+    filt = model.filtering_module if hasattr(model, "filtering_module") else model
+    if e > s:
+        prev = filt.guard_group
+        filt.guard_group = group
+        try:
+            out = model.filter_correspondences({"xs": xs[s:e]}) if hasattr(model, "filter_correspondences") \
+                else model({"xs": xs[s:e]})
+        finally:
+            filt.guard_group = prev
+        rec = pack_records(s, out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1],
+                           out.get("gradient_flag"))
+    else:
+        rec = torch.zeros(0, REC, device=xs.device)
+    return gather_records(rec, P, world, group)

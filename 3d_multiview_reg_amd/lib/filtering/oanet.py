@@ -145,6 +145,9 @@ class OANet(nn.Module):
         self.reg_iter = _Slots({i: OANBlock(C, 8 + self.side_channel, depth_each_stage, K, nrm)
                                 for i in range(self.iter_num)})
         self.device = torch.device("cuda" if (torch.cuda.is_available() and cfg["misc"]["use_gpu"]) else "cpu")
+        # zero-row guard (oanet.py:177-178) scope: 0 = the whole forward batch (the reference);
+        # lib.distributed sets 32 (the evaluation batch) when a batch is split across ranks
+        self.guard_group = 0
 
     def forward(self, data):
         xs_in = data["xs"]
@@ -184,7 +187,7 @@ class OANet(nn.Module):
                 ctypes.byref(params), N.ptr(inp), rows * ld, ld, N.ptr(xs), Npts * Cxs, Cxs, P, Npts, int(self.training),
                 N.ptr(logits), N.ptr(scores), N.ptr(R), N.ptr(t), N.ptr(res), N.ptr(latent) if last else None,
                 None if last else N.ptr(inp[:, Cxs]), None if last else N.ptr(inp[:, Cxs + 1]), rows * ld,
-                N.ptr(guard), N.ptr(status[bi]), N.ptr(ws), ws.numel(), st)
+                N.ptr(guard), N.ptr(status[bi]), int(self.guard_group), N.ptr(ws), ws.numel(), st)
             N.check(rc, "mvr_oan_block_forward")
             if bi == 0 and not last:
                 blk_in_ch = blocks[1].in_channels

@@ -105,7 +105,7 @@ def kabsch_transformation_estimation(x1, x2, weights=None, normalize_w=True, eps
     L = N.lib()
     fn = L.mvr_procrustes if dt == torch.float32 else L.mvr_procrustes_f64
     N.check(fn(N.ptr(x1c), N.ptr(x2c), Np * 3, 3, N.ptr(w), Np, None, None, 0, B, Np, int(normalize), eps,
-               N.ptr(R), N.ptr(t), N.ptr(res), Np, None, 0, N.ptr(status), N.stream()), "mvr_procrustes")
+               N.ptr(R), N.ptr(t), N.ptr(res), Np, None, 0, N.ptr(status), 0, N.stream()), "mvr_procrustes")
     return R, t, res, bool(status.any().item())
 
 

@@ -34,6 +34,8 @@ typedef struct ihipStream_t* mvr_stream_t; /* == hipStream_t */
  * lib/utils.py:240-256), and — when guard_pos != NULL — the batch-coupled
  * zero-weight guard of lib/filtering/oanet.py:177-178 (if any pair q has
  * guard_pos[q]==0, every pair's weights get +1/N; w and w_copy are rewritten).
+ * guard_group > 0 evaluates the guard per group of that many consecutive pairs (the reference
+ * evaluation batch of 32 when a batch is split across ranks); 0 = the whole batch.
  *   x1(p,n,:) = x1[p*x_pstride + n*x_nstride + 0..2], x2 likewise.
  *   w may be NULL (all ones).  R [P,3,3] row-major, t [P,3], res [P, res_pstride],
  *   status[P]: 0 ok, 1 non-finite covariance (reference's SVD-exception branch:
@@ -42,12 +44,13 @@ typedef struct ihipStream_t* mvr_stream_t; /* == hipStream_t */
 int mvr_procrustes(const float* x1, const float* x2, int64_t x_pstride, int64_t x_nstride, float* w,
                    int64_t w_pstride, const int32_t* guard_pos, float* w_copy, int64_t wc_pstride, int P, int N,
                    int normalize, float eps, float* R, float* t, float* res, int64_t res_pstride, float* res_copy,
-                   int64_t rc_pstride, int32_t* status, mvr_stream_t stream);
+                   int64_t rc_pstride, int32_t* status, int guard_group, mvr_stream_t stream);
 /* fp64 variant (fp64 inputs compute in fp64 in the reference, utils.py:164). */
 int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_pstride, int64_t x_nstride, double* w,
                        int64_t w_pstride, const int32_t* guard_pos, double* w_copy, int64_t wc_pstride, int P, int N,
                        int normalize, double eps, double* R, double* t, double* res, int64_t res_pstride,
-                       double* res_copy, int64_t rc_pstride, int32_t* status, mvr_stream_t stream);
+                       double* res_copy, int64_t rc_pstride, int32_t* status, int guard_group,
+                       mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * One fused fp32-MFMA batched GEMM of the OANet schedule (exposed for tests):
@@ -114,7 +117,8 @@ int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_
                           const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N, int bn_train,
                           float* logits,
                           float* scores, float* R, float* t, float* res, float* latent, float* res_row,
-                          float* score_row, int64_t row_pstride, int32_t* guard_pos, int32_t* status, void* workspace,
+                          float* score_row, int64_t row_pstride, int32_t* guard_pos, int32_t* status, int guard_group,
+                          void* workspace,
                           size_t workspace_bytes, mvr_stream_t stream);
 
 /* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*out_ld + n]
