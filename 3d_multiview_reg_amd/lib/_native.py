@@ -62,6 +62,7 @@ _SIGS = {
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "mvr_fps": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "mvr_hash_table_bytes": (c_size, [c_i64]),
     "mvr_voxelize_workspace_bytes": (c_size, [c_i64]),
     "mvr_voxelize": (c_int, [c_vp, c_vp, c_int, c_i64, c_float, c_vp, c_size, c_vp, c_vp, c_vp, c_vp]),

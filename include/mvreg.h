@@ -126,6 +126,14 @@ int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_
 int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N, float* out,
                        int64_t out_pstride, int64_t out_ld, mvr_stream_t stream);
 
+/* Farthest point sampling per fragment (Sampler 'fps', lib/layers.py:134-141 — pointnet2
+ * furthest_point_sample semantics of oracle/fps.py: seed = first point, running min of squared
+ * distances, first maximum on ties).  xyz [sum n][3] with fragment row offsets (device `offsets`
+ * and the same values on the host, B+1 entries); idx_out [B][m] int64 global rows.  n >= m for
+ * every fragment, n <= 81920. */
+int mvr_fps(const float* xyz, const int64_t* offsets, const int64_t* offsets_host, int B, int m, int64_t* idx_out,
+            mvr_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * Feature-space (soft) nearest neighbour for a batch of fragment pairs.
  * Replaces lib/layers.py:44-88 Soft_NN.forward (+ pairwise_distance

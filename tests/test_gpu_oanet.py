@@ -120,3 +120,33 @@ def test_oanet_matches_oracle_batch_and_ragged_n(gpu):
         g["logits%d" % i], g["scores%d" % i] = o["logits"][i], o["scores"][i]
         g["R%d" % i], g["t%d" % i] = o["rot_est"][i], o["trans_est"][i]
     _check(out, g, atol_logit=2e-3)
+
+
+def test_procrustes_guard_group(gpu):
+    """Zero-row guard scope (oanet.py:177-178): guard_group=2 adds 1/N only to the group holding the
+    all-zero pair; guard_group=0 (the reference's single batch) adds it to every pair."""
+    import torch
+    from lib import _native as NV
+    from oracle.kabsch import kabsch
+    r = np.random.RandomState(4)
+    P, Npt = 4, 50
+    x1 = r.standard_normal((P, Npt, 3)).astype(np.float32)
+    x2 = (x1 @ np.linalg.qr(r.standard_normal((3, 3)))[0].astype(np.float32)) + 0.01 * r.standard_normal(
+        (P, Npt, 3)).astype(np.float32)
+    w = r.uniform(0.1, 1.0, (P, Npt)).astype(np.float32)
+    w[0] = 0.0
+    pos = (w > 0).sum(1).astype(np.int32)
+    for group, hit in ((2, [True, True, False, False]), (0, [True] * 4)):
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+        tx1, tx2, tw, tpos = t(x1), t(x2), t(w), t(pos)
+        R = torch.empty(P, 3, 3, device=gpu)
+        tt = torch.empty(P, 3, 1, device=gpu)
+        res = torch.empty(P, Npt, device=gpu)
+        L = NV.lib()
+        assert L.mvr_procrustes(NV.ptr(tx1), NV.ptr(tx2), Npt * 3, 3, NV.ptr(tw), Npt, NV.ptr(tpos), None, 0, P, Npt, 1,
+                                1e-7, NV.ptr(R), NV.ptr(tt), NV.ptr(res), Npt, None, 0, None, group, NV.stream()) == 0
+        wexp = w + np.where(np.array(hit)[:, None], np.float32(1.0 / Npt), np.float32(0))
+        np.testing.assert_allclose(tw.cpu().numpy(), wexp, rtol=1e-6, atol=1e-7)
+        Ro, to, _, _ = kabsch(x1, x2, wexp)
+        np.testing.assert_allclose(R.cpu().numpy(), Ro, atol=1e-5)
+        np.testing.assert_allclose(tt.cpu().numpy(), to, atol=1e-5)
