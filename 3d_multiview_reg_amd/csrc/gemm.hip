@@ -56,6 +56,7 @@ constexpr float NEG_BIG = -3.0e38f;
 struct KArgs {
   GemmArgs g;
   int persist;  // number of persistent workgroups
+  int m_fast;   // tile order: m-tiles fastest (see tile_of)
 };
 
 __device__ __forceinline__ float& f4(float4& v, int i) { return reinterpret_cast<float*>(&v)[i]; }
@@ -574,12 +575,21 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   const int S = my_tiles * nk;
   if (S <= 0) return;
 
+  // tile order: consecutive tiles share the operand that is re-read from HBM — the m-tiles of one
+  // B column block when A is batch-shared weights (L2-resident), else the n-tiles of one A row block
   auto tile_of = [&](int i, int& b, int& tm, int& tn) {
     const int t = xcd_slot() + i * gridDim.x;
-    tn = t % ntn;
-    const int r = t / ntn;
-    tm = r % ntm;
-    b = r / ntm;
+    if (ka.m_fast) {
+      tm = t % ntm;
+      const int r = t / ntm;
+      tn = r % ntn;
+      b = r / ntn;
+    } else {
+      tn = t % ntn;
+      const int r = t / ntn;
+      tm = r % ntm;
+      b = r / ntm;
+    }
   };
 
   // per-tile prologue vectors -> LDS (wave 0): per-k scale/shift (IN/BN)
@@ -846,6 +856,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   KArgs ka;
   ka.g = g;
   ka.persist = 2 * 256;  // 2 workgroups per CU (LDS-bound), 256 CUs
+  ka.m_fast = (g.sAb == 0 && gemm_mtiles(g.M) > 1) ? 1 : 0;
   const long long tiles = (long long)gemm_ntiles(g.N) * gemm_mtiles(g.M) * g.batch;
   if (tiles > 0x7fffffffLL) return MVR_EINVAL;
   const double fl = 2.0 * g.M * g.N * (double)g.K * g.batch;

@@ -13,6 +13,8 @@ bool enabled = false;
 std::vector<Rec> recs;
 std::vector<hipEvent_t> pool;
 std::vector<int> open_idx;  // stack of records awaiting their end event
+std::vector<int> seq_kind;  // launch order since mvr_prof_set (PMC attribution, tools/pmc_traffic.py)
+std::vector<double> seq_bytes;
 hipEvent_t get_ev() {
   if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
   hipEvent_t e;
@@ -40,6 +42,8 @@ void prof_begin(int kind, double flops, double bytes, hipStream_t s) {
   std::lock_guard<std::mutex> g(mu);
   Rec r{kind, get_ev(), nullptr, flops, bytes};
   (void)hipEventRecord(r.a, s);
+  seq_kind.push_back(kind);
+  seq_bytes.push_back(bytes);
   recs.push_back(r);
   open_idx.push_back((int)recs.size() - 1);
 }
@@ -60,6 +64,8 @@ extern "C" int mvr_prof_set(int on) {
   std::lock_guard<std::mutex> g(mu);
   drain();
   for (int k = 0; k < PK_COUNT; ++k) { tot_ms[k] = tot_fl[k] = tot_by[k] = 0; tot_n[k] = 0; }
+  seq_kind.clear();
+  seq_bytes.clear();
   enabled = on != 0;
   return MVR_OK;
 }
@@ -74,4 +80,16 @@ extern "C" int mvr_prof_get(int kind, double* ms, long long* launches, double* f
   if (flops) *flops = tot_fl[kind];
   if (bytes) *bytes = tot_by[kind];
   return MVR_OK;
+}
+
+// Launch sequence since mvr_prof_set(1): kind and algorithmic bytes of each profiled launch, in
+// order (up to cap entries); returns the number of launches recorded.
+extern "C" int mvr_prof_seq(int* kinds, double* bytes, int cap) {
+  std::lock_guard<std::mutex> g(mu);
+  const int n = (int)seq_kind.size();
+  for (int i = 0; i < n && i < cap; ++i) {
+    if (kinds) kinds[i] = seq_kind[i];
+    if (bytes) bytes[i] = seq_bytes[i];
+  }
+  return n;
 }

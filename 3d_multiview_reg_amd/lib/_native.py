@@ -80,6 +80,7 @@ _SIGS = {
                               c_vp, c_i64, c_vp]),
     "mvr_l2norm_rows": (c_int, [c_vp, c_i64, c_int, c_i64, c_vp]),
     "mvr_prof_set": (c_int, [c_int]),
+    "mvr_prof_seq": (c_int, [c_vp, c_vp, c_int]),
     "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "mvr_xs_to_channels": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp]),
@@ -133,6 +134,18 @@ PROF_KINDS = {"conv_pts": 0, "embed": 1, "pool": 2, "unpool": 3, "oafilter": 4, 
 
 def prof_set(on):
     check(lib().mvr_prof_set(int(on)), "mvr_prof_set")
+
+
+def prof_seq():
+    """[(kind name, algorithmic bytes)] of every profiled launch since prof_set(1), in order."""
+    import numpy as np
+    L = lib()
+    n = L.mvr_prof_seq(None, None, 0)
+    k = np.zeros(max(n, 1), np.int32)
+    b = np.zeros(max(n, 1), np.float64)
+    L.mvr_prof_seq(k.ctypes.data, b.ctypes.data, n)
+    names = {v: s for s, v in PROF_KINDS.items()}
+    return [(names.get(int(k[i]), str(int(k[i]))), float(b[i])) for i in range(n)]
 
 
 def prof_get(kind):

@@ -36,7 +36,13 @@ import torch  # noqa: E402
 
 METRIC = "point-cloud pairs/s (feat+match+filter+SVD), 3DMatch 20k-pt, 1/2/4/8 GPU"
 PEAK_FP32_TFLOPS = 157.3    # MI355X dense fp32 (vector == MFMA), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 16 * PEAK_FP32_TFLOPS   # dense bf16 MFMA (fp32 MFMA is 1/16 of it)
+# the OANet GEMMs run the 3-term bf16 split (6 bf16 MFMA products per fp32 product, csrc/gemm.hpp):
+# their fp32-equivalent MFMA ceiling
+PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
+GEMM_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter")
+MFMA_PEAKS = {"feat_nn": PEAK_SPLIT_TFLOPS, "spconv": PEAK_FP32_TFLOPS}
 
 
 def log(*a):
@@ -195,6 +201,8 @@ def main():
     ap.add_argument("--npts", type=int, default=5000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
+                    "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -234,6 +242,9 @@ def main():
         t1 = time.perf_counter()
         dt = t1 - t0
         prof = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
+        if args.prof_seq and rank == 0:
+            with open(args.prof_seq, "w") as f:
+                json.dump(_native.prof_seq(), f)
         _native.prof_set(0)
     if world > 1:
         import torch.distributed as dist
@@ -243,21 +254,35 @@ def main():
     pairs_per_step = int(rec.shape[-2]) * world
     value = pairs_per_step * args.steps / dt
 
-    # dominant kernel class by device time inside the timed region
+    # dominant kernel class by device time inside the timed region, priced against the roofline
+    # that binds it: arithmetic intensity vs the ridge of the MFMA path it runs on
     dom = max(prof, key=lambda k: prof[k][0])
     ms, nl, fl, by = prof[dom]
-    bound = "hbm" if dom in ("procrustes", "small", "sparse_misc") else "mfma"
+    mpeak = PEAK_SPLIT_TFLOPS if dom in GEMM_CLASSES else MFMA_PEAKS.get(dom, PEAK_FP32_TFLOPS)
+    ridge = mpeak * 1e12 / (PEAK_HBM_GBS * 1e9)                     # FLOP per byte
+    bound = "mfma" if (by > 0 and fl / by >= ridge) else "hbm"
+    avg_s = ms * 1e-3 / max(nl, 1)
     if bound == "mfma":
-        achieved = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-        peak, unit = PEAK_FP32_TFLOPS, "TFLOP/s"
+        achieved, peak, unit = fl / max(nl, 1) / avg_s / 1e12, mpeak, "TFLOP/s"
     else:
-        achieved = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        peak, unit = PEAK_HBM_GBS, "GB/s"
-    traffic = os.environ.get("MVR_PMC_TRAFFIC_BYTES")
-    roof = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": (float(traffic) if traffic else None),
+        achieved, peak, unit = by / max(nl, 1) / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    traffic, tsrc = None, None
+    tfile = os.environ.get("MVR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    if os.path.exists(tfile):
+        with open(tfile) as f:
+            tr = json.load(f)
+        if dom in tr.get("classes", {}):
+            traffic = tr["classes"][dom]["pmc_bytes_per_launch"]
+            tsrc = tr.get("source")
+    roof = {"bound": bound, "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": traffic,
             "kernel": dom, "launches_per_step": nl / max(args.steps, 1),
             "avg_launch_ms": round(ms / max(nl, 1), 4), "share_of_step": round(ms / (dt * 1e3), 3),
+            "arith_intensity": round(fl / by, 2) if by else None, "ridge": round(ridge, 1),
+            "algorithmic_bytes_per_launch": by / max(nl, 1),
+            "peak_note": ("split-bf16 MFMA fp32-equivalent peak = 16*157.3/6 TF" if dom in GEMM_CLASSES else
+                          "MI355X_MICROARCH.md"),
+            "traffic_source": tsrc,
             # per kernel class: [ms per step, algorithmic TFLOP/s, algorithmic GB/s]
             "classes": {k: [round(v[0] / args.steps, 3), round(v[2] / (v[0] * 1e9), 1), round(v[3] / (v[0] * 1e6))]
                         for k, v in prof.items() if v[1] and v[0] > 0}}
@@ -272,7 +297,7 @@ def main():
     line = {"metric": METRIC if args.workload == "scene" else METRIC + " [filter+SVD only: precomputed corr.]",
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32(bf16x3)", "data": "synthetic",
             "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:

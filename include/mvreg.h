@@ -210,6 +210,9 @@ int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, mvr_stream_t stream)
  * recorded events and returns totals since then (kinds: csrc/prof.hpp ProfKind). */
 int mvr_prof_set(int on);
 int mvr_prof_get(int kind, double* ms, long long* launches, double* flops, double* bytes);
+/* launch order since mvr_prof_set(1): kind and algorithmic bytes per profiled launch (<= cap);
+ * returns the count (joins rocprofv3 PMC dispatch rows to kernel classes) */
+int mvr_prof_seq(int* kinds, double* bytes, int cap);
 
 #ifdef __cplusplus
 }
