@@ -1,0 +1,87 @@
+// Split-bf16 matrix-core helpers shared by the fused kernels (gfx950, v_mfma_f32_32x32x16_bf16).
+//
+// fp32 operands are split into three bf16 terms, x = h + m + l to 2^-25 |x| (RNE at each step;
+// x - h and r - m are exact in fp32), and the products hh, hm, mh, mm, hl, lh are accumulated in
+// fp32 — fp32-level accuracy (the dropped ml, lm, ll terms are <= 2^-23 relative), see gemm.hpp
+// MATH_BF16X3.
+//
+// Operand maps of v_mfma_f32_32x32x16_bf16 (lane l, r = l & 31, h = l >> 5): A[row r][k = 8h + i],
+// B[k = 8h + i][col r] in element i = 0..7; C[row (q & 3) + 8 (q >> 2) + 4h][col r] in register q.
+// Registers 8s .. 8s+7 of a C tile are, as a B (or A) fragment of k-step s, its rows
+// 16s + 8(i >> 2) + 4h + (i & 3): the other operand must supply that same k order.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mvr {
+namespace bx {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned cvt_pk(f32x2 x) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
+}
+__device__ __forceinline__ f32x2 unpack(unsigned p) {
+  f32x2 r;
+  r.x = __uint_as_float(p << 16);
+  r.y = __uint_as_float(p & 0xffff0000u);
+  return r;
+}
+// two fp32 -> packed (h, m, l) bf16 pairs
+__device__ __forceinline__ void split2(f32x2 x, unsigned& H, unsigned& M, unsigned& L) {
+  H = cvt_pk(x);
+  const f32x2 r = x - unpack(H);
+  M = cvt_pk(r);
+  L = cvt_pk(r - unpack(M));
+}
+__device__ __forceinline__ void split4(const float4& a, u32x2& H, u32x2& M, u32x2& L) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split2(f32x2{a.x, a.y}, h0, m0, l0);
+  split2(f32x2{a.z, a.w}, h1, m1, l1);
+  H = u32x2{h0, h1};
+  M = u32x2{m0, m1};
+  L = u32x2{l0, l1};
+}
+__device__ __forceinline__ void split8(const float* v, bf16x8& h, bf16x8& m, bf16x8& l) {
+  unsigned hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split2(f32x2{v[2 * i], v[2 * i + 1]}, hh[i], mm[i], ll[i]);
+  const u32x4 H{hh[0], hh[1], hh[2], hh[3]}, M{mm[0], mm[1], mm[2], mm[3]}, L{ll[0], ll[1], ll[2], ll[3]};
+  h = __builtin_bit_cast(bf16x8, H);
+  m = __builtin_bit_cast(bf16x8, M);
+  l = __builtin_bit_cast(bf16x8, L);
+}
+
+struct Frag {
+  bf16x8 h, m, l;
+};
+
+// acc += A . B over the six significant split products, small terms first
+__device__ __forceinline__ floatx16 mfma6(const Frag& a, const Frag& b, floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
+  return acc;
+}
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q, columns 4p..4p+3 of a 4x16
+// block of 16-bit elements; lane i of the group receives column i (rows 0..3 in elements 0..3).
+// EXEC must be all ones.
+__device__ __forceinline__ u32x2 ds_read_tr(const char* lds) {
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  const i16x4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_i16x4*)(const __attribute__((address_space(3))) char*)lds);
+  return __builtin_bit_cast(u32x2, r);
+}
+
+}  // namespace bx
+}  // namespace mvr

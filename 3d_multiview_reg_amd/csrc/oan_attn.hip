@@ -1,0 +1,581 @@
+// Fused diff_pool / diff_unpool of the OANet block (lib/filtering/oanet.py:96-129) as flash-style
+// attention on the split-bf16 matrix cores (mfma_bf16.hpp).
+//
+// diff_pool (oanet.py:96-110), per pair:   x_down[c][j] = sum_n x[c][n] softmax_n(e[j][n])
+// diff_unpool (oanet.py:113-129), per pair: out[c][n]   = sum_j x_down[c][j] softmax_j(e[j][n])
+// with e = W . relu(x * sc + sh) + b (the InstanceNorm + BatchNorm + ReLU of the embedding conv
+// folded per (pair, channel) by in_finalize_kernel).  The reference materialises the [clusters x
+// points] embedding and softmax (10 MB per pair, written and re-read twice per block); here it
+// never leaves registers: each 512-thread workgroup owns 256 queries (8 waves x 32, one query per
+// lane column, two waves per SIMD) and streams the keys through a double-buffered LDS ring shared
+// by the 8 waves, with an online softmax (running max / sum per query, base 2).
+//
+//   pool:   queries j (clusters, W rows held split in registers), keys n (points, 32 per stage).
+//           S^T[n][j] = xn^T . W^T  -> softmax over n is over the rows of a lane's column
+//           O[c][j]  += x[c][n] . P[n][j]   (P taken from the S^T registers, no LDS trip)
+//           The x tile of a stage is split on its way into LDS twice: normalised (K image, read
+//           transposed with ds_read_b64_tr_b16) and raw (V image, n in the C-register k order).
+//   unpool: queries n (points, xn split in registers), keys j (clusters, 32 per stage) from
+//           images pre-split in HBM by split_w_kernel / split_xd_kernel and staged by LDS-DMA.
+// Inside a stage the operand fragments are software-pipelined one MFMA group ahead
+// (sched_barrier fences keep the compiler from sinking the reads to their uses).
+//
+// Channels are fixed at 128 (OANet net_channels, RegBlock.yaml).  Epilogue: the output tile goes
+// through LDS for coalesced row stores and the per-(pair, channel, 128-column tile) (sum, squared
+// deviations) partials that the next InstanceNorm needs (gemm.hpp ST_ROW).
+//
+// Roofline: 4 * C * clusters * points flops per pair on the split MFMA (6 bf16 MFMAs per fp32
+// product: 16 * 157.3 / 6 = 419 TF/s fp32-equivalent); HBM traffic ~ x once + the output.
+#include "common.hpp"
+#include "mfma_bf16.hpp"
+#include "prof.hpp"
+#include "mvreg.h"
+
+namespace mvr {
+
+using namespace bx;
+
+constexpr int AC = 128;                  // channels
+constexpr int AKB = 32;                  // keys per stage
+constexpr int AQ = 256;                  // queries per workgroup (8 waves x 32)
+constexpr int ATHREADS = 512;
+constexpr int ATL = AQ + 4;              // fp32 row stride of the epilogue tile in LDS
+constexpr int PLANE = AC * AKB * 2;      // bytes of one bf16 plane of a stage image (8 KB)
+constexpr int IMG = 3 * PLANE;           // h, m, l planes (24 KB)
+constexpr int STAGE_B = 2 * IMG;         // one stage: two images (48 KB)
+constexpr int MAX_CLUSTERS = 1024;
+// unpool W image: [32 j][128 c] bf16 rows padded to 272 bytes (row r starts 17 r bank quads in, so
+// the 16 rows of a ds_read_b128 lane group are conflict-free and a k-step is an immediate offset),
+// image padded to 27 KB so that a stage (W image + x_down image) is a whole number of 1 KB DMAs
+constexpr int WROW = 272;
+constexpr int WPLANE = 32 * WROW;
+constexpr int WIMG = 27 * 1024;
+constexpr int USTAGE = WIMG + IMG;       // 51 KB
+static_assert(3 * WPLANE <= WIMG, "W image padding");
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float A_NEG = -3.0e38f;
+static_assert(64 * ATL * 4 <= 2 * STAGE_B, "epilogue half tile must fit the stage ring");
+
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// Byte offset of the 4 keys 4q .. 4q+3 (q = 0..7) of row `row` in a [row][32 keys] bf16 image
+// whose 16-byte chunk (s, h) holds the 8 keys of k-step s, lane half h in the C-register k order
+// (keys 16s + 4h + 0..3 and 16s + 8 + 4h + 0..3), chunk slot XOR-swizzled by (row >> 2) & 3 so
+// that the 32 rows of an A-fragment read are conflict-free.
+__device__ __forceinline__ int kord_off(int row, int q) {
+  const int s = q >> 2, a = (q >> 1) & 1, h = q & 1;
+  return row * 64 + 16 * ((2 * s + h) ^ ((row >> 2) & 3)) + 8 * a;
+}
+// A fragment (row = 32 cb + lane row, k-step s) of such an image
+__device__ __forceinline__ Frag kord_frag(const char* img, int row, int s, int h) {
+  const int off = row * 64 + 16 * ((2 * s + h) ^ ((row >> 2) & 3));
+  Frag f;
+  f.h = *reinterpret_cast<const bf16x8*>(img + off);
+  f.m = *reinterpret_cast<const bf16x8*>(img + PLANE + off);
+  f.l = *reinterpret_cast<const bf16x8*>(img + 2 * PLANE + off);
+  return f;
+}
+
+template <int X>
+__device__ __forceinline__ float swz_x(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (X << 10)));
+}
+__device__ __forceinline__ float half_sum(float v) {   // sum over the 32 lanes of a wave half
+  v += swz_x<1>(v);
+  v += swz_x<2>(v);
+  v += swz_x<4>(v);
+  v += swz_x<8>(v);
+  v += swz_x<16>(v);
+  return v;
+}
+
+// Workgroup -> (pair, block): the blocks of 8 consecutive pairs are interleaved so that all
+// blocks of one pair are dealt to the same XCD (round-robin dispatch: b and b + 8 share one),
+// where they share the pair's operands in L2.
+__device__ __forceinline__ void pair_block(int nblk, int& p, int& blk) {
+  const int b = blockIdx.x, x = b & 7, t = b >> 3;
+  blk = t % nblk;
+  p = (t / nblk) * 8 + x;
+}
+
+// Online softmax over the 16 rows of a lane column (+ the partner half): v holds logits * log2e.
+// Updates (m, l), rescales O, and leaves the probabilities in v.
+__device__ __forceinline__ void online_softmax(float (&v)[16], float& m, float& l, floatx16 (&O)[4]) {
+  float bm = v[0];
+#pragma unroll
+  for (int r = 1; r < 16; ++r) bm = fmaxf(bm, v[r]);
+  bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+  const float mn = fmaxf(m, bm);
+  const float alpha = __builtin_amdgcn_exp2f(m - mn);
+  m = mn;
+  float ps = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    v[r] = __builtin_amdgcn_exp2f(v[r] - mn);
+    ps += v[r];
+  }
+  l = fmaf(l, alpha, ps);
+  if (__any(alpha != 1.f)) {
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) O[cb] *= alpha;
+  }
+}
+
+// O (rows c = 32 cb + (q & 3) + 8 (q >> 2) + 4h, column = 32 w + lane row) * inv -> out[c][col0 + col]
+// for columns < L (zeros in [L, round4(L))), and, per 128-column tile t of the 256 (tile index
+// col0 / 128 + t), st[t * st_tile + c] = (sum, squared deviations) over the tile's valid columns.
+// T: LDS scratch of 64 x ATL floats (two passes of 64 rows); the caller has synchronised.
+__device__ __forceinline__ void tile_out(float* T, const floatx16 (&O)[4], float inv, bool colok, float* out,
+                                         int64_t ld, int col0, int L, float2* st, int64_t st_tile) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int col = 32 * w + l32;
+  const int Lp = (L + 3) & ~3;
+  const int nv = min(max(L - col0 - 128 * h, 0), 128);   // valid columns of this lane half's tile
+  const float rnv = nv > 0 ? 1.f / (float)nv : 0.f;
+  bool ok[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ok[u] = 4 * l32 + u < nv;
+  const bool sok = col0 + 4 * lane < Lp;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = 32 * cc + (q & 3) + 8 * (q >> 2) + 4 * h;
+        T[c * ATL + col] = colok ? O[2 * hf + cc][q] * inv : 0.f;
+      }
+    __syncthreads();
+    for (int it = 0; it < 8; ++it) {
+      const int cl = 8 * w + it, c = 64 * hf + cl;
+      float4 x = *reinterpret_cast<const float4*>(T + cl * ATL + 4 * lane);
+      if (!ok[0]) x.x = 0.f;
+      if (!ok[1]) x.y = 0.f;
+      if (!ok[2]) x.z = 0.f;
+      if (!ok[3]) x.w = 0.f;
+      if (st) {
+        const float sm = half_sum((x.x + x.y) + (x.z + x.w));
+        const float mu = sm * rnv;
+        const float d0 = ok[0] ? x.x - mu : 0.f, d1 = ok[1] ? x.y - mu : 0.f, d2 = ok[2] ? x.z - mu : 0.f,
+                    d3 = ok[3] ? x.w - mu : 0.f;
+        const float m2 = half_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+        if (l32 == 0 && nv > 0) st[h * st_tile + c] = make_float2(sm, m2);
+      }
+      if (sok) *reinterpret_cast<float4*>(out + (int64_t)c * ld + col0 + 4 * lane) = x;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// diff_pool
+// ---------------------------------------------------------------------------------------------
+struct PoolArgs {
+  const float* X; int64_t xps, xld;                // x [P][128][xld] (raw)
+  const float* sc; const float* sh; int64_t sps;   // folded IN+BN: xn = relu(x * sc[c] + sh[c])
+  const float* W; const float* bias;               // embedding conv [Kc][128], [Kc]
+  int P, N, Kc, nqb;                               // nqb = ceil(Kc / 256) query blocks
+  float* out; int64_t ops, old;                    // x_down [P][128][old]
+  float2* stats; int64_t st_ld; int st_off;        // [P][ceil(Kc/128)][st_ld] (+ st_off + c), nullable
+};
+
+__global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  int p, jb;
+  pair_block(a.nqb, p, jb);
+  if (p >= a.P) return;   // uniform over the workgroup
+  const float* X = a.X + (int64_t)p * a.xps;
+  const int N = a.N;
+  const int nkb = (N + AKB - 1) / AKB;
+  const int nlast = ((N + 3) & ~3) - 4;   // last readable 4-key group of a row
+
+  // staging map: thread tid, i = 0..1 -> channel c = tid / 8 + 64 i, keys 4 (tid & 7) .. +3
+  const int sq = tid & 7;
+  float4 xr[2];
+  auto load_tile = [&](int kb) {
+    const int n = kb * AKB + 4 * sq;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = (tid >> 3) + 64 * i;
+      const float4 v = *reinterpret_cast<const float4*>(X + (int64_t)c * a.xld + min(n, nlast));
+      xr[i] = n < N ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  load_tile(0);
+
+  // queries: this lane's W row (column j of S^T) as split B fragments, one per 16-channel k-step
+  const int j = jb * AQ + 32 * w + l32;
+  const bool jok = j < a.Kc;
+  const float* wr = a.W + (int64_t)min(j, a.Kc - 1) * AC + 8 * h;
+  Frag q[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * ks);
+    const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * ks + 4);
+    float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = jok ? v[i] : 0.f;
+    split8(v, q[ks].h, q[ks].m, q[ks].l);
+  }
+  const float bj = (jok && a.bias) ? a.bias[j] : 0.f;
+  float scv[2], shv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = (tid >> 3) + 64 * i;
+    scv[i] = a.sc[(int64_t)p * a.sps + c];
+    shv[i] = a.sh[(int64_t)p * a.sps + c];
+  }
+  auto store_tile = [&](int st) {
+    char* K = smem + st * STAGE_B;
+    char* V = K + IMG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = (tid >> 3) + 64 * i;
+      u32x2 H, M, L;
+      split4(xr[i], H, M, L);
+      const int vo = kord_off(c, sq);
+      *reinterpret_cast<u32x2*>(V + vo) = H;
+      *reinterpret_cast<u32x2*>(V + PLANE + vo) = M;
+      *reinterpret_cast<u32x2*>(V + 2 * PLANE + vo) = L;
+      const float4 xn = make_float4(fmaxf(fmaf(xr[i].x, scv[i], shv[i]), 0.f), fmaxf(fmaf(xr[i].y, scv[i], shv[i]), 0.f),
+                                    fmaxf(fmaf(xr[i].z, scv[i], shv[i]), 0.f), fmaxf(fmaf(xr[i].w, scv[i], shv[i]), 0.f));
+      split4(xn, H, M, L);
+      const int ko = c * 64 + 8 * sq;
+      *reinterpret_cast<u32x2*>(K + ko) = H;
+      *reinterpret_cast<u32x2*>(K + PLANE + ko) = M;
+      *reinterpret_cast<u32x2*>(K + 2 * PLANE + ko) = L;
+    }
+  };
+
+  floatx16 O[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[cb][r] = 0.f;
+  float m = A_NEG, l = 0.f;
+
+  // transposed-read address of the K image: row c0 + (lane & 15) / 4, keys 16 (g & 1) + 4 (lane & 3)
+  const int g = lane >> 4;
+  const int tr_off = ((lane & 15) >> 2) * 64 + 32 * (g & 1) + 8 * (lane & 3);
+  auto read_k = [&](const char* K, int ks) {
+    const int o0 = (16 * ks + 8 * h) * 64 + tr_off, o1 = o0 + 4 * 64;
+    Frag f;
+    u32x2 t0 = ds_read_tr(K + o0), t1 = ds_read_tr(K + o1);
+    f.h = __builtin_bit_cast(bf16x8, u32x4{t0[0], t0[1], t1[0], t1[1]});
+    t0 = ds_read_tr(K + PLANE + o0);
+    t1 = ds_read_tr(K + PLANE + o1);
+    f.m = __builtin_bit_cast(bf16x8, u32x4{t0[0], t0[1], t1[0], t1[1]});
+    t0 = ds_read_tr(K + 2 * PLANE + o0);
+    t1 = ds_read_tr(K + 2 * PLANE + o1);
+    f.l = __builtin_bit_cast(bf16x8, u32x4{t0[0], t0[1], t1[0], t1[1]});
+    return f;
+  };
+
+  store_tile(0);
+  load_tile(1);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int st = kb & 1;
+    store_tile(st ^ 1);   // tile kb + 1 (zeros past the end)
+    load_tile(kb + 2);
+    const char* K = smem + st * STAGE_B;
+    const char* V = K + IMG;
+    // S^T[n][j] = sum_c xn[c][n] W[j][c], fragments one k-step ahead
+    floatx16 S;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) S[r] = 0.f;
+    Frag cur = read_k(K, 0);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      Frag nxt;
+      if (ks < 7) nxt = read_k(K, ks + 1);
+      SCHED_FENCE();
+      S = mfma6(cur, q[ks], S);
+      SCHED_FENCE();
+      if (ks < 7) cur = nxt;
+    }
+    Frag vf = kord_frag(V, l32, 0, h);   // first V fragment, in flight during the softmax
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = kb * AKB + (r & 3) + 8 * (r >> 2) + 4 * h;
+      v[r] = n < N ? (S[r] + bj) * LOG2E : -__builtin_inff();
+    }
+    online_softmax(v, m, l, O);
+    Frag pf[2];
+    split8(v, pf[0].h, pf[0].m, pf[0].l);
+    split8(v + 8, pf[1].h, pf[1].m, pf[1].l);
+    // O[c][j] += sum_n x[c][n] P[n][j]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int s = i >> 2, cb = i & 3;
+      Frag nxt;
+      if (i < 7) nxt = kord_frag(V, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2, h);
+      SCHED_FENCE();
+      O[cb] = mfma6(vf, pf[s], O[cb]);
+      SCHED_FENCE();
+      if (i < 7) vf = nxt;
+    }
+    __syncthreads();
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const int ntile = (a.Kc + 127) / 128;
+  tile_out(reinterpret_cast<float*>(smem), O, inv, jok, a.out + (int64_t)p * a.ops, a.old, jb * AQ, a.Kc,
+           a.stats ? a.stats + ((int64_t)p * ntile + 2 * jb) * a.st_ld + a.st_off : nullptr, a.st_ld);
+}
+
+// ---------------------------------------------------------------------------------------------
+// diff_unpool
+// ---------------------------------------------------------------------------------------------
+// W [Kc][128] -> image [nkb][3 planes][32 j][WROW bytes] bf16 (WIMG bytes per block); rows j >= Kc zero.
+__global__ void split_w_kernel(const float* __restrict__ W, int Kc, int nkb, char* img) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nkb * 512) return;
+  const int ch = i & 15, jj = (i >> 4) & 31, kb = i >> 9;
+  const int j = kb * AKB + jj;
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = j < Kc ? W[(int64_t)j * AC + 8 * ch + e] : 0.f;
+  Frag f;
+  split8(v, f.h, f.m, f.l);
+  char* base = img + (int64_t)kb * WIMG + jj * WROW + 16 * ch;
+  *reinterpret_cast<bf16x8*>(base) = f.h;
+  *reinterpret_cast<bf16x8*>(base + WPLANE) = f.m;
+  *reinterpret_cast<bf16x8*>(base + 2 * WPLANE) = f.l;
+}
+
+// x_down [P][128][ld] (Kc valid columns) -> image [P][nkb][3 planes][128 c][32 j] (kord_off order)
+__global__ void split_xd_kernel(const float* __restrict__ XD, int64_t ps, int64_t ld, int P, int Kc, int nkb,
+                                char* img) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)P * nkb * 1024) return;
+  const int q = (int)(i & 7), c = (int)((i >> 3) & 127);
+  const int64_t pk = i >> 10;   // p * nkb + kb
+  const int kb = (int)(pk % nkb);
+  const int64_t p = pk / nkb;
+  const int j0 = kb * AKB + 4 * q;
+  const float* src = XD + p * ps + (int64_t)c * ld;
+  const float4 x = make_float4(j0 < Kc ? src[j0] : 0.f, j0 + 1 < Kc ? src[j0 + 1] : 0.f,
+                               j0 + 2 < Kc ? src[j0 + 2] : 0.f, j0 + 3 < Kc ? src[j0 + 3] : 0.f);
+  u32x2 H, M, L;
+  split4(x, H, M, L);
+  char* base = img + pk * IMG + kord_off(c, q);
+  *reinterpret_cast<u32x2*>(base) = H;
+  *reinterpret_cast<u32x2*>(base + PLANE) = M;
+  *reinterpret_cast<u32x2*>(base + 2 * PLANE) = L;
+}
+
+struct UnpoolArgs {
+  const float* X; int64_t xps, xld;                // x_up [P][128][xld] (raw)
+  const float* sc; const float* sh; int64_t sps;   // folded IN+BN of the embedding input
+  const char* wimg;                                // split_w_kernel image [nkb][WIMG]
+  const float* bias;                               // [Kc], nullable
+  const char* dimg;                                // split_xd_kernel image [P][nkb][IMG]
+  int P, N, Kc, nkb, nqb;                          // nqb = ceil(N / 256) query blocks
+  float* out; int64_t ops, old;                    // [P][128][old]
+  float2* stats; int64_t st_ld; int st_off;        // [P][ceil(N/128)][st_ld] (+ st_off + c), nullable
+};
+
+__device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+
+__global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * USTAGE];
+  __shared__ __attribute__((aligned(16))) float bsh[MAX_CLUSTERS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  int p, nb;
+  pair_block(a.nqb, p, nb);
+  if (p >= a.P) return;
+  const int N = a.N, nkb = a.nkb;
+  const char* dimg = a.dimg + (int64_t)p * nkb * IMG;
+
+  // a 51 KB stage (W image block, then x_down image block) as 1 KB LDS-DMAs dealt over the 8 waves
+  auto issue = [&](int kb, int st) {
+    char* dst = smem + st * USTAGE;
+    for (int off = w * 1024; off < USTAGE; off += 8 * 1024) {
+      const char* src = off < WIMG ? a.wimg + (int64_t)kb * WIMG + off : dimg + (int64_t)kb * IMG + (off - WIMG);
+      glds16b(src + 16 * lane, dst + off);
+    }
+  };
+  issue(0, 0);
+
+  // queries: this lane's point n (column), xn[c][n] for c = 16 ks + 8h + i as split B fragments
+  const int n = nb * AQ + 32 * w + l32;
+  const bool nok = n < N;
+  const float* xq = a.X + (int64_t)p * a.xps + min(n, N - 1);
+  const float* sc = a.sc + (int64_t)p * a.sps;
+  const float* sh = a.sh + (int64_t)p * a.sps;
+  Frag q[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = 16 * ks + 8 * h + i;
+      const float x = fmaxf(fmaf(xq[(int64_t)c * a.xld], sc[c], sh[c]), 0.f);
+      v[i] = nok ? x : 0.f;
+    }
+    split8(v, q[ks].h, q[ks].m, q[ks].l);
+  }
+  for (int i = tid; i < nkb * AKB; i += ATHREADS)
+    bsh[i] = i < a.Kc ? (a.bias ? a.bias[i] : 0.f) : -__builtin_inff();
+
+  floatx16 O[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[cb][r] = 0.f;
+  float m = A_NEG, l = 0.f;
+
+  const int wbase = l32 * WROW + 16 * h;
+  auto read_w = [&](const char* Wi, int ks) {
+    const int off = wbase + 32 * ks;
+    Frag f;
+    f.h = *reinterpret_cast<const bf16x8*>(Wi + off);
+    f.m = *reinterpret_cast<const bf16x8*>(Wi + WPLANE + off);
+    f.l = *reinterpret_cast<const bf16x8*>(Wi + 2 * WPLANE + off);
+    return f;
+  };
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int st = kb & 1;
+    if (kb + 1 < nkb) issue(kb + 1, st ^ 1);
+    const char* Wi = smem + st * USTAGE;
+    const char* D = Wi + WIMG;
+    // S[j][n] = sum_c W[j][c] xn[c][n], fragments one k-step ahead
+    floatx16 S;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) S[r] = 0.f;
+    Frag cur = read_w(Wi, 0);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      Frag nxt;
+      if (ks < 7) nxt = read_w(Wi, ks + 1);
+      SCHED_FENCE();
+      S = mfma6(cur, q[ks], S);
+      SCHED_FENCE();
+      if (ks < 7) cur = nxt;
+    }
+    Frag df = kord_frag(D, l32, 0, h);
+    float v[16];
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const float4 b = *reinterpret_cast<const float4*>(bsh + kb * AKB + 8 * r4 + 4 * h);
+      v[4 * r4 + 0] = (S[4 * r4 + 0] + b.x) * LOG2E;
+      v[4 * r4 + 1] = (S[4 * r4 + 1] + b.y) * LOG2E;
+      v[4 * r4 + 2] = (S[4 * r4 + 2] + b.z) * LOG2E;
+      v[4 * r4 + 3] = (S[4 * r4 + 3] + b.w) * LOG2E;
+    }
+    online_softmax(v, m, l, O);
+    Frag pf[2];
+    split8(v, pf[0].h, pf[0].m, pf[0].l);
+    split8(v + 8, pf[1].h, pf[1].m, pf[1].l);
+    // O[c][n] += sum_j x_down[c][j] P[j][n]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int s = i >> 2, cb = i & 3;
+      Frag nxt;
+      if (i < 7) nxt = kord_frag(D, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2, h);
+      SCHED_FENCE();
+      O[cb] = mfma6(df, pf[s], O[cb]);
+      SCHED_FENCE();
+      if (i < 7) df = nxt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  const int ntile = (N + 127) / 128;
+  tile_out(reinterpret_cast<float*>(smem), O, inv, nok, a.out + (int64_t)p * a.ops, a.old, nb * AQ, N,
+           a.stats ? a.stats + ((int64_t)p * ntile + 2 * nb) * a.st_ld + a.st_off : nullptr, a.st_ld);
+}
+
+}  // namespace mvr
+
+using namespace mvr;
+
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+static int64_t round_up4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+
+extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int clusters) {
+  if (P <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return 0;
+  const size_t nkb = (size_t)(clusters + AKB - 1) / AKB;
+  return nkb * (WIMG + (size_t)P * IMG) + 256;
+}
+
+extern "C" int mvr_oan_diff_pool(const float* x, int64_t x_pstride, int64_t x_ld, const float* sc, const float* sh,
+                                 int64_t s_pstride, const float* weight, const float* bias, int P, int channels, int N,
+                                 int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats,
+                                 int64_t st_ld, int st_off, hipStream_t stream) {
+  if (!x || !sc || !sh || !weight || !out || P < 0 || N <= 0 || channels != AC || clusters <= 0 ||
+      clusters > MAX_CLUSTERS)
+    return MVR_EINVAL;
+  if (x_ld < round_up4(N) || (x_ld & 3) || (x_pstride & 3) || !al16(x) || !al16(weight) || !al16(out) ||
+      out_ld < round_up4(clusters) || (out_ld & 3) || (out_pstride & 3) || (stats && (st_ld < channels + st_off)))
+    return MVR_EINVAL;
+  if (P == 0) return MVR_OK;
+  PoolArgs a{};
+  a.X = x; a.xps = x_pstride; a.xld = x_ld;
+  a.sc = sc; a.sh = sh; a.sps = s_pstride;
+  a.W = weight; a.bias = bias;
+  a.P = P; a.N = N; a.Kc = clusters; a.nqb = (clusters + AQ - 1) / AQ;
+  a.out = out; a.ops = out_pstride; a.old = out_ld;
+  a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
+  const double fl = 4.0 * AC * clusters * (double)N * P;
+  const double by = 4.0 * AC * ((double)N + clusters) * P;
+  ProfScope prof(PK_POOL, fl, by, stream);
+  const int grid = ((P + 7) / 8) * 8 * a.nqb;
+  hipLaunchKernelGGL(oan_pool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t x_ld, const float* sc,
+                                   const float* sh, int64_t s_pstride, const float* weight, const float* bias,
+                                   const float* x_down, int64_t xd_pstride, int64_t xd_ld, int P, int channels,
+                                   int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats,
+                                   int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
+                                   hipStream_t stream) {
+  if (!x_up || !sc || !sh || !weight || !x_down || !out || !workspace || P < 0 || N <= 0 || channels != AC ||
+      clusters <= 0 || clusters > MAX_CLUSTERS)
+    return MVR_EINVAL;
+  if ((x_ld < round_up4(N)) || (x_ld & 3) || (x_pstride & 3) || xd_ld < clusters || out_ld < round_up4(N) ||
+      (out_ld & 3) || (out_pstride & 3) || !al16(out) || !al16(workspace) || (stats && (st_ld < channels + st_off)))
+    return MVR_EINVAL;
+  if (P == 0) return MVR_OK;
+  if (workspace_bytes < mvr_oan_diff_unpool_workspace_bytes(P, channels, clusters)) return MVR_EINVAL;
+  const int nkb = (clusters + AKB - 1) / AKB;
+  char* wimg = reinterpret_cast<char*>(workspace);
+  char* dimg = wimg + (size_t)nkb * WIMG;
+  const double fl = 4.0 * AC * clusters * (double)N * P;
+  const double by = 4.0 * AC * (2.0 * N + clusters) * P;
+  ProfScope prof(PK_UNPOOL, fl, by, stream);
+  hipLaunchKernelGGL(split_w_kernel, dim3((nkb * 512 + 255) / 256), dim3(256), 0, stream, weight, clusters, nkb, wimg);
+  MVR_CHECK_LAUNCH();
+  const int64_t nx = (int64_t)P * nkb * 1024;
+  hipLaunchKernelGGL(split_xd_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, stream, x_down, xd_pstride,
+                     xd_ld, P, clusters, nkb, dimg);
+  MVR_CHECK_LAUNCH();
+  UnpoolArgs a{};
+  a.X = x_up; a.xps = x_pstride; a.xld = x_ld;
+  a.sc = sc; a.sh = sh; a.sps = s_pstride;
+  a.wimg = wimg; a.bias = bias; a.dimg = dimg;
+  a.P = P; a.N = N; a.Kc = clusters; a.nkb = nkb; a.nqb = (N + AQ - 1) / AQ;
+  a.out = out; a.ops = out_pstride; a.old = out_ld;
+  a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
+  const int grid = ((P + 7) / 8) * 8 * a.nqb;
+  hipLaunchKernelGGL(oan_unpool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}

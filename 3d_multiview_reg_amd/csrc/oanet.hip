@@ -166,6 +166,8 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
+int g_oan_fused = 1;   // mvr_set_oan_fused
+
 namespace {
 
 struct Act {
@@ -193,24 +195,30 @@ struct Ws {
 struct Plan {
   int P, N, C, Kc, Cin;
   int64_t Np, Kp, Cinp;  // padded row lengths (points, clusters, conv1 input channels)
+  bool fused;            // diff_pool / diff_unpool as fused attention kernels (oan_attn.hip)
+  char* uimg;            // their split-bf16 operand images
+  size_t uimg_bytes;
   size_t bytes;
   float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *fac, *W1;
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
 };
 
 // Activations [P][C][Np] over points and [P][C][Kp] over clusters, rows padded to a multiple of 4
-// floats (16-byte rows for the LDS-DMA staging of gemm.hip).
+// floats (16-byte rows for the LDS-DMA staging of gemm.hip).  With 128 channels (the reference
+// configuration) diff_pool / diff_unpool run fused (oan_attn.hip) and the [clusters x points]
+// embedding buffer and its softmax factors are not allocated.
 Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   Plan pl{};
   pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc; pl.Cin = Cin;
   pl.Np = round4(N); pl.Kp = round4(Kc); pl.Cinp = round4(Cin);
+  pl.fused = g_oan_fused && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
   Ws w{reinterpret_cast<char*>(base), 0, 0};
   const size_t PN = (size_t)P * pl.Np, PK = (size_t)P * pl.Kp;
   const int TN = gemm_ntiles(N), TK = gemm_ntiles(Kc), MK = gemm_mtiles(Kc), MC = gemm_mtiles(C);
   pl.X11 = w.take<float>(PN * 2 * C);
   pl.XA = w.take<float>(PN * C);
   pl.T1 = w.take<float>(PN * C);
-  pl.E = w.take<float>(PN * Kc);
+  pl.E = pl.fused ? nullptr : w.take<float>(PN * Kc);
   pl.XD = w.take<float>(PK * C);
   pl.O1 = w.take<float>(PK * C);
   pl.O2 = w.take<float>(PK * C);
@@ -220,7 +228,7 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.shK = w.take<float>(pl.Kp);
   size_t nf = (size_t)P * TN * pl.Kp;
   if ((size_t)P * MK * pl.Np > nf) nf = (size_t)P * MK * pl.Np;
-  pl.fac = w.take<float>(nf);
+  pl.fac = pl.fused ? nullptr : w.take<float>(nf);
   pl.W1 = w.take<float>((size_t)C * pl.Cinp);
   pl.st11 = w.take<float2>((size_t)P * TN * 2 * C);
   pl.stA = w.take<float2>((size_t)P * TN * C);
@@ -229,7 +237,9 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.stO = w.take<float2>((size_t)P * TK * C);
   size_t smx = (size_t)P * TN * Kc;
   if ((size_t)P * MK * N > smx) smx = (size_t)P * MK * N;
-  pl.smx = w.take<float2>(smx);
+  pl.smx = pl.fused ? nullptr : w.take<float2>(smx);
+  pl.uimg_bytes = pl.fused ? mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) : 0;
+  pl.uimg = pl.fused ? w.take<char>(pl.uimg_bytes) : nullptr;
   pl.mv = w.take<float2>((size_t)P * 2 * C);
   pl.stcol = w.take<float2>((size_t)P * MC * Kc);
   pl.bytes = w.off + 256;
@@ -334,6 +344,12 @@ struct Ctx {
 
 using namespace mvr;
 
+extern "C" int mvr_set_oan_fused(int on) {
+  const int prev = g_oan_fused;
+  g_oan_fused = on != 0;
+  return prev;
+}
+
 extern "C" size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N) {
   return plan(channels, clusters, in_channels, P, N, nullptr).bytes;
 }
@@ -375,11 +391,14 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
 
   // diff_pool (oanet.py:96-110): E = exp(embed - tile max) over points, x_down = x . softmax(E)^T
   cx.finalize_in(x11top, 1e-3f, blk->down_bn);
-  Act e{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, Kc, 0};
-  cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);
-  cx.smx_factors(TN, Kc, Kp);
   Act xd{pl.XD, (int64_t)C * Kp, Kp, C, Kc, pl.stD, C, 0};
-  {
+  if (pl.fused) {
+    cx.chk(mvr_oan_diff_pool(pl.X11, 2 * CN, Np, pl.sc, pl.sh, C, blk->down_conv.weight, blk->down_conv.bias, P, C,
+                             N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD), C, 0, s));
+  } else {
+    Act e{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, Kc, 0};
+    cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);
+    cx.smx_factors(TN, Kc, Kp);
     GemmArgs g{};
     g.math = g_default_math;
     g.M = C; g.N = Kc; g.K = N; g.batch = P;
@@ -396,11 +415,15 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
 
   // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C): softmax over clusters
   cx.finalize_in(x11top, 1e-3f, blk->up_bn);
-  Act e2{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, N, 0};
-  cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX);
-  const int MK = gemm_mtiles(Kc);
-  cx.smx_factors(MK, N, Np);
-  {
+  if (pl.fused) {
+    cx.chk(mvr_oan_diff_unpool(pl.X11, 2 * CN, Np, pl.sc, pl.sh, C, blk->up_conv.weight, blk->up_conv.bias, pl.XD,
+                               (int64_t)C * Kp, Kp, P, C, N, Kc, pl.X11 + CN, 2 * CN, Np,
+                               reinterpret_cast<float*>(pl.st11), 2 * C, C, pl.uimg, pl.uimg_bytes, s));
+  } else {
+    Act e2{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, N, 0};
+    cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX);
+    const int MK = gemm_mtiles(Kc);
+    cx.smx_factors(MK, N, Np);
     GemmArgs g{};
     g.math = g_default_math;
     g.M = C; g.N = N; g.K = Kc; g.batch = P;

@@ -56,6 +56,12 @@ _SIGS = {
                              c_int, c_int, c_vp]),
     "mvr_set_gemm_math": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
+    "mvr_set_oan_fused": (c_int, [c_int]),
+    "mvr_oan_diff_pool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                  c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp]),
+    "mvr_oan_diff_unpool_workspace_bytes": (c_size, [c_int, c_int, c_int]),
+    "mvr_oan_diff_unpool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_int,
+                                    c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp, c_size, c_vp]),
     "mvr_oan_block_forward": (c_int, [ctypes.POINTER(OanBlockP), c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_vp,
                                       c_size, c_vp]),

@@ -104,6 +104,10 @@ typedef struct {
 } mvr_oan_block_p;
 
 size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N);
+/* diff_pool / diff_unpool inside mvr_oan_block_forward: 1 (default) = fused attention kernels
+ * (mvr_oan_diff_pool / _unpool) when channels == 128 and clusters <= 1024, 0 = embedding GEMM + softmax
+ * factors + pooling GEMM.  Process-wide; query workspace bytes after setting it.  Returns the previous value. */
+int mvr_set_oan_fused(int on);
 
 /* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
  * a multiple of 4, input 16-byte aligned, padding columns [N, ld) finite (zero).
@@ -120,6 +124,33 @@ int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_
                           float* score_row, int64_t row_pstride, int32_t* guard_pos, int32_t* status, int guard_group,
                           void* workspace,
                           size_t workspace_bytes, mvr_stream_t stream);
+
+/* Fused diff_pool (lib/filtering/oanet.py:96-110), channels == 128, clusters <= 1024:
+ *   x_down(p,c,j) = sum_n x(p,c,n) softmax_n(e(p,j,n)),  e = W . relu(x * sc + sh) + b
+ * x(p,c,n) = x[p*x_pstride + c*x_ld + n] (x_ld >= round_up(N,4), multiple of 4, 16-byte aligned);
+ * sc/sh(p,c) = sc[p*s_pstride + c] (the embedding conv's InstanceNorm+BatchNorm folded to an affine);
+ * weight [clusters][128] (16-byte aligned), bias [clusters] (may be NULL);
+ * out(p,c,j) = out[p*out_pstride + c*out_ld + j], out_ld >= round_up(clusters,4), columns [clusters,
+ * round_up(clusters,4)) written 0.  stats (may be NULL): float pairs (sum, squared deviations from the
+ * tile mean) of row c over the 128-column tile t at stats[2*((p*ceil(clusters/128) + t)*st_ld + st_off + c)].
+ * The [clusters x N] embedding never leaves the chip (flash-style online softmax). */
+int mvr_oan_diff_pool(const float* x, int64_t x_pstride, int64_t x_ld, const float* sc, const float* sh,
+                      int64_t s_pstride, const float* weight, const float* bias, int P, int channels, int N,
+                      int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld,
+                      int st_off, mvr_stream_t stream);
+
+/* Fused diff_unpool (lib/filtering/oanet.py:113-129), channels == 128, clusters <= 1024:
+ *   out(p,c,n) = sum_j x_down(p,c,j) softmax_j(e(p,j,n)),  e = W . relu(x_up * sc + sh) + b
+ * x_up as x above; x_down(p,c,j) = x_down[p*xd_pstride + c*xd_ld + j]; out like x (columns [N,
+ * round_up(N,4)) written 0); stats per 128-column tile of N as above (ceil(N/128) tiles per pair).
+ * workspace: mvr_oan_diff_unpool_workspace_bytes(P, 128, clusters) bytes, 16-byte aligned (the
+ * split-bf16 images of W and x_down). */
+size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int clusters);
+int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t x_ld, const float* sc, const float* sh,
+                        int64_t s_pstride, const float* weight, const float* bias, const float* x_down,
+                        int64_t xd_pstride, int64_t xd_ld, int P, int channels, int N, int clusters, float* out,
+                        int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld, int st_off,
+                        void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 
 /* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*out_ld + n]
  * (the transpose of lib/filtering/oanet.py:234). */

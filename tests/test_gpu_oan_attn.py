@@ -1,0 +1,149 @@
+"""Fused diff_pool / diff_unpool (csrc/oan_attn.hip) against a float64 torch statement of
+lib/filtering/oanet.py:96-129 on the same inputs, including ragged sizes (N and clusters not tile
+multiples, pair counts not a multiple of the 8-pair XCD group), the per-tile InstanceNorm
+partials, and the whole OANet block with the fused path on vs off.
+
+Tolerance: the kernels compute in fp32 with split-bf16 MFMA products (fp32-level accuracy), so
+outputs are compared to fp64 at 2e-5 relative to the output scale."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+C = 128
+
+
+def _inputs(P, N, Kc, seed):
+    r = np.random.RandomState(seed)
+    ld = (N + 3) // 4 * 4
+    x = np.zeros((P, C, ld), np.float32)
+    x[:, :, :N] = r.standard_normal((P, C, N))
+    sc = r.uniform(0.5, 1.5, (P, C)).astype(np.float32)
+    sh = r.uniform(-0.5, 0.5, (P, C)).astype(np.float32)
+    W = (0.15 * r.standard_normal((Kc, C))).astype(np.float32)
+    b = (0.1 * r.standard_normal(Kc)).astype(np.float32)
+    return x, sc, sh, W, b, ld
+
+
+def _embed(x, sc, sh, W, b, N):
+    import torch
+    xd = torch.from_numpy(x[:, :, :N]).double()
+    xn = torch.relu(xd * torch.from_numpy(sc).double()[:, :, None] + torch.from_numpy(sh).double()[:, :, None])
+    return xd, torch.from_numpy(W).double() @ xn + torch.from_numpy(b).double()[None, :, None]   # [P, Kc, N]
+
+
+def _tile_stats(y, L):
+    """(sum, squared deviations from the tile mean) per 128-column tile of y [P, C, L] -> [P, T, C, 2]"""
+    T = (L + 127) // 128
+    out = np.zeros((y.shape[0], T, y.shape[1], 2))
+    for t in range(T):
+        blk = y[:, :, 128 * t:min(L, 128 * t + 128)]
+        out[:, t, :, 0] = blk.sum(-1)
+        out[:, t, :, 1] = ((blk - blk.mean(-1, keepdims=True)) ** 2).sum(-1)
+    return out
+
+
+@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33)])
+def test_diff_pool_matches_fp64(gpu, P, N, Kc):
+    import torch
+    from lib import _native as NV
+    x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 1000 + N)
+    xd, e = _embed(x, sc, sh, W, b, N)
+    ref = (xd @ torch.softmax(e, dim=2).transpose(1, 2)).numpy()          # oanet.py:106-110
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    Kp = (Kc + 3) // 4 * 4
+    T = (Kc + 127) // 128
+    out = torch.full((P, C, Kp), float("nan"), device=gpu)
+    st = torch.zeros((P, T, C, 2), device=gpu)
+    gx, gsc, gsh, gW, gb = t(x), t(sc), t(sh), t(W), t(b)
+    assert NV.lib().mvr_oan_diff_pool(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
+                                      P, C, N, Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.stream()) == 0
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(o[:, :, :Kc], ref, atol=2e-5 * scale, rtol=0)
+    assert np.all(o[:, :, Kc:] == 0)
+    sref = _tile_stats(ref, Kc)
+    np.testing.assert_allclose(st.cpu().numpy()[..., 0], sref[..., 0], atol=2e-5 * scale * 128, rtol=0)
+    np.testing.assert_allclose(st.cpu().numpy()[..., 1], sref[..., 1], rtol=1e-4, atol=1e-6 * scale ** 2 * 128)
+
+
+@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33)])
+def test_diff_unpool_matches_fp64(gpu, P, N, Kc):
+    import torch
+    from lib import _native as NV
+    x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 7 + N)
+    r = np.random.RandomState(N)
+    Kp = (Kc + 3) // 4 * 4
+    xdn = np.zeros((P, C, Kp), np.float32)
+    xdn[:, :, :Kc] = r.standard_normal((P, C, Kc))
+    xdn[:, :, Kc:] = 123.0   # padding columns must not enter
+    _, e = _embed(x, sc, sh, W, b, N)
+    ref = (torch.from_numpy(xdn[:, :, :Kc]).double() @ torch.softmax(e, dim=1)).numpy()   # oanet.py:124-128
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    L = NV.lib()
+    ws = L.mvr_oan_diff_unpool_workspace_bytes(P, C, Kc)
+    assert ws > 0
+    wbuf = torch.empty(ws, dtype=torch.uint8, device=gpu)
+    T = (N + 127) // 128
+    out = torch.full((P, 2 * C, ld), float("nan"), device=gpu)   # writes rows [C, 2C) like the block
+    st = torch.zeros((P, T, 2 * C, 2), device=gpu)
+    gx, gsc, gsh, gW, gb, gxd = t(x), t(sc), t(sh), t(W), t(b), t(xdn)
+    assert L.mvr_oan_diff_unpool(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
+                                 NV.ptr(gxd), C * Kp, Kp, P, C, N, Kc, NV.ptr(out[:, C:]), 2 * C * ld, ld,
+                                 NV.ptr(st), 2 * C, C, NV.ptr(wbuf), ws, NV.stream()) == 0
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert np.isnan(o[:, :C]).all()
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(o[:, C:, :N], ref, atol=2e-5 * scale, rtol=0)
+    assert np.all(o[:, C:, N:] == 0)
+    sref = _tile_stats(ref, N)
+    s = st.cpu().numpy()
+    assert np.all(s[:, :, :C] == 0)
+    np.testing.assert_allclose(s[:, :, C:, 0], sref[..., 0], atol=2e-5 * scale * 128, rtol=0)
+    np.testing.assert_allclose(s[:, :, C:, 1], sref[..., 1], rtol=1e-4, atol=1e-6 * scale ** 2 * 128)
+
+
+def test_diff_pool_rejects_bad_layout(gpu):
+    import torch
+    from lib import _native as NV
+    x = torch.zeros(1, C, 8, device=gpu)
+    s = torch.zeros(1, C, device=gpu)
+    W = torch.zeros(16, C, device=gpu)
+    out = torch.zeros(1, C, 16, device=gpu)
+    L = NV.lib()
+    args = lambda ld, ch: (NV.ptr(x), C * 8, ld, NV.ptr(s), NV.ptr(s), C, NV.ptr(W), None, 1, ch, 8, 16,
+                           NV.ptr(out), C * 16, 16, None, 0, 0, NV.stream())
+    assert L.mvr_oan_diff_pool(*args(8, C)) == 0
+    assert L.mvr_oan_diff_pool(*args(6, C)) == -1     # ld not a multiple of 4 / < round_up(N, 4)
+    assert L.mvr_oan_diff_pool(*args(8, 64)) == -1    # channels != 128
+    assert L.mvr_oan_diff_unpool_workspace_bytes(1, 64, 16) == 0
+
+
+def test_oanet_fused_vs_gemm_path(gpu):
+    """Whole filter with the fused diff_pool/diff_unpool vs the embedding-GEMM + softmax-factor path:
+    same R, t (1e-4) and inlier masks."""
+    import torch
+    from lib import _native as NV
+    from test_gpu_oanet import _oanet
+    from synth import synth_correspondences
+    xs, _, _ = synth_correspondences(6, 2000, seed=11)
+    net = _oanet(128, 500, 7, gpu, which="full")
+    outs = []
+    L = NV.lib()
+    try:
+        for fused in (1, 0):
+            L.mvr_set_oan_fused(fused)
+            with torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    finally:
+        L.mvr_set_oan_fused(1)
+    a, b = outs
+    for i in range(2):
+        np.testing.assert_allclose(a["logits"][i].cpu().numpy(), b["logits"][i].cpu().numpy(), atol=2e-3, rtol=1e-4)
+        np.testing.assert_allclose(a["rot_est"][i].cpu().numpy(), b["rot_est"][i].cpu().numpy(), atol=1e-4)
+        np.testing.assert_allclose(a["trans_est"][i].cpu().numpy(), b["trans_est"][i].cpu().numpy(), atol=1e-4)
+        sa, sb = a["scores"][i].cpu().numpy(), b["scores"][i].cpu().numpy()
+        near = np.abs(sb - 0.5) < 1e-4
+        assert np.array_equal((sa > 0.5)[~near], (sb > 0.5)[~near])
