@@ -99,26 +99,32 @@ __device__ __forceinline__ void pair_block(int nblk, int& p, int& blk) {
 }
 
 // Online softmax over the 16 rows of a lane column (+ the partner half): v holds logits * log2e.
-// Updates (m, l), rescales O, and leaves the probabilities in v.
+// Lazy rescaling: the running max m moves only when a block exceeds it by more than RESCALE (log2
+// units), so the probabilities exp2(v - m) stay <= 2^RESCALE and O, l are rescaled a few times per
+// query instead of every block; O / l is the softmax-weighted sum whichever m was used.
+// Leaves the probabilities in v.
+constexpr float RESCALE = 8.f;
 __device__ __forceinline__ void online_softmax(float (&v)[16], float& m, float& l, floatx16 (&O)[4]) {
-  float bm = v[0];
+  float bm = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), v[2]);
 #pragma unroll
-  for (int r = 1; r < 16; ++r) bm = fmaxf(bm, v[r]);
+  for (int r = 3; r < 15; r += 2) bm = __builtin_fmaxf(__builtin_fmaxf(bm, v[r]), v[r + 1]);
+  bm = fmaxf(bm, v[15]);
   bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-  const float mn = fmaxf(m, bm);
-  const float alpha = __builtin_amdgcn_exp2f(m - mn);
-  m = mn;
-  float ps = 0.f;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    v[r] = __builtin_amdgcn_exp2f(v[r] - mn);
-    ps += v[r];
-  }
-  l = fmaf(l, alpha, ps);
-  if (__any(alpha != 1.f)) {
+  if (__any(bm > m + RESCALE)) {
+    const float mn = fmaxf(m, bm);
+    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    m = mn;
+    l *= alpha;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) O[cb] *= alpha;
   }
+  float ps = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    v[r] = __builtin_amdgcn_exp2f(v[r] - m);
+    ps += v[r];
+  }
+  l += ps;
 }
 
 // O (rows c = 32 cb + (q & 3) + 8 (q >> 2) + 4h, column = 32 w + lane row) * inv -> out[c][col0 + col]
@@ -179,8 +185,21 @@ struct PoolArgs {
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(Kc/128)][st_ld] (+ st_off + c), nullable
 };
 
+__device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+
+constexpr int XT = AC * AKB * 4;   // raw fp32 key tile [128 c][32 n] (16 KB)
+
 __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_B];
+  __shared__ __attribute__((aligned(16))) char xraw[2 * XT];   // LDS-DMA ring of raw key tiles
+  __shared__ float2 ssh[AC];                                  // (sc, sh) of this pair
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   int p, jb;
   pair_block(a.nqb, p, jb);
@@ -190,19 +209,20 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   const int nkb = (N + AKB - 1) / AKB;
   const int nlast = ((N + 3) & ~3) - 4;   // last readable 4-key group of a row
 
-  // staging map: thread tid, i = 0..1 -> channel c = tid / 8 + 64 i, keys 4 (tid & 7) .. +3
-  const int sq = tid & 7;
-  float4 xr[2];
-  auto load_tile = [&](int kb) {
-    const int n = kb * AKB + 4 * sq;
+  // raw tile kb -> xraw[kb & 1] as [c][32] fp32 rows: wave w moves rows 16 w .. 16 w + 15 in two
+  // 1 KB DMAs (lane: row + lane / 8, keys 4 (lane & 7)); keys past the end read a clamped column
+  // and are zeroed when the tile is split
+  auto dma_tile = [&](int kb) {
+    const int n = min(kb * AKB + 4 * (lane & 7), nlast);
+    char* dst = xraw + (kb & 1) * XT;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int c = (tid >> 3) + 64 * i;
-      const float4 v = *reinterpret_cast<const float4*>(X + (int64_t)c * a.xld + min(n, nlast));
-      xr[i] = n < N ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int r0 = 16 * w + 8 * i;
+      glds16b(reinterpret_cast<const char*>(X + (int64_t)(r0 + (lane >> 3)) * a.xld + n), dst + r0 * 128);
     }
   };
-  load_tile(0);
+  dma_tile(0);
+  if (tid < AC) ssh[tid] = make_float2(a.sc[(int64_t)p * a.sps + tid], a.sh[(int64_t)p * a.sps + tid]);
 
   // queries: this lane's W row (column j of S^T) as split B fragments, one per 16-channel k-step
   const int j = jb * AQ + 32 * w + l32;
@@ -215,31 +235,33 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * ks + 4);
     float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = jok ? v[i] : 0.f;
+    for (int i = 0; i < 8; ++i) v[i] = jok ? v[i] * LOG2E : 0.f;   // logits in log2 units
     split8(v, q[ks].h, q[ks].m, q[ks].l);
   }
-  const float bj = (jok && a.bias) ? a.bias[j] : 0.f;
-  float scv[2], shv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = (tid >> 3) + 64 * i;
-    scv[i] = a.sc[(int64_t)p * a.sps + c];
-    shv[i] = a.sh[(int64_t)p * a.sps + c];
-  }
-  auto store_tile = [&](int st) {
+  const float bj = (jok && a.bias) ? a.bias[j] * LOG2E : 0.f;
+
+  // split raw tile kb (xraw[kb & 1]) into stage st: thread -> channel c = tid / 8 + 64 i, keys
+  // 4 (tid & 7) .. +3
+  const int sq = tid & 7;
+  auto store_tile = [&](int kb, int st) {
     char* K = smem + st * STAGE_B;
     char* V = K + IMG;
+    const char* xt = xraw + (kb & 1) * XT;
+    const bool nok = kb * AKB + 4 * sq < N;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = (tid >> 3) + 64 * i;
+      float4 x = *reinterpret_cast<const float4*>(xt + c * 128 + 16 * sq);
+      if (!nok) x = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float2 f = ssh[c];
       u32x2 H, M, L;
-      split4(xr[i], H, M, L);
+      split4(x, H, M, L);
       const int vo = kord_off(c, sq);
       *reinterpret_cast<u32x2*>(V + vo) = H;
       *reinterpret_cast<u32x2*>(V + PLANE + vo) = M;
       *reinterpret_cast<u32x2*>(V + 2 * PLANE + vo) = L;
-      const float4 xn = make_float4(fmaxf(fmaf(xr[i].x, scv[i], shv[i]), 0.f), fmaxf(fmaf(xr[i].y, scv[i], shv[i]), 0.f),
-                                    fmaxf(fmaf(xr[i].z, scv[i], shv[i]), 0.f), fmaxf(fmaf(xr[i].w, scv[i], shv[i]), 0.f));
+      const float4 xn = make_float4(fmaxf(fmaf(x.x, f.x, f.y), 0.f), fmaxf(fmaf(x.y, f.x, f.y), 0.f),
+                                    fmaxf(fmaf(x.z, f.x, f.y), 0.f), fmaxf(fmaf(x.w, f.x, f.y), 0.f));
       split4(xn, H, M, L);
       const int ko = c * 64 + 8 * sq;
       *reinterpret_cast<u32x2*>(K + ko) = H;
@@ -272,19 +294,23 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     return f;
   };
 
-  store_tile(0);
-  load_tile(1);
+  // ring: raw tile kb + 2 lands while stage kb & 1 is consumed and tile kb + 1 is split into the other
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  dma_tile(1);
+  store_tile(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kb = 0; kb < nkb; ++kb) {
     const int st = kb & 1;
-    store_tile(st ^ 1);   // tile kb + 1 (zeros past the end)
-    load_tile(kb + 2);
+    store_tile(kb + 1, st ^ 1);   // zeros past the end
+    dma_tile(kb + 2);             // into the buffer of tile kb, split one iteration ago
     const char* K = smem + st * STAGE_B;
     const char* V = K + IMG;
-    // S^T[n][j] = sum_c xn[c][n] W[j][c], fragments one k-step ahead
+    // S^T[n][j] = b[j] + sum_c xn[c][n] W[j][c] (log2 units), fragments one k-step ahead
     floatx16 S;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) S[r] = 0.f;
+    for (int r = 0; r < 16; ++r) S[r] = bj;
     Frag cur = read_k(K, 0);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
@@ -298,9 +324,11 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     Frag vf = kord_frag(V, l32, 0, h);   // first V fragment, in flight during the softmax
     float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = kb * AKB + (r & 3) + 8 * (r >> 2) + 4 * h;
-      v[r] = n < N ? (S[r] + bj) * LOG2E : -__builtin_inff();
+    for (int r = 0; r < 16; ++r) v[r] = S[r];
+    if (kb * AKB + AKB > N) {   // ragged last block
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kb * AKB + (r & 3) + 8 * (r >> 2) + 4 * h >= N) v[r] = -__builtin_inff();
     }
     online_softmax(v, m, l, O);
     Frag pf[2];
@@ -317,6 +345,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       SCHED_FENCE();
       if (i < 7) vf = nxt;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   const float lt = l + __shfl_xor(l, 32, 64);
@@ -337,7 +366,7 @@ __global__ void split_w_kernel(const float* __restrict__ W, int Kc, int nkb, cha
   const int j = kb * AKB + jj;
   float v[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = j < Kc ? W[(int64_t)j * AC + 8 * ch + e] : 0.f;
+  for (int e = 0; e < 8; ++e) v[e] = j < Kc ? W[(int64_t)j * AC + 8 * ch + e] * LOG2E : 0.f;   // log2 units
   Frag f;
   split8(v, f.h, f.m, f.l);
   char* base = img + (int64_t)kb * WIMG + jj * WROW + 16 * ch;
@@ -378,18 +407,12 @@ struct UnpoolArgs {
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(N/128)][st_ld] (+ st_off + c), nullable
 };
 
-__device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
-  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
 
 __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * USTAGE];
+  // stage ring; the query prologue double-buffers 32 KB quarters at [USTAGE, USTAGE + 64 KB)
+  __shared__ __attribute__((aligned(16))) char smem[USTAGE + 64 * 1024];
   __shared__ __attribute__((aligned(16))) float bsh[MAX_CLUSTERS];
+  __shared__ float2 ssh[AC];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   int p, nb;
   pair_block(a.nqb, p, nb);
@@ -407,26 +430,53 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
   };
   issue(0, 0);
 
-  // queries: this lane's point n (column), xn[c][n] for c = 16 ks + 8h + i as split B fragments
+  for (int i = tid; i < nkb * AKB; i += ATHREADS)
+    bsh[i] = i < a.Kc ? (a.bias ? a.bias[i] * LOG2E : 0.f) : -__builtin_inff();
+  if (tid < AC) ssh[tid] = make_float2(a.sc[(int64_t)p * a.sps + tid], a.sh[(int64_t)p * a.sps + tid]);
+
+  // queries: this lane's point n (column), xn[c][n] for c = 16 ks + 8h + i as split B fragments.
+  // The workgroup's x_up rows (128 channels x 256 points) are staged through LDS in quarters of 32
+  // channels (whole 1 KB row segments by LDS-DMA, double-buffered behind stage 0) and read back as
+  // columns; points past the end read a clamped column and are zeroed.
   const int n = nb * AQ + 32 * w + l32;
   const bool nok = n < N;
-  const float* xq = a.X + (int64_t)p * a.xps + min(n, N - 1);
-  const float* sc = a.sc + (int64_t)p * a.sps;
-  const float* sh = a.sh + (int64_t)p * a.sps;
+  const int nlast = ((N + 3) & ~3) - 4;
+  const float* xb = a.X + (int64_t)p * a.xps + min(nb * AQ + 4 * lane, nlast);
+  auto qdma = [&](int qt) {
+    char* dst = smem + USTAGE + (qt & 1) * 32768;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * w + i;
+      glds16b(reinterpret_cast<const char*>(xb + (int64_t)(32 * qt + r) * a.xld), dst + r * 1024);
+    }
+  };
+  qdma(0);
   Frag q[8];
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    float v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = 16 * ks + 8 * h + i;
-      const float x = fmaxf(fmaf(xq[(int64_t)c * a.xld], sc[c], sh[c]), 0.f);
-      v[i] = nok ? x : 0.f;
+  for (int qt = 0; qt < 4; ++qt) {
+    if (qt < 3) {
+      qdma(qt + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // all but quarter qt + 1 landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    split8(v, q[ks].h, q[ks].m, q[ks].l);
+    __syncthreads();
+    const float* xt = reinterpret_cast<const float*>(smem + USTAGE + (qt & 1) * 32768) + 32 * w + l32;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ks = 2 * qt + kk;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = 16 * ks + 8 * h + i;
+        const float2 f = ssh[c];
+        const float x = fmaxf(fmaf(xt[(c - 32 * qt) * 256], f.x, f.y), 0.f);
+        v[i] = nok ? x : 0.f;
+      }
+      split8(v, q[ks].h, q[ks].m, q[ks].l);
+    }
+    __syncthreads();
   }
-  for (int i = tid; i < nkb * AKB; i += ATHREADS)
-    bsh[i] = i < a.Kc ? (a.bias ? a.bias[i] : 0.f) : -__builtin_inff();
 
   floatx16 O[4];
 #pragma unroll
@@ -452,10 +502,17 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
     if (kb + 1 < nkb) issue(kb + 1, st ^ 1);
     const char* Wi = smem + st * USTAGE;
     const char* D = Wi + WIMG;
-    // S[j][n] = sum_c W[j][c] xn[c][n], fragments one k-step ahead
+    // S[j][n] = b[j] + sum_c W[j][c] xn[c][n] (log2 units; -inf rows past the clusters), fragments
+    // one k-step ahead
     floatx16 S;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) S[r] = 0.f;
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const float4 b = *reinterpret_cast<const float4*>(bsh + kb * AKB + 8 * r4 + 4 * h);
+      S[4 * r4 + 0] = b.x;
+      S[4 * r4 + 1] = b.y;
+      S[4 * r4 + 2] = b.z;
+      S[4 * r4 + 3] = b.w;
+    }
     Frag cur = read_w(Wi, 0);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
@@ -469,13 +526,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
     Frag df = kord_frag(D, l32, 0, h);
     float v[16];
 #pragma unroll
-    for (int r4 = 0; r4 < 4; ++r4) {
-      const float4 b = *reinterpret_cast<const float4*>(bsh + kb * AKB + 8 * r4 + 4 * h);
-      v[4 * r4 + 0] = (S[4 * r4 + 0] + b.x) * LOG2E;
-      v[4 * r4 + 1] = (S[4 * r4 + 1] + b.y) * LOG2E;
-      v[4 * r4 + 2] = (S[4 * r4 + 2] + b.z) * LOG2E;
-      v[4 * r4 + 3] = (S[4 * r4 + 3] + b.w) * LOG2E;
-    }
+    for (int r = 0; r < 16; ++r) v[r] = S[r];
     online_softmax(v, m, l, O);
     Frag pf[2];
     split8(v, pf[0].h, pf[0].m, pf[0].l);

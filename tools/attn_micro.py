@@ -1,0 +1,74 @@
+"""Micro-benchmark of the fused diff_pool / diff_unpool kernels (csrc/oan_attn.hip) at the scene
+shape (435 pairs x 5000 points, 128 channels, 500 clusters), timed with HIP events.
+usage: python tools/attn_micro.py [--iters N] [--only pool|unpool]"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d_multiview_reg_amd"))
+import torch  # noqa: E402
+from lib import _native as NV  # noqa: E402
+
+P, N, C, K = 435, 5000, 128, 500
+PEAK = 16 * 157.3 / 6   # split-bf16 fp32-equivalent TF/s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--clusters", type=int, default=K)
+    ap.add_argument("--points", type=int, default=N)
+    a = ap.parse_args()
+    run(a, a.clusters, a.points)
+
+
+def run(a, K, N):
+    d = torch.device("cuda")
+    g = torch.Generator(device=d).manual_seed(0)
+    x = torch.randn(P, C, N, device=d, generator=g)
+    sc = torch.rand(P, C, device=d, generator=g) + 0.5
+    sh = torch.rand(P, C, device=d, generator=g) - 0.5
+    W = torch.randn(K, C, device=d, generator=g) * 0.1
+    b = torch.randn(K, device=d, generator=g) * 0.1
+    xd = torch.randn(P, C, K, device=d, generator=g)
+    out_d = torch.empty(P, C, K, device=d)
+    out_u = torch.empty(P, C, N, device=d)
+    st_d = torch.empty(P, (K + 127) // 128, C, 2, device=d)
+    st_u = torch.empty(P, (N + 127) // 128, C, 2, device=d)
+    L = NV.lib()
+    ws = L.mvr_oan_diff_unpool_workspace_bytes(P, C, K)
+    wbuf = torch.empty(ws, dtype=torch.uint8, device=d)
+    s = NV.stream()
+
+    def pool():
+        assert L.mvr_oan_diff_pool(NV.ptr(x), C * N, N, NV.ptr(sc), NV.ptr(sh), C, NV.ptr(W), NV.ptr(b), P, C, N, K,
+                                   NV.ptr(out_d), C * K, K, NV.ptr(st_d), C, 0, s) == 0
+
+    def unpool():
+        assert L.mvr_oan_diff_unpool(NV.ptr(x), C * N, N, NV.ptr(sc), NV.ptr(sh), C, NV.ptr(W), NV.ptr(b), NV.ptr(xd),
+                                     C * K, K, P, C, N, K, NV.ptr(out_u), C * N, N, NV.ptr(st_u), C, 0, NV.ptr(wbuf),
+                                     ws, s) == 0
+
+    flops = 4.0 * C * K * N * P
+    print("P=%d N=%d clusters=%d" % (P, N, K))
+    for name, fn in (("pool", pool), ("unpool", unpool)):
+        if a.only and a.only != name:
+            continue
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.iters
+        print("%-7s %.3f ms  %.1f TF/s  (%.2f of split peak)" % (name, ms, flops / ms / 1e9, flops / ms / 1e9 / PEAK),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
