@@ -69,6 +69,12 @@ _SIGS = {
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
     "mvr_fps": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
+    "mvr_voxel_centroids_workspace_bytes": (c_size, [c_i64]),
+    "mvr_voxel_centroids": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_vp, c_size, c_vp, c_vp, c_vp]),
+    "mvr_radius_index_bytes": (c_size, [c_i64]),
+    "mvr_radius_index_build": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_vp, c_size, c_vp]),
+    "mvr_radius_overlap_count": (c_int, [c_vp, c_size, c_vp, c_vp, c_int, c_i64, c_vp, c_vp, c_int, c_i64,
+                                         ctypes.c_double, c_vp, c_vp]),
     "mvr_hash_table_bytes": (c_size, [c_i64]),
     "mvr_voxelize_workspace_bytes": (c_size, [c_i64]),
     "mvr_voxelize": (c_int, [c_vp, c_vp, c_int, c_i64, c_float, c_vp, c_size, c_vp, c_vp, c_vp, c_vp]),

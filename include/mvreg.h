@@ -157,6 +157,30 @@ int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t x_ld, cons
 int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N, float* out,
                        int64_t out_pstride, int64_t out_ld, mvr_stream_t stream);
 
+/* ------------------------------------------------------------------------
+ * Overlap gate (lib/utils.py:713-786 compute_overlap_ratio; benchmark:219-220).
+ * Open3D VoxelDownSample restated: per fragment b (xyz float32 [n,3], frag_off [B+1] device int64),
+ * voxel index floor((p - (min_b - v/2)) / v) in fp64, centroid = fp64 sum of the voxel's points in input
+ * order / count.  out_xyz fp64 [n,3] capacity (voxels of a fragment contiguous, fragments in order),
+ * out_off [B+1] (device).  Voxel coordinates must stay below 65536 per axis; B <= 4096.
+ * ---------------------------------------------------------------------- */
+size_t mvr_voxel_centroids_workspace_bytes(int64_t n);
+int mvr_voxel_centroids(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* workspace,
+                        size_t workspace_bytes, double* out_xyz, int64_t* out_off, mvr_stream_t stream);
+/* Radius index over fp64 points [M,3] in fragments off [B+1] (device): points sorted by (fragment, cell of
+ * size r) + a hash of the occupied cells.  `index` holds mvr_radius_index_bytes(M) bytes and stays valid
+ * for mvr_radius_overlap_count calls on the same points. */
+size_t mvr_radius_index_bytes(int64_t M);
+int mvr_radius_index_build(const double* xyz, const int64_t* off, int B, int64_t M, double r, void* index,
+                           size_t bytes, mvr_stream_t stream);
+/* counts[2p + d] = number of points q of fragment pairs[2p + d] whose image T[p][d] q (3x4 row-major fp64,
+ * T [P][2][12]) lies at Euclidean distance < r from some point of fragment pairs[2p + 1 - d].
+ * With trans the reference's argument: T[p][0] = inv(trans) (pc_i side), T[p][1] = trans (pc_j side).
+ * max_points >= the largest fragment. */
+int mvr_radius_overlap_count(const void* index, size_t bytes, const double* xyz, const int64_t* off, int B,
+                             int64_t M, const int64_t* pairs, const double* T, int P, int64_t max_points, double r,
+                             int32_t* counts, mvr_stream_t stream);
+
 /* Farthest point sampling per fragment (Sampler 'fps', lib/layers.py:134-141 — pointnet2
  * furthest_point_sample semantics of oracle/fps.py: seed = first point, running min of squared
  * distances, first maximum on ties).  xyz [sum n][3] with fragment row offsets (device `offsets`
