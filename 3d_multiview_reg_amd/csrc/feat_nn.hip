@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
     const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + 16 * shalf);
 #pragma unroll
     for (int v = 0; v < 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < NN_STAGE) {
+    if (MODE != 2 && tid < NN_STAGE) {
       const int gc = t0 + tid;
       if (gc < Mt) {
         const float* xp = Xt + (int64_t)gc * 3;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
     n2 += __shfl_xor(n2, 1, 64);
     // invalid targets: +inf -> logit -inf -> weight 0, never the argmax
     if (shalf == 0) Xs[buf][3][srow] = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
-    if (tid < NN_STAGE) {
+    if (MODE != 2 && tid < NN_STAGE) {
       Xs[buf][0][tid] = xr0;
       Xs[buf][1][tid] = xr1;
       Xs[buf][2][tid] = xr2;
@@ -143,8 +143,8 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
 
   float run_m = NN_NEG;
   f32x2 s2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f}, az2 = {0.f, 0.f};
-  float best = NN_NEG;
-  int besti = 0x7fffffff;
+  float best = NN_NEG, second = NN_NEG;
+  int besti = 0x7fffffff, secondi = 0x7fffffff;
   const float kk2 = 2.f * a.k2;
 
   const int nst = (Mt + NN_STAGE - 1) / NN_STAGE;
@@ -197,6 +197,18 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
             besti = t0 + i0 + 8 * (r >> 2) + 4 * kh + (r & 3);
           }
         }
+      } else if (MODE == 2) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {   // two best (smallest distance), first index on ties
+          const float v = z[r >> 1][r & 1];
+          const int i = t0 + i0 + 8 * (r >> 2) + 4 * kh + (r & 3);
+          if (v > best) {
+            second = best; secondi = besti;
+            best = v; besti = i;
+          } else if (v > second) {
+            second = v; secondi = i;
+          }
+        }
       } else {
         float cm = nn_max3(z[0].x, z[0].y, z[1].x);
         cm = nn_max3(cm, z[1].y, z[2].x);
@@ -244,6 +256,25 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
     cur ^= 1;
   }
 
+  if (MODE == 2) {   // merge the two lane halves' disjoint candidate sets
+    const float ob = __shfl_xor(best, 32, 64), os = __shfl_xor(second, 32, 64);
+    const int oi = __shfl_xor(besti, 32, 64), osi = __shfl_xor(secondi, 32, 64);
+    auto better = [](float v, int i, float w, int k) { return v > w || (v == w && i < k); };
+    float v1 = best, v2 = second;
+    int i1 = besti, i2 = secondi;
+    if (better(ob, oi, v1, i1)) {
+      // other's best leads: second is the better of (mine best, other's second)
+      if (better(v1, i1, os, osi)) { v2 = v1; i2 = i1; } else { v2 = os; i2 = osi; }
+      v1 = ob; i1 = oi;
+    } else if (better(ob, oi, v2, i2)) {
+      v2 = ob; i2 = oi;
+    }
+    if (jok && kh == 0) {
+      a.idx[((int64_t)p * a.Nq + j) * 2] = i1;
+      a.idx[((int64_t)p * a.Nq + j) * 2 + 1] = i2;
+    }
+    return;
+  }
   float ox, oy, oz;
   if (MODE == 0) {
     const float run_s = s2.x + s2.y, ax = ax2.x + ax2.y, ay = ay2.x + ay2.y, az = az2.x + az2.y;
@@ -268,6 +299,26 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
     o[0] = ox; o[1] = oy; o[2] = oz;
     if (a.idx && MODE == 1) a.idx[(int64_t)p * a.Nq + j] = besti;
   }
+}
+
+// exact fp64 distances of the two neighbours: d[p][j][k] = |Fq(src, j) - Ft(tgt, idx[p][j][k])|
+__global__ void knn2_dist_kernel(const float* __restrict__ Fq, int64_t fq_fs, const float* __restrict__ Ft,
+                                 int64_t ft_fs, const int64_t* __restrict__ pairs, int P, int Nq, int Mt,
+                                 const int32_t* __restrict__ idx, double* dist) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)P * Nq * 2) return;
+  const int64_t pj = e >> 1;
+  const int p = (int)(pj / Nq), j = (int)(pj - (int64_t)p * Nq);
+  const int t = idx[e];
+  if (t < 0 || t >= Mt) { dist[e] = __builtin_inf(); return; }
+  const float* q = Fq + pairs[2 * p] * fq_fs + (int64_t)j * 32;
+  const float* f = Ft + pairs[2 * p + 1] * ft_fs + (int64_t)t * 32;
+  double s = 0.0;
+  for (int c = 0; c < 32; ++c) {
+    const double d = (double)q[c] - (double)f[c];
+    s += d * d;
+  }
+  dist[e] = sqrt(s);
 }
 
 // rows gather: dst[i][:] = src[idx[i]][:]  (Sampler.forward, lib/layers.py:151-152)
@@ -301,6 +352,29 @@ extern "C" int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft,
   else
     hipLaunchKernelGGL(mvr::feat_nn_kernel<1>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_feat_knn2(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride,
+                             const int64_t* pairs, int P, int Nq, int Mt, int C, int32_t* idx2_out, double* dist2_out,
+                             hipStream_t stream) {
+  if (!Fq || !Ft || !pairs || !idx2_out || P < 0 || Nq < 0 || Mt < 2 || C != 32) return MVR_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(Fq) & 15) || (reinterpret_cast<uintptr_t>(Ft) & 15) || (fq_fstride & 3) ||
+      (ft_fstride & 3))
+    return MVR_EINVAL;
+  if (P == 0 || Nq == 0) return MVR_OK;
+  mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, nullptr, 0, Ft, 0, pairs, P, Nq, Mt, 1.4426950408889634f, 2,
+                nullptr, 0, 0, idx2_out};
+  mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * C * 4 + P * Nq * 8.0,
+                      stream);
+  hipLaunchKernelGGL(mvr::feat_nn_kernel<2>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
+  MVR_CHECK_LAUNCH();
+  if (dist2_out) {
+    const int64_t n = (int64_t)P * Nq * 2;
+    hipLaunchKernelGGL(mvr::knn2_dist_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, Fq, fq_fstride,
+                       Ft, ft_fstride, pairs, P, Nq, Mt, idx2_out, dist2_out);
+    MVR_CHECK_LAUNCH();
+  }
   return MVR_OK;
 }
 

@@ -68,6 +68,7 @@ _SIGS = {
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "mvr_feat_knn2": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "mvr_fps": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "mvr_voxel_centroids_workspace_bytes": (c_size, [c_i64]),
     "mvr_voxel_centroids": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_vp, c_size, c_vp, c_vp, c_vp]),

@@ -206,6 +206,14 @@ int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft
                 int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
                 int32_t* idx_out, mvr_stream_t stream);
 
+/* Two nearest neighbours in feature space (scripts/extract_data.py:178-184, sklearn NearestNeighbors
+ * kneighbors(n_neighbors=2), Euclidean): for pair p and query j of fragment pairs[2p] (Fq rows, fragment stride
+ * fq_fstride), idx2_out[(p*Nq + j)*2 + k] = k-th nearest row of fragment pairs[2p+1] (Ft, Mt >= 2 rows),
+ * smallest distance first, first index on ties (split-bf16 MFMA distances; fp32-level near-ties may order
+ * differently from fp64).  dist2_out (may be NULL): the fp64 distances of those two rows.  C == 32. */
+int mvr_feat_knn2(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride, const int64_t* pairs,
+                  int P, int Nq, int Mt, int C, int32_t* idx2_out, double* dist2_out, mvr_stream_t stream);
+
 /* Row gather dst[i][:] = src[idx[i]][:] (C floats per row): the Sampler's
  * index_select (lib/layers.py:151-152) with host-drawn (np.random) indices. */
 int mvr_gather_rows(const float* src, int C, const int64_t* idx, int n, float* dst, mvr_stream_t stream);
