@@ -246,7 +246,8 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx16 (&acc)
           if (BIAS == BIAS_N) { x.x += bn[j][0]; x.y += bn[j][1]; x.z += bn[j][2]; x.w += bn[j][3]; }
           if (RES) { x.x += w[j][q].x; x.y += w[j][q].y; x.z += w[j][q].z; x.w += w[j][q].w; }
           w[j][q] = x;
-          if (rok && sok[j]) *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + n0 + wn * 64 + j * 32 + 4 * p8) = x;
+          if (rok && sok[j] && !g.no_store)
+            *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + n0 + wn * 64 + j * 32 + 4 * p8) = x;
         }
         if (STATS == ST_ROW) {   // (sum, squared deviations from the wave-local mean) of this row
           float sm = 0.f, s2 = 0.f;
@@ -836,7 +837,8 @@ static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) 
 
 int launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return MVR_OK;
-  if (!g.A || !g.B || !g.C || g.K <= 0) return MVR_EINVAL;
+  if (!g.A || !g.B || (!g.C && !g.no_store) || g.K <= 0) return MVR_EINVAL;
+  if (g.no_store && (g.stats_mode != ST_ROW || g.has_res)) return MVR_EINVAL;   // stats-only: row statistics
   if (g.pro != PRO_NONE && !g.psc) return MVR_EINVAL;
   if ((g.pro == PRO_A_K || g.pro == PRO_B_K) && !g.psh) return MVR_EINVAL;
   if (g.stats_mode != ST_NONE && !g.stats) return MVR_EINVAL;
@@ -861,7 +863,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (tiles > 0x7fffffffLL) return MVR_EINVAL;
   const double fl = 2.0 * g.M * g.N * (double)g.K * g.batch;
   const double by = 4.0 * ((double)g.M * g.K * (g.sAb ? g.batch : 1) + (double)g.K * g.N * (g.sBb ? g.batch : 1) +
-                           (double)g.M * g.N * g.batch * (g.has_res ? 2 : 1));
+                           (double)g.M * g.N * g.batch * ((g.has_res ? 2 : 1) - (g.no_store ? 1 : 0)));
   ProfScope prof(g.prof_kind, fl, by, s);
   // Dispatch only the combinations the OANet schedule uses (oanet.hip).
 #define MVR_CASE(P, BKC_, BI, ST, RS)                                                                     \

@@ -50,6 +50,7 @@ struct GemmArgs {
   int pro, bias_mode, stats_mode, has_res;
   int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
   int math;                                            // Math (MATH_F32 = 0 by default)
+  int no_store;                                        // 1: statistics only, C is not written (may be null)
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the

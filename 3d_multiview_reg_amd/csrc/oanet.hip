@@ -24,17 +24,20 @@ namespace mvr {
 // mean_b var_b/(var_b+eps_in)) — written as per-(p,c) (mu, r_in) into `mv`,
 // finished by in_bn_train_kernel.
 // ----------------------------------------------------------------------------
-__global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld, int st_off, int T, int C, int L,
-                                   float eps_in, mvr_bn_p bn, int train, float* sc, float* sh, int64_t out_ld,
-                                   float2* mv) {
+__global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld, int st_off, int tw0, int csplit,
+                                   int tw1, int C, int L, float eps_in, mvr_bn_p bn, int train, float* sc, float* sh,
+                                   int64_t out_ld, float2* mv) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
   if (c >= C) return;
-  // tiles of 128 columns carry (sum, squared deviations from the tile mean): Chan's merge
+  // column tiles of tw (128 from the GEMM epilogues, 32 from the fused PointCN) carry (sum, squared
+  // deviations from the tile mean): Chan's merge
+  const int tw = c < csplit ? tw0 : tw1;
+  const int T = (L + tw - 1) / tw;
   double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int t = 0; t < T; ++t) {
     const float2 v = st[((int64_t)p * T + t) * st_ld + st_off + c];
-    const double nb = (double)min(128, L - 128 * t);
+    const double nb = (double)min(tw, L - tw * t);
     const double d = (double)v.x / nb - mean, tot = n + nb;
     mean += d * nb / tot;
     m2 += (double)v.y + d * d * n * nb / tot;
@@ -166,7 +169,7 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
-int g_oan_fused = 1;   // mvr_set_oan_fused
+int g_oan_fused = 1;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 1 PointCN (off: not faster yet)
 
 namespace {
 
@@ -175,10 +178,15 @@ struct Act {
   int64_t ps;    // pair stride
   int64_t ld;    // channel (row) stride
   int C, L;      // channels, length
-  float2* st;    // row statistics partials [P][T][st_ld] (+st_off)
+  float2* st;    // row statistics partials [P][T][st_ld] (+st_off), T = ceil(L / tile width)
   int64_t st_ld;
   int st_off;
+  int tw0 = 128;              // tile width of the partials of channels [0, csplit) (set by the writer)
+  int csplit = 1 << 30;
+  int tw1 = 128;              // ... and of channels [csplit, C)
 };
+
+constexpr int PCN_TILE = 32;   // statistics tile of the fused PointCN (pointcn.hip)
 
 struct Ws {
   char* base;
@@ -196,10 +204,11 @@ struct Plan {
   int P, N, C, Kc, Cin;
   int64_t Np, Kp, Cinp;  // padded row lengths (points, clusters, conv1 input channels)
   bool fused;            // diff_pool / diff_unpool as fused attention kernels (oan_attn.hip)
+  bool fused_pcn;        // PointCN(C -> C) as statistics-only conv3 + fused kernel (pointcn.hip)
   char* uimg;            // their split-bf16 operand images
   size_t uimg_bytes;
   size_t bytes;
-  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *fac, *W1;
+  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *sc2, *sh2, *scK, *shK, *fac, *W1;
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
 };
 
@@ -211,7 +220,9 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   Plan pl{};
   pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc; pl.Cin = Cin;
   pl.Np = round4(N); pl.Kp = round4(Kc); pl.Cinp = round4(Cin);
-  pl.fused = g_oan_fused && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
+  pl.fused = (g_oan_fused & 1) && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
+  pl.fused_pcn = (g_oan_fused & 2) && C == 128;
+  const int TS = pl.fused_pcn ? (N + PCN_TILE - 1) / PCN_TILE : gemm_ntiles(N);   // statistics tiles over points
   Ws w{reinterpret_cast<char*>(base), 0, 0};
   const size_t PN = (size_t)P * pl.Np, PK = (size_t)P * pl.Kp;
   const int TN = gemm_ntiles(N), TK = gemm_ntiles(Kc), MK = gemm_mtiles(Kc), MC = gemm_mtiles(C);
@@ -224,14 +235,16 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.O2 = w.take<float>(PK * C);
   pl.sc = w.take<float>((size_t)P * 2 * C);
   pl.sh = w.take<float>((size_t)P * 2 * C);
+  pl.sc2 = w.take<float>((size_t)P * C);
+  pl.sh2 = w.take<float>((size_t)P * C);
   pl.scK = w.take<float>(pl.Kp);
   pl.shK = w.take<float>(pl.Kp);
   size_t nf = (size_t)P * TN * pl.Kp;
   if ((size_t)P * MK * pl.Np > nf) nf = (size_t)P * MK * pl.Np;
   pl.fac = pl.fused ? nullptr : w.take<float>(nf);
   pl.W1 = w.take<float>((size_t)C * pl.Cinp);
-  pl.st11 = w.take<float2>((size_t)P * TN * 2 * C);
-  pl.stA = w.take<float2>((size_t)P * TN * C);
+  pl.st11 = w.take<float2>((size_t)P * TS * 2 * C);
+  pl.stA = w.take<float2>((size_t)P * TS * C);
   pl.stT = w.take<float2>((size_t)P * TN * C);
   pl.stD = w.take<float2>((size_t)P * TK * C);
   pl.stO = w.take<float2>((size_t)P * TK * C);
@@ -258,24 +271,25 @@ struct Ctx {
     if (hipGetLastError() != hipSuccess && !err) err = MVR_ELAUNCH;
   }
 
-  // IN(eps)+BN fold of activation `a` -> pl.sc / pl.sh ([P][a.C])
-  void finalize_in(const Act& a, float eps, const mvr_bn_p& bn) {
-    const int T = gemm_ntiles(a.L);
+  // IN(eps)+BN fold of activation `a` -> sc / sh ([P][a.C], default pl.sc / pl.sh)
+  void finalize_in(const Act& a, float eps, const mvr_bn_p& bn, float* sc = nullptr, float* sh = nullptr) {
+    if (!sc) { sc = pl.sc; sh = pl.sh; }
     dim3 grid((a.C + 255) / 256, pl.P);
-    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(256), 0, s, a.st, a.st_ld, a.st_off, T, a.C, a.L, eps, bn, train,
-                       pl.sc, pl.sh, (int64_t)a.C, pl.mv);
+    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(256), 0, s, a.st, a.st_ld, a.st_off, a.tw0, a.csplit, a.tw1, a.C,
+                       a.L, eps, bn, train, sc, sh, (int64_t)a.C, pl.mv);
     chk_launch();
     if (train) {
       hipLaunchKernelGGL(in_bn_train_kernel, dim3((a.C + 255) / 256), dim3(256), 0, s, pl.mv, pl.P, a.C, eps, bn,
-                         pl.sc, pl.sh, (int64_t)a.C);
+                         sc, sh, (int64_t)a.C);
       chk_launch();
     }
   }
 
   // 1x1 conv: out = W . pro(in) + b (+res); stats into out.st when `stats`
   void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
-            const float* w_padded = nullptr) {
+            const float* w_padded = nullptr, bool no_store = false) {
     GemmArgs g{};
+    g.no_store = no_store ? 1 : 0;
     g.math = g_default_math;
     g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
     g.A = w_padded ? w_padded : cv.weight; g.sAb = 0; g.lda = w_padded ? round4(in.C) : in.C;
@@ -290,10 +304,26 @@ struct Ctx {
     chk(launch_gemm(g, s));
   }
 
-  void pointcn(const mvr_pointcn_p& pc, const Act& x, const Act& y) {
+  // PointCN (oanet.py:18-43) from x to y (y may be x); sets the statistics tile width of y
+  void pointcn(const mvr_pointcn_p& pc, const Act& x, Act& y) {
     finalize_in(x, 1e-5f, pc.bn1);
     Act t{pl.T1, (int64_t)y.C * pl.Np, pl.Np, y.C, pl.N, pl.stT, y.C, 0};
     const bool sc = pc.shortcut.weight != nullptr;
+    if (pl.fused_pcn && !sc && x.C == pl.C && y.C == pl.C && y.st_off + pl.C <= y.st_ld) {
+      // statistics-only conv3 -> fold of t -> fused conv3 . IN/BN/ReLU . conv7 + x
+      Act ts = t;
+      ts.p = nullptr;
+      conv(pc.conv3, x, true, ts, nullptr, ST_ROW, nullptr, true);
+      finalize_in(t, 1e-5f, pc.bn5, pl.sc2, pl.sh2);
+      chk(mvr_pointcn_fused(x.p, x.ps, x.ld, y.p, y.ps, y.ld, pl.sc, pl.sh, pl.sc2, pl.sh2, pc.conv3.weight,
+                            pc.conv3.bias, pc.conv7.weight, pc.conv7.bias, pl.P, pl.C, pl.N,
+                            reinterpret_cast<float*>(y.st), y.st_ld, y.st_off, s));
+      y.tw0 = PCN_TILE;
+      y.csplit = 1 << 30;
+      return;
+    }
+    y.tw0 = 128;
+    y.csplit = 1 << 30;
     if (sc) conv(pc.shortcut, x, false, y, nullptr, ST_NONE);
     conv(pc.conv3, x, true, t, nullptr, ST_ROW);
     finalize_in(t, 1e-5f, pc.bn5);
@@ -346,7 +376,7 @@ using namespace mvr;
 
 extern "C" int mvr_set_oan_fused(int on) {
   const int prev = g_oan_fused;
-  g_oan_fused = on != 0;
+  g_oan_fused = on & 3;
   return prev;
 }
 
@@ -437,6 +467,9 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   }
   // l1_2: PointCN(2C -> C, shortcut) + (H-1) PointCN(C)
   Act x11{pl.X11, 2 * CN, Np, 2 * C, N, pl.st11, 2 * C, 0};
+  x11.tw0 = x11top.tw0;   // rows [0, C): the last l1_1 PointCN; rows [C, 2C): diff_unpool (128)
+  x11.csplit = C;
+  x11.tw1 = 128;
   Act out{latent ? latent : pl.XA, latent ? (int64_t)C * ld : CN, latent ? ld : Np, C, N, pl.stA, C, 0};
   cx.pointcn(blk->l1_2[0], x11, out);
   for (int i = 1; i < H; ++i) cx.pointcn(blk->l1_2[i], out, out);

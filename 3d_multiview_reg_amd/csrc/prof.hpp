@@ -15,6 +15,7 @@ enum ProfKind : int {
   PK_FEAT_NN = 7,
   PK_SPCONV = 8,     // FCGF sparse conv
   PK_SPARSE_MISC = 9,
+  PK_POINTCN = 10,   // fused PointCN (pointcn.hip)
   PK_COUNT = 16
 };
 bool prof_on();

@@ -10,7 +10,7 @@ import os
 import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "libmvreg_hip.so")
+LIB_PATH = os.environ.get("MVR_LIB") or os.path.join(_PKG, "libmvreg_hip.so")   # MVR_LIB: tools' variant builds
 _lib = None
 
 c_i64 = ctypes.c_int64
@@ -57,6 +57,8 @@ _SIGS = {
     "mvr_set_gemm_math": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),
+    "mvr_pointcn_fused": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                  c_vp, c_int, c_int, c_int, c_vp, c_i64, c_int, c_vp]),
     "mvr_oan_diff_pool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp]),
     "mvr_oan_diff_unpool_workspace_bytes": (c_size, [c_int, c_int, c_int]),
@@ -142,7 +144,7 @@ def check(rc, name):
 
 
 PROF_KINDS = {"conv_pts": 0, "embed": 1, "pool": 2, "unpool": 3, "oafilter": 4, "small": 5, "procrustes": 6,
-              "feat_nn": 7, "spconv": 8, "sparse_misc": 9}
+              "feat_nn": 7, "spconv": 8, "sparse_misc": 9, "pointcn": 10}
 
 
 def prof_set(on):

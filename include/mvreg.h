@@ -104,9 +104,12 @@ typedef struct {
 } mvr_oan_block_p;
 
 size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N);
-/* diff_pool / diff_unpool inside mvr_oan_block_forward: 1 (default) = fused attention kernels
- * (mvr_oan_diff_pool / _unpool) when channels == 128 and clusters <= 1024, 0 = embedding GEMM + softmax
- * factors + pooling GEMM.  Process-wide; query workspace bytes after setting it.  Returns the previous value. */
+/* Fused paths inside mvr_oan_block_forward (process-wide; default 1; query workspace bytes after setting):
+ *   bit 0: diff_pool / diff_unpool as the fused attention kernels (mvr_oan_diff_pool / _unpool) when
+ *          channels == 128 and clusters <= 1024 (else embedding GEMM + softmax factors + pooling GEMM);
+ *   bit 1: PointCN(128 -> 128) as a statistics-only conv3 pass + mvr_pointcn_fused (else conv3, conv7);
+ *          correct (tested) but not yet faster than the two GEMMs, so off by default.
+ * Returns the previous value. */
 int mvr_set_oan_fused(int on);
 
 /* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
@@ -151,6 +154,18 @@ int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t x_ld, cons
                         int64_t xd_pstride, int64_t xd_ld, int P, int channels, int N, int clusters, float* out,
                         int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld, int st_off,
                         void* workspace, size_t workspace_bytes, mvr_stream_t stream);
+
+/* Fused PointCN (lib/filtering/oanet.py:18-43) with channels == out_channels == 128 (identity shortcut):
+ *   y = W7 . relu(t * sc2 + sh2) + b7 + x,   t = W3 . relu(x * sc1 + sh1) + b3
+ * sc1/sh1, sc2/sh2 [P][128]: the two InstanceNorm+BatchNorm layers folded per (pair, channel) — sc2/sh2 come
+ * from the statistics of t (a statistics-only conv3 pass), so t is never stored.  x, y [P][128][ld] (y may
+ * be x), ld >= round_up(N,4), multiples of 4, 16-byte aligned; columns [N, round_up(N,4)) of y written 0.
+ * stats (may be NULL): float pairs (sum, squared deviations from the chunk mean) of y per 32-point chunk,
+ * at stats[2*((p*ceil(N/32) + chunk)*st_ld + st_off + c)]. */
+int mvr_pointcn_fused(const float* x, int64_t x_pstride, int64_t x_ld, float* y, int64_t y_pstride, int64_t y_ld,
+                      const float* sc1, const float* sh1, const float* sc2, const float* sh2, const float* w3,
+                      const float* b3, const float* w7, const float* b7, int P, int channels, int N, float* stats,
+                      int64_t st_ld, int st_off, mvr_stream_t stream);
 
 /* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*out_ld + n]
  * (the transpose of lib/filtering/oanet.py:234). */

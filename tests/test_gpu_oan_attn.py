@@ -121,9 +121,10 @@ def test_diff_pool_rejects_bad_layout(gpu):
     assert L.mvr_oan_diff_unpool_workspace_bytes(1, 64, 16) == 0
 
 
-def test_oanet_fused_vs_gemm_path(gpu):
-    """Whole filter with the fused diff_pool/diff_unpool vs the embedding-GEMM + softmax-factor path:
-    same R, t (1e-4) and inlier masks."""
+@pytest.mark.parametrize("fused", [1, 2, 3])
+def test_oanet_fused_vs_gemm_path(gpu, fused):
+    """Whole filter with the fused kernels (bit 0: diff_pool/diff_unpool, bit 1: PointCN) vs the plain
+    GEMM path: same R, t (1e-4) and inlier masks."""
     import torch
     from lib import _native as NV
     from test_gpu_oanet import _oanet
@@ -133,8 +134,8 @@ def test_oanet_fused_vs_gemm_path(gpu):
     outs = []
     L = NV.lib()
     try:
-        for fused in (1, 0):
-            L.mvr_set_oan_fused(fused)
+        for f in (fused, 0):
+            L.mvr_set_oan_fused(f)
             with torch.no_grad():
                 outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
     finally:
