@@ -13,6 +13,7 @@
 // matching W[k] slice into LDS, then runs v_mfma_f32_32x32x2_f32.  No atomics: every
 // output row is owned by exactly one workgroup (deterministic results).
 #include "common.hpp"
+#include "mfma_bf16.hpp"
 #include "prof.hpp"
 #include "sparse.hpp"
 
@@ -180,14 +181,234 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 variant (the default): the same output-stationary gather-GEMM on
+// v_mfma_f32_32x32x16_bf16 with both operands as three bf16 terms (fp32-level accuracy, see
+// mfma_bf16.hpp) — 2.7x the fp32 MFMA rate.  32 input channels per step; the gathered input rows
+// are staged as fp32 [row][32] (144-byte rows: conflict-free 16-byte row reads) and split per
+// fragment; the weights come pre-split (mvr_spconv_wimage) as [k][32-channel block][plane][Cout]
+// rows of 32 bf16 padded to 80 bytes, staged by LDS-DMA.
+constexpr int SB_K = 32;     // input channels per step
+constexpr int SB_AST = 36;   // fp32 row stride of the gathered tile
+constexpr int SB_BST = 40;   // bf16 row stride of the weight image (80 B)
+constexpr int SB_CP = 128;   // output-channel padding of the weight image (largest TN)
+
+__device__ __forceinline__ void sp_glds16(const char* src, char* lds_base) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+
+template <int TM, int TN, int WM, int WN>
+__global__ __launch_bounds__(256) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP) {
+  using namespace bx;
+  constexpr int WTN = TN / WN;
+  constexpr int NJ = WTN / 32;
+  static_assert(TM / WM == 32, "wave tile rows must be 32");
+  constexpr int BPL = TN * SB_BST;          // bf16 elements of one plane of a B stage
+  constexpr int BG = 3 * BPL * 2 / 16;      // 16-byte granules of a B stage
+  __shared__ __attribute__((aligned(16))) float As[2][TM * SB_AST];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * BPL];
+  __shared__ int32_t nb[TM][SP_KMAX + 1];
+  __shared__ int kact[SP_KMAX];
+  __shared__ int klist[SP_KMAX];
+  __shared__ int nk;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int64_t o0 = (int64_t)blockIdx.x * TM;
+  const int c0 = blockIdx.y * TN;
+  const int K = a.K;
+
+  if (tid < SP_KMAX) kact[tid] = 0;
+  __syncthreads();
+  for (int e = tid; e < TM * K; e += 256) {
+    const int row = e / K, k = e - row * K;
+    const int64_t o = o0 + row;
+    int v = -1;
+    if (o < a.Mout) {
+      const int64_t orow = a.perm ? a.perm[o] : o;
+      v = a.nbr ? a.nbr[orow * K + k] : (int)orow;
+    }
+    nb[row][k] = v;
+    if (v >= 0) kact[k] = 1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;
+    for (int k = 0; k < K; ++k)
+      if (kact[k]) klist[n++] = k;
+    nk = n;
+  }
+  __syncthreads();
+
+  const int nci = (a.Cin + SB_K - 1) / SB_K;
+  const int steps = nk * nci;
+  constexpr int AV = TM * (SB_K / 4) / 256;   // float4 of the gathered tile per thread
+  float4 ra[AV];
+
+  auto load_a = [&](int s) {
+    const int k = klist[s / nci];
+    const int ci0 = (s % nci) * SB_K;
+#pragma unroll
+    for (int r = 0; r < AV; ++r) {
+      const int idx = tid + 256 * r;
+      const int row = idx >> 3, ci = ci0 + 4 * (idx & 7);
+      const int src = nb[row][k];
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (src >= 0 && ci < a.Cin) v = *reinterpret_cast<const float4*>(a.in + (int64_t)src * a.ldin + ci);
+      ra[r] = v;
+    }
+  };
+  auto store_a = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < AV; ++r) {
+      const int idx = tid + 256 * r;
+      *reinterpret_cast<float4*>(&As[buf][(idx >> 3) * SB_AST + 4 * (idx & 7)]) = ra[r];
+    }
+  };
+  // weight stage: granule g of [plane][TN rows][40] <- image row block (k, channel block) at column c0
+  auto dma_b = [&](int s, int buf) {
+    const int k = klist[s / nci], cb = s % nci;
+    const char* base = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * 3 * CoutP + c0) * SB_BST * 2;
+    char* dst = reinterpret_cast<char*>(Bs[buf]);
+    for (int g0 = wid * 64; g0 < BG; g0 += 256) {
+      const int g = g0 + lane;
+      const int pl = g / (TN * 5), wi = g - pl * (TN * 5);
+      if (g < BG) sp_glds16(base + ((int64_t)pl * CoutP * SB_BST * 2) + wi * 16, dst + g0 * 16);
+    }
+  };
+
+  floatx16 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  if (steps > 0) {
+    load_a(0);
+    dma_b(0, 0);
+    store_a(0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int s = 0; s < steps; ++s) {
+    if (s + 1 < steps) {
+      load_a(s + 1);
+      dma_b(s + 1, cur ^ 1);
+    }
+    const float* A = As[cur];
+    const uint16_t* Bq = Bs[cur];
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const float* ap = A + (wm * 32 + l32) * SB_AST + 16 * st + 8 * h;
+      const float4 a0 = *reinterpret_cast<const float4*>(ap), a1 = *reinterpret_cast<const float4*>(ap + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      Frag fa;
+      split8(av, fa.h, fa.m, fa.l);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const uint16_t* bp = Bq + (wn * WTN + 32 * j + l32) * SB_BST + 16 * st + 8 * h;
+        Frag fb;
+        fb.h = *reinterpret_cast<const bf16x8*>(bp);
+        fb.m = *reinterpret_cast<const bf16x8*>(bp + BPL);
+        fb.l = *reinterpret_cast<const bf16x8*>(bp + 2 * BPL);
+        acc[j] = mfma6(fa, fb, acc[j]);
+      }
+    }
+    if (s + 1 < steps) store_a(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    cur ^= 1;
+  }
+
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = c0 + wn * WTN + j * 32 + l32;
+    if (c >= a.Cout) continue;
+    float bsc = 1.f, bsh = 0.f;
+    if (a.bn.gamma) {
+      bsc = a.bn.gamma[c] / sqrtf(a.bn.var[c] + a.bn_eps);
+      bsh = a.bn.beta[c] - a.bn.mean[c] * bsc;
+    }
+    const float bias = a.bias ? a.bias[c] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t ot = o0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      if (ot >= a.Mout) continue;
+      const int64_t o = a.perm ? a.perm[ot] : ot;
+      float v = acc[j][r] + bias;
+      v = fmaf(v, bsc, bsh);
+      if (a.res) v += a.res[o * a.ldres + c];
+      if (a.relu) v = fmaxf(v, 0.f);
+      a.out[o * a.ldout + c] = v;
+    }
+  }
+}
+
+// W [K][Cin][Cout] fp32 -> image [K][nci][3][CoutP][40] bf16 (h, m, l planes; zero padding)
+__global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin, int Cout, int nci, int64_t CoutP,
+                                     uint16_t* img) {
+  using namespace bx;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (k, cb, c, 4 groups of 8 channels)
+  const int64_t total = (int64_t)K * nci * CoutP * 4;
+  if (e >= total) return;
+  const int q = (int)(e & 3);
+  const int64_t t = e >> 2;
+  const int c = (int)(t % CoutP);
+  const int64_t kb = t / CoutP;   // k * nci + cb
+  const int cb = (int)(kb % nci), k = (int)(kb / nci);
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int ci = cb * SB_K + 8 * q + i;
+    v[i] = (ci < Cin && c < Cout) ? W[((int64_t)k * Cin + ci) * Cout + c] : 0.f;
+  }
+  Frag f;
+  split8(v, f.h, f.m, f.l);
+  uint16_t* row = img + ((kb * 3) * CoutP + c) * SB_BST + 8 * q;
+  *reinterpret_cast<bf16x8*>(row) = f.h;
+  *reinterpret_cast<bf16x8*>(row + CoutP * SB_BST) = f.m;
+  *reinterpret_cast<bf16x8*>(row + 2 * CoutP * SB_BST) = f.l;
+}
+
 }  // namespace mvr
 
 using namespace mvr;
 
+static int64_t sp_coutp(int Cout) { return ((int64_t)Cout + SB_CP - 1) / SB_CP * SB_CP; }
+
+extern "C" size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout) {
+  if (K <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  const int64_t nci = (Cin + SB_K - 1) / SB_K;
+  return (size_t)(K * nci * 3 * sp_coutp(Cout) * SB_BST * 2);
+}
+
+extern "C" int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, hipStream_t s) {
+  if (!W || !img || K <= 0 || K > SP_KMAX || Cin <= 0 || Cout <= 0 || bytes < mvr_spconv_wimage_bytes(K, Cin, Cout) ||
+      (reinterpret_cast<uintptr_t>(img) & 15))
+    return MVR_EINVAL;
+  const int nci = (Cin + SB_K - 1) / SB_K;
+  const int64_t CoutP = sp_coutp(Cout);
+  const int64_t total = (int64_t)K * nci * CoutP * 4;
+  hipLaunchKernelGGL(spconv_wimage_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, K, Cin, Cout, nci,
+                     CoutP, reinterpret_cast<uint16_t*>(img));
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
 extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K,
                           int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
-                          const float* res, int64_t ldres, int relu, float* out, int64_t ldout, hipStream_t s) {
+                          const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
+                          hipStream_t s) {
   if (!in || !W || !out || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
+  if (wimg && (reinterpret_cast<uintptr_t>(wimg) & 15)) return MVR_EINVAL;
   if (!nbr && K != 1) return MVR_EINVAL;
   if ((Cin & 3) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
       (reinterpret_cast<uintptr_t>(W) & 15))
@@ -195,6 +416,22 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
   if (Mout == 0) return MVR_OK;
   SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout};
   ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
+  if (wimg) {   // split-bf16 path (weights pre-split by mvr_spconv_wimage)
+    const uint16_t* wi = reinterpret_cast<const uint16_t*>(wimg);
+    const int64_t CoutP = sp_coutp(Cout);
+    if (Cout <= 32) {
+      hipLaunchKernelGGL((spconv_bx_kernel<128, 32, 4, 1>), dim3((unsigned)((Mout + 127) / 128), (Cout + 31) / 32),
+                         dim3(256), 0, s, a, wi, CoutP);
+    } else if (Cout <= 64) {
+      hipLaunchKernelGGL((spconv_bx_kernel<64, 64, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 63) / 64),
+                         dim3(256), 0, s, a, wi, CoutP);
+    } else {
+      hipLaunchKernelGGL((spconv_bx_kernel<64, 128, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 127) / 128),
+                         dim3(256), 0, s, a, wi, CoutP);
+    }
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
   if (Cout <= 32) {
     hipLaunchKernelGGL((spconv_kernel<128, 32, 4, 1>), dim3((unsigned)((Mout + 127) / 128), (Cout + 31) / 32),
                        dim3(256), 0, s, a);

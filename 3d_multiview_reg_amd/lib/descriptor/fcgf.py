@@ -10,11 +10,19 @@ CoordinateManager) and the gather-GEMM sparse convolution with BatchNorm,
 residual and ReLU fused into its epilogue; skip concatenations are free (the
 producers write straight into the halves of the concatenated buffers).
 """
+import os
+
 import torch
 import torch.nn as nn
 
 from lib import _native as N
 from lib.sparse import SparseTensor
+
+
+# split-bf16 sparse convs (csrc/spconv.hip spconv_bx_kernel): correct but slower than the exact-fp32
+# MFMA kernel here (the convs are gather-latency bound and the bf16 staging lowers occupancy), so off
+# unless MVR_SPCONV_BF16=1
+SPLIT_BF16 = os.environ.get("MVR_SPCONV_BF16", "0") == "1"
 
 
 class _MEConv(nn.Module):
@@ -26,6 +34,21 @@ class _MEConv(nn.Module):
         self.kernel = nn.Parameter(torch.empty(ksize ** 3, cin, cout))
         nn.init.kaiming_normal_(self.kernel.data.view(-1, cout), nonlinearity="relu")
         self.bias = nn.Parameter(torch.zeros(1, cout)) if has_bias else None
+        self._wimg = None
+        self._wimg_key = None
+
+    def wimage(self):
+        """Split-bf16 weight image (mvr_spconv_wimage), rebuilt when the kernel tensor changes."""
+        k = self.kernel
+        key = (k.data_ptr(), k._version, k.device)
+        if self._wimg is None or self._wimg_key != key:
+            K, cin, cout = k.shape
+            nb = N.lib().mvr_spconv_wimage_bytes(K, cin, cout)
+            self._wimg = torch.empty(nb, dtype=torch.uint8, device=k.device)
+            N.check(N.lib().mvr_spconv_wimage(N.ptr(k.data), K, cin, cout, N.ptr(self._wimg), nb, N.stream()),
+                    "mvr_spconv_wimage")
+            self._wimg_key = key
+        return self._wimg
 
 
 class _MENorm(nn.Module):
@@ -97,9 +120,10 @@ class FCGFNet(nn.Module):
         bnp, eps = _bn(norm)
         K, cin, cout = conv.kernel.shape
         nbr, perm = km if km is not None else (None, None)
+        wimg = conv.wimage() if SPLIT_BF16 else None
         N.check(N.lib().mvr_spconv(N.ptr(x), ldx, cin, N.ptr(nbr), N.ptr(perm), K, M, N.ptr(conv.kernel), cout,
-                                   N.ptr(bias), bnp, eps, N.ptr(res), ldres, int(relu), N.ptr(out), ldout, N.stream()),
-                "mvr_spconv")
+                                   N.ptr(bias), bnp, eps, N.ptr(res), ldres, int(relu), N.ptr(out), ldout,
+                                   N.ptr(wimg), N.stream()), "mvr_spconv")
         return out
 
     def _block(self, blk, x, ldx, km, M, out, ldout):

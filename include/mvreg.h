@@ -266,10 +266,16 @@ int mvr_kernel_map_order(const int32_t* nbr, int64_t Mout, int K, int32_t* perm,
  * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
  * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
  * perm (optional): order in which output rows are tiled (mvr_kernel_map_order); results are
- * written to their own rows either way. */
+ * written to their own rows either way.
+ * wimg (optional, 16-byte aligned): the weights pre-split by mvr_spconv_wimage -> split-bf16 MFMA path
+ * (fp32-level accuracy, ~2.7x the exact-fp32 MFMA rate); NULL -> exact fp32 MFMA on W. */
 int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K, int64_t Mout,
                const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
-               int64_t ldres, int relu, float* out, int64_t ldout, mvr_stream_t stream);
+               int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg, mvr_stream_t stream);
+/* Weight image of mvr_spconv's split-bf16 path: W [K][Cin][Cout] fp32 -> three bf16 planes in
+ * [K][ceil(Cin/32)][plane][round_up(Cout,128)][40] rows (80-byte rows, zero padded). */
+size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout);
+int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, mvr_stream_t stream);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
 size_t mvr_brick_map_bytes(int64_t M);

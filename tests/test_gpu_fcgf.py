@@ -52,9 +52,13 @@ def test_kernel_map_k7_property(gpu, frags):
     assert np.array_equal(nbr[nbr[o, k], K - 1 - k], o)
 
 
-def test_fcgf_forward_matches_oracle(gpu, frags):
+@pytest.mark.parametrize("split_bf16", [False, True])
+def test_fcgf_forward_matches_oracle(gpu, frags, split_bf16, monkeypatch):
+    """both sparse-conv paths: exact fp32 MFMA (default) and split-bf16 (mvr_spconv_wimage images)"""
     import torch
+    from lib.descriptor import fcgf as fcgf_mod
     from lib.descriptor.fcgf import FCGFNet
+    monkeypatch.setattr(fcgf_mod, "SPLIT_BF16", split_bf16)
     from lib.sparse import voxelize, SparseTensor
     from oracle.fcgf import fcgf_forward
     net = FCGFNet()
