@@ -85,6 +85,7 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
   __shared__ __attribute__((aligned(16))) float ybuf[4][32 * YLD];
   __shared__ __attribute__((aligned(16))) float f2s[2][2][PC];   // (sc2, sh2) of pairs by parity
   __shared__ __attribute__((aligned(16))) float f1s[2][2][PC];   // (sc1, sh1) of pairs by parity
+  __shared__ __attribute__((aligned(16))) float bsh[2][PC];       // (b3, b7), read at each GEMM start
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t per = (a.total + gridDim.x - 1) / gridDim.x;
   const int64_t g0 = min(a.total, (int64_t)blockIdx.x * per), g1 = min(a.total, g0 + per);
@@ -97,7 +98,6 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
   // weights as split A fragments (loaded once): A waves W3 rows 32 blk + l32 over k = c;
   // B waves W7 rows 32 blk + l32 over k-step q = 2 ab + s: o = 32 ab + 16 s + 8 (i >> 2) + 4h + (i & 3)
   Frag wf[8];
-  float bias[16];
   {
     const float* W = isA ? a.W3 : a.W7;
     const float* wr = W + (int64_t)(32 * blk + l32) * PC;
@@ -110,10 +110,20 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
       const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
       split8(v, wf[q].h, wf[q].m, wf[q].l);
     }
-    const float* bv = isA ? a.b3 : a.b7;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bias[r] = bv ? bv[32 * blk + (r & 3) + 8 * (r >> 2) + 4 * h] : 0.f;
+    if (tid < PC) {
+      bsh[0][tid] = a.b3 ? a.b3[tid] : 0.f;
+      bsh[1][tid] = a.b7 ? a.b7[tid] : 0.f;
+    }
   }
+  // accumulator initialised with this wave's bias rows 32 blk + 8 q + 4h + 0..3
+  auto bias_init = [&](floatx16& S) {
+    const float* bv = bsh[isA ? 0 : 1] + 32 * blk + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 u = *reinterpret_cast<const float4*>(bv + 8 * q);
+      S[4 * q + 0] = u.x; S[4 * q + 1] = u.y; S[4 * q + 2] = u.z; S[4 * q + 3] = u.w;
+    }
+  };
 
   // raw chunk g -> raw[slot], by the A waves only (their only vector-memory traffic, so vmcnt(0)
   // before the step barrier waits for exactly this); wave w: rows 32 w .. 32 w + 31
@@ -139,16 +149,21 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
     }
   };
 
-  // split: thread -> fragment (k-step w, lane): xn[16 w + 8h + i][n = lane row]
-  auto split = [&](int p, int kc, int slot, bool first, bool next_new) {
+  // split: thread -> fragment (k-step w, lane): xn[16 w + 8h + i][n = lane row].  Two halves so that
+  // they can be interleaved with a GEMM's MFMA groups: split_load issues the LDS reads, split_finish
+  // normalises, splits and writes the fragment.
+  float sv[8];
+  auto split_load = [&](int p, int kc, int slot, bool first, bool next_new) {
     if (PCN_ABL & 2) return;
     if (first) stage_fold(f2s[p & 1], a.sc2, a.sh2, p);
     if (next_new) stage_fold(f1s[(p + 1) & 1], a.sc1, a.sh1, p + 1);
-    const bool nok = kc * PCH + l32 < N;
     const float* rw = reinterpret_cast<const float*>(raw[slot]);
-    float v[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = rw[(16 * w + 8 * h + i) * PCH + l32];
+    for (int i = 0; i < 8; ++i) sv[i] = rw[(16 * w + 8 * h + i) * PCH + l32];
+  };
+  auto split_finish = [&](int p, int kc, int slot) {
+    if (PCN_ABL & 2) return;
+    const bool nok = kc * PCH + l32 < N;
     const float* f1 = &f1s[p & 1][0][16 * w + 8 * h];
     const float4 sa = *reinterpret_cast<const float4*>(f1), sb = *reinterpret_cast<const float4*>(f1 + 4);
     const float4 ha = *reinterpret_cast<const float4*>(f1 + PC), hb = *reinterpret_cast<const float4*>(f1 + PC + 4);
@@ -156,19 +171,19 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
     const float h1[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float y = fmaxf(fmaf(v[i], s1[i], h1[i]), 0.f);
-      v[i] = nok ? y : 0.f;
+      const float y = fmaxf(fmaf(sv[i], s1[i], h1[i]), 0.f);
+      sv[i] = nok ? y : 0.f;
     }
     Frag f;
-    split8(v, f.h, f.m, f.l);
+    split8(sv, f.h, f.m, f.l);
     write_frag(xnI[slot] + w * FRB + lane * 16, f);
   };
 
-  // A: t = W3 . xn + b3 -> relu(t * sc2 + sh2) -> conv7 B fragments
-  auto gemm1 = [&](int p, int slot) {
+  // A: t = W3 . xn + b3 -> relu(t * sc2 + sh2) -> conv7 B fragments; hook(ks) runs after the ks-th
+  // MFMA group (independent work interleaved with the matrix pipe)
+  auto gemm1 = [&](int p, int slot, auto&& hook) {
     floatx16 S;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) S[r] = bias[r];
+    bias_init(S);
     const char* xi = xnI[slot] + lane * 16;
     Frag cur = read_frag(xi, 0);
 #pragma unroll
@@ -178,6 +193,7 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
       PCN_FENCE();
       if (PCN_ABL & 1) asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l), "v"(wf[ks].h));
       else S = mfma6(wf[ks], cur, S);
+      hook(ks);
       PCN_FENCE();
       if (ks < 7) cur = nxt;
     }
@@ -202,7 +218,8 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
   // B: y = W7 . tn + b7 + x, stored, with per-chunk statistics.  The residual x of the wave's 32 rows
   // of the next chunk is DMA'd one step ahead into the wave's scratch ([32 rows][32] fp32) — asm
   // loads the compiler does not track, waited for explicitly — which then doubles as the transpose
-  // buffer ([32][YLD]).
+  // buffer ([32][YLD]).  The epilogue of chunk k - 3 (still in acc) runs before GEMM2 of chunk k - 2,
+  // whose MFMA groups carry the split of chunk k.
   auto dma_res = [&](int p, int kc) {
     if (PCN_ABL & 8) return;
     const int n = min(kc * PCH + 4 * (lane & 7), nlast);
@@ -212,10 +229,9 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
     for (int i = 0; i < 4; ++i)
       glds16c(reinterpret_cast<const char*>(src + (int64_t)(8 * i + (lane >> 3)) * a.xld), dst + i * 1024);
   };
-  floatx16 acc;   // B: y of the chunk whose epilogue runs at the next step
-  auto gemm2 = [&](int slot) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = bias[r];
+  floatx16 acc;
+  auto gemm2 = [&](int slot, auto&& hook) {
+    bias_init(acc);
     const char* ti = tnI[slot] + lane * 16;
     Frag cur = read_frag(ti, 0);
 #pragma unroll
@@ -225,43 +241,41 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
       PCN_FENCE();
       if (PCN_ABL & 1) asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l), "v"(wf[q].h));
       else acc = mfma6(wf[q], cur, acc);
+      hook(q);
       PCN_FENCE();
       if (q < 7) cur = nxt;
     }
   };
-  auto epilogue = [&](int p, int kc, bool has_next) {
-    if (PCN_ABL & 4) {
-      asm volatile("" ::"v"(acc));
-      return;
-    }
-    float* yb = ybuf[blk];
-    // row-per-lane-pair: lane -> row lane / 2, columns 16 (lane & 1) .. +15
-    const int row = lane >> 1, c0 = 16 * (lane & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this chunk's residual DMA (one step old)
-    float4 res[4];
+  // epilogue (chunk (ep, ekc), accumulator acc)
+  const int erow = lane >> 1, ec0 = 16 * (lane & 1);
+  float4 eres[4];
+  float ev[16];
+  float* yb = ybuf[blk];
+  auto ep_read_res = [&]() {
+    if (!(PCN_ABL & 32)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this chunk's residual DMA (one step old)
 #pragma unroll
-    for (int i4 = 0; i4 < 4; ++i4) res[i4] = *reinterpret_cast<const float4*>(yb + row * PCH + c0 + 4 * i4);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // read before the transpose overwrites it
+    for (int i4 = 0; i4 < 4; ++i4) eres[i4] = *reinterpret_cast<const float4*>(yb + erow * PCH + ec0 + 4 * i4);
+  };
+  auto ep_transpose = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // residual read before the transpose overwrites it
 #pragma unroll
     for (int r = 0; r < 16; ++r) yb[((r & 3) + 8 * (r >> 2) + 4 * h) * YLD + l32] = acc[r];
-    const int n0 = kc * PCH + c0;
-    const int o = 32 * blk + row;
-    const int nv = min(max(N - n0, 0), 16);
-    float* yr = a.Y + (int64_t)p * a.yps + (int64_t)o * a.yld + n0;
-    float v[16];
+  };
+  auto ep_read_y = [&]() {
 #pragma unroll
-    for (int i4 = 0; i4 < 4; ++i4) {
-      const float4 x = res[i4];
-      v[4 * i4 + 0] = yb[row * YLD + c0 + 4 * i4 + 0] + x.x;
-      v[4 * i4 + 1] = yb[row * YLD + c0 + 4 * i4 + 1] + x.y;
-      v[4 * i4 + 2] = yb[row * YLD + c0 + 4 * i4 + 2] + x.z;
-      v[4 * i4 + 3] = yb[row * YLD + c0 + 4 * i4 + 3] + x.w;
-    }
+    for (int i = 0; i < 16; ++i) ev[i] = yb[erow * YLD + ec0 + i];
+  };
+  auto ep_finish = [&](int p, int kc, bool has_next) {
+    const int n0 = kc * PCH + ec0;
+    const int o = 32 * blk + erow;
+    const int nv = min(max(N - n0, 0), 16);
     float sm = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      v[i] = i < nv ? v[i] : 0.f;
-      sm += v[i];
+      const float x = i < 4 ? (&eres[0].x)[i] : (i < 8 ? (&eres[1].x)[i - 4] : (i < 12 ? (&eres[2].x)[i - 8] : (&eres[3].x)[i - 12]));
+      const float y = ev[i] + x;
+      ev[i] = i < nv ? y : 0.f;
+      sm += ev[i];
     }
     sm += __shfl_xor(sm, 1, 64);
     const int cnt = min(max(N - kc * PCH, 0), PCH);
@@ -269,15 +283,16 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
     float m2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float d = i < nv ? v[i] - mu : 0.f;
+      const float d = i < nv ? ev[i] - mu : 0.f;
       m2 = fmaf(d, d, m2);
     }
     m2 += __shfl_xor(m2, 1, 64);
-    if (a.stats && (lane & 1) == 0) a.stats[((int64_t)p * a.nch + kc) * a.st_ld + a.st_off + o] = make_float2(sm, m2);
+    if (!(PCN_ABL & 16) && a.stats && (lane & 1) == 0) a.stats[((int64_t)p * a.nch + kc) * a.st_ld + a.st_off + o] = make_float2(sm, m2);
+    float* yr = a.Y + (int64_t)p * a.yps + (int64_t)o * a.yld + n0;
 #pragma unroll
     for (int i4 = 0; i4 < 4; ++i4)
-      if (n0 + 4 * i4 < N4)
-        *reinterpret_cast<float4*>(yr + 4 * i4) = make_float4(v[4 * i4], v[4 * i4 + 1], v[4 * i4 + 2], v[4 * i4 + 3]);
+      if (!(PCN_ABL & 16) && n0 + 4 * i4 < N4)
+        *reinterpret_cast<float4*>(yr + 4 * i4) = make_float4(ev[4 * i4], ev[4 * i4 + 1], ev[4 * i4 + 2], ev[4 * i4 + 3]);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // transpose reads done before the DMA lands
     if (has_next) dma_res(kc + 1 == a.nch ? p + 1 : p, kc + 1 == a.nch ? 0 : kc + 1);
   };
@@ -310,20 +325,40 @@ __global__ __launch_bounds__(512) void pointcn_chain_kernel(PcnArgs a) {
   for (int k = 0; k < nloc + 3; ++k) {
     const bool do_split = k < nloc;
     const bool split_first = k == 0 || cs.kc == 0, split_next_new = k + 1 < nloc && cs.kc == nch - 1;
+    const int slot = k & 1;
     if (isA) {
       if (k + 1 < nloc) dma(cn.p, cn.kc, (k + 1) & 1);
       if (k >= 1 && k <= nloc) {
-        gemm1(ca.p, (k - 1) & 1);
+        gemm1(ca.p, (k - 1) & 1, [&](int ks) {
+          if (!do_split) return;
+          if (ks == 1) split_load(cs.p, cs.kc, slot, split_first, split_next_new);
+          if (ks == 4) split_finish(cs.p, cs.kc, slot);
+        });
         adv(ca);
+      } else if (do_split) {
+        split_load(cs.p, cs.kc, slot, split_first, split_next_new);
+        split_finish(cs.p, cs.kc, slot);
       }
-      if (do_split) split(cs.p, cs.kc, k & 1, split_first, split_next_new);
     } else {
-      if (k >= 3 && k - 3 < nloc) {
-        epilogue(ce.p, ce.kc, k - 2 < nloc);
-        adv(ce);
+      const bool do_ep = k >= 3 && k - 3 < nloc;
+      const bool ep_next = k - 2 < nloc;
+      if (do_ep && !(PCN_ABL & 4)) {
+        ep_read_res();
+        ep_transpose();
+        ep_read_y();
+        ep_finish(ce.p, ce.kc, ep_next);
       }
-      if (do_split) split(cs.p, cs.kc, k & 1, split_first, split_next_new);
-      if (k >= 2 && k - 2 < nloc) gemm2(k & 1);
+      if (k >= 2 && k - 2 < nloc) {
+        gemm2(k & 1, [&](int q) {
+          if (!do_split) return;
+          if (q == 1) split_load(cs.p, cs.kc, slot, split_first, split_next_new);
+          if (q == 4) split_finish(cs.p, cs.kc, slot);
+        });
+      } else if (do_split) {
+        split_load(cs.p, cs.kc, slot, split_first, split_next_new);
+        split_finish(cs.p, cs.kc, slot);
+      }
+      if (do_ep) adv(ce);
     }
     if (k + 1 < nloc) adv(cn);
     if (do_split) adv(cs);
