@@ -29,7 +29,31 @@
 #include "gemm.hpp"
 #include "prof.hpp"
 
+#ifndef GEMM_EARLY
+#define GEMM_EARLY 1   // 0: refill after the MFMAs (ablation)
+#endif
+
+#ifndef GEMM_TRACE
+#define GEMM_TRACE 0   // 1: per-phase cycle totals per wave (s_memtime), tools only
+#endif
+
 namespace mvr {
+
+#if GEMM_TRACE
+__device__ unsigned long long g_gemm_trace[8];
+#define TSTAMP(slot)                                                   \
+  do {                                                                 \
+    unsigned long long t_;                                             \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));  \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    tr[prev_slot] += t_ - t_last;                                      \
+    t_last = t_;                                                       \
+    prev_slot = (slot);                                                \
+  } while (0)
+#else
+#define TSTAMP(slot) do {} while (0)
+#endif
 
 int g_default_math = MATH_BF16X3;
 
@@ -111,6 +135,17 @@ template <int X>
 __device__ __forceinline__ float swz(float v) {
   return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x1F | (X << 10)));
 }
+// sum over the 8 lanes of a 32-lane half that share (lane & 3): two DPP row rotations (by 4 and 8
+// lanes inside a 16-lane row, no LDS round trip) and one swizzle across the two rows
+template <int R>
+__device__ __forceinline__ float dpp_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float sum8_p8(float v) {
+  v += dpp_ror<4>(v);
+  v += dpp_ror<8>(v);
+  return v + swz<16>(v);
+}
 
 // 4x4 transpose across the 4 lanes t of a quad: on return register u of lane t holds what
 // register t of lane u held.
@@ -145,8 +180,16 @@ __device__ __forceinline__ f32x2 unpack_bf16(unsigned p) {
   r.y = __uint_as_float(p & 0xffff0000u);
   return r;
 }
+#ifndef GEMM_ABL
+#define GEMM_ABL 0   // ablation bits (timing only, wrong results): 1 = single-term split, 2 = one MFMA per product
+#endif
 __device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& H, u32x4& Mm, u32x4& L) {
   const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+  if (GEMM_ABL & 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) H[i] = Mm[i] = L[i] = cvt_pk_bf16(x[i]);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const unsigned hp = cvt_pk_bf16(x[i]);
@@ -216,60 +259,75 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs& g, floatx16 (&acc)
 #pragma unroll
         for (int u = 0; u < 4; ++u) bn[j][u] = cok[j][u] ? g.bias[n0 + wn * 64 + j * 32 + 4 * p8 + u] : 0.f;
     }
+    // all global loads of the epilogue up front (one latency): row biases and both blocks' residuals
+    float bm[2][4];
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii) {
-      asm volatile("" ::: "memory");   // keep each block's loads in its own iteration (VGPRs)
-      float4 w[2][4];
-      if (RES) {
-        const float* Rr = g.R + (int64_t)b * g.sRb;
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bm[ii][q] = BIAS == BIAS_M ? g.bias[min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1)] : 0.f;
+    float4 w[2][2][4];
+    if (RES) {
+      const float* Rr = g.R + (int64_t)b * g.sRb;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int gm = min(m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4, M - 1);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int gn = min(n0 + wn * 64 + j * 32 + 4 * p8, N4 - 4);
-            w[j][q] = *reinterpret_cast<const float4*>(Rr + (int64_t)gm * g.ldc + gn);
+            w[ii][j][q] = *reinterpret_cast<const float4*>(Rr + (int64_t)gm * g.ldc + gn);
           }
         }
-      }
+    }
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int gm = m0 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
         const bool rok = gm < M;
-        const float bm = BIAS == BIAS_M ? g.bias[min(gm, M - 1)] : 0.f;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           float a0 = acc[ii][j][4 * q], a1 = acc[ii][j][4 * q + 1], a2 = acc[ii][j][4 * q + 2],
                 a3 = acc[ii][j][4 * q + 3];
           quad_transpose(a0, a1, a2, a3, h1, h2);
-          float4 x = make_float4(a0 + bm, a1 + bm, a2 + bm, a3 + bm);
+          const float bq = bm[ii][q];
+          float4 x = make_float4(a0 + bq, a1 + bq, a2 + bq, a3 + bq);
           if (BIAS == BIAS_N) { x.x += bn[j][0]; x.y += bn[j][1]; x.z += bn[j][2]; x.w += bn[j][3]; }
-          if (RES) { x.x += w[j][q].x; x.y += w[j][q].y; x.z += w[j][q].z; x.w += w[j][q].w; }
-          w[j][q] = x;
+          if (RES) { x.x += w[ii][j][q].x; x.y += w[ii][j][q].y; x.z += w[ii][j][q].z; x.w += w[ii][j][q].w; }
+          w[ii][j][q] = x;
           if (rok && sok[j] && !g.no_store)
             *reinterpret_cast<float4*>(C + (int64_t)gm * g.ldc + n0 + wn * 64 + j * 32 + 4 * p8) = x;
         }
-        if (STATS == ST_ROW) {   // (sum, squared deviations from the wave-local mean) of this row
-          float sm = 0.f, s2 = 0.f;
+      }
+      if (STATS == ST_ROW) {   // (sum, squared deviations from the wave-local mean) of each row
+        float sm[4], s2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sm[q] = 0.f;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) sm += cok[j][u] ? f4(w[j][q], u) : 0.f;
-          sm += swz<4>(sm);
-          sm += swz<8>(sm);
-          sm += swz<16>(sm);
-          const float mu = sm * rnw;
+            for (int u = 0; u < 4; ++u) sm[q] += cok[j][u] ? f4(w[ii][j][q], u) : 0.f;
+          sm[q] = sum8_p8(sm[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float mu = sm[q] * rnw;
+          s2[q] = 0.f;
 #pragma unroll
           for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const float d = cok[j][u] ? f4(w[j][q], u) - mu : 0.f;
-              s2 = fmaf(d, d, s2);
+              const float d = cok[j][u] ? f4(w[ii][j][q], u) - mu : 0.f;
+              s2[q] = fmaf(d, d, s2[q]);
             }
-          s2 += swz<4>(s2);
-          s2 += swz<8>(s2);
-          s2 += swz<16>(s2);
-          if (p8 == 0) red[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(sm, s2);
+          s2[q] = sum8_p8(s2[q]);
+        }
+        if (p8 == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) red[wn * BM + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(sm[q], s2[q]);
         }
       }
     }
@@ -677,6 +735,15 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     for (int e = tid; e < 4 * KV; e += 256) vec[e] = 0.f;
     lds_barrier();
   }
+  // Stage ring (2 LDS slots).  Early issue: once every wave holds stage gs in registers, slot gs&1
+  // is refilled with stage gs + 2, so two stages are in flight during stage gs's MFMAs.  A per-tile
+  // prologue vector issued with stage gs + 2 may then belong to tile i + 2 (same parity slot as the
+  // tile being multiplied) when a tile has a single stage: those GEMMs refill after the MFMAs.
+  const bool early = GEMM_EARLY && !((PRO == PRO_A_K || PRO == PRO_B_K) && nk < 2);
+#if GEMM_TRACE
+  unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime();
+  int prev_slot = 7;
+#endif
   issue(0);
   glds_wait_all();
   __syncthreads();
@@ -686,6 +753,14 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     if (++ks == nk) {
       ks = 0;
       ++i;
+    }
+    TSTAMP(0);
+    if (early && gs > 0) {
+      // stage gs landed: loads complete in order, and stage gs + 1 (if issued) put at least 8
+      // younger LDS-DMAs per lane behind it (4 A + 4 B chunks)
+      if (gs + 1 < S) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
     }
     const int par = i & 1;
     const float* vsc = vec + (2 * par) * KV;
@@ -737,6 +812,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
         }
       }
     }
+    float fm[2] = {1.f, 1.f};
+    if (PRO == PRO_B_SMX) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fm[j] = fac[(gs & 1) * BN + wn * 64 + j * 32 + l32];
+    }
     if (!BKC) {
       lds_wait_regs(bkr);   // the asm reads' registers are tied to the wait: no use can move above it
 #pragma unroll
@@ -745,11 +825,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
         for (int s4 = 0; s4 < 4; ++s4)
           b4[j][s4] = make_float4(bkr[j][s4][0].x, bkr[j][s4][0].y, bkr[j][s4][1].x, bkr[j][s4][1].y);
     }
-    float fm[2] = {1.f, 1.f};
-    if (PRO == PRO_B_SMX) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) fm[j] = fac[(gs & 1) * BN + wn * 64 + j * 32 + l32];
+    TSTAMP(2);
+    if (early) {
+      lds_barrier();                                  // every wave holds stage gs: refill its slot
+      if (gs + 2 < S) issue(gs + 2);
     }
+    TSTAMP(3);
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const int kb = k0 + 4 * chunk_of<MATH>(s4, kh);
@@ -800,6 +881,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             // small terms first
+            if (GEMM_ABL & 2) {
+              acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bh[j], acc[ii][j], 0, 0, 0);
+              continue;
+            }
             acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ii], bh[j], acc[ii][j], 0, 0, 0);
             acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bl[j], acc[ii][j], 0, 0, 0);
             acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ii], bm[j], acc[ii][j], 0, 0, 0);
@@ -809,9 +894,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
           }
       }
     }
-    glds_wait_all();                                  // stage gs+1 (issued one stage ago) landed
-    __syncthreads();                                  // ... for every wave; stage gs fully read
-    if (gs + 2 < S) issue(gs + 2);
+    TSTAMP(4);
+    if (!early) {
+      glds_wait_all();                                // stage gs+1 (issued one stage ago) landed
+      __syncthreads();                                // ... for every wave; stage gs fully read
+      if (gs + 2 < S) issue(gs + 2);
+    }
     if (ks != nk - 1) continue;
 
     // -------------------------------------------------------------- epilogue of tile i
@@ -819,9 +907,16 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     //   C(m0 + 64wm + 32ii + 8q + 4kh + t4,  n0 + 64wn + 32j + 4p8 + u),  u = 0..3
     int b, tm, tn;
     tile_of(i, b, tm, tn);
+    TSTAMP(5);
     tile_epilogue<BIAS, STATS, RES>(g, acc, b, tm, tn, red, redm);
+    TSTAMP(6);
     // (red / redm are next written in the next tile's epilogue, after at least one stage barrier)
   }
+#if GEMM_TRACE
+  TSTAMP(7);
+  if (lane == 0)
+    for (int q = 0; q < 8; ++q) atomicAdd(&g_gemm_trace[q], tr[q]);
+#endif
 }
 
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
@@ -909,6 +1004,17 @@ extern "C" int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int6
   g.stats = reinterpret_cast<float2*>(stats); g.st_ld = st_ld; g.st_off = st_off; g.stats_mode = stats_mode;
   return mvr::launch_gemm(g, stream);
 }
+
+#if GEMM_TRACE
+extern "C" int mvr_gemm_trace(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mvr::g_gemm_trace), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mvr::g_gemm_trace), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" int mvr_set_gemm_math(int math) {
   if (math != mvr::MATH_F32 && math != mvr::MATH_BF16X3) return MVR_EINVAL;

@@ -21,6 +21,9 @@ CASES = {
 }
 
 
+TRACE = False
+
+
 def run(name, iters, math):
     M, Nn, Kk, pro, bkc, bias, stats, res = CASES[name]
     d = torch.device("cuda")
@@ -62,6 +65,18 @@ def run(name, iters, math):
     fl = 2.0 * M * Nn * Kk * P
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
     print("%-16s m%d %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
+    if TRACE:
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        L.mvr_gemm_trace(buf, 1)
+        go()
+        torch.cuda.synchronize()
+        L.mvr_gemm_trace(buf, 1)
+        tot = sum(buf)
+        names = ["stage-wait+barrier", "ktail+lds-reads", "barrier+issue", "transform+split+mfma",
+                 "refill(late)/loop", "tile_of", "epilogue", "tail"]
+        print("   phase shares (wave-cycles, one launch): " +
+              ", ".join("%s %.1f%%" % (names[q], 100.0 * buf[q] / max(tot, 1)) for q in range(8)), flush=True)
 
 
 def copy_bw(iters):
@@ -86,7 +101,12 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
     ap.add_argument("--math", default="01")
+    ap.add_argument("--trace", action="store_true", help="library built with -DGEMM_TRACE=1 (MVR_LIB)")
     a = ap.parse_args()
+    TRACE = a.trace
+    if TRACE:
+        import ctypes
+        NV.lib().mvr_gemm_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
     copy_bw(a.iters)
     for n in CASES:
         if a.only and n != a.only:
