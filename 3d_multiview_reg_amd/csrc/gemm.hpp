@@ -63,8 +63,13 @@ struct GemmArgs {
 // contract).
 int launch_gemm(const GemmArgs& g, hipStream_t stream);
 
+// 128 -> 128 point convolutions (pconv.hip): launch_gemm routes the shapes pconv_covers() accepts there
+bool pconv_covers(const GemmArgs& g);
+int launch_pconv(const GemmArgs& g, hipStream_t stream);
+
 inline int gemm_ntiles(int N) { return (N + GEMM_BN - 1) / GEMM_BN; }
 inline int gemm_mtiles(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }
 inline int64_t round4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+inline int64_t round32(int64_t x) { return (x + 31) & ~(int64_t)31; }
 
 }  // namespace mvr

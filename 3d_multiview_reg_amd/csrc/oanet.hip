@@ -212,14 +212,16 @@ struct Plan {
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
 };
 
-// Activations [P][C][Np] over points and [P][C][Kp] over clusters, rows padded to a multiple of 4
-// floats (16-byte rows for the LDS-DMA staging of gemm.hip).  With 128 channels (the reference
+// Activations [P][C][Np] over points and [P][C][Kp] over clusters, rows padded to a multiple of 32
+// floats: 128-byte rows, so that row segments written by the epilogues cover whole cache lines
+// (partial-line stores cut the streaming rate of a read+write pass from 4.8 to 3.2 TB/s,
+// tools/ld_micro.hip).  With 128 channels (the reference
 // configuration) diff_pool / diff_unpool run fused (oan_attn.hip) and the [clusters x points]
 // embedding buffer and its softmax factors are not allocated.
 Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   Plan pl{};
   pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc; pl.Cin = Cin;
-  pl.Np = round4(N); pl.Kp = round4(Kc); pl.Cinp = round4(Cin);
+  pl.Np = round32(N); pl.Kp = round32(Kc); pl.Cinp = round4(Cin);
   pl.fused = (g_oan_fused & 1) && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
   pl.fused_pcn = (g_oan_fused & 2) && C == 128;
   const int TS = pl.fused_pcn ? (N + PCN_TILE - 1) / PCN_TILE : gemm_ntiles(N);   // statistics tiles over points

@@ -157,7 +157,7 @@ class OANet(nn.Module):
         N.require_hip(self.reg_init.conv1.weight)
         xs = xs_in.to(dev, torch.float32)[:, 0].contiguous()           # [P, N, Cxs]
         P, Npts, Cxs = xs.shape
-        ld = (Npts + 3) // 4 * 4            # point rows padded to 16 bytes (csrc/gemm.hpp layout contract)
+        ld = (Npts + 31) // 32 * 32         # point rows padded to 128 bytes (whole cache lines per row segment)
         if Cxs < 6:
             raise ValueError("xs must have at least 6 channels (x1 | x2)")
         L = N.lib()

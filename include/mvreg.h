@@ -73,6 +73,10 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
                  mvr_stream_t stream);
 /* GEMM arithmetic used by mvr_oan_block_forward (process-wide; default 1 = bf16 split). */
 int mvr_set_gemm_math(int math);
+/* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
+ * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
+ * (A/B timing).  Returns the previous setting. */
+int mvr_set_pconv(int on);
 
 /* ------------------------------------------------------------------------
  * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters

@@ -127,7 +127,8 @@ COMBOS = [(0, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 0), (2, 0, 1, 0, 0), (2
 @pytest.mark.parametrize("math", [0, 1])       # exact fp32 MFMA / 3-term bf16 split
 @pytest.mark.parametrize("combo", COMBOS)
 @pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 36, 3), (500, 300, 64, 1), (1, 40, 8, 2),
-                                   (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2)])
+                                   (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2),
+                                   (128, 5000, 128, 3), (128, 517, 128, 2), (128, 500, 128, 5), (128, 31, 128, 2)])
 def test_gemm_modes(gpu, combo, shape, math):
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo

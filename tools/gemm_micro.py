@@ -24,14 +24,15 @@ CASES = {
 TRACE = False
 
 
-def run(name, iters, math):
+def run(name, iters, math, pconv=1):
     M, Nn, Kk, pro, bkc, bias, stats, res = CASES[name]
     d = torch.device("cuda")
     A = torch.randn(M, Kk, device=d) * 0.1 if name.startswith(("conv", "embed")) else torch.randn(P, M, Kk, device=d)
     sAb = 0 if A.dim() == 2 else M * Kk
-    Bt = torch.randn(P, Nn, Kk, device=d) if bkc else torch.randn(P, Kk, Nn, device=d)
-    Cout = torch.empty(P, M, Nn, device=d)
-    R = torch.randn(P, M, Nn, device=d) if res else None
+    Nl = (Nn + 31) // 32 * 32   # 128-byte rows, as the OANet activations (csrc/oanet.hip plan)
+    Bt = torch.randn(P, Nn, Kk, device=d) if bkc else torch.randn(P, Kk, Nl, device=d)
+    Cout = torch.empty(P, M, Nl, device=d)
+    R = torch.randn(P, M, Nl, device=d) if res else None
     bvec = torch.randn(M if bias == 1 else Nn, device=d) if bias else None
     kt = (Kk + 127) // 128
     if pro in (1, 2):
@@ -46,10 +47,11 @@ def run(name, iters, math):
     st = torch.empty(P, max(nt, mt), max(M, Nn), 2, device=d) if stats else None
     st_ld = M if stats in (1, 2) else Nn
     L = NV.lib()
+    L.mvr_set_pconv(pconv)
 
     def go():
-        rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk, Kk if bkc else Nn, bkc,
-                            NV.ptr(Cout), M * Nn, Nn, NV.ptr(R), M * Nn, NV.ptr(bvec), bias, NV.ptr(sc),
+        rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk if bkc else Kk * Nl, Kk if bkc else Nl, bkc,
+                            NV.ptr(Cout), M * Nl, Nl, NV.ptr(R), M * Nl, NV.ptr(bvec), bias, NV.ptr(sc),
                             NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, math, NV.stream())
         assert rc == 0
     for _ in range(2):
@@ -64,7 +66,8 @@ def run(name, iters, math):
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * M * Nn * Kk * P
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
-    print("%-16s m%d %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
+    print("%-16s m%d%s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, " pconv" if pconv and M == C and Kk == C else "",
+                                                          ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
     if TRACE:
         import ctypes
         buf = (ctypes.c_ulonglong * 8)()
@@ -112,4 +115,6 @@ if __name__ == "__main__":
         if a.only and n != a.only:
             continue
         for m in a.math:
-            run(n, a.iters, int(m))
+            run(n, a.iters, int(m), 0)
+            if m == "1" and n.startswith("conv"):
+                run(n, a.iters, int(m), 1)
