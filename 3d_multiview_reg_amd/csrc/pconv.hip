@@ -31,6 +31,11 @@
 
 namespace mvr {
 
+#ifndef PCONV_ABL
+#define PCONV_ABL 0   // timing ablations (wrong results; tools/build_variant.sh): 1 no MFMA, 2 no split,
+                      // 4 no epilogue, 8 no activation loads
+#endif
+
 int g_pconv = 1;   // mvr_set_pconv: 0 routes these convs to gemm_kernel (A/B timing)
 
 namespace {
@@ -42,7 +47,7 @@ constexpr int CH = 32;               // points per chunk (one MFMA column block)
 constexpr int GRP = 4;               // chunks per statistics group (128 points, gemm.hpp GEMM_BN)
 constexpr int FRB = 3 * 64 * 16;     // one k-step's fragment set: h, m, l planes x 64 lanes x 16 B
 constexpr int XIB = 8 * FRB;         // one chunk's B-fragment image (8 k-steps): 24 KB
-constexpr int YLD = 33;              // row stride (floats) of the per-wave transpose scratch
+constexpr int YLD = 32;              // row stride (floats) of the per-wave transpose scratch
 
 struct PcArgs {
   const float* X; int64_t xps, xld;     // input [P][128][xld]
@@ -56,11 +61,33 @@ struct PcArgs {
   int64_t groups;                       // P * ngrp
 };
 
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_base + 16 l.
+// Not tracked by the compiler: completion is awaited with an explicit s_waitcnt vmcnt.
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+
+#define PC_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// sum over the 8 lanes 8g .. 8g+7 (all of them receive it): quad butterflies, then the half-row mirror
+__device__ __forceinline__ float sum8(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
+  return v;
+}
+
 template <int PRO, int RES, int STATS>
 __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   __shared__ __attribute__((aligned(16))) char xi[2][XIB];
-  __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];
-  __shared__ __attribute__((aligned(16))) float fold[2][2][PC];   // (sc, sh) by pair parity
+  __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
+  __shared__ __attribute__((aligned(16))) float fold[2][2][PC];    // (sc, sh) by pair parity
+  __shared__ float sbias[PC];
 
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -87,18 +114,22 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
       split8(v, wf[q].h, wf[q].m, wf[q].l);
     }
   }
-  // epilogue ownership: row 32w + erow, columns ec0 .. ec0 + 15 of the chunk
-  const int erow = lane >> 1, ec0 = 16 * (lane & 1);
-  const int orow = 32 * w + erow;
-  const float bias = a.bias ? a.bias[orow] : 0.f;
+  // epilogue ownership: rows 32w + erow + 8q (q = 0..3), columns ec0 .. ec0 + 3 of the chunk — each
+  // float4 store instruction of the wave then writes 8 whole 128-byte row segments
+  const int erow = lane >> 3, ec0 = 4 * (lane & 7);
+  if (tid < PC) sbias[tid] = a.bias ? a.bias[tid] : 0.f;   // published by the prologue barriers
 
+  // chunk cursor (pair, chunk in pair); cursors past the range stay on the last chunk (clamped
+  // re-reads keep the issue unconditional, hence every s_waitcnt the compiler derives exact)
   struct Cur {
-    int p, kc;
+    int p, kc, j;
   };
   auto adv = [&](Cur& c) {
+    if (c.j + 1 >= nloc) return;
+    ++c.j;
     if (++c.kc == nch) { c.kc = 0; ++c.p; }
   };
-  const Cur cstart{p0, (int)(c0 - (int64_t)p0 * nch)};
+  const Cur cstart{p0, (int)(c0 - (int64_t)p0 * nch), 0};
 
   auto stage_fold = [&](int p) {
     if (PRO && tid < PC) {
@@ -113,141 +144,205 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) r[8 * t + i] = src[(int64_t)(16 * t + i) * a.xld];
+      for (int i = 0; i < 8; ++i) r[8 * t + i] = (PCONV_ABL & 8) ? (float)(i + t) : src[(int64_t)(16 * t + i) * a.xld];
   };
-  // normalise + split chunk registers -> fragment image slot
-  auto split_x = [&](const Cur& c, const float (&r)[16], int slot) {
+  // normalise + split half t of a chunk's registers -> its k-step fragment in image slot
+  auto split_half = [&](const Cur& c, const float (&r)[16], int slot, int t) {
+    float v[8];
+    if (PRO) {
+      const float* f = &fold[c.p & 1][0][32 * w + 16 * t + 8 * h];
+      const float4 sa = *reinterpret_cast<const float4*>(f), sb = *reinterpret_cast<const float4*>(f + 4);
+      const float4 ha = *reinterpret_cast<const float4*>(f + PC), hb = *reinterpret_cast<const float4*>(f + PC + 4);
+      const float s1[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
+      const float h1[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float v[8];
-      if (PRO) {
-        const float* f = &fold[c.p & 1][0][32 * w + 16 * t + 8 * h];
-        const float4 sa = *reinterpret_cast<const float4*>(f), sb = *reinterpret_cast<const float4*>(f + 4);
-        const float4 ha = *reinterpret_cast<const float4*>(f + PC), hb = *reinterpret_cast<const float4*>(f + PC + 4);
-        const float s1[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-        const float h1[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
+      for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(r[8 * t + i], s1[i], h1[i]), 0.f);
+    } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(r[8 * t + i], s1[i], h1[i]), 0.f);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = r[8 * t + i];
-      }
-      Frag f;
-      split8(v, f.h, f.m, f.l);
-      char* dst = xi[slot] + (2 * w + t) * FRB + lane * 16;
-      *reinterpret_cast<bf16x8*>(dst) = f.h;
-      *reinterpret_cast<bf16x8*>(dst + 1024) = f.m;
-      *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
+      for (int i = 0; i < 8; ++i) v[i] = r[8 * t + i];
     }
+    Frag f;
+    if (PCONV_ABL & 2) {
+      f.h = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+      f.m = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
+      f.l = f.h;
+    } else {
+      split8(v, f.h, f.m, f.l);
+    }
+    char* dst = xi[slot] + (2 * w + t) * FRB + lane * 16;
+    *reinterpret_cast<bf16x8*>(dst) = f.h;
+    *reinterpret_cast<bf16x8*>(dst + 1024) = f.m;
+    *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
   };
 
-  float rn = 0.f, rs = 0.f, rm2 = 0.f;   // running statistics of row orow over the current group
+  // residual of chunk c, rows 32w .. 32w+31 x 32 columns, by LDS-DMA into the wave's scratch as
+  // [row][32] (lane: row 8i + lane/8, columns 4 (lane & 7)); columns clamped into the padded row
   float* yb = ys[w];
-  // residual of chunk c (rows orow, columns ec0 .. ec0 + 15), addresses clamped into the padded row:
-  // issued unconditionally one step ahead so that the compiler's vmcnt bookkeeping stays exact
-  float4 rr[4];
-  auto issue_r = [&](const Cur& c) {
+  auto dma_r = [&](const Cur& c) {
     if (!RES) return;
-    const float* rsrc = a.R + (int64_t)c.p * a.rps + (int64_t)orow * a.yld;
+    const int n = min(c.kc * CH + 4 * (lane & 7), N4 - 4);
+    const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + (lane >> 3)) * a.yld + n;
 #pragma unroll
-    for (int i4 = 0; i4 < 4; ++i4)
-      rr[i4] = *reinterpret_cast<const float4*>(rsrc + min(c.kc * CH + ec0 + 4 * i4, N4 - 4));
+    for (int i = 0; i < 4; ++i) glds16(src + (int64_t)(8 * i) * a.yld, yb + 256 * i);
   };
-  auto compute = [&](const Cur& c, int slot) {
+
+  float rn = 0.f, rs[4] = {0.f, 0.f, 0.f, 0.f}, rm2[4] = {0.f, 0.f, 0.f, 0.f};   // running group statistics
+  // multiply chunk c (image slot) with hook(ks) after each k-step's MFMA group, then the epilogue
+  auto compute = [&](const Cur& c, int slot, auto&& hook) {
     const int n0 = c.kc * CH;
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const char* img = xi[slot] + lane * 16;
+    Frag cur;
+    cur.h = *reinterpret_cast<const bf16x8*>(img);
+    cur.m = *reinterpret_cast<const bf16x8*>(img + 1024);
+    cur.l = *reinterpret_cast<const bf16x8*>(img + 2048);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      Frag b;
-      b.h = *reinterpret_cast<const bf16x8*>(img + ks * FRB);
-      b.m = *reinterpret_cast<const bf16x8*>(img + ks * FRB + 1024);
-      b.l = *reinterpret_cast<const bf16x8*>(img + ks * FRB + 2048);
-      acc = mfma6(wf[ks], b, acc);
-    }
-    // transpose through the wave's scratch: register q = row (q & 3) + 8 (q >> 2) + 4h, column l32
-#pragma unroll
-    for (int q = 0; q < 16; ++q) yb[((q & 3) + 8 * (q >> 2) + 4 * h) * YLD + l32] = acc[q];
-    float ev[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) ev[i] = yb[erow * YLD + ec0 + i] + bias;
-    if (RES) {
-#pragma unroll
-      for (int i4 = 0; i4 < 4; ++i4) {
-        ev[4 * i4] += rr[i4].x; ev[4 * i4 + 1] += rr[i4].y; ev[4 * i4 + 2] += rr[i4].z; ev[4 * i4 + 3] += rr[i4].w;
+      Frag nxt;
+      if (ks < 7) {
+        nxt.h = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB);
+        nxt.m = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 1024);
+        nxt.l = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 2048);
       }
+      PC_FENCE();
+      if (PCONV_ABL & 1) asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l), "v"(wf[ks].h));
+      else acc = mfma6(wf[ks], cur, acc);
+      hook(ks);
+      PC_FENCE();
+      if (ks < 7) cur = nxt;
     }
-    float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)orow * a.yld + n0 + ec0;
+    if (PCONV_ABL & 4) {
+      asm volatile("" ::"v"(acc));
+      return;
+    }
+    // value (q, e) of this lane: row erow + 8q of the wave's 32, column n0 + ec0 + e
+    float4 ev[4];
+    if (RES) {   // the residual DMA (issued one step ago; 16 younger activation loads since)
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 #pragma unroll
-    for (int i4 = 0; i4 < 4; ++i4)
-      if (n0 + ec0 + 4 * i4 < N4)
-        reinterpret_cast<float4*>(ydst)[i4] = make_float4(ev[4 * i4], ev[4 * i4 + 1], ev[4 * i4 + 2], ev[4 * i4 + 3]);
+      for (int q = 0; q < 4; ++q) ev[q] = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // residual read before the transpose overwrites it
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ev[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // transpose through the wave's scratch: accumulator register r = row (r & 3) + 8 (r >> 2) + 4h, column l32
+#pragma unroll
+    for (int r = 0; r < 16; ++r) yb[((r & 3) + 8 * (r >> 2) + 4 * h) * YLD + l32] = acc[r];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
+      const float bq = sbias[32 * w + erow + 8 * q];
+      ev[q].x += v.x + bq; ev[q].y += v.y + bq; ev[q].z += v.z + bq; ev[q].w += v.w + bq;
+    }
+    float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + n0 + ec0;
+    const bool full = n0 + CH <= N;   // uniform: every column of the chunk is valid
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (full || n0 + ec0 < N4) *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
     if (STATS) {
-      const int nv = min(max(N - n0 - ec0, 0), 16);      // valid columns of this lane
-      const int cnt = min(N - n0, CH);                    // ... of the chunk (>= 1)
-      float s = 0.f;
+      const int cnt = min(N - n0, CH);   // valid columns of the chunk (>= 1)
+      const int nv = full ? 4 : min(max(N - n0 - ec0, 0), 4);
+      if (!full) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s += i < nv ? ev[i] : 0.f;
-      s += __shfl_xor(s, 1, 64);
-      const float mu = s / (float)cnt;
-      float m2 = 0.f;
+        for (int q = 0; q < 4; ++q) {
+          if (nv < 4) ev[q].w = 0.f;
+          if (nv < 3) ev[q].z = 0.f;
+          if (nv < 2) ev[q].y = 0.f;
+          if (nv < 1) ev[q].x = 0.f;
+        }
+      }
+      const float rc = 1.f / (float)cnt, fc = (float)cnt;
+      const float inv = rn == 0.f ? 0.f : 1.f / rn, wgt = rn == 0.f ? 0.f : rn * fc / (rn + fc);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float d = i < nv ? ev[i] - mu : 0.f;
-        m2 = fmaf(d, d, m2);
+      for (int q = 0; q < 4; ++q) {
+        const float s = sum8(ev[q].x + ev[q].y + ev[q].z + ev[q].w);
+        const float mu = s * rc;
+        float m2 = 0.f;
+        {
+          const float d0 = ev[q].x - mu, d1 = ev[q].y - mu, d2 = ev[q].z - mu, d3 = ev[q].w - mu;
+          m2 = fmaf(d0, d0, m2);
+          if (full || nv > 1) m2 = fmaf(d1, d1, m2);
+          if (full || nv > 2) m2 = fmaf(d2, d2, m2);
+          if (full || nv > 3) m2 = fmaf(d3, d3, m2);
+          if (!full && nv < 1) m2 = 0.f;
+        }
+        m2 = sum8(m2);
+        const float d = mu - rs[q] * inv;   // Chan's merge (a no-op blend while the group is empty)
+        rm2[q] += m2 + d * d * wgt;
+        rs[q] += s;
       }
-      m2 += __shfl_xor(m2, 1, 64);
-      const float fc = (float)cnt;
-      if (rn == 0.f) {
-        rn = fc; rs = s; rm2 = m2;
-      } else {   // Chan's merge
-        const float d = mu - rs / rn;
-        rm2 += m2 + d * d * (rn * fc / (rn + fc));
-        rs += s;
-        rn += fc;
-      }
+      rn += fc;
       if ((c.kc % GRP) == GRP - 1 || c.kc == nch - 1) {
-        if ((lane & 1) == 0)
-          a.stats[((int64_t)c.p * a.ngrp + c.kc / GRP) * a.st_ld + a.st_off + orow] = make_float2(rs, rm2);
+        if ((lane & 7) == 0) {
+          float2* st = a.stats + ((int64_t)c.p * a.ngrp + c.kc / GRP) * a.st_ld + a.st_off + 32 * w + erow;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) st[8 * q] = make_float2(rs[q], rm2[q]);
+        }
         rn = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rs[q] = rm2[q] = 0.f;
       }
     }
+    if (RES) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before the next DMA
   };
 
-  // Step j: split chunk j (registers -> image j & 1), refill the registers with chunk j + 2, stage the
-  // fold of chunk j + 1's pair when it starts one, barrier, multiply + epilogue of chunk j, then the
-  // residual of chunk j + 1.  Loads past the range re-read the last chunk (unconditional issue keeps
-  // every s_waitcnt the compiler derives a partial one: two chunks stay in flight).
-  float xa[16], xb[16];
-  Cur cs = cstart, cc = cstart, ci = cstart, cr = cstart;   // split, compute, x-issue, residual cursors
-  stage_fold(cstart.p);
-  issue_x(ci, xa);
-  if (1 < nloc) adv(ci);
-  issue_x(ci, xb);
-  if (2 < nloc) adv(ci);
-  issue_r(cr);
-  if (1 < nloc) adv(cr);
+  // Software pipeline (chunk j of this workgroup's range; register set (j % 3)):
+  //   step j: MFMAs of chunk j from image slot j & 1, with the split of chunk j + 1 (registers ->
+  //   slot (j + 1) & 1) and the load of chunk j + 4 into the freed registers interleaved between
+  //   the MFMA groups; epilogue of chunk j; residual DMA of chunk j + 1; fold of chunk j + 2's pair
+  //   when it starts one; one barrier.
+  float x0[16], x1[16], x2[16];
+  Cur cc = cstart, cs = cstart, ci = cstart, cf = cstart, cr = cstart;   // compute, split, issue, fold, residual
+  stage_fold(cf.p);
+  adv(cf);
+  if (cf.p != cstart.p) stage_fold(cf.p);
+  issue_x(ci, x0);
+  adv(ci);
+  issue_x(ci, x1);
+  adv(ci);
+  issue_x(ci, x2);
+  adv(ci);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  auto step = [&](int j, float (&xr)[16]) {
-    split_x(cs, xr, j & 1);
-    issue_x(ci, xr);
-    if (j + 3 < nloc) adv(ci);
-    adv(cs);
-    if (j + 1 < nloc && cs.kc == 0) stage_fold(cs.p);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    compute(cc, j & 1);
+  split_half(cs, x0, 0, 0);
+  split_half(cs, x0, 0, 1);
+  adv(cs);
+  issue_x(ci, x0);
+  adv(ci);
+  dma_r(cr);
+  adv(cr);
+  {
+    const Cur prev = cf;
+    adv(cf);
+    if (cf.p != prev.p) stage_fold(cf.p);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  auto step = [&](int j, float (&xs)[16]) {
+    compute(cc, j & 1, [&](int ks) {
+      if (ks == 1) split_half(cs, xs, (j + 1) & 1, 0);
+      if (ks == 3) split_half(cs, xs, (j + 1) & 1, 1);
+      if (ks == 4) issue_x(ci, xs);
+    });
     adv(cc);
-    issue_r(cr);
-    if (j + 2 < nloc) adv(cr);
+    adv(cs);
+    adv(ci);
+    dma_r(cr);
+    adv(cr);
+    const Cur prev = cf;
+    adv(cf);
+    if (cf.p != prev.p) stage_fold(cf.p);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
   int j = 0;
-  for (; j + 1 < nloc; j += 2) {
-    step(j, xa);
-    step(j + 1, xb);
+  for (; j + 2 < nloc; j += 3) {
+    step(j, x1);
+    step(j + 1, x2);
+    step(j + 2, x0);
   }
-  if (j < nloc) step(j, xa);
+  if (j < nloc) step(j, x1);
+  if (j + 1 < nloc) step(j + 1, x2);
 }
 
 }  // namespace

@@ -40,7 +40,15 @@ __global__ __launch_bounds__(256, 2) void stream_kernel(const float* X, float* Y
       const float* f = reinterpret_cast<const float*>(&r[q]);
 #pragma unroll
       for (int e = 0; e < V; ++e) acc += f[e];
-      if (STORE) *reinterpret_cast<T*>(Y + addr(s, q >> 3, q & 7)) = r[q];
+      if (STORE == 1) *reinterpret_cast<T*>(Y + addr(s, q >> 3, q & 7)) = r[q];
+    }
+    if (STORE == 2) {   // pconv's epilogue pattern: lane -> row (lane >> 1) of the wave's 32, 16 columns
+      const long p = s / nst;
+      const int n0 = (int)(s - p * nst) * PTS;
+      float* dst = Y + p * 128L * ld + (long)(32 * w + (lane >> 1)) * ld + min(n0 + 16 * (lane & 1), N - 16);
+      const float* f = reinterpret_cast<const float*>(&r[0]);
+#pragma unroll
+      for (int i4 = 0; i4 < 4; ++i4) reinterpret_cast<float4*>(dst)[i4] = make_float4(f[0], f[1], acc, f[0]);
     }
   };
   issue(s0, xa);
@@ -89,10 +97,11 @@ int main() {
       float t1 = run<1, 1>(X, Y, P, N, ld, sink, grid);
       float t2 = run<2, 1>(X, Y, P, N, ld, sink, grid);
       float t4 = run<4, 1>(X, Y, P, N, ld, sink, grid);
+      float e1 = run<1, 2>(X, Y, P, N, ld, sink, grid);
       float r1 = run<1, 0>(X, Y, P, N, ld, sink, grid);
       float r4 = run<4, 0>(X, Y, P, N, ld, sink, grid);
-      printf("ld %d grid %4d  read+write: V1 %.3f ms (%.0f GB/s)  V2 %.3f (%.0f)  V4 %.3f (%.0f) | read only: V1 %.3f (%.0f) V4 %.3f (%.0f)\n",
-             ld, grid, t1, gb / t1 * 1e3, t2, gb / t2 * 1e3, t4, gb / t4 * 1e3, r1, gb / 2 / r1 * 1e3, r4,
+      printf("ld %d grid %4d  read+write: V1 %.3f ms (%.0f GB/s)  V2 %.3f (%.0f)  V4 %.3f (%.0f) | pconv-store V1 %.3f (%.0f) | read only: V1 %.3f (%.0f) V4 %.3f (%.0f)\n",
+             ld, grid, t1, gb / t1 * 1e3, t2, gb / t2 * 1e3, t4, gb / t4 * 1e3, e1, gb / e1 * 1e3, r1, gb / 2 / r1 * 1e3, r4,
              gb / 2 / r4 * 1e3);
     }
   }
