@@ -34,6 +34,9 @@ constexpr int NN_STAGE = 128;      // targets per LDS stage
 constexpr int NN_ROW = 32;         // bf16 per LDS plane row; 16-byte chunk c of row r sits at slot
                                    // c ^ ((r >> 2) & 3): conflict-free ds_read_b128 down 16 rows
 constexpr float NN_NEG = -3.0e38f;
+#ifndef NN_ABL
+#define NN_ABL 0   // timing ablations of the fast path (wrong results): 1 no MFMA, 2 no softmax, 4 no staging
+#endif
 
 struct NNArgs {
   const float* Fq; int64_t fq_fs;    // query features [*][Nq][32], fragment stride (elements)
@@ -46,6 +49,7 @@ struct NNArgs {
   int mode;                          // 0 soft, 1 argmax (soft+st / hard)
   float* out; int64_t o_ps, o_ns;    // out(p,n,:) = [x_q(0..2) |] x_corr(0..2)
   int32_t* idx;                      // optional argmax index [P][Nq]
+  int fast;                          // soft mode: try the bounded-shift path first (feat_nn_fast)
 };
 
 __device__ __forceinline__ unsigned nn_cvt_pk(f32x2 x) {
@@ -72,10 +76,20 @@ __device__ __forceinline__ void nn_split8(const float4& a, const float4& b, u32x
 }
 __device__ __forceinline__ float nn_max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
+struct NNSmem {
+  unsigned short Fp[2][3][NN_STAGE][NN_ROW];   // bf16 planes h, m, l of the target features
+  union {
+    float Xs[2][4][NN_STAGE];                  // online path: x, y, z, |ft|^2 k2 (SoA)
+    float4 Xf[2][NN_STAGE];                    // fast path: (x, y, z, |ft|^2 k2) per target
+  };
+  int flag;
+};
+
+// Online-softmax path (any temperature / feature scale; argmax modes).
 template <int MODE>
-__global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Fp[2][3][NN_STAGE][NN_ROW];   // bf16 planes h, m, l
-  __shared__ __attribute__((aligned(16))) float Xs[2][4][NN_STAGE];                    // x, y, z, |ft|^2 k2
+__device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
+  auto& Fp = sm.Fp;
+  auto& Xs = sm.Xs;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l32 = lane & 31, kh = lane >> 5;
   const int p = blockIdx.y;
@@ -275,6 +289,7 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
     }
     return;
   }
+  (void)Fp;
   float ox, oy, oz;
   if (MODE == 0) {
     const float run_s = s2.x + s2.y, ax = ax2.x + ax2.y, ay = ay2.x + ay2.y, az = az2.x + az2.y;
@@ -299,6 +314,207 @@ __global__ __launch_bounds__(256, 3) void feat_nn_kernel(NNArgs a) {
     o[0] = ox; o[1] = oy; o[2] = oz;
     if (a.idx && MODE == 1) a.idx[(int64_t)p * a.Nq + j] = besti;
   }
+}
+
+
+// Fast soft path.  Two changes against the online path:
+//  * the softmax shift is the per-query bound k2 |fs|^2 instead of a running maximum: the
+//    accumulator starts at -|fs|^2 / 2, so logit = 2 k2 acc - k2 |ft|^2 = -k2 |fs - ft|^2 <= 0 (log2
+//    units) — exp2 never overflows, no maximum is tracked, nothing is rescaled.  Valid while a query's
+//    softmax sum stays >= 2^-60 (its nearest target within sqrt(60 / k2) in feature space; unit-norm
+//    descriptors at tau = 0.3 always are); the kernel re-runs a workgroup on the online path otherwise;
+//  * S = Fs . Ft^T with the TARGET as the lane column: a lane's 16 accumulator registers are 16
+//    queries against one target, so the target's (x, y, z, k2 |ft|^2) is one LDS read per 32-target
+//    chunk, and each lane keeps per-query partial sums over the targets it saw (4 x 16 registers),
+//    reduced across the 32 lanes once at the end.
+// Per (query, target): one fma, one exp2, one add, three fmas.
+__device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
+  auto& Fp = sm.Fp;
+  auto& Xf = sm.Xf;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int p = blockIdx.y;
+  const int64_t src = a.pairs[2 * p], tgt = a.pairs[2 * p + 1];
+  const float* Fq = a.Fq + src * a.fq_fs;
+  const float* Ft = a.Ft + tgt * a.ft_fs;
+  const float* Xt = a.Xt + tgt * a.xt_fs;
+  const int q0 = blockIdx.x * 128 + wid * 32;   // this wave's 32 queries
+  const int Mt = a.Mt;
+
+  // queries = A operand rows: lane row l32, dims 16s + 8kh + (0..7)
+  bf16x8 qh[2], qm[2], ql[2];
+  float q2 = 0.f;
+  {
+    const int jq = q0 + l32;
+    const float4* qp = reinterpret_cast<const float4*>(Fq + (int64_t)(jq < a.Nq ? jq : 0) * 32);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const float4 u = qp[v];
+      q2 += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 H, Mm, L;
+      nn_split8(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], H, Mm, L);
+      qh[s] = __builtin_bit_cast(bf16x8, H);
+      qm[s] = __builtin_bit_cast(bf16x8, Mm);
+      ql[s] = __builtin_bit_cast(bf16x8, L);
+    }
+  }
+  // accumulator register r holds query row 8 (r >> 2) + 4 kh + (r & 3): its start value -|fs|^2 / 2
+  floatx16 init;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) init[r] = -0.5f * __shfl(q2, 8 * (r >> 2) + 4 * kh + (r & 3), 64);
+
+  const int srow = tid >> 1, shalf = tid & 1;
+  float4 fr[4];
+  float xr0 = 0.f, xr1 = 0.f, xr2 = 0.f;
+  auto load_regs = [&](int t0) {
+    const int gi = t0 + srow;
+    const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + 16 * shalf);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < NN_STAGE) {
+      const int gc = t0 + tid;
+      if (gc < Mt) {
+        const float* xp = Xt + (int64_t)gc * 3;
+        xr0 = xp[0]; xr1 = xp[1]; xr2 = xp[2];
+      }
+    }
+  };
+  auto store_lds = [&](int buf, int t0) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      u32x4 H, Mm, L;
+      nn_split8(fr[2 * g], fr[2 * g + 1], H, Mm, L);
+      const int c = 8 * ((2 * shalf + g) ^ ((srow >> 2) & 3));
+      *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = H;
+      *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = Mm;
+      *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
+    }
+    float n2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
+    n2 += __shfl_xor(n2, 1, 64);
+    if (tid < NN_STAGE) {
+      Xf[buf][tid].x = xr0;
+      Xf[buf][tid].y = xr1;
+      Xf[buf][tid].z = xr2;
+    }
+    // invalid targets: +inf -> logit -inf -> weight 0 (their coordinates stay finite)
+    if (shalf == 0) Xf[buf][srow].w = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
+  };
+
+  float S[16], AX[16], AY[16], AZ[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) S[r] = AX[r] = AY[r] = AZ[r] = 0.f;
+  const float kk2 = 2.f * a.k2;
+  const int nst = (Mt + NN_STAGE - 1) / NN_STAGE;
+  load_regs(0);
+  store_lds(0, 0);
+  __syncthreads();
+  int cur = 0;
+  auto mfma_chunk = [&](int i0) {
+    floatx16 acc = init;
+    const int row = i0 + l32;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int c = 8 * ((2 * s + kh) ^ ((row >> 2) & 3));
+      const bf16x8 th = *reinterpret_cast<const bf16x8*>(&Fp[cur][0][row][c]);
+      const bf16x8 tm = *reinterpret_cast<const bf16x8*>(&Fp[cur][1][row][c]);
+      const bf16x8 tl = *reinterpret_cast<const bf16x8*>(&Fp[cur][2][row][c]);
+      if (NN_ABL & 1) {
+        asm volatile("" ::"v"(th), "v"(tm), "v"(tl));
+        acc[s] += 1.f;
+        continue;
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql[s], th, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], tl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm[s], tm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], tm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm[s], th, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], th, acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  // acc[r] = fs[query row(r)] . ft[i0 + l32] - |fs|^2 / 2
+  auto consume = [&](const floatx16& acc, int i0) {
+    const float4 X = Xf[cur][i0 + l32];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float pw = __builtin_amdgcn_exp2f(fmaf(acc[r], kk2, -X.w));
+      S[r] += pw;
+      AX[r] = fmaf(pw, X.x, AX[r]);
+      AY[r] = fmaf(pw, X.y, AY[r]);
+      AZ[r] = fmaf(pw, X.z, AZ[r]);
+    }
+  };
+  for (int st = 0; st < nst; ++st) {
+    const int t0 = st * NN_STAGE;
+    if (st + 1 < nst) load_regs(t0 + NN_STAGE);
+    floatx16 acc = mfma_chunk(0);
+#pragma unroll 1
+    for (int i0 = 0; i0 < NN_STAGE - 32; i0 += 32) {
+      const floatx16 nxt = mfma_chunk(i0 + 32);
+      consume(acc, i0);
+      acc = nxt;
+    }
+    consume(acc, NN_STAGE - 32);
+    if (st + 1 < nst) store_lds(cur ^ 1, t0 + NN_STAGE);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // reduce the per-lane partial sums over the 32 targets-lanes of each half
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      S[r] += __shfl_xor(S[r], o, 64);
+      AX[r] += __shfl_xor(AX[r], o, 64);
+      AY[r] += __shfl_xor(AY[r], o, 64);
+      AZ[r] += __shfl_xor(AZ[r], o, 64);
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int jq = q0 + 8 * (r >> 2) + 4 * kh + (r & 3);
+    bad |= jq < a.Nq && !(S[r] >= 0x1p-60f);   // underflowed (or non-finite) softmax sum
+  }
+  if (tid == 0) sm.flag = 0;
+  __syncthreads();
+  if (bad) sm.flag = 1;
+  __syncthreads();
+  if (sm.flag) return false;
+  // lane l32 = r of each half writes register r's query
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int jq = q0 + 8 * (r >> 2) + 4 * kh + (r & 3);
+    if (l32 == r && jq < a.Nq) {
+      float* o = a.out + (int64_t)p * a.o_ps + (int64_t)jq * a.o_ns;
+      if (a.Xq) {
+        const float* xq = a.Xq + src * a.xq_fs + (int64_t)jq * 3;
+        o[0] = xq[0]; o[1] = xq[1]; o[2] = xq[2];
+        o += 3;
+      }
+      o[0] = AX[r] / S[r]; o[1] = AY[r] / S[r]; o[2] = AZ[r] / S[r];
+    }
+  }
+  return true;
+}
+
+int g_nn_fast = 1;   // mvr_set_feat_nn_fast
+
+// MODE 0 (soft) with a.fast: the bounded-shift path, falling back to the online path for a workgroup
+// whose softmax sums underflowed; otherwise the online path (MODE 1 argmax, 2 two nearest).
+template <int MODE>
+__global__ __launch_bounds__(256, MODE == 0 ? 2 : 3) void feat_nn_kernel(NNArgs a) {
+  __shared__ __attribute__((aligned(16))) NNSmem sm;
+  if (MODE == 0 && a.fast) {
+    if (feat_nn_fast(a, sm)) return;
+    __syncthreads();
+  }
+  feat_nn_online<MODE>(a, sm);
 }
 
 // exact fp64 distances of the two neighbours: d[p][j][k] = |Fq(src, j) - Ft(tgt, idx[p][j][k])|
@@ -344,13 +560,14 @@ extern "C" int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft,
   if (mode != 0 && mode != 1) return MVR_EINVAL;
   if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt,
-                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out};
+                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out, mvr::g_nn_fast};
   mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * (C + 3) * 4 + P * Nq * 24.0,
                       stream);
+  const dim3 grid((Nq + 127) / 128, P);
   if (mode == 0)
-    hipLaunchKernelGGL(mvr::feat_nn_kernel<0>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(mvr::feat_nn_kernel<0>, grid, dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL(mvr::feat_nn_kernel<1>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(mvr::feat_nn_kernel<1>, grid, dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }
@@ -364,7 +581,7 @@ extern "C" int mvr_feat_knn2(const float* Fq, int64_t fq_fstride, const float* F
     return MVR_EINVAL;
   if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, nullptr, 0, Ft, 0, pairs, P, Nq, Mt, 1.4426950408889634f, 2,
-                nullptr, 0, 0, idx2_out};
+                nullptr, 0, 0, idx2_out, 0};
   mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * C * 4 + P * Nq * 8.0,
                       stream);
   hipLaunchKernelGGL(mvr::feat_nn_kernel<2>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);
@@ -386,4 +603,10 @@ extern "C" int mvr_gather_rows(const float* src, int C, const int64_t* idx, int 
                      dst);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_set_feat_nn_fast(int on) {
+  const int prev = mvr::g_nn_fast;
+  mvr::g_nn_fast = on ? 1 : 0;
+  return prev;
 }

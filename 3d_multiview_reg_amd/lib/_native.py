@@ -56,6 +56,7 @@ _SIGS = {
                              c_int, c_int, c_vp]),
     "mvr_set_gemm_math": (c_int, [c_int]),
     "mvr_set_pconv": (c_int, [c_int]),
+    "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),
     "mvr_pointcn_fused": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -224,6 +224,10 @@ int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft
                 int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P, int Nq, int Mt,
                 int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
                 int32_t* idx_out, mvr_stream_t stream);
+/* Soft mode runs a bounded-shift softmax first (shift k2 |fs|^2 per query instead of a running maximum:
+ * no max tracking or rescaling) and falls back to the online softmax per 128-query workgroup where a
+ * softmax sum underflows (< 2^-60).  1 (default) on, 0 online only.  Returns the previous setting. */
+int mvr_set_feat_nn_fast(int on);
 
 /* Two nearest neighbours in feature space (scripts/extract_data.py:178-184, sklearn NearestNeighbors
  * kneighbors(n_neighbors=2), Euclidean): for pair p and query j of fragment pairs[2p] (Fq rows, fragment stride

@@ -51,6 +51,35 @@ def test_feat_nn_pairs_vs_oracle(gpu, n, m):
             assert bad.mean() < 1e-3, bad.mean()
 
 
+@pytest.mark.parametrize("scale", [1.0, 2.5])
+def test_feat_nn_fast_path_matches_online(gpu, scale):
+    """Soft mode: the bounded-shift path (feat_nn_fast) against the online-softmax path; at scale 2.5
+    some queries' softmax sums underflow the fast path and their workgroups fall back."""
+    import torch
+    from lib import _native as NV
+    from oracle.soft_nn import soft_nn
+    B, n = 3, 2000
+    f = unit_features(B, n, 32, seed=7)
+    f[1] *= np.float32(scale)           # fragment 1 farther from everything in feature space
+    x = np.random.RandomState(6).uniform(-2, 2, (B, n, 3)).astype(np.float32)
+    pairs = np.array([[0, 1], [1, 2], [2, 0]], dtype=np.int64)
+    tf, tx, tp = (torch.from_numpy(a).to(gpu) for a in (f, x, pairs))
+    L = NV.lib()
+    outs = []
+    for fast in (1, 0):
+        prev = L.mvr_set_feat_nn_fast(fast)
+        out = torch.empty(len(pairs), n, 6, device=gpu)
+        rc = L.mvr_feat_nn(NV.ptr(tf), n * 32, NV.ptr(tf), n * 32, NV.ptr(tx), n * 3, NV.ptr(tx), n * 3, NV.ptr(tp),
+                           len(pairs), n, n, 32, 1.0 / 0.09, 0, NV.ptr(out), n * 6, 6, None, NV.stream())
+        L.mvr_set_feat_nn_fast(prev)
+        assert rc == 0
+        outs.append(out.cpu().numpy())
+    ref = soft_nn(f[pairs[:, 0]], f[pairs[:, 1]], x[pairs[:, 1]], "soft", st=False)
+    assert np.all(np.isfinite(outs[0]))
+    np.testing.assert_allclose(outs[0][..., 3:], ref, atol=3e-5)
+    np.testing.assert_allclose(outs[0], outs[1], atol=3e-5)
+
+
 def test_sampler_indices_and_gather(gpu):
     import torch
     from lib.layers import Sampler
