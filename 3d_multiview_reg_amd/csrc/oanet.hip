@@ -34,14 +34,18 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
   // deviations from the tile mean): Chan's merge
   const int tw = c < csplit ? tw0 : tw1;
   const int T = (L + tw - 1) / tw;
-  double n = 0.0, mean = 0.0, m2 = 0.0;
+  const float2* sp = st + (int64_t)p * T * st_ld + st_off + c;
+  // two passes over the tiles: the pooled mean, then M2 = sum_t (M2_t + n_t (mean_t - mean)^2)
+  // (tiles are full except the last, so one reciprocal serves all but one)
+  double tot = 0.0;
+  for (int t = 0; t < T; ++t) tot += (double)sp[(int64_t)t * st_ld].x;
+  const double mean = tot / L, rtw = 1.0 / tw;
+  double m2 = 0.0;
   for (int t = 0; t < T; ++t) {
-    const float2 v = st[((int64_t)p * T + t) * st_ld + st_off + c];
-    const double nb = (double)min(tw, L - tw * t);
-    const double d = (double)v.x / nb - mean, tot = n + nb;
-    mean += d * nb / tot;
-    m2 += (double)v.y + d * d * n * nb / tot;
-    n = tot;
+    const float2 v = sp[(int64_t)t * st_ld];
+    const int nb = min(tw, L - tw * t);
+    const double d = (double)v.x * (nb == tw ? rtw : 1.0 / nb) - mean;
+    m2 += (double)v.y + d * d * nb;
   }
   const double var = fmax(m2 / L, 0.0);
   const float rin = (float)(1.0 / sqrt(var + (double)eps_in));
@@ -276,8 +280,9 @@ struct Ctx {
   // IN(eps)+BN fold of activation `a` -> sc / sh ([P][a.C], default pl.sc / pl.sh)
   void finalize_in(const Act& a, float eps, const mvr_bn_p& bn, float* sc = nullptr, float* sh = nullptr) {
     if (!sc) { sc = pl.sc; sh = pl.sh; }
-    dim3 grid((a.C + 255) / 256, pl.P);
-    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(256), 0, s, a.st, a.st_ld, a.st_off, a.tw0, a.csplit, a.tw1, a.C,
+    const int bs = a.C >= 256 ? 256 : (a.C + 63) & ~63;
+    dim3 grid((a.C + bs - 1) / bs, pl.P);
+    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(bs), 0, s, a.st, a.st_ld, a.st_off, a.tw0, a.csplit, a.tw1, a.C,
                        a.L, eps, bn, train, sc, sh, (int64_t)a.C, pl.mv);
     chk_launch();
     if (train) {
