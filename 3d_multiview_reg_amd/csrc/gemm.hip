@@ -961,6 +961,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
                            (double)g.M * g.N * g.batch * ((g.has_res ? 2 : 1) - (g.no_store ? 1 : 0)));
   ProfScope prof(g.prof_kind, fl, by, s);
   if (pconv_covers(g)) return launch_pconv(g, s);
+  if (g.head_w) return MVR_EINVAL;   // the fused head exists on the point-conv kernel only
   // Dispatch only the combinations the OANet schedule uses (oanet.hip).
 #define MVR_CASE(P, BKC_, BI, ST, RS)                                                                     \
   if (g.pro == P && g.bkc == BKC_ && g.bias_mode == BI && g.stats_mode == ST && (g.has_res != 0) == RS) { \

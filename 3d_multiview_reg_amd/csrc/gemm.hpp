@@ -51,6 +51,9 @@ struct GemmArgs {
   int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
   int math;                                            // Math (MATH_F32 = 0 by default)
   int no_store;                                        // 1: statistics only, C is not written (may be null)
+  // output head fused into the epilogue (pconv only, M = 128): logits[b*N + n] = head_w . C(:, n) + head_bp[0] (nullable),
+  // scores = relu(tanh(logits)), pos[b] += #positive scores (oanet.py:163,174-178)
+  const float* head_w; const float* head_bp; float* logits; float* scores; int32_t* pos;
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the
@@ -64,7 +67,7 @@ struct GemmArgs {
 int launch_gemm(const GemmArgs& g, hipStream_t stream);
 
 // 128 -> 128 point convolutions (pconv.hip): launch_gemm routes the shapes pconv_covers() accepts there
-bool pconv_covers(const GemmArgs& g);
+bool pconv_covers(const GemmArgs& g);   // head fields set: only pconv can run it
 int launch_pconv(const GemmArgs& g, hipStream_t stream);
 
 inline int gemm_ntiles(int N) { return (N + GEMM_BN - 1) / GEMM_BN; }

@@ -293,9 +293,19 @@ struct Ctx {
   }
 
   // 1x1 conv: out = W . pro(in) + b (+res); stats into out.st when `stats`
+  // output head to fuse into the next conv (pconv epilogue), consumed by it
+  const mvr_conv_p* head = nullptr;
+  float* h_logits = nullptr;
+  float* h_scores = nullptr;
+  int32_t* h_pos = nullptr;
+
   void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
             const float* w_padded = nullptr, bool no_store = false) {
     GemmArgs g{};
+    if (head) {
+      g.head_w = head->weight; g.head_bp = head->bias;
+      g.logits = h_logits; g.scores = h_scores; g.pos = h_pos;
+    }
     g.no_store = no_store ? 1 : 0;
     g.math = g_default_math;
     g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
@@ -331,10 +341,14 @@ struct Ctx {
     }
     y.tw0 = 128;
     y.csplit = 1 << 30;
+    const mvr_conv_p* hd = head;   // the head goes with conv7 only
+    head = nullptr;
     if (sc) conv(pc.shortcut, x, false, y, nullptr, ST_NONE);
     conv(pc.conv3, x, true, t, nullptr, ST_ROW);
     finalize_in(t, 1e-5f, pc.bn5);
-    conv(pc.conv7, t, true, y, sc ? &y : &x, ST_ROW);
+    head = hd;
+    conv(pc.conv7, t, true, y, sc ? &y : &x, hd ? ST_NONE : ST_ROW);
+    head = nullptr;
   }
 
   void oafilter(const mvr_oafilter_p& f, const Act& xd) {
@@ -478,14 +492,25 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   x11.csplit = C;
   x11.tw1 = 128;
   Act out{latent ? latent : pl.XA, latent ? (int64_t)C * ld : CN, latent ? ld : Np, C, N, pl.stA, C, 0};
-  cx.pointcn(blk->l1_2[0], x11, out);
-  for (int i = 1; i < H; ++i) cx.pointcn(blk->l1_2[i], out, out);
-
-  // head + guard + Kabsch
+  // the output head (oanet.py:163,174-178) runs in the epilogue of the last PointCN conv when the
+  // point-conv kernel takes it; the guard counts start at zero either way
   (void)hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s);
-  hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, out.ps, out.ld, C, N,
-                     blk->output.weight, blk->output.bias, logits, scores, guard_pos);
-  cx.chk_launch();
+  GemmArgs probe{};
+  probe.math = g_default_math; probe.M = C; probe.N = N; probe.K = C; probe.batch = P; probe.pro = PRO_B_K;
+  probe.has_res = 1; probe.bias_mode = BIAS_M; probe.head_w = blk->output.weight;
+  const bool fuse_head = !pl.fused_pcn && pconv_covers(probe);   // (the fused-PointCN experiment keeps the head kernel)
+  for (int i = 0; i < H; ++i) {
+    if (fuse_head && i == H - 1) {
+      cx.head = &blk->output;
+      cx.h_logits = logits; cx.h_scores = scores; cx.h_pos = guard_pos;
+    }
+    cx.pointcn(blk->l1_2[i], i == 0 ? x11 : out, out);
+  }
+  if (!fuse_head) {
+    hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, out.ps, out.ld, C, N,
+                       blk->output.weight, blk->output.bias, logits, scores, guard_pos);
+    cx.chk_launch();
+  }
   if (cx.err) return cx.err;
   // weights = relu(tanh(logits)) already in `scores`; the guard (oanet.py:177-178) and
   // Kabsch (oanet.py:180-183, normalize_w=True, eps=1e-7)

@@ -59,6 +59,8 @@ struct PcArgs {
   float2* stats; int64_t st_ld; int st_off;        // [P][ngrp][st_ld] (+ st_off + m) (STATS)
   int N, nch, ngrp;
   int64_t groups;                       // P * ngrp
+  const float* hw; const float* hb;     // HEAD: output conv 128 -> 1 (oanet.py:163)
+  float* logits; float* scores; int32_t* pos;   // [P][N], [P][N], [P]
 };
 
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_base + 16 l.
@@ -82,12 +84,14 @@ __device__ __forceinline__ float sum8(float v) {
   return v;
 }
 
-template <int PRO, int RES, int STATS>
+template <int PRO, int RES, int STATS, int HEAD>
 __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   __shared__ __attribute__((aligned(16))) char xi[2][XIB];
   __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
   __shared__ __attribute__((aligned(16))) float fold[2][2][PC];    // (sc, sh) by pair parity
   __shared__ float sbias[PC];
+  __shared__ float shw[HEAD ? PC : 1];
+  __shared__ __attribute__((aligned(16))) float hpart[HEAD ? 2 : 1][4][CH];   // HEAD: per-wave partial logits by step parity
 
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -118,6 +122,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   // float4 store instruction of the wave then writes 8 whole 128-byte row segments
   const int erow = lane >> 3, ec0 = 4 * (lane & 7);
   if (tid < PC) sbias[tid] = a.bias ? a.bias[tid] : 0.f;   // published by the prologue barriers
+  if (HEAD && tid < PC) shw[tid] = a.hw[tid];
 
   // chunk cursor (pair, chunk in pair); cursors past the range stay on the last chunk (clamped
   // re-reads keep the issue unconditional, hence every s_waitcnt the compiler derives exact)
@@ -242,6 +247,22 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (full || n0 + ec0 < N4) *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
+    if (HEAD) {   // partial logits of the wave's 32 rows for the chunk's columns, summed over lanes l ^ 8, 16, 32
+      float hp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float wq = shw[32 * w + erow + 8 * q];
+        hp[0] = fmaf(wq, ev[q].x, hp[0]); hp[1] = fmaf(wq, ev[q].y, hp[1]);
+        hp[2] = fmaf(wq, ev[q].z, hp[2]); hp[3] = fmaf(wq, ev[q].w, hp[3]);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        hp[e] += __shfl_xor(hp[e], 8, 64);
+        hp[e] += __shfl_xor(hp[e], 16, 64);
+        hp[e] += __shfl_xor(hp[e], 32, 64);
+      }
+      if (lane < 8) *reinterpret_cast<float4*>(&hpart[c.j & 1][w][ec0]) = make_float4(hp[0], hp[1], hp[2], hp[3]);
+    }
     if (STATS) {
       const int cnt = min(N - n0, CH);   // valid columns of the chunk (>= 1)
       const int nv = full ? 4 : min(max(N - n0 - ec0, 0), 4);
@@ -319,7 +340,29 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     if (cf.p != prev.p) stage_fold(cf.p);
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  // HEAD: wave 0 completes the logits of the chunk computed one step ago (its partials are published
+  // by the step barrier): sum of the 4 waves' rows + bias, scores, positive count for the guard
+  auto head_finish = [&](const Cur& c) {
+    if (!HEAD || w != 0) return;
+    const int col = c.kc * CH + l32;
+    float lg = a.hb ? a.hb[0] : 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) lg += hpart[c.j & 1][ww][l32];
+    const float sc = fmaxf(tanhf(lg), 0.f);
+    const bool ok = lane < 32 && col < N;
+    if (ok) {
+      a.logits[(int64_t)c.p * N + col] = lg;
+      a.scores[(int64_t)c.p * N + col] = sc;
+    }
+    const int np = __popcll(__ballot(ok && sc > 0.f));
+    if (lane == 0 && np) atomicAdd(a.pos + c.p, np);
+  };
+  Cur ch = cstart;   // head cursor (one step behind compute)
   auto step = [&](int j, float (&xs)[16]) {
+    if (HEAD && j > 0) {
+      head_finish(ch);
+      adv(ch);
+    }
     compute(cc, j & 1, [&](int ks) {
       if (ks == 1) split_half(cs, xs, (j + 1) & 1, 0);
       if (ks == 3) split_half(cs, xs, (j + 1) & 1, 1);
@@ -343,12 +386,14 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   }
   if (j < nloc) step(j, x1);
   if (j + 1 < nloc) step(j + 1, x2);
+  if (HEAD) head_finish(ch);   // the last chunk (published by the last step's barrier)
 }
 
 }  // namespace
 
 // Dispatched by launch_gemm for the shapes it covers; the caller has checked the common contract.
 bool pconv_covers(const GemmArgs& g) {
+  if (g.head_w && g.stats_mode != ST_NONE) return false;
   return g_pconv && g.math == MATH_BF16X3 && g.M == PC && g.K == PC && !g.bkc && g.sAb == 0 && !g.no_store &&
          (g.pro == PRO_NONE || g.pro == PRO_B_K) && (g.stats_mode == ST_NONE || g.stats_mode == ST_ROW) &&
          g.bias_mode != BIAS_N && g.N > 0;
@@ -367,22 +412,25 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   a.nch = (g.N + CH - 1) / CH;
   a.ngrp = (a.nch + GRP - 1) / GRP;
   a.groups = (int64_t)g.batch * a.ngrp;
+  a.hw = g.head_w; a.hb = g.head_bp; a.logits = g.logits; a.scores = g.scores; a.pos = g.pos;
   const int grid = (int)(a.groups < 512 ? a.groups : 512);
-  const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
-#define MVR_PC(P_, R_, S_)                                                                  \
-  if (pro == P_ && res == R_ && st == S_) {                                                 \
-    hipLaunchKernelGGL((pconv_kernel<P_, R_, S_>), dim3(grid), dim3(256), 0, s, a);         \
+  const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW, head = g.head_w != nullptr;
+  if (head && (!g.logits || !g.scores || !g.pos)) return MVR_EINVAL;
+#define MVR_PC(P_, R_, S_, H_)                                                              \
+  if (pro == P_ && res == R_ && st == S_ && head == H_) {                                   \
+    hipLaunchKernelGGL((pconv_kernel<P_, R_, S_, H_>), dim3(grid), dim3(256), 0, s, a);     \
     MVR_CHECK_LAUNCH();                                                                     \
     return MVR_OK;                                                                          \
   }
-  MVR_PC(1, 0, 1)
-  MVR_PC(1, 1, 1)
-  MVR_PC(1, 0, 0)
-  MVR_PC(1, 1, 0)
-  MVR_PC(0, 0, 1)
-  MVR_PC(0, 1, 1)
-  MVR_PC(0, 0, 0)
-  MVR_PC(0, 1, 0)
+  MVR_PC(1, 0, 1, 0)
+  MVR_PC(1, 1, 1, 0)
+  MVR_PC(1, 0, 0, 0)
+  MVR_PC(1, 1, 0, 0)
+  MVR_PC(0, 0, 1, 0)
+  MVR_PC(0, 1, 1, 0)
+  MVR_PC(0, 0, 0, 0)
+  MVR_PC(0, 1, 0, 0)
+  MVR_PC(1, 1, 0, 1)   // the last PointCN conv of a block with the output head (oanet.py:174-175)
 #undef MVR_PC
   return MVR_EINVAL;
 }

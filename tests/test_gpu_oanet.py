@@ -150,3 +150,37 @@ def test_procrustes_guard_group(gpu):
         Ro, to, _, _ = kabsch(x1, x2, wexp)
         np.testing.assert_allclose(R.cpu().numpy(), Ro, atol=1e-5)
         np.testing.assert_allclose(tt.cpu().numpy(), to, atol=1e-5)
+
+
+def test_oanet_fused_head_guard_and_pconv_off(gpu):
+    """128 channels: the output head fused into the last point conv (pconv.hip) — with the zero-row guard
+    triggered for every pair (output bias -1e4) against the oracle, and the default path against the
+    generic-GEMM path (mvr_set_pconv(0), separate head kernel)."""
+    import torch
+    from lib import _native as NV
+    from oracle.oanet import oanet_forward
+    xs, _, _ = synth_correspondences(3, 777, seed=78)
+    ovr = {"reg_init.output.bias": [-1.0e4]}
+    net = _oanet(128, 500, 9, gpu, which="full", overrides=ovr)
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
+    o = oanet_forward(synth_state(_shapes("full"), seed=9, overrides=ovr), xs)
+    g = {}
+    for i in range(2):
+        g["logits%d" % i], g["scores%d" % i] = o["logits"][i], o["scores"][i]
+        g["R%d" % i], g["t%d" % i] = o["rot_est"][i], o["trans_est"][i]
+    _check(out, g, atol_logit=2e-3)
+    assert np.all(out["logits"][0].cpu().numpy() < 0)     # every weight zero: the guard's branch ran
+    net2 = _oanet(128, 500, 7, gpu, which="full")
+    xs2, _, _ = synth_correspondences(4, 1000, seed=79)
+    L = NV.lib()
+    res = []
+    for on in (1, 0):
+        prev = L.mvr_set_pconv(on)
+        with torch.no_grad():
+            res.append(net2({"xs": torch.from_numpy(xs2).unsqueeze(1)}))
+        L.mvr_set_pconv(prev)
+    for i in range(2):
+        np.testing.assert_allclose(res[0]["logits"][i].cpu().numpy(), res[1]["logits"][i].cpu().numpy(), atol=2e-3,
+                                   rtol=1e-4)
+        np.testing.assert_allclose(res[0]["rot_est"][i].cpu().numpy(), res[1]["rot_est"][i].cpu().numpy(), atol=1e-4)
