@@ -33,7 +33,8 @@ def attribute(disp, seq):
     """-> {class: [bytes...]} for the timed step: GEMM dispatches joined to the sequence in order,
     other profiled kernels by name."""
     out = defaultdict(list)
-    gemm = [v for n, v in disp if "gemm_kernel" in n]
+    # launch_gemm's launches (gemm_kernel, or pconv_kernel for the 128 -> 128 point convs) in launch order
+    gemm = [v for n, v in disp if "gemm_kernel" in n or "pconv_kernel" in n]
     seq_g = [c for c, _ in seq if c in GEMM_CLASSES]
     for c, v in zip(seq_g, gemm[len(gemm) - len(seq_g):]):
         out[c].append(v)
