@@ -37,10 +37,13 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
   const float2* sp = st + (int64_t)p * T * st_ld + st_off + c;
   // two passes over the tiles: the pooled mean, then M2 = sum_t (M2_t + n_t (mean_t - mean)^2)
   // (tiles are full except the last, so one reciprocal serves all but one)
+  // (8 independent loads in flight per thread: the loop is latency-bound otherwise)
   double tot = 0.0;
-  for (int t = 0; t < T; ++t) tot += (double)sp[(int64_t)t * st_ld].x;
+#pragma unroll 8
+  for (int t = 0; t < T; ++t) tot += (double)__builtin_nontemporal_load(&sp[(int64_t)t * st_ld].x);
   const double mean = tot / L, rtw = 1.0 / tw;
   double m2 = 0.0;
+#pragma unroll 8
   for (int t = 0; t < T; ++t) {
     const float2 v = sp[(int64_t)t * st_ld];
     const int nb = min(tw, L - tw * t);

@@ -17,6 +17,8 @@
 //   every dedup in first-occurrence order of the input rows.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "prof.hpp"
 #include "sparse.hpp"
@@ -168,30 +170,31 @@ __global__ void scan_add_kernel(int32_t* out, int64_t n, const int32_t* __restri
   if (i < n) out[i] += bsum[blockIdx.x];
 }
 
-// compact selected rows (first occurrences) in source order; per-batch counts aggregated per wave
-// (one atomic per distinct batch index in the wave — inputs are batch-major, so usually one)
+// compact selected rows (first occurrences) in source order
 __global__ void compact_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ pos, int64_t n,
-                               const int4* __restrict__ cc, int4* coords_out, int64_t* sel_out, int64_t* counts) {
+                               const int4* __restrict__ cc, int4* coords_out, int64_t* sel_out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < n && flags[i];
-  int bx = -1;
-  if (active) {
+  if (i < n && flags[i]) {
     const int p = pos[i];
-    const int4 c = cc[i];
-    coords_out[p] = c;
+    coords_out[p] = cc[i];
     if (sel_out) sel_out[p] = i;
-    bx = c.x;
   }
-  if (!counts) return;
-  unsigned long long act = __ballot(active);
-  while (act) {
-    const int leader = __ffsll((long long)act) - 1;
-    const int bl = __shfl(bx, leader, 64);
-    const unsigned long long same = __ballot(active && bx == bl);
-    if ((int)(threadIdx.x & 63) == leader)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&counts[1 + bl]), (unsigned long long)__popcll(same));
-    act &= ~same;
-  }
+}
+
+// per-batch row counts of the compacted set: a block-private LDS histogram over a contiguous run of
+// output rows, then one global atomic per non-empty bin (batch-major rows: one or two per block, so
+// no contention on the per-batch counters, whatever the input order)
+__global__ void batch_count_kernel(const int4* __restrict__ coords, int B, int64_t* counts) {
+  extern __shared__ int hist[];
+  const int64_t total = counts[0];
+  const int64_t per = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per, r1 = min(total, r0 + per);
+  for (int b = threadIdx.x; b < B; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(&hist[coords[r].x], 1);
+  __syncthreads();
+  for (int b = threadIdx.x; b < B; b += blockDim.x)
+    if (hist[b]) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[1 + b]), (unsigned long long)hist[b]);
 }
 
 __global__ void build_table_kernel(const int4* __restrict__ c, int64_t M, HashView h) {
@@ -407,8 +410,9 @@ static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel
   hipLaunchKernelGGL(scan_block_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.flags, n, d.pos, d.bsum);
   hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SCAN_B), 0, s, d.bsum, nb, counts);
   hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.pos, n, d.bsum);
-  hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, d.flags, d.pos, n, d.cc, coords_out, sel_out,
-                     counts);
+  hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, d.flags, d.pos, n, d.cc, coords_out, sel_out);
+  const int cb = (int)std::min<int64_t>(nblk(n), 512);
+  hipLaunchKernelGGL(batch_count_kernel, dim3(cb), dim3(256), sizeof(int) * B, s, coords_out, B, counts);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }
