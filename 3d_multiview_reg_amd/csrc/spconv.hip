@@ -82,49 +82,57 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
 
   constexpr int AV = TM * SP_BK / 4 / 256;                       // float4 per thread for A (1 or 2)
   constexpr int BV = (SP_BK * TN / 4 + 255) / 256;               // float4 per thread for B (1 or 2)
-  float4 ra[AV], rb[BV];
+  // Three steps of gathered rows in flight in registers (the gather is latency-bound: a step's
+  // MFMAs are far shorter than a dependent HBM/L2 round trip), two LDS buffers.
+  // Loads are issued unconditionally (clamped addresses, validity kept as bit masks applied when the
+  // registers are stored) so that the compiler's vmcnt bookkeeping keeps the steps in flight.
+  // Register set i: a_i (gathered rows), b_i (weights), m_i (validity bits: A in 0..AV-1, B above).
+  float4 a_0[AV], a_1[AV], a_2[AV], b_0[BV], b_1[BV], b_2[BV];
+  uint32_t m_0 = 0, m_1 = 0, m_2 = 0;
 
-  auto load = [&](int s) {
+  auto load = [&](int s, float4 (&ra)[AV], float4 (&rb)[BV], uint32_t& msk) {
+    if (s >= steps) s = steps - 1;   // clamped re-read past the end
     const int k = klist[s / nch];
     const int ci0 = (s % nch) * SP_BK;
+    uint32_t mm = 0;
 #pragma unroll
     for (int r = 0; r < AV; ++r) {
       const int idx = tid + 256 * r;
       const int row = idx >> 2, ciq = (idx & 3) * 4;
       const int src = nb[row][k];
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (src >= 0 && ci0 + ciq < a.Cin) v = *reinterpret_cast<const float4*>(a.in + (int64_t)src * a.ldin + ci0 + ciq);
-      ra[r] = v;
+      mm |= (src >= 0 && ci0 + ciq < a.Cin) ? (1u << r) : 0u;
+      ra[r] = *reinterpret_cast<const float4*>(a.in + (int64_t)(src >= 0 ? src : 0) * a.ldin + min(ci0 + ciq, a.Cin - 4));
     }
 #pragma unroll
     for (int r = 0; r < BV; ++r) {
       const int idx = tid + 256 * r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (idx < SP_BK * TN / 4) {
-        const int kk = idx / (TN / 4), nq = (idx % (TN / 4)) * 4;
-        const int ci = ci0 + kk, c = c0 + nq;
-        if (ci < a.Cin && c < a.Cout)
-          v = *reinterpret_cast<const float4*>(a.W + ((int64_t)k * a.Cin + ci) * a.Cout + c);
-      }
-      rb[r] = v;
+      const int kk = min(idx / (TN / 4), SP_BK - 1), nq = (idx % (TN / 4)) * 4;
+      const int ci = ci0 + kk, c = c0 + nq;
+      mm |= (idx < SP_BK * TN / 4 && ci < a.Cin && c < a.Cout) ? (1u << (AV + r)) : 0u;
+      rb[r] = *reinterpret_cast<const float4*>(a.W + ((int64_t)k * a.Cin + min(ci, a.Cin - 1)) * a.Cout + min(c, a.Cout - 4));
     }
+    msk = mm;
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const float4 (&ra)[AV], const float4 (&rb)[BV], uint32_t msk) {
 #pragma unroll
     for (int r = 0; r < AV; ++r) {
       const int idx = tid + 256 * r;
       const int row = idx >> 2, ciq = (idx & 3) * 4;
-      As[buf][ciq + 0][row] = ra[r].x;
-      As[buf][ciq + 1][row] = ra[r].y;
-      As[buf][ciq + 2][row] = ra[r].z;
-      As[buf][ciq + 3][row] = ra[r].w;
+      const bool ok = (msk >> r) & 1;   // value selects (a select of references would go through scratch)
+      const float4 v = make_float4(ok ? ra[r].x : 0.f, ok ? ra[r].y : 0.f, ok ? ra[r].z : 0.f, ok ? ra[r].w : 0.f);
+      As[buf][ciq + 0][row] = v.x;
+      As[buf][ciq + 1][row] = v.y;
+      As[buf][ciq + 2][row] = v.z;
+      As[buf][ciq + 3][row] = v.w;
     }
 #pragma unroll
     for (int r = 0; r < BV; ++r) {
       const int idx = tid + 256 * r;
       if (idx < SP_BK * TN / 4) {
         const int kk = idx / (TN / 4), nq = (idx % (TN / 4)) * 4;
-        *reinterpret_cast<float4*>(&Bs[buf][kk][nq]) = rb[r];
+        const bool ok = (msk >> (AV + r)) & 1;
+        *reinterpret_cast<float4*>(&Bs[buf][kk][nq]) =
+            make_float4(ok ? rb[r].x : 0.f, ok ? rb[r].y : 0.f, ok ? rb[r].z : 0.f, ok ? rb[r].w : 0.f);
       }
     }
   };
@@ -136,13 +144,15 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
   if (steps > 0) {
-    load(0);
-    store(0);
+    load(0, a_0, b_0, m_0);
+    load(1, a_1, b_1, m_1);
+    load(2, a_2, b_2, m_2);
+    store(0, a_0, b_0, m_0);
   }
   __syncthreads();
-  int cur = 0;
-  for (int s = 0; s < steps; ++s) {
-    if (s + 1 < steps) load(s + 1);
+  // step s: MFMAs on buffer s & 1, store step s + 1 (set (s+1) % 3) into the other buffer, refill
+  // set s % 3 (stored one step ago) with step s + 3
+  auto mfmas = [&](int cur) {
 #pragma unroll
     for (int kk = 0; kk < SP_BK; kk += 2) {
       const float av = As[cur][kk + kh][wm * 32 + l32];
@@ -152,10 +162,21 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
         acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j], 0, 0, 0);
       }
     }
-    if (s + 1 < steps) store(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
+  };
+#define SP_STEP(S_, AS, BS, MS, AN, BN, MN) \
+  mfmas((S_) & 1);                          \
+  store(((S_) & 1) ^ 1, AN, BN, MN);        \
+  load((S_) + 3, AS, BS, MS);               \
+  __syncthreads();
+  int s = 0;
+  for (; s + 2 < steps; s += 3) {
+    SP_STEP(s, a_0, b_0, m_0, a_1, b_1, m_1)
+    SP_STEP(s + 1, a_1, b_1, m_1, a_2, b_2, m_2)
+    SP_STEP(s + 2, a_2, b_2, m_2, a_0, b_0, m_0)
   }
+  if (s < steps) { SP_STEP(s, a_0, b_0, m_0, a_1, b_1, m_1) }
+  if (s + 1 < steps) { SP_STEP(s + 1, a_1, b_1, m_1, a_2, b_2, m_2) }
+#undef SP_STEP
 
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
