@@ -20,6 +20,7 @@
 #include <algorithm>
 
 #include "common.hpp"
+#include "mfma_bf16.hpp"
 #include "prof.hpp"
 #include "sparse.hpp"
 
@@ -227,10 +228,12 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
 // <= 8 hash probes per output instead of 343, and neighbouring outputs read the same bricks
 // (L1/L2 locality the per-voxel hash scatters away).
 //   workspace: [16 B header: int32 brick counter] [keys u64 x cap] [rep/ids i32 x cap] [rows i32 x 64 x M]
+//              [slot_of i32 x M] [brick coordinates int4 x M]
 struct BrickView {
   HashView h;      // vals: representative row during the build, then the brick id
   int32_t* count;  // number of bricks
   int32_t* rows;   // [bricks][64]
+  int4* bcoord;    // [bricks]: (batch, x >> 2, y >> 2, z >> 2)
 };
 
 __device__ __forceinline__ int brick_cell(int x, int y, int z) { return (x & 3) | ((y & 3) << 2) | ((z & 3) << 4); }
@@ -245,7 +248,7 @@ __global__ void brick_insert_kernel(const int4* __restrict__ c, int64_t M, HashV
 
 // representatives (the minimum row of each brick) draw brick ids; wave-aggregated counter
 __global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView h, int32_t* count,
-                                 int32_t* slot_of) {
+                                 int32_t* slot_of, int4* bcoord) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t sl = -1;
   bool rep = false;
@@ -261,6 +264,7 @@ __global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView
   if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
   base = __shfl(base, 0, 64);
   if (rep) h.vals[sl] = base + __popcll(m & ((1ULL << lane) - 1));
+  if (rep) bcoord[h.vals[sl]] = make_int4(c[i].x, c[i].y >> 2, c[i].z >> 2, c[i].w >> 2);
 }
 
 __global__ void brick_fill_kernel(const int4* __restrict__ c, int64_t M, HashView h, const int32_t* __restrict__ slot_of,
@@ -281,9 +285,12 @@ __global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__
                                                         const float* __restrict__ feat, int ks, int step,
                                                         const float* __restrict__ W, mvr_bn_p bn, float bn_eps,
                                                         int relu, float* __restrict__ out, int64_t ldout) {
-  extern __shared__ float sW[];  // [K][CO]
+  // [K][CO + 1]: lanes read different stencil rows k at the same channel — the odd row stride puts
+  // them in different banks (a CO-float stride maps every lane of the wave to bank c)
+  extern __shared__ float sW[];
+  constexpr int WLD = CO + 1;
   const int K = ks * ks * ks;
-  for (int e = threadIdx.x; e < K * CO; e += blockDim.x) sW[e] = W[e];
+  for (int e = threadIdx.x; e < K * CO; e += blockDim.x) sW[(e / CO) * WLD + e % CO] = W[e];
   __syncthreads();
   const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= Mo) return;
@@ -309,7 +316,7 @@ __global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__
               const int row = br[brick_cell(cx, cy, cz)];
               if (row < 0) continue;
               const float f = feat[row];
-              const float* w = sW + ((cx - x + r) + ks * (cy - y + r) + ks * ks * (cz - z + r)) * CO;
+              const float* w = sW + ((cx - x + r) + ks * (cy - y + r) + ks * ks * (cz - z + r)) * WLD;
 #pragma unroll
               for (int c = 0; c < CO; ++c) acc[c] = fmaf(f, w[c], acc[c]);
             }
@@ -323,6 +330,131 @@ __global__ __launch_bounds__(256) void spconv_c1_kernel(const int4* __restrict__
     }
     if (relu) v = fmaxf(v, 0.f);
     out[o * ldout + c] = v;
+  }
+}
+
+// ------------------------------------------------------------------ conv1 over its own set, brick-tiled
+// FCGF conv1 (fcgf.py:118-125: 7^3 stencil, 1 -> 32 channels, stride 1) maps the voxel set onto
+// itself, so the output rows are the brick map's own rows.  One wave per 4x4x4 brick of output cells:
+//   * the 10^3 window of input cells its 64 stencils read (cells 4b-3 .. 4b+6 per axis) is gathered
+//     once into the wave's LDS grid (27 brick probes, then one row + one feature load per cell);
+//   * out[64 cells][32] = im2col[64][343] . W[343][32] runs dense on v_mfma_f32_32x32x16_bf16 with
+//     both operands split into three bf16 terms (mfma_bf16.hpp: fp32-level accuracy); the im2col
+//     operand is read straight from the grid through a window-offset table, W is split once per
+//     workgroup into B fragments in LDS; empty cells multiply zeros, empty output cells are skipped.
+// Per brick: 22 k-steps x 2 row blocks x 6 MFMAs, instead of 343 dependent gathers per output row.
+constexpr int C1_KSZ = 7, C1_K = 343, C1_NS = 22;   // 22 k-steps of 16 (343 padded with zero weights)
+constexpr int C1_G = 10;                            // window edge (cells)
+constexpr int C1_WAVES = 8;
+constexpr int C1_GRID = 1024;                       // grid floats per wave (1000 used)
+
+struct C1Smem {
+  bx::bf16x8 wf[C1_NS][3][64];    // W as B fragments [k-step][term h, m, l][lane]   (66 KB)
+  short off[C1_NS * 16];           // window offset of k: dx + 10 dy + 100 dz
+  float grid[C1_WAVES][C1_GRID];   // per wave: the input window of its brick        (32 KB)
+  float sc[32], sh[32];            // eval BatchNorm folded per channel
+};
+
+__global__ __launch_bounds__(512) void spconv_c1_brick_kernel(BrickView bv, const float* __restrict__ feat,
+                                                              const float* __restrict__ W, mvr_bn_p bn,
+                                                              float bn_eps, int relu, float* __restrict__ out,
+                                                              int64_t ldout) {
+  using namespace bx;
+  __shared__ __attribute__((aligned(16))) C1Smem sm;
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
+  const int w = tid >> 6;
+  // B fragment of k-step s for lane ln: W[16 s + 8 (ln >> 5) + i][ln & 31], i = 0..7
+  for (int e = tid; e < C1_NS * 64; e += blockDim.x) {
+    const int s = e >> 6, ln = e & 63, k0 = 16 * s + 8 * (ln >> 5), c = ln & 31;
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = k0 + i < C1_K ? W[(k0 + i) * 32 + c] : 0.f;
+    Frag f;
+    split8(v, f.h, f.m, f.l);
+    sm.wf[s][0][ln] = f.h;
+    sm.wf[s][1][ln] = f.m;
+    sm.wf[s][2][ln] = f.l;
+  }
+  for (int k = tid; k < C1_NS * 16; k += blockDim.x)
+    sm.off[k] = (short)(k < C1_K ? k % C1_KSZ + C1_G * ((k / C1_KSZ) % C1_KSZ) + C1_G * C1_G * (k / (C1_KSZ * C1_KSZ))
+                                 : 0);
+  if (tid < 32) {
+    float sc = 1.f, sh = 0.f;
+    if (bn.gamma) {
+      sc = bn.gamma[tid] / sqrtf(bn.var[tid] + bn_eps);
+      sh = bn.beta[tid] - bn.mean[tid] * sc;
+    }
+    sm.sc[tid] = sc;
+    sm.sh[tid] = sh;
+  }
+  __syncthreads();
+  const float csc = sm.sc[l32], csh = sm.sh[l32];
+  // this lane's output cells 32 rb + l32 = (l32 & 3, (l32 >> 2) & 3, (l32 >> 4) + 2 rb) -> grid base
+  const int base0 = (l32 & 3) + C1_G * ((l32 >> 2) & 3) + C1_G * C1_G * (l32 >> 4);
+  const int base1 = base0 + 2 * C1_G * C1_G;
+  float* g = sm.grid[w];
+  const int nb = *bv.count;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  for (int b = blockIdx.x * C1_WAVES + w; b < nb; b += gridDim.x * C1_WAVES) {
+    const int4 bc = bv.bcoord[b];
+    int nid = -1;   // lane n < 27: id of the neighbour brick (n % 3, n / 3 % 3, n / 9) - 1
+    if (lane < 27) {
+      const int64_t sl =
+          hash_slot(bv.h, pack_key(bc.x, bc.y + lane % 3 - 1, bc.z + (lane / 3) % 3 - 1, bc.w + lane / 9 - 1));
+      nid = sl >= 0 ? bv.h.vals[sl] : -1;
+    }
+    // grid cell gi = lane + 64 i = (gx, gy, gz) sits at (gx + 1, gy + 1, gz + 1) from cell 4 (b - 1)
+    int rw[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int gi = lane + 64 * i;
+      const int ux = gi % C1_G + 1, uy = (gi / C1_G) % C1_G + 1, uz = gi / (C1_G * C1_G) + 1;
+      const int id = __shfl(nid, (ux >> 2) + 3 * (uy >> 2) + 9 * min(uz >> 2, 2), 64);
+      rw[i] = (gi < C1_G * C1_G * C1_G && id >= 0) ? bv.rows[(int64_t)id * 64 + brick_cell(ux, uy, uz)] : -1;
+    }
+    float fv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) fv[i] = rw[i] >= 0 ? feat[rw[i]] : 0.f;
+    const int myrow = bv.rows[(int64_t)b * 64 + lane];   // output row of cell `lane` (-1: empty)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous brick's grid reads are done
+#pragma unroll
+    for (int i = 0; i < 16; ++i) g[lane + 64 * i] = fv[i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+#pragma unroll 2
+    for (int s = 0; s < C1_NS; ++s) {
+      const s16x8 o = *reinterpret_cast<const s16x8*>(&sm.off[16 * s + 8 * hh]);
+      Frag wf;
+      wf.h = sm.wf[s][0][lane];
+      wf.m = sm.wf[s][1][lane];
+      wf.l = sm.wf[s][2][lane];
+      float v0[8], v1[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v0[i] = g[base0 + o[i]];
+        v1[i] = g[base1 + o[i]];
+      }
+      Frag a0, a1;
+      split8(v0, a0.h, a0.m, a0.l);
+      split8(v1, a1.h, a1.m, a1.l);
+      acc0 = mfma6(a0, wf, acc0);
+      acc1 = mfma6(a1, wf, acc1);
+    }
+    // C[row (q & 3) + 8 (q >> 2) + 4 hh][column l32] of row block rb = cell 32 rb + row
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = (q & 3) + 8 * (q >> 2) + 4 * hh;
+      const int r0 = __shfl(myrow, r, 64), r1 = __shfl(myrow, 32 + r, 64);
+      float v0 = fmaf(acc0[q], csc, csh), v1 = fmaf(acc1[q], csc, csh);
+      if (relu) {
+        v0 = fmaxf(v0, 0.f);
+        v1 = fmaxf(v1, 0.f);
+      }
+      if (r0 >= 0) out[(int64_t)r0 * ldout + l32] = v0;
+      if (r1 >= 0) out[(int64_t)r1 * ldout + l32] = v1;
+    }
   }
 }
 
@@ -491,19 +623,24 @@ extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const voi
   return MVR_OK;
 }
 
+static size_t brick_slot_of_bytes(int64_t M) { return ((size_t)(M > 0 ? M : 1) * 4 + 15) & ~(size_t)15; }
 static size_t brick_map_bytes(int64_t M) {
   const uint64_t cap = next_pow2((uint64_t)(2 * (M > 0 ? M : 1)));
-  return 16 + cap * 12 + (size_t)(M > 0 ? M : 1) * 64 * 4 + (size_t)(M > 0 ? M : 1) * 4;
+  const size_t m = (size_t)(M > 0 ? M : 1);
+  return 16 + cap * 12 + m * 64 * 4 + brick_slot_of_bytes(M) + m * 16;
 }
 static BrickView brick_view(void* ws, int64_t M) {
   BrickView v{};
   const uint64_t cap = next_pow2((uint64_t)(2 * (M > 0 ? M : 1)));
+  const size_t m = (size_t)(M > 0 ? M : 1);
   char* base = reinterpret_cast<char*>(ws);
   v.count = reinterpret_cast<int32_t*>(base);
   v.h.cap = cap;
   v.h.keys = reinterpret_cast<uint64_t*>(base + 16);
   v.h.vals = reinterpret_cast<int32_t*>(base + 16 + cap * 8);
   v.rows = reinterpret_cast<int32_t*>(base + 16 + cap * 12);
+  // after the rows and slot_of: 16-byte aligned (cap >= 1024)
+  v.bcoord = reinterpret_cast<int4*>(base + 16 + cap * 12 + m * 64 * 4 + brick_slot_of_bytes(M));
   return v;
 }
 
@@ -520,7 +657,7 @@ extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, s
     (void)hipMemsetAsync(v.rows, 0xff, (size_t)M * 64 * 4, s);
     const int4* c = reinterpret_cast<const int4*>(coords);
     hipLaunchKernelGGL(brick_insert_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h);
-    hipLaunchKernelGGL(brick_ids_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, v.count, slot_of);
+    hipLaunchKernelGGL(brick_ids_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, v.count, slot_of, v.bcoord);
     hipLaunchKernelGGL(brick_fill_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, slot_of, v.rows);
   }
   MVR_CHECK_LAUNCH();
@@ -530,14 +667,24 @@ extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, s
 extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
                              size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
                              mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, hipStream_t s) {
-  if (!out_coords || Mout < 0 || !in_bricks || !feat || !W || !out || (ksize & 1) == 0 || step <= 0 || Min < 0)
-    return MVR_EINVAL;
+  if (Mout < 0 || !in_bricks || !feat || !W || !out || (ksize & 1) == 0 || step <= 0 || Min < 0) return MVR_EINVAL;
   if (Cout != 32) return MVR_EINVAL;  // FCGF conv1: 1 -> CHANNELS[1] = 32 (fcgf.py:118-125)
   if (in_bricks_bytes < brick_map_bytes(Min)) return MVR_EINVAL;
+  if (!out_coords) {   // the output set is the brick map's own set: output row o = input row o
+    if (Mout != Min || step != 1 || ksize != C1_KSZ || ldout < 32) return MVR_EINVAL;
+    if (Mout == 0) return MVR_OK;
+    BrickView v = brick_view(const_cast<void*>(in_bricks), Min);
+    ProfScope prof(PK_SPCONV, 2.0 * Mout * C1_K * Cout, (double)Mout * (16 + Cout * 4), s);
+    const int grid = (int)std::min<int64_t>(256, (Mout + 63) / 64);
+    hipLaunchKernelGGL(spconv_c1_brick_kernel, dim3(grid), dim3(512), 0, s, v, feat, W, bn, bn_eps, relu, out,
+                       ldout);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
   if (Mout == 0) return MVR_OK;
   BrickView v = brick_view(const_cast<void*>(in_bricks), Min);
   const int K = ksize * ksize * ksize;
-  const size_t lds = (size_t)K * Cout * sizeof(float);
+  const size_t lds = (size_t)K * (Cout + 1) * sizeof(float);
   if (lds > 160 * 1024) return MVR_EINVAL;
   ProfScope prof(PK_SPCONV, 2.0 * Mout * K * Cout, (double)Mout * (16 + Cout * 4), s);
   hipLaunchKernelGGL(spconv_c1_kernel<32>, dim3(nblk(Mout)), dim3(256), lds, s,

@@ -23,6 +23,9 @@ from lib.sparse import SparseTensor
 # MFMA kernel here (the convs are gather-latency bound and the bf16 staging lowers occupancy), so off
 # unless MVR_SPCONV_BF16=1
 SPLIT_BF16 = os.environ.get("MVR_SPCONV_BF16", "0") == "1"
+# conv1 (7^3) as brick-tiled dense windows on split-bf16 MFMA (csrc/sparse.hip spconv_c1_brick_kernel);
+# MVR_CONV1_BRICKS=0 selects the per-row gather kernel (A/B timing)
+CONV1_BRICKS = os.environ.get("MVR_CONV1_BRICKS", "1") == "1"
 
 
 class _MEConv(nn.Module):
@@ -157,7 +160,9 @@ class FCGFNet(nn.Module):
         s1 = torch.empty(M[0], C[1], device=dev)
         bnp, eps = _bn(self.norm1)
         bricks = cm.brick_map(1)
-        N.check(L.mvr_spconv_c1(N.ptr(cm.coords_at(1)), M[0], N.ptr(bricks), M[0], bricks.numel(), N.ptr(feat),
+        # the output set is the input set: out_coords NULL selects the brick-tiled MFMA kernel (7^3 only)
+        oc = None if (self.conv1_kernel_size == 7 and CONV1_BRICKS) else N.ptr(cm.coords_at(1))
+        N.check(L.mvr_spconv_c1(oc, M[0], N.ptr(bricks), M[0], bricks.numel(), N.ptr(feat),
                                 self.conv1_kernel_size, 1, N.ptr(self.conv1.kernel), C[1], bnp, eps, 0, N.ptr(s1),
                                 C[1], N.stream()), "mvr_spconv_c1")
         # concatenation buffers: [tr-branch | skip]
