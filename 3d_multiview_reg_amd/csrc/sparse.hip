@@ -52,14 +52,19 @@ __device__ __forceinline__ int64_t hash_find(const HashView& h, uint64_t key) {
   return -1;
 }
 
-// insert `key` with value candidate v; keeps the minimum v per key
+// insert `key` with value candidate v; keeps the minimum v per key.  Plain reads first: a slot's key
+// never changes once set and its value only decreases, so a (possibly stale) read that already shows
+// the key with a value <= v proves the atomic unnecessary — duplicate keys (raw points of one voxel)
+// then skip the contended CAS / atomicMin on their slot.
 __device__ __forceinline__ void hash_insert_min(HashView h, uint64_t key, int32_t v) {
   uint64_t s = mix64(key) & (h.cap - 1);
   for (uint64_t probe = 0; probe < h.cap; ++probe) {
-    unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(&h.keys[s]),
-                                        (unsigned long long)EMPTY_KEY, (unsigned long long)key);
-    if (prev == EMPTY_KEY || prev == key) {
-      atomicMin(&h.vals[s], v);
+    unsigned long long cur = h.keys[s];
+    if (cur == EMPTY_KEY)
+      cur = atomicCAS(reinterpret_cast<unsigned long long*>(&h.keys[s]), (unsigned long long)EMPTY_KEY,
+                      (unsigned long long)key);
+    if (cur == EMPTY_KEY || cur == key) {
+      if (h.vals[s] > v) atomicMin(&h.vals[s], v);
       return;
     }
     s = (s + 1) & (h.cap - 1);

@@ -290,7 +290,9 @@ size_t mvr_brick_map_bytes(int64_t M);
 int mvr_brick_map_build(const int32_t* coords, int64_t M, void* workspace, size_t workspace_bytes,
                         mvr_stream_t stream);
 /* single-input-channel conv with a large stencil (FCGF conv1, 7^3) over the input set's brick map
- * (in_bricks built from the Min input coordinates; input cell = coordinate / step) */
+ * (in_bricks built from the Min input coordinates; input cell = coordinate / step).
+ * out_coords NULL: the output set is the input set itself (Mout == Min, step 1, ksize 7; output row o =
+ * input row o) — computed brick by brick as dense 7^3 windows on split-bf16 MFMA. */
 int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min, size_t in_bricks_bytes,
                   const float* feat, int ksize, int step, const float* W, int Cout, mvr_bn_p bn, float bn_eps,
                   int relu, float* out, int64_t ldout, mvr_stream_t stream);
