@@ -183,7 +183,11 @@ struct PoolArgs {
   int P, N, Kc, nqb;                               // nqb = ceil(Kc / 256) query blocks
   float* out; int64_t ops, old;                    // x_down [P][128][old]
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(Kc/128)][st_ld] (+ st_off + c), nullable
+  int nks;                                         // key splits per (pair, query block); 1: none
+  float* part; int* cnt;                           // nks > 1: per-split (O, m, l) slabs, arrival tickets
 };
+
+constexpr int PSLAB = 66 * ATHREADS;               // floats of one split's slab: O (64 / thread), m, l
 
 __device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
   const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
@@ -201,12 +205,22 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   __shared__ __attribute__((aligned(16))) char xraw[2 * XT];   // LDS-DMA ring of raw key tiles
   __shared__ float2 ssh[AC];                                  // (sc, sh) of this pair
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  int p, jb;
-  pair_block(a.nqb, p, jb);
+  int p, jb, ks = 0;
+  if (a.nks > 1) {   // the splits of one (pair, query block) are blocks b, b + 8, ..: one XCD, adjacent
+    const int b = blockIdx.x, x = b & 7;
+    int t = b >> 3;
+    ks = t % a.nks;
+    t /= a.nks;
+    jb = t % a.nqb;
+    p = (t / a.nqb) * 8 + x;
+  } else {
+    pair_block(a.nqb, p, jb);
+  }
   if (p >= a.P) return;   // uniform over the workgroup
   const float* X = a.X + (int64_t)p * a.xps;
   const int N = a.N;
   const int nkb = (N + AKB - 1) / AKB;
+  const int kb0 = nkb * ks / a.nks, kb1 = nkb * (ks + 1) / a.nks;   // this split's key blocks
   const int nlast = ((N + 3) & ~3) - 4;   // last readable 4-key group of a row
 
   // raw tile kb -> xraw[kb & 1] as [c][32] fp32 rows: wave w moves rows 16 w .. 16 w + 15 in two
@@ -221,7 +235,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       glds16b(reinterpret_cast<const char*>(X + (int64_t)(r0 + (lane >> 3)) * a.xld + n), dst + r0 * 128);
     }
   };
-  dma_tile(0);
+  dma_tile(kb0);
   if (tid < AC) ssh[tid] = make_float2(a.sc[(int64_t)p * a.sps + tid], a.sh[(int64_t)p * a.sps + tid]);
 
   // queries: this lane's W row (column j of S^T) as split B fragments, one per 16-channel k-step
@@ -297,11 +311,11 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   // ring: raw tile kb + 2 lands while stage kb & 1 is consumed and tile kb + 1 is split into the other
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  dma_tile(1);
-  store_tile(0, 0);
+  dma_tile(kb0 + 1);
+  store_tile(kb0, kb0 & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  for (int kb = kb0; kb < kb1; ++kb) {
     const int st = kb & 1;
     store_tile(kb + 1, st ^ 1);   // zeros past the end
     dma_tile(kb + 2);             // into the buffer of tile kb, split one iteration ago
@@ -347,6 +361,46 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  if (a.nks > 1) {
+    // publish this split's (O, m, l); the last split to arrive merges all of them (counter hand-off:
+    // plain stores, agent-scope release before the ticket, agent-scope acquire by the reducer)
+    const int64_t slot = (int64_t)p * a.nqb + jb;
+    float* mine = a.part + (slot * a.nks + ks) * PSLAB + tid;
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mine[(16 * cb + r) * ATHREADS] = O[cb][r];
+    mine[64 * ATHREADS] = m;
+    mine[65 * ATHREADS] = l;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(xraw);   // the raw-tile ring is drained
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int tk = __hip_atomic_fetch_add(a.cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = tk == a.nks - 1;
+      if (tk == a.nks - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!flag[0]) return;   // uniform
+    for (int o = 0; o < a.nks; ++o) {
+      if (o == ks) continue;
+      const float* th = a.part + (slot * a.nks + o) * PSLAB + tid;
+      const float m2 = th[64 * ATHREADS], l2 = th[65 * ATHREADS];
+      const float mn = fmaxf(m, m2);
+      const float f1 = __builtin_amdgcn_exp2f(m - mn), f2 = __builtin_amdgcn_exp2f(m2 - mn);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) O[cb][r] = O[cb][r] * f1 + th[(16 * cb + r) * ATHREADS] * f2;
+      l = l * f1 + l2 * f2;
+      m = mn;
+    }
   }
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
@@ -565,10 +619,59 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
   return nkb * (WIMG + (size_t)P * IMG) + 256;
 }
 
+// Key splits of the pool launch: with one 512-thread workgroup per CU, P x ceil(Kc / 256) workgroups
+// leave a partial last round (435 pairs: 880 workgroups = 3.44 rounds of 256); splitting the keys
+// (points) of every (pair, query block) shortens the rounds.  Picks nks in {1, 2, 4} minimising
+// rounds / nks (ties: fewer splits), with >= 8 key blocks per split.
+static int pool_splits(int P, int nqb, int N) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int64_t wg = (int64_t)((P + 7) / 8) * 8 * nqb;
+  const int nkb = (N + AKB - 1) / AKB;
+  int best = 1;
+  double tbest = (double)((wg + cus - 1) / cus);
+  for (int k = 2; k <= 4; k *= 2) {
+    if (nkb < 8 * k) break;
+    const double t = (double)((wg * k + cus - 1) / cus) / k;
+    if (t < tbest - 1e-9) { tbest = t; best = k; }
+  }
+  return best;
+}
+
+static size_t pool_ws_bytes(int P, int clusters, int nks) {
+  const size_t slots = (size_t)P * ((clusters + AQ - 1) / AQ);
+  return nks > 1 ? slots * ((size_t)nks * PSLAB * 4 + 4) + 512 : 0;
+}
+
+extern "C" size_t mvr_oan_diff_pool_workspace_bytes(int P, int channels, int clusters) {
+  if (P <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return 0;
+  return pool_ws_bytes(P, clusters, 4);
+}
+
+extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x_ld, const float* sc,
+                                    const float* sh, int64_t s_pstride, const float* weight, const float* bias, int P,
+                                    int channels, int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld,
+                                    float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
+                                    hipStream_t stream);
+
 extern "C" int mvr_oan_diff_pool(const float* x, int64_t x_pstride, int64_t x_ld, const float* sc, const float* sh,
                                  int64_t s_pstride, const float* weight, const float* bias, int P, int channels, int N,
                                  int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats,
                                  int64_t st_ld, int st_off, hipStream_t stream) {
+  return mvr_oan_diff_pool_ws(x, x_pstride, x_ld, sc, sh, s_pstride, weight, bias, P, channels, N, clusters, out,
+                              out_pstride, out_ld, stats, st_ld, st_off, nullptr, 0, stream);
+}
+
+extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x_ld, const float* sc,
+                                    const float* sh, int64_t s_pstride, const float* weight, const float* bias, int P,
+                                    int channels, int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld,
+                                    float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
+                                    hipStream_t stream) {
   if (!x || !sc || !sh || !weight || !out || P < 0 || N <= 0 || channels != AC || clusters <= 0 ||
       clusters > MAX_CLUSTERS)
     return MVR_EINVAL;
@@ -583,10 +686,21 @@ extern "C" int mvr_oan_diff_pool(const float* x, int64_t x_pstride, int64_t x_ld
   a.P = P; a.N = N; a.Kc = clusters; a.nqb = (clusters + AQ - 1) / AQ;
   a.out = out; a.ops = out_pstride; a.old = out_ld;
   a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
+  a.nks = 1;
+  if (workspace && al16(workspace)) {
+    const int k = pool_splits(P, a.nqb, N);
+    if (k > 1 && workspace_bytes >= pool_ws_bytes(P, clusters, k)) {
+      const size_t slots = (size_t)P * a.nqb;
+      a.nks = k;
+      a.part = reinterpret_cast<float*>(workspace);
+      a.cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + slots * (size_t)k * PSLAB * 4);
+      if (hipMemsetAsync(a.cnt, 0, slots * sizeof(int), stream) != hipSuccess) return MVR_ELAUNCH;
+    }
+  }
   const double fl = 4.0 * AC * clusters * (double)N * P;
   const double by = 4.0 * AC * ((double)N + clusters) * P;
   ProfScope prof(PK_POOL, fl, by, stream);
-  const int grid = ((P + 7) / 8) * 8 * a.nqb;
+  const int grid = ((P + 7) / 8) * 8 * a.nqb * a.nks;
   hipLaunchKernelGGL(oan_pool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;

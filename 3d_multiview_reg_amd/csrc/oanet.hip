@@ -9,6 +9,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 #include "gemm.hpp"
 #include "prof.hpp"
@@ -177,6 +179,7 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // Host orchestration
 // ----------------------------------------------------------------------------
 int g_oan_fused = 1;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 1 PointCN (off: not faster yet)
+int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B timing)
 
 namespace {
 
@@ -260,7 +263,10 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   size_t smx = (size_t)P * TN * Kc;
   if ((size_t)P * MK * N > smx) smx = (size_t)P * MK * N;
   pl.smx = pl.fused ? nullptr : w.take<float2>(smx);
-  pl.uimg_bytes = pl.fused ? mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) : 0;
+  // one region for both fused kernels (stream-ordered: the pool's split partials are dead before
+  // the unpool's operand images are written)
+  pl.uimg_bytes = pl.fused ? std::max(mvr_oan_diff_unpool_workspace_bytes(P, C, Kc),
+                                      mvr_oan_diff_pool_workspace_bytes(P, C, Kc)) : 0;
   pl.uimg = pl.fused ? w.take<char>(pl.uimg_bytes) : nullptr;
   pl.mv = w.take<float2>((size_t)P * 2 * C);
   pl.stcol = w.take<float2>((size_t)P * MC * Kc);
@@ -398,6 +404,12 @@ struct Ctx {
 
 using namespace mvr;
 
+extern "C" int mvr_set_pool_split(int on) {
+  const int prev = g_pool_split;
+  g_pool_split = on ? 1 : 0;
+  return prev;
+}
+
 extern "C" int mvr_set_oan_fused(int on) {
   const int prev = g_oan_fused;
   g_oan_fused = on & 3;
@@ -447,8 +459,9 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   cx.finalize_in(x11top, 1e-3f, blk->down_bn);
   Act xd{pl.XD, (int64_t)C * Kp, Kp, C, Kc, pl.stD, C, 0};
   if (pl.fused) {
-    cx.chk(mvr_oan_diff_pool(pl.X11, 2 * CN, Np, pl.sc, pl.sh, C, blk->down_conv.weight, blk->down_conv.bias, P, C,
-                             N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD), C, 0, s));
+    cx.chk(mvr_oan_diff_pool_ws(pl.X11, 2 * CN, Np, pl.sc, pl.sh, C, blk->down_conv.weight, blk->down_conv.bias, P,
+                                C, N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD), C, 0,
+                                g_pool_split ? pl.uimg : nullptr, pl.uimg_bytes, s));
   } else {
     Act e{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, Kc, 0};
     cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);

@@ -59,10 +59,14 @@ _SIGS = {
     "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),
+    "mvr_set_pool_split": (c_int, [c_int]),
     "mvr_pointcn_fused": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_vp, c_int, c_int, c_int, c_vp, c_i64, c_int, c_vp]),
     "mvr_oan_diff_pool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp]),
+    "mvr_oan_diff_pool_ws": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                  c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp, c_size, c_vp]),
+    "mvr_oan_diff_pool_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "mvr_oan_diff_unpool_workspace_bytes": (c_size, [c_int, c_int, c_int]),
     "mvr_oan_diff_unpool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_int,
                                     c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp, c_size, c_vp]),

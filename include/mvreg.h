@@ -115,6 +115,9 @@ size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels
  *          correct (tested) but not yet faster than the two GEMMs, so off by default.
  * Returns the previous value. */
 int mvr_set_oan_fused(int on);
+/* Key-split diff_pool launches inside mvr_oan_block_forward (mvr_oan_diff_pool_ws): 1 (default) on, 0 off
+ * (A/B timing).  Returns the previous setting. */
+int mvr_set_pool_split(int on);
 
 /* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
  * a multiple of 4, input 16-byte aligned, padding columns [N, ld) finite (zero).
@@ -145,6 +148,15 @@ int mvr_oan_diff_pool(const float* x, int64_t x_pstride, int64_t x_ld, const flo
                       int64_t s_pstride, const float* weight, const float* bias, int P, int channels, int N,
                       int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld,
                       int st_off, mvr_stream_t stream);
+/* The same with a workspace (mvr_oan_diff_pool_workspace_bytes(P, 128, clusters) bytes, 16-byte aligned):
+ * when one workgroup per (pair, 256-cluster block) leaves the last dispatch round partly idle, the
+ * points of each block are split over 2 or 4 workgroups whose partial (output, running max, sum) the
+ * last one to finish merges.  Same results up to fp32 summation order. */
+size_t mvr_oan_diff_pool_workspace_bytes(int P, int channels, int clusters);
+int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x_ld, const float* sc, const float* sh,
+                         int64_t s_pstride, const float* weight, const float* bias, int P, int channels, int N,
+                         int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld,
+                         int st_off, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 
 /* Fused diff_unpool (lib/filtering/oanet.py:113-129), channels == 128, clusters <= 1024:
  *   out(p,c,n) = sum_j x_down(p,c,j) softmax_j(e(p,j,n)),  e = W . relu(x_up * sc + sh) + b

@@ -43,8 +43,11 @@ def _tile_stats(y, L):
     return out
 
 
-@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33)])
-def test_diff_pool_matches_fp64(gpu, P, N, Kc):
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (41, 700, 300)])
+def test_diff_pool_matches_fp64(gpu, P, N, Kc, split):
+    """split: mvr_oan_diff_pool_ws with a workspace (points split over 2-4 workgroups per (pair, cluster
+    block) and merged by the last one; N >= 256 here always splits on a 256-CU part)"""
     import torch
     from lib import _native as NV
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 1000 + N)
@@ -56,8 +59,18 @@ def test_diff_pool_matches_fp64(gpu, P, N, Kc):
     out = torch.full((P, C, Kp), float("nan"), device=gpu)
     st = torch.zeros((P, T, C, 2), device=gpu)
     gx, gsc, gsh, gW, gb = t(x), t(sc), t(sh), t(W), t(b)
-    assert NV.lib().mvr_oan_diff_pool(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
-                                      P, C, N, Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.stream()) == 0
+    L = NV.lib()
+    if split:
+        nb = L.mvr_oan_diff_pool_workspace_bytes(P, C, Kc)
+        assert nb > 0
+        wbuf = torch.full((nb,), 0xAB, dtype=torch.uint8, device=gpu)   # poisoned: tickets must be reset
+        for _ in range(2):   # twice: the arrival tickets are re-armed per launch
+            assert L.mvr_oan_diff_pool_ws(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
+                                          P, C, N, Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.ptr(wbuf), nb,
+                                          NV.stream()) == 0
+    else:
+        assert L.mvr_oan_diff_pool(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
+                                   P, C, N, Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.stream()) == 0
     torch.cuda.synchronize()
     o = out.cpu().numpy()
     scale = np.abs(ref).max()
