@@ -29,29 +29,43 @@ namespace mvr {
 __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld, int st_off, int tw0, int csplit,
                                    int tw1, int C, int L, float eps_in, mvr_bn_p bn, int train, float* sc, float* sh,
                                    int64_t out_ld, float2* mv) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  // blockDim = nb channels x G tile groups: group tg reads tiles tg, tg + G, ... (G times fewer dependent
+  // loads per thread), the groups' partials meet in LDS
+  extern __shared__ double red[];   // [G][nb]
+  const int G = blockDim.y, nb = blockDim.x, lt = threadIdx.x, tg = threadIdx.y;
+  const int c = blockIdx.x * nb + lt;
   const int p = blockIdx.y;
-  if (c >= C) return;
+  const bool ok = c < C;
+  const int cc = ok ? c : 0;
   // column tiles of tw (128 from the GEMM epilogues, 32 from the fused PointCN) carry (sum, squared
   // deviations from the tile mean): Chan's merge
-  const int tw = c < csplit ? tw0 : tw1;
+  const int tw = cc < csplit ? tw0 : tw1;
   const int T = (L + tw - 1) / tw;
-  const float2* sp = st + (int64_t)p * T * st_ld + st_off + c;
+  const float2* sp = st + (int64_t)p * T * st_ld + st_off + cc;
   // two passes over the tiles: the pooled mean, then M2 = sum_t (M2_t + n_t (mean_t - mean)^2)
   // (tiles are full except the last, so one reciprocal serves all but one)
-  // (8 independent loads in flight per thread: the loop is latency-bound otherwise)
   double tot = 0.0;
-#pragma unroll 8
-  for (int t = 0; t < T; ++t) tot += (double)__builtin_nontemporal_load(&sp[(int64_t)t * st_ld].x);
+#pragma unroll 4
+  for (int t = tg; t < T; t += G) tot += (double)__builtin_nontemporal_load(&sp[(int64_t)t * st_ld].x);
+  red[tg * nb + lt] = tot;
+  __syncthreads();
+  tot = 0.0;
+  for (int j = 0; j < G; ++j) tot += red[j * nb + lt];
   const double mean = tot / L, rtw = 1.0 / tw;
   double m2 = 0.0;
-#pragma unroll 8
-  for (int t = 0; t < T; ++t) {
+#pragma unroll 4
+  for (int t = tg; t < T; t += G) {
     const float2 v = sp[(int64_t)t * st_ld];
-    const int nb = min(tw, L - tw * t);
-    const double d = (double)v.x * (nb == tw ? rtw : 1.0 / nb) - mean;
-    m2 += (double)v.y + d * d * nb;
+    const int nv = min(tw, L - tw * t);
+    const double d = (double)v.x * (nv == tw ? rtw : 1.0 / nv) - mean;
+    m2 += (double)v.y + d * d * nv;
   }
+  __syncthreads();   // every group has read the sums
+  red[tg * nb + lt] = m2;
+  __syncthreads();
+  if (tg != 0 || !ok) return;
+  m2 = 0.0;
+  for (int j = 0; j < G; ++j) m2 += red[j * nb + lt];
   const double var = fmax(m2 / L, 0.0);
   const float rin = (float)(1.0 / sqrt(var + (double)eps_in));
   if (train) {
@@ -290,9 +304,10 @@ struct Ctx {
   void finalize_in(const Act& a, float eps, const mvr_bn_p& bn, float* sc = nullptr, float* sh = nullptr) {
     if (!sc) { sc = pl.sc; sh = pl.sh; }
     const int bs = a.C >= 256 ? 256 : (a.C + 63) & ~63;
+    const int G = 1024 / bs < 4 ? 1024 / bs : 4;   // tile groups per channel
     dim3 grid((a.C + bs - 1) / bs, pl.P);
-    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(bs), 0, s, a.st, a.st_ld, a.st_off, a.tw0, a.csplit, a.tw1, a.C,
-                       a.L, eps, bn, train, sc, sh, (int64_t)a.C, pl.mv);
+    hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(bs, G), sizeof(double) * bs * G, s, a.st, a.st_ld, a.st_off,
+                       a.tw0, a.csplit, a.tw1, a.C, a.L, eps, bn, train, sc, sh, (int64_t)a.C, pl.mv);
     chk_launch();
     if (train) {
       hipLaunchKernelGGL(in_bn_train_kernel, dim3((a.C + 255) / 256), dim3(256), 0, s, pl.mv, pl.P, a.C, eps, bn,
