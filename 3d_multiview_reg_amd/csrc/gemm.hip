@@ -933,7 +933,8 @@ static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) 
 int launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return MVR_OK;
   if (!g.A || !g.B || (!g.C && !g.no_store) || g.K <= 0) return MVR_EINVAL;
-  if (g.no_store && (g.stats_mode != ST_ROW || g.has_res)) return MVR_EINVAL;   // stats-only: row statistics
+  // no_store: statistics only (row statistics), or the output head only (point-conv kernel)
+  if (g.no_store && !g.head_w && (g.stats_mode != ST_ROW || g.has_res)) return MVR_EINVAL;
   if (g.pro != PRO_NONE && !g.psc) return MVR_EINVAL;
   if ((g.pro == PRO_A_K || g.pro == PRO_B_K) && !g.psh) return MVR_EINVAL;
   if (g.stats_mode != ST_NONE && !g.stats) return MVR_EINVAL;

@@ -319,6 +319,7 @@ struct Ctx {
   // 1x1 conv: out = W . pro(in) + b (+res); stats into out.st when `stats`
   // output head to fuse into the next conv (pconv epilogue), consumed by it
   const mvr_conv_p* head = nullptr;
+  bool head_only = false;   // the head's conv does not store its output (not returned by the block)
   float* h_logits = nullptr;
   float* h_scores = nullptr;
   int32_t* h_pos = nullptr;
@@ -371,7 +372,7 @@ struct Ctx {
     conv(pc.conv3, x, true, t, nullptr, ST_ROW);
     finalize_in(t, 1e-5f, pc.bn5);
     head = hd;
-    conv(pc.conv7, t, true, y, sc ? &y : &x, hd ? ST_NONE : ST_ROW);
+    conv(pc.conv7, t, true, y, sc ? &y : &x, hd ? ST_NONE : ST_ROW, nullptr, hd && head_only);
     head = nullptr;
   }
 
@@ -529,10 +530,12 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   GemmArgs probe{};
   probe.math = g_default_math; probe.M = C; probe.N = N; probe.K = C; probe.batch = P; probe.pro = PRO_B_K;
   probe.has_res = 1; probe.bias_mode = BIAS_M; probe.head_w = blk->output.weight;
+  probe.no_store = latent ? 0 : 1;   // a block whose activation is not returned keeps only the head's output
   const bool fuse_head = !pl.fused_pcn && pconv_covers(probe);   // (the fused-PointCN experiment keeps the head kernel)
   for (int i = 0; i < H; ++i) {
     if (fuse_head && i == H - 1) {
       cx.head = &blk->output;
+      cx.head_only = latent == nullptr;
       cx.h_logits = logits; cx.h_scores = scores; cx.h_pos = guard_pos;
     }
     cx.pointcn(blk->l1_2[i], i == 0 ? x11 : out, out);

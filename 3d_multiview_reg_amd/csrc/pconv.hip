@@ -1,7 +1,8 @@
-// Point convolution of the OANet filter, 128 -> 128 channels over points (the PointCN convs,
-// lib/filtering/oanet.py:18-43, and OAFilter conv3 on clusters, :86-92):
+// Point convolution of the OANet filter, 128 (or 256) -> 128 channels over points (the PointCN convs,
+// lib/filtering/oanet.py:18-43, the 256-channel first PointCN after diff_unpool, :155, and OAFilter
+// conv3 on clusters, :86-92):
 //
-//   Y[b](m, n) = sum_k W(m, k) * pro(X[b](k, n)) + bias(m) (+ R[b](m, n)),   m, k < 128
+//   Y[b](m, n) = sum_k W(m, k) * pro(X[b](k, n)) + bias(m) (+ R[b](m, n)),   m < 128, k < 128 (256)
 //   pro(x) = relu(x * sc[b][k] + sh[b][k])   (InstanceNorm + BatchNorm + ReLU folded) or identity
 //
 // with the per-(pair, channel, 128-point tile) partial statistics of Y (sum, squared deviations
@@ -42,11 +43,10 @@ namespace {
 
 using namespace bx;
 
-constexpr int PC = 128;              // input = output channels
+constexpr int PC = 128;              // output channels (input channels: 16 KS, KS = 8 or 16 k-steps)
 constexpr int CH = 32;               // points per chunk (one MFMA column block)
 constexpr int GRP = 4;               // chunks per statistics group (128 points, gemm.hpp GEMM_BN)
 constexpr int FRB = 3 * 64 * 16;     // one k-step's fragment set: h, m, l planes x 64 lanes x 16 B
-constexpr int XIB = 8 * FRB;         // one chunk's B-fragment image (8 k-steps): 24 KB
 constexpr int YLD = 32;              // row stride (floats) of the per-wave transpose scratch
 
 struct PcArgs {
@@ -84,12 +84,21 @@ __device__ __forceinline__ float sum8(float v) {
   return v;
 }
 
-template <int PRO, int RES, int STATS, int HEAD>
-__global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
-  __shared__ __attribute__((aligned(16))) char xi[2][XIB];
+// KS = 8: 128 input channels, two workgroups per CU (weights 96 VGPRs per lane).  KS = 16: the
+// 256 -> 128 convs of the first PointCN after diff_unpool (oanet.py:155), one workgroup per CU
+// (weights 192 VGPRs, chunk images 2 x 48 KB).  HEAD = 2: output head only, Y not stored (the
+// block's last conv when its activation is not returned).
+template <int KS, int PRO, int RES, int STATS, int HEAD>
+__global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
+  constexpr int CIN = 16 * KS;   // input channels
+  constexpr int NT = KS / 4;     // 16-row k-steps each wave loads and splits per chunk
+  constexpr int RW = CIN / 4;    // input rows per wave
+  constexpr int NX = 8 * NT;     // activation registers per chunk
+  __shared__ __attribute__((aligned(16))) char xi[2][KS * FRB];      // chunk images (B fragments)
   __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
-  __shared__ __attribute__((aligned(16))) float fold[2][2][PC];    // (sc, sh) by pair parity
+  __shared__ __attribute__((aligned(16))) float fold[2][2][CIN];   // (sc, sh) by pair parity
   __shared__ float sbias[PC];
+  __shared__ __attribute__((aligned(16))) float skl[STATS ? 4 : 1][STATS ? 32 : 4];   // row shifts [wave][erow][q]
   __shared__ float shw[HEAD ? PC : 1];
   __shared__ __attribute__((aligned(16))) float hpart[HEAD ? 2 : 1][4][CH];   // HEAD: per-wave partial logits by step parity
 
@@ -107,11 +116,11 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   const int nloc = (int)(c1 - c0);
 
   // weights -> split A fragments: row 32w + l32, k = 16q + 8h + 0..7
-  Frag wf[8];
+  Frag wf[KS];
   {
     const float* wr = a.W + (int64_t)(32 * w + l32) * a.wld + 8 * h;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < KS; ++q) {
       const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * q);
       const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * q + 4);
       const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
@@ -137,27 +146,36 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   const Cur cstart{p0, (int)(c0 - (int64_t)p0 * nch), 0};
 
   auto stage_fold = [&](int p) {
-    if (PRO && tid < PC) {
+    if (PRO && tid < CIN) {
       fold[p & 1][0][tid] = a.sc[(int64_t)p * a.sPb + tid];
       fold[p & 1][1][tid] = a.sh[(int64_t)p * a.sPb + tid];
     }
   };
-  // chunk c -> 16 registers in B-fragment order: k = 32w + 16t + 8h + i -> r[8t + i]
-  auto issue_x = [&](const Cur& c, float (&r)[16]) {
+  // chunk c -> NX registers in B-fragment order: k = RW w + 16t + 8h + i -> r[8t + i].  Buffer loads on
+  // a per-(pair, wave) descriptor: the row offsets (16t + i) ld are wave-uniform (soffset), the lane's
+  // (8h rows, column) part one voffset per chunk — no per-load 64-bit address arithmetic.
+  const int xld4 = (int)a.xld * 4;
+  auto issue_x = [&](const Cur& c, float (&r)[NX]) {
     const int n = min(c.kc * CH + l32, N - 1);
-    const float* src = a.X + (int64_t)c.p * a.xps + (int64_t)(32 * w + 8 * h) * a.xld + n;
+    const float* base = a.X + (int64_t)c.p * a.xps + (int64_t)(RW * w) * a.xld;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+    const int vo = 8 * h * xld4 + 4 * n;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) r[8 * t + i] = (PCONV_ABL & 8) ? (float)(i + t) : src[(int64_t)(16 * t + i) * a.xld];
+      for (int i = 0; i < 8; ++i)
+        r[8 * t + i] = (PCONV_ABL & 8) ? (float)(i + t)
+                                       : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                       rs, vo, (16 * t + i) * xld4, 0));
   };
   // normalise + split half t of a chunk's registers -> its k-step fragment in image slot
-  auto split_half = [&](const Cur& c, const float (&r)[16], int slot, int t) {
+  auto split_half = [&](const Cur& c, const float (&r)[NX], int slot, int t) {
     float v[8];
     if (PRO) {
-      const float* f = &fold[c.p & 1][0][32 * w + 16 * t + 8 * h];
+      const float* f = &fold[c.p & 1][0][RW * w + 16 * t + 8 * h];
       const float4 sa = *reinterpret_cast<const float4*>(f), sb = *reinterpret_cast<const float4*>(f + 4);
-      const float4 ha = *reinterpret_cast<const float4*>(f + PC), hb = *reinterpret_cast<const float4*>(f + PC + 4);
+      const float4 ha = *reinterpret_cast<const float4*>(f + CIN), hb = *reinterpret_cast<const float4*>(f + CIN + 4);
       const float s1[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
       const float h1[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
@@ -174,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     } else {
       split8(v, f.h, f.m, f.l);
     }
-    char* dst = xi[slot] + (2 * w + t) * FRB + lane * 16;
+    char* dst = xi[slot] + (NT * w + t) * FRB + lane * 16;
     *reinterpret_cast<bf16x8*>(dst) = f.h;
     *reinterpret_cast<bf16x8*>(dst + 1024) = f.m;
     *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
@@ -191,7 +209,11 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     for (int i = 0; i < 4; ++i) glds16(src + (int64_t)(8 * i) * a.yld, yb + 256 * i);
   };
 
-  float rn = 0.f, rs[4] = {0.f, 0.f, 0.f, 0.f}, rm2[4] = {0.f, 0.f, 0.f, 0.f};   // running group statistics
+  // running statistics of the current 128-point group, per lane (its 4 rows x 4 columns of each chunk):
+  // sums of d = y - K and d^2 with the row shift K = the mean of the group's first chunk (8-lane sums);
+  // the lanes of a row meet once per group
+  int rn = 0;
+  float ls[4], lss[4];
   // multiply chunk c (image slot) with hook(ks) after each k-step's MFMA group, then the epilogue
   auto compute = [&](const Cur& c, int slot, auto&& hook) {
     const int n0 = c.kc * CH;
@@ -204,9 +226,9 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     cur.m = *reinterpret_cast<const bf16x8*>(img + 1024);
     cur.l = *reinterpret_cast<const bf16x8*>(img + 2048);
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+    for (int ks = 0; ks < KS; ++ks) {
       Frag nxt;
-      if (ks < 7) {
+      if (ks < KS - 1) {
         nxt.h = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB);
         nxt.m = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 1024);
         nxt.l = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 2048);
@@ -216,7 +238,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
       else acc = mfma6(wf[ks], cur, acc);
       hook(ks);
       PC_FENCE();
-      if (ks < 7) cur = nxt;
+      if (ks < KS - 1) cur = nxt;
     }
     if (PCONV_ABL & 4) {
       asm volatile("" ::"v"(acc));
@@ -224,7 +246,8 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     }
     // value (q, e) of this lane: row erow + 8q of the wave's 32, column n0 + ec0 + e
     float4 ev[4];
-    if (RES) {   // the residual DMA (issued one step ago; 16 younger activation loads since)
+    if (RES) {   // the residual DMA (issued one step ago; NX younger activation loads since)
+      static_assert(!RES || NX == 16, "residual wait count");
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < 4; ++q) ev[q] = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
@@ -244,9 +267,11 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     }
     float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + n0 + ec0;
     const bool full = n0 + CH <= N;   // uniform: every column of the chunk is valid
+    if (HEAD != 2) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (full || n0 + ec0 < N4) *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
+      for (int q = 0; q < 4; ++q)
+        if (full || n0 + ec0 < N4) *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
+    }
     if (HEAD) {   // partial logits of the wave's 32 rows for the chunk's columns, summed over lanes l ^ 8, 16, 32
       float hp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -275,36 +300,48 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
           if (nv < 1) ev[q].x = 0.f;
         }
       }
-      const float rc = 1.f / (float)cnt, fc = (float)cnt;
-      const float inv = rn == 0.f ? 0.f : 1.f / rn, wgt = rn == 0.f ? 0.f : rn * fc / (rn + fc);
+      float4* skp = reinterpret_cast<float4*>(&skl[w][4 * erow]);   // (kept in LDS: registers are full)
+      float sK[4];
+      if (c.kc % GRP == 0) {   // the group's first chunk: row shifts
+        const float rc = __builtin_amdgcn_rcpf((float)cnt);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sK[q] = sum8(ev[q].x + ev[q].y + ev[q].z + ev[q].w) * rc;
+          ls[q] = lss[q] = 0.f;
+        }
+        *skp = make_float4(sK[0], sK[1], sK[2], sK[3]);   // the 8 lanes of a row write the same values
+        rn = 0;
+      } else {
+        const float4 k4 = *skp;
+        sK[0] = k4.x; sK[1] = k4.y; sK[2] = k4.z; sK[3] = k4.w;
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float s = sum8(ev[q].x + ev[q].y + ev[q].z + ev[q].w);
-        const float mu = s * rc;
-        float m2 = 0.f;
-        {
-          const float d0 = ev[q].x - mu, d1 = ev[q].y - mu, d2 = ev[q].z - mu, d3 = ev[q].w - mu;
-          m2 = fmaf(d0, d0, m2);
-          if (full || nv > 1) m2 = fmaf(d1, d1, m2);
-          if (full || nv > 2) m2 = fmaf(d2, d2, m2);
-          if (full || nv > 3) m2 = fmaf(d3, d3, m2);
-          if (!full && nv < 1) m2 = 0.f;
+        float d0 = ev[q].x - sK[q], d1 = ev[q].y - sK[q], d2 = ev[q].z - sK[q], d3 = ev[q].w - sK[q];
+        if (!full) {
+          if (nv < 4) d3 = 0.f;
+          if (nv < 3) d2 = 0.f;
+          if (nv < 2) d1 = 0.f;
+          if (nv < 1) d0 = 0.f;
         }
-        m2 = sum8(m2);
-        const float d = mu - rs[q] * inv;   // Chan's merge (a no-op blend while the group is empty)
-        rm2[q] += m2 + d * d * wgt;
-        rs[q] += s;
+        ls[q] += (d0 + d1) + (d2 + d3);
+        lss[q] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, lss[q]))));
       }
-      rn += fc;
+      rn += cnt;
       if ((c.kc % GRP) == GRP - 1 || c.kc == nch - 1) {
+        // (sum, squared deviations from the group mean) = (n K + S, SS - S^2 / n) over the row's 8 lanes
+        const float fn = (float)rn, rinv = __builtin_amdgcn_rcpf(fn);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float S = sum8(ls[q]), SS = sum8(lss[q]);
+          ls[q] = fmaf(fn, sK[q], S);
+          lss[q] = fmaxf(SS - S * S * rinv, 0.f);
+        }
         if ((lane & 7) == 0) {
           float2* st = a.stats + ((int64_t)c.p * a.ngrp + c.kc / GRP) * a.st_ld + a.st_off + 32 * w + erow;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) st[8 * q] = make_float2(rs[q], rm2[q]);
+          for (int q = 0; q < 4; ++q) st[8 * q] = make_float2(ls[q], lss[q]);
         }
-        rn = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rs[q] = rm2[q] = 0.f;
       }
     }
     if (RES) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before the next DMA
@@ -315,7 +352,7 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   //   slot (j + 1) & 1) and the load of chunk j + 4 into the freed registers interleaved between
   //   the MFMA groups; epilogue of chunk j; residual DMA of chunk j + 1; fold of chunk j + 2's pair
   //   when it starts one; one barrier.
-  float x0[16], x1[16], x2[16];
+  float x0[NX], x1[NX], x2[NX];
   Cur cc = cstart, cs = cstart, ci = cstart, cf = cstart, cr = cstart;   // compute, split, issue, fold, residual
   stage_fold(cf.p);
   adv(cf);
@@ -327,8 +364,8 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
   issue_x(ci, x2);
   adv(ci);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  split_half(cs, x0, 0, 0);
-  split_half(cs, x0, 0, 1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) split_half(cs, x0, 0, t);
   adv(cs);
   issue_x(ci, x0);
   adv(ci);
@@ -358,15 +395,14 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
     if (lane == 0 && np) atomicAdd(a.pos + c.p, np);
   };
   Cur ch = cstart;   // head cursor (one step behind compute)
-  auto step = [&](int j, float (&xs)[16]) {
+  auto step = [&](int j, float (&xs)[NX]) {
     if (HEAD && j > 0) {
       head_finish(ch);
       adv(ch);
     }
     compute(cc, j & 1, [&](int ks) {
-      if (ks == 1) split_half(cs, xs, (j + 1) & 1, 0);
-      if (ks == 3) split_half(cs, xs, (j + 1) & 1, 1);
-      if (ks == 4) issue_x(ci, xs);
+      if ((ks & 1) && ks < 2 * NT) split_half(cs, xs, (j + 1) & 1, ks >> 1);
+      if (ks == 2 * NT) issue_x(ci, xs);
     });
     adv(cc);
     adv(cs);
@@ -392,11 +428,16 @@ __global__ __launch_bounds__(256, 2) void pconv_kernel(PcArgs a) {
 }  // namespace
 
 // Dispatched by launch_gemm for the shapes it covers; the caller has checked the common contract.
+// N > CH: with one chunk per pair the fold of chunk j + 3's pair (staged at the end of step j) could
+// land in the slot another wave still reads while splitting chunk j + 1 (pairs j + 1 and j + 3 then
+// differ by 2, same parity); with >= 2 chunks per pair consecutive staged pairs always alternate.
 bool pconv_covers(const GemmArgs& g) {
   if (g.head_w && g.stats_mode != ST_NONE) return false;
-  return g_pconv && g.math == MATH_BF16X3 && g.M == PC && g.K == PC && !g.bkc && g.sAb == 0 && !g.no_store &&
+  if (g.no_store && !g.head_w) return false;   // statistics-only passes stay on gemm_kernel
+  if (g.K == 2 * PC && (g.has_res || g.head_w)) return false;   // KS = 16 runs the 256 -> 128 convs only
+  return g_pconv && g.math == MATH_BF16X3 && g.M == PC && (g.K == PC || g.K == 2 * PC) && !g.bkc && g.sAb == 0 &&
          (g.pro == PRO_NONE || g.pro == PRO_B_K) && (g.stats_mode == ST_NONE || g.stats_mode == ST_ROW) &&
-         g.bias_mode != BIAS_N && g.N > 0;
+         g.bias_mode != BIAS_N && g.N > CH;
 }
 
 int launch_pconv(const GemmArgs& g, hipStream_t s) {
@@ -413,24 +454,32 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   a.ngrp = (a.nch + GRP - 1) / GRP;
   a.groups = (int64_t)g.batch * a.ngrp;
   a.hw = g.head_w; a.hb = g.head_bp; a.logits = g.logits; a.scores = g.scores; a.pos = g.pos;
-  const int grid = (int)(a.groups < 512 ? a.groups : 512);
-  const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW, head = g.head_w != nullptr;
+  const int ks = g.K / 16;
+  const int64_t slots = ks == 8 ? 512 : 256;   // resident workgroups (2 / 1 per CU)
+  const int grid = (int)(a.groups < slots ? a.groups : slots);
+  const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
+  const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
   if (head && (!g.logits || !g.scores || !g.pos)) return MVR_EINVAL;
-#define MVR_PC(P_, R_, S_, H_)                                                              \
-  if (pro == P_ && res == R_ && st == S_ && head == H_) {                                   \
-    hipLaunchKernelGGL((pconv_kernel<P_, R_, S_, H_>), dim3(grid), dim3(256), 0, s, a);     \
+#define MVR_PC(K_, P_, R_, S_, H_)                                                          \
+  if (ks == K_ && pro == P_ && res == R_ && st == S_ && head == H_) {                       \
+    hipLaunchKernelGGL((pconv_kernel<K_, P_, R_, S_, H_>), dim3(grid), dim3(256), 0, s, a); \
     MVR_CHECK_LAUNCH();                                                                     \
     return MVR_OK;                                                                          \
   }
-  MVR_PC(1, 0, 1, 0)
-  MVR_PC(1, 1, 1, 0)
-  MVR_PC(1, 0, 0, 0)
-  MVR_PC(1, 1, 0, 0)
-  MVR_PC(0, 0, 1, 0)
-  MVR_PC(0, 1, 1, 0)
-  MVR_PC(0, 0, 0, 0)
-  MVR_PC(0, 1, 0, 0)
-  MVR_PC(1, 1, 0, 1)   // the last PointCN conv of a block with the output head (oanet.py:174-175)
+  MVR_PC(8, 1, 0, 1, 0)
+  MVR_PC(8, 1, 1, 1, 0)
+  MVR_PC(8, 1, 0, 0, 0)
+  MVR_PC(8, 1, 1, 0, 0)
+  MVR_PC(8, 0, 0, 1, 0)
+  MVR_PC(8, 0, 1, 1, 0)
+  MVR_PC(8, 0, 0, 0, 0)
+  MVR_PC(8, 0, 1, 0, 0)
+  MVR_PC(8, 1, 1, 0, 1)    // the last PointCN conv of a block with the output head (oanet.py:174-175)
+  MVR_PC(8, 1, 1, 0, 2)    // ... when the block's output activation is not returned (head only)
+  MVR_PC(16, 1, 0, 1, 0)   // PointCN(2C -> C) conv3 (IN/BN/ReLU prologue, statistics)
+  MVR_PC(16, 0, 0, 0, 0)   // PointCN(2C -> C) shortcut (raw input)
+  MVR_PC(16, 1, 0, 0, 0)
+  MVR_PC(16, 0, 0, 1, 0)
 #undef MVR_PC
   return MVR_EINVAL;
 }

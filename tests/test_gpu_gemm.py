@@ -128,7 +128,8 @@ COMBOS = [(0, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 0), (2, 0, 1, 0, 0), (2
 @pytest.mark.parametrize("combo", COMBOS)
 @pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 36, 3), (500, 300, 64, 1), (1, 40, 8, 2),
                                    (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2),
-                                   (128, 5000, 128, 3), (128, 517, 128, 2), (128, 500, 128, 5), (128, 31, 128, 2)])
+                                   (128, 5000, 128, 3), (128, 517, 128, 2), (128, 500, 128, 5), (128, 31, 128, 2),
+                                   (128, 517, 256, 3), (128, 5000, 256, 2)])
 def test_gemm_modes(gpu, combo, shape, math):
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo
@@ -136,6 +137,16 @@ def test_gemm_modes(gpu, combo, shape, math):
         pytest.skip("per-k prologue needs K % 4 == 0")
     _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1),
          math=math)
+
+
+@pytest.mark.parametrize("shape", [(128, 32, 128, 1200), (128, 20, 128, 1100), (128, 33, 128, 1100)])
+@pytest.mark.parametrize("combo", [(2, 0, 1, 1, 1), (2, 0, 1, 1, 0)])
+def test_gemm_short_rows_many_pairs(gpu, combo, shape):
+    """<= 1 point chunk per pair over > 1024 pairs: several pair changes per workgroup range (the point-conv
+    kernel's per-pair fold staging; N <= 32 routes to the generic kernel)."""
+    M, N, K, b = shape
+    pro, bkc, bias, stats, res = combo
+    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=5, shared_a=True, math=1)
 
 
 @pytest.mark.parametrize("math", [0, 1])

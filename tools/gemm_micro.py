@@ -15,6 +15,8 @@ CASES = {
     "conv_plain": (C, N, C, 0, 0, 0, 0, 0),
     "conv_pro_stats": (C, N, C, 2, 0, 1, 1, 0),
     "conv_res": (C, N, C, 2, 0, 1, 1, 1),
+    "conv256_pro_stats": (C, N, 2 * C, 2, 0, 1, 1, 0),   # PointCN(2C -> C) conv3
+    "conv256_plain": (C, N, 2 * C, 0, 0, 1, 0, 0),       # PointCN(2C -> C) shortcut
     "embed_rowsmx": (K, N, C, 2, 0, 1, 2, 0),
     "pool": (C, K, N, 3, 1, 0, 1, 0),
     "unpool": (C, N, K, 3, 0, 0, 1, 0),
@@ -66,7 +68,7 @@ def run(name, iters, math, pconv=1):
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * M * Nn * Kk * P
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
-    print("%-16s m%d%s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, " pconv" if pconv and M == C and Kk == C else "",
+    print("%-16s m%d%s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, " pconv" if pconv and M == C and Kk in (C, 2 * C) else "",
                                                           ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
     if TRACE:
         import ctypes

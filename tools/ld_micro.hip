@@ -66,6 +66,38 @@ __global__ __launch_bounds__(256, 2) void stream_kernel(const float* X, float* Y
   if (acc == 12345.f) sink[0] = acc;
 }
 
+// reference: the same bytes as one contiguous stream (a point-major [P][N][128] layout), 16 B per lane,
+// 4 KB per wave-instruction group, UNR loads in flight per lane
+template <int UNR>
+__global__ __launch_bounds__(256, 2) void copy_kernel(const float4* X, float4* Y, long n4) {
+  const long stride = (long)gridDim.x * 256 * UNR;
+  for (long base = (long)blockIdx.x * 256 * UNR + threadIdx.x; base < n4; base += stride) {
+    float4 r[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) r[u] = base + 256L * u < n4 ? X[base + 256L * u] : make_float4(0, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u)
+      if (base + 256L * u < n4) Y[base + 256L * u] = r[u];
+  }
+}
+
+template <int UNR>
+static float run_copy(const float* X, float* Y, long n4, int grid) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int it = 0; it < 2; ++it)
+    hipLaunchKernelGGL((copy_kernel<UNR>), dim3(grid), dim3(256), 0, 0, (const float4*)X, (float4*)Y, n4);
+  hipEventRecord(e0);
+  for (int it = 0; it < 10; ++it)
+    hipLaunchKernelGGL((copy_kernel<UNR>), dim3(grid), dim3(256), 0, 0, (const float4*)X, (float4*)Y, n4);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  return ms / 10;
+}
+
 template <int V, int STORE>
 static float run(const float* X, float* Y, int P, int N, int ld, float* sink, int grid) {
   hipEvent_t e0, e1;
@@ -91,6 +123,15 @@ int main() {
   hipMalloc(&Y, bytes);
   hipMalloc(&sink, 64);
   hipMemset(X, 0, bytes);
+  {
+    const long n4 = (long)P * 128 * N / 4;
+    const double gb = 2.0 * P * 128.0 * N * 4 / 1e9;
+    for (int grid : {512, 1024, 2048}) {
+      const float a = run_copy<4>(X, Y, n4, grid), b = run_copy<8>(X, Y, n4, grid);
+      printf("contiguous copy grid %4d: UNR4 %.3f ms (%.0f GB/s)  UNR8 %.3f ms (%.0f GB/s)\n", grid, a, gb / a * 1e3, b,
+             gb / b * 1e3);
+    }
+  }
   for (int ld : {5000, 5024}) {
     const double gb = 2.0 * P * 128.0 * N * 4 / 1e9;
     for (int grid : {512, 1024}) {

@@ -8,7 +8,7 @@ OUT="$R/$1"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/$c" -o pmc --output-format csv -- \
+  MVR_PROF_MARK=1 timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/$c" -o pmc --output-format csv -- \
     python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --prof-seq "$OUT/seq_$c.json" \
     > "$OUT/bench_$c.log" 2>&1 || exit $?
 done
