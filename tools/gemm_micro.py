@@ -68,7 +68,7 @@ def run(name, iters, math, pconv=1):
     ms = e0.elapsed_time(e1) / iters
     fl = 2.0 * M * Nn * Kk * P
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
-    print("%-16s m%d%s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (name, math, " pconv" if pconv and M == C and Kk in (C, 2 * C) else "",
+    print("P%-4d %-16s m%d%s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (P, name, math, " pconv" if pconv and M == C and Kk in (C, 2 * C) else "",
                                                           ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
     if TRACE:
         import ctypes
@@ -107,7 +107,9 @@ if __name__ == "__main__":
     ap.add_argument("--only", default=None)
     ap.add_argument("--math", default="01")
     ap.add_argument("--trace", action="store_true", help="library built with -DGEMM_TRACE=1 (MVR_LIB)")
+    ap.add_argument("--pairs", type=int, default=P, help="pair batch (small batches stay in the Infinity Cache)")
     a = ap.parse_args()
+    P = a.pairs
     TRACE = a.trace
     if TRACE:
         import ctypes

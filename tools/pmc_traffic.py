@@ -49,7 +49,7 @@ def attribute(disp, seq):
             stack.pop()
         elif stack:   # innermost open region
             per_region[stack[-1]] += v
-            kernels[stack[-1]][name.split("(")[0]] += 1
+            kernels[stack[-1]][name.replace("(anonymous namespace)::", "").split("(")[0]] += 1
     assert k == len(seq) and not stack, "marked regions (%d) != sequence entries (%d)" % (k, len(seq))
     out, names = defaultdict(list), defaultdict(lambda: defaultdict(int))
     for (cls, _), v, ks in zip(seq, per_region, kernels):
