@@ -20,6 +20,7 @@ struct Rec { int kind; hipEvent_t a, b; double flops, bytes; };
 std::mutex mu;
 bool enabled = false;
 bool marks = false;
+uint32_t kind_mask = ~0u;   // kinds that get events (mvr_prof_mask)
 std::vector<Rec> recs;
 std::vector<hipEvent_t> pool;
 std::vector<int> open_idx;  // stack of records awaiting their end event
@@ -47,7 +48,7 @@ void drain() {
 }
 }  // namespace
 
-bool prof_on() { return enabled; }
+bool prof_on(int kind) { return enabled && ((kind_mask >> kind) & 1u); }
 void prof_begin(int kind, double flops, double bytes, hipStream_t s) {
   std::lock_guard<std::mutex> g(mu);
   Rec r{kind, get_ev(), nullptr, flops, bytes};
@@ -81,6 +82,14 @@ extern "C" int mvr_prof_set(int on) {
   enabled = on != 0;
   const char* m = getenv("MVR_PROF_MARK");
   marks = enabled && m && m[0] == '1';
+  return MVR_OK;
+}
+
+// Kinds recorded while enabled (bit k = kind k; default all): the bench times only the dominant
+// class inside its timed region, so the other launches carry no event records.
+extern "C" int mvr_prof_mask(unsigned mask) {
+  std::lock_guard<std::mutex> g(mu);
+  kind_mask = mask;
   return MVR_OK;
 }
 

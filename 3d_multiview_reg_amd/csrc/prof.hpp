@@ -18,12 +18,12 @@ enum ProfKind : int {
   PK_POINTCN = 10,   // fused PointCN (pointcn.hip)
   PK_COUNT = 16
 };
-bool prof_on();
+bool prof_on(int kind);
 void prof_begin(int kind, double flops, double bytes, hipStream_t s);
 void prof_end(int kind, hipStream_t s);
 struct ProfScope {
   int k; hipStream_t s; bool on;
-  ProfScope(int kind, double flops, double bytes, hipStream_t st) : k(kind), s(st), on(prof_on()) {
+  ProfScope(int kind, double flops, double bytes, hipStream_t st) : k(kind), s(st), on(prof_on(kind)) {
     if (on) prof_begin(kind, flops, bytes, st);
   }
   ~ProfScope() { if (on) prof_end(k, s); }

@@ -76,6 +76,7 @@ _SIGS = {
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
+    "mvr_sample_rand_mt19937": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "mvr_feat_knn2": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "mvr_fps": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "mvr_voxel_centroids_workspace_bytes": (c_size, [c_i64]),
@@ -103,6 +104,7 @@ _SIGS = {
                               c_vp, c_i64, c_vp]),
     "mvr_l2norm_rows": (c_int, [c_vp, c_i64, c_int, c_i64, c_vp]),
     "mvr_prof_set": (c_int, [c_int]),
+    "mvr_prof_mask": (c_int, [ctypes.c_uint]),
     "mvr_prof_seq": (c_int, [c_vp, c_vp, c_int]),
     "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
@@ -129,9 +131,15 @@ def lib():
     return _lib
 
 
+_hip_ok = False
+
+
 def require_hip(t=None):
-    if not torch.cuda.is_available():
-        raise RuntimeError("mvreg HIP path: no HIP device available (no CPU fallback)")
+    global _hip_ok
+    if not _hip_ok:   # torch.cuda.is_available() queries the runtime (microseconds): ask once
+        if not torch.cuda.is_available():
+            raise RuntimeError("mvreg HIP path: no HIP device available (no CPU fallback)")
+        _hip_ok = True
     if t is not None and t.device.type != "cuda":
         raise RuntimeError("mvreg HIP path: tensor on %s, expected a HIP device" % t.device)
 
@@ -157,6 +165,12 @@ PROF_KINDS = {"conv_pts": 0, "embed": 1, "pool": 2, "unpool": 3, "oafilter": 4, 
 
 def prof_set(on):
     check(lib().mvr_prof_set(int(on)), "mvr_prof_set")
+
+
+def prof_mask(kinds=None):
+    """Record only these kinds (names or ids; None = all) while profiling is enabled."""
+    m = 0xFFFFFFFF if kinds is None else sum(1 << (PROF_KINDS[k] if isinstance(k, str) else int(k)) for k in kinds)
+    check(lib().mvr_prof_mask(m), "mvr_prof_mask")
 
 
 def prof_seq():

@@ -138,11 +138,11 @@ class FCGFNet(nn.Module):
         return out
 
     def forward(self, x):
-        for t in list(self.parameters()) + list(self.buffers()):
-            if t.dtype.is_floating_point:
-                N.require_hip(t)
-                if t.dtype != torch.float32 or not t.is_contiguous():
-                    raise RuntimeError("FCGFNet parameters must be contiguous float32 on a HIP device")
+        N.require_hip()
+        f32 = torch.float32
+        if not all(t.is_cuda and t.dtype is f32 and t.is_contiguous()
+                   for t in (*self.parameters(), *self.buffers()) if t.dtype.is_floating_point):
+            raise RuntimeError("FCGFNet parameters must be contiguous float32 on a HIP device")
         if self.training:
             raise NotImplementedError("FCGFNet on the HIP path runs in eval mode (BatchNorm running statistics)")
         cm = x.coords_man

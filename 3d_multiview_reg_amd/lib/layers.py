@@ -86,20 +86,42 @@ class Sampler(torch.nn.Module):
         self.samp_type = samp_type
         self.targeted_num_points = targeted_num_points
 
-    def indices(self, pts_list, input_C=None):
-        """Global row indices [B, targeted] (int64, on the device of input_C for 'fps')."""
-        pts = [int(p) for p in (pts_list.cpu().numpy() if torch.is_tensor(pts_list) else pts_list)]
+    @staticmethod
+    def _pts(pts_list):
+        return tuple(int(p) for p in (pts_list.cpu().numpy() if torch.is_tensor(pts_list) else pts_list))
+
+    def _rand_indices(self, pts):
+        """The reference's draws (lib/layers.py:128-148): one np.random.choice per fragment, in order, on
+        numpy's global RandomState.  Without replacement (every fragment has >= targeted points) the
+        library replays numpy's own shuffle draw for draw (mvr_sample_rand_mt19937: ~10x numpy's loop)
+        and hands the advanced MT19937 state back to numpy."""
         tgt = self.targeted_num_points
         num_points = min(tgt, min(pts))
+        st = np.random.get_state()
+        if num_points >= tgt and st[0] == "MT19937":
+            key = np.array(st[1], dtype=np.uint32, copy=True)
+            pos = np.array([st[2]], dtype=np.int32)
+            counts = np.asarray(pts, dtype=np.int64)
+            out = np.empty((len(pts), tgt), dtype=np.int64)
+            ws = np.empty(max(max(pts), 1), dtype=np.int64)
+            N.check(N.lib().mvr_sample_rand_mt19937(key.ctypes.data, pos.ctypes.data, counts.ctypes.data, len(pts),
+                                                    tgt, out.ctypes.data, ws.ctypes.data), "mvr_sample_rand_mt19937")
+            np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
+            return torch.from_numpy(out)
+        out, start = [], 0
+        for n in pts:
+            rng = np.arange(start, start + n)
+            out.append(np.random.choice(rng, tgt, replace=not (num_points >= tgt)))
+            start += n
+        return torch.from_numpy(np.stack(out).astype(np.int64))
+
+    def indices(self, pts_list, input_C=None):
+        """Global row indices [B, targeted] (int64, on the device of input_C for 'fps')."""
+        pts = self._pts(pts_list)
         if self.samp_type == "rand":
-            out, start = [], 0
-            for n in pts:
-                rng = np.arange(start, start + n)
-                out.append(np.random.choice(rng, tgt, replace=not (num_points >= tgt)))
-                start += n
-            return torch.from_numpy(np.stack(out).astype(np.int64))
+            return self._rand_indices(pts)
         from lib.fps import furthest_point_sample
-        return furthest_point_sample(input_C, pts, num_points)
+        return furthest_point_sample(input_C, pts, min(self.targeted_num_points, min(pts)))
 
     def forward(self, input_C, input_F, pts_list):
         N.require_hip(input_F)

@@ -51,14 +51,15 @@ class PairwiseReg(nn.Module):
             return input_dict, None, None
         dev = next(self.descriptor_module.parameters()).device
         xyz_down = input_dict["pcd0"].to(dev).float().contiguous()
-        sinput0 = SparseTensor(input_dict["sinput0_F"], coords=input_dict["sinput0_C"]).to(dev)
+        pts_list = input_dict["pts_list"]
+        sinput0 = SparseTensor(input_dict["sinput0_F"], coords=input_dict["sinput0_C"],
+                               batch_size=len(pts_list)).to(dev)
         F0 = self.descriptor_module(sinput0).F
         if self.train_descriptor:
             sinput1 = SparseTensor(input_dict["sinput1_F"], coords=input_dict["sinput1_C"]).to(dev)
             F1 = self.descriptor_module(sinput1).F
         else:
             F1 = torch.empty(F0.shape[0], 0, device=dev)
-        pts_list = input_dict["pts_list"]
         xyz_b, f_b = self.sampler(xyz_down, F0, pts_list)                      # [B, n, 3], [B, n, 32]
         B, n = xyz_b.shape[0], xyz_b.shape[1]
         if self.connectivity_info is not None:

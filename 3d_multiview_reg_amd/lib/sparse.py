@@ -98,7 +98,7 @@ class CoordinateManager:
 class SparseTensor:
     """ME.SparseTensor(feats, coords=...) / (feats, coords_key=..., coords_manager=...)."""
 
-    def __init__(self, feats, coords=None, coords_key=None, coords_manager=None, tensor_stride=1):
+    def __init__(self, feats, coords=None, coords_key=None, coords_manager=None, tensor_stride=1, batch_size=None):
         self.F = feats
         self.tensor_stride = tensor_stride
         if coords_manager is not None:
@@ -108,7 +108,8 @@ class SparseTensor:
             if coords is None:
                 raise ValueError("SparseTensor needs coords or a coords_manager")
             c = torch.as_tensor(coords).to(torch.int32)
-            B = int(c[:, 0].max().item()) + 1 if c.numel() else 1
+            # batch_size (when the caller knows it, e.g. len(pts_list)) spares a device sync
+            B = int(batch_size) if batch_size is not None else (int(c[:, 0].max().item()) + 1 if c.numel() else 1)
             self._pending = (c, B)
             self.coords_man = None
             self.coords_key = 1

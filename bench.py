@@ -201,6 +201,7 @@ def main():
     ap.add_argument("--npts", type=int, default=5000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events in the timed region (A/B timing)")
     ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
                     "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -230,8 +231,22 @@ def main():
     with torch.no_grad():
         for _ in range(args.warmup):
             records_allgather(wl.step(), world)
+        # one untimed step with events on every launch: the per-class breakdown and the dominant class;
+        # the timed region then records events only around the dominant class's launches (events on
+        # every launch cost ~1 ms per step).  --prof-seq (PMC attribution of exactly the timed steps'
+        # launches) records every class in the timed region instead.
+        prof_all, dom = None, None
         torch.cuda.synchronize()
-        _native.prof_set(1)
+        _native.prof_mask(None)
+        if not args.prof_seq:
+            _native.prof_set(1)
+            records_allgather(wl.step(), world)
+            torch.cuda.synchronize()
+            prof_all = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
+            _native.prof_set(0)
+            dom = max(prof_all, key=lambda k: prof_all[k][0])
+            _native.prof_mask([dom])
+        _native.prof_set(0 if args.no_prof else 1)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -242,10 +257,14 @@ def main():
         t1 = time.perf_counter()
         dt = t1 - t0
         prof = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
+        if prof_all is None:
+            prof_all = {k: tuple(x / max(args.steps, 1) for x in v) for k, v in prof.items()}
+            dom = max(prof, key=lambda k: prof[k][0])
         if args.prof_seq and rank == 0:
             with open(args.prof_seq, "w") as f:
                 json.dump(_native.prof_seq(), f)
         _native.prof_set(0)
+        _native.prof_mask(None)
     if world > 1:
         import torch.distributed as dist
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
@@ -254,10 +273,12 @@ def main():
     pairs_per_step = int(rec.shape[-2]) * world
     value = pairs_per_step * args.steps / dt
 
-    # dominant kernel class by device time inside the timed region, priced against the roofline
-    # that binds it: arithmetic intensity vs the ridge of the MFMA path it runs on
-    dom = max(prof, key=lambda k: prof[k][0])
+    # dominant kernel class (by device time in the profiled untimed step), timed with HIP events around
+    # each of its launches inside the timed region and priced against the roofline that binds it:
+    # arithmetic intensity vs the ridge of the MFMA path it runs on
     ms, nl, fl, by = prof[dom]
+    if ms <= 0:   # --no-prof: no per-launch timings
+        ms, nl = 1e-9, 1
     mpeak = PEAK_SPLIT_TFLOPS if dom in GEMM_CLASSES else MFMA_PEAKS.get(dom, PEAK_FP32_TFLOPS)
     ridge = mpeak * 1e12 / (PEAK_HBM_GBS * 1e9)                     # FLOP per byte
     bound = "mfma" if (by > 0 and fl / by >= ridge) else "hbm"
@@ -283,9 +304,10 @@ def main():
             "peak_note": ("split-bf16 MFMA fp32-equivalent peak = 16*157.3/6 TF" if dom in GEMM_CLASSES else
                           "MI355X_MICROARCH.md"),
             "traffic_source": tsrc,
-            # per kernel class: [ms per step, algorithmic TFLOP/s, algorithmic GB/s]
-            "classes": {k: [round(v[0] / args.steps, 3), round(v[2] / (v[0] * 1e9), 1), round(v[3] / (v[0] * 1e6))]
-                        for k, v in prof.items() if v[1] and v[0] > 0}}
+            # per kernel class, from the profiled untimed step (events on every launch):
+            # [ms per step, algorithmic TFLOP/s, algorithmic GB/s]
+            "classes": {k: [round(v[0], 3), round(v[2] / (v[0] * 1e9), 1), round(v[3] / (v[0] * 1e6))]
+                        for k, v in prof_all.items() if v[1] and v[0] > 0}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -311,10 +311,20 @@ int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks
 /* x[o][:C] /= ||x[o][:C]||  (fcgf.py:274-278) */
 int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, mvr_stream_t stream);
 
+/* Sampler 'rand' (lib/layers.py:145-148) on the host: for each fragment b in order,
+ * np.random.choice(arange(start_b, start_b + counts[b]), tgt, replace=False) drawn from numpy's
+ * legacy MT19937 RandomState (key uint32[624] and *pos as np.random.get_state() gives them; advanced
+ * in place for np.random.set_state()).  out int64 [B][tgt]; ws int64 scratch of max(counts).
+ * Requires tgt <= counts[b].  Host-only (no device work, no stream). */
+int mvr_sample_rand_mt19937(uint32_t* key, int32_t* pos, const int64_t* counts, int B, int tgt, int64_t* out,
+                            int64_t* ws);
+
 /* Opt-in per-kernel-class device timing (hipEvents on the launching stream).
  * mvr_prof_set(1) resets and enables; mvr_prof_get(kind, ...) synchronises the
  * recorded events and returns totals since then (kinds: csrc/prof.hpp ProfKind). */
 int mvr_prof_set(int on);
+/* kinds that get event records while enabled: bit k = kind k (default: all) */
+int mvr_prof_mask(unsigned mask);
 int mvr_prof_get(int kind, double* ms, long long* launches, double* flops, double* bytes);
 /* launch order since mvr_prof_set(1): kind and algorithmic bytes per profiled launch (<= cap);
  * returns the count (joins rocprofv3 PMC dispatch rows to kernel classes) */
