@@ -958,8 +958,12 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   const long long tiles = (long long)gemm_ntiles(g.N) * gemm_mtiles(g.M) * g.batch;
   if (tiles > 0x7fffffffLL) return MVR_EINVAL;
   const double fl = 2.0 * g.M * g.N * (double)g.K * g.batch;
-  const double by = 4.0 * ((double)g.M * g.K * (g.sAb ? g.batch : 1) + (double)g.K * g.N * (g.sBb ? g.batch : 1) +
-                           (double)g.M * g.N * g.batch * ((g.has_res ? 2 : 1) - (g.no_store ? 1 : 0)));
+  double by = 4.0 * ((double)g.M * g.K * (g.sAb ? g.batch : 1) + (double)g.K * g.N * (g.sBb ? g.batch : 1) +
+                     (double)g.M * g.N * g.batch * ((g.has_res ? 2 : 1) - (g.no_store ? 1 : 0)));
+  if (g.xin) {   // folded conv1 (pconv): the block input's xci rows replace B (xin 1) or the residual (xin 2)
+    if (!pconv_covers(g)) return MVR_EINVAL;
+    by = 4.0 * ((double)g.M * g.K + (double)g.N * g.batch * (g.xin == 1 ? g.xci + g.M : g.K + g.xci + g.M));
+  }
   ProfScope prof(g.prof_kind, fl, by, s);
   if (pconv_covers(g)) return launch_pconv(g, s);
   if (g.head_w) return MVR_EINVAL;   // the fused head exists on the point-conv kernel only

@@ -54,6 +54,12 @@ struct GemmArgs {
   // output head fused into the epilogue (pconv only, M = 128): logits[b*N + n] = head_w . C(:, n) + head_bp[0] (nullable),
   // scores = relu(tanh(logits)), pos[b] += #positive scores (oanet.py:163,174-178)
   const float* head_w; const float* head_bp; float* logits; float* scores; int32_t* pos;
+  // the block's conv1 folded into its first PointCN (pconv only, M = K = 128): xin = 1, the B operand
+  // rows are x(k, n) = xb[k] + xw[k][:xci] . B(:xci, n) (B then holds the block input, xci <= 8 rows);
+  // xin = 2, the residual is x(m, n) recomputed the same way from R (the block input).  xw [128][8]
+  // (columns >= xci zero), xb [128] (nullable)
+  int xin; int xci; const float* xw; const float* xb;
+  int64_t xld;   // row stride of the block input (xin = 2: R's rows; xin = 1 uses ldb)
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the

@@ -104,6 +104,98 @@ __global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int C, 
   }
 }
 
+// The block's conv1 folded into its first PointCN (pconv XI): the InstanceNorm statistics of
+// x = W1 . in + b1 (oanet.py:144-145 conv1, then PointCN's IN, :27) follow exactly from the first and
+// second moments of the block input over the points, so x itself is never stored.
+// Per pair: mom[p] = {S1[c] = sum_n in[c][n] (c < 8), S2[c][c'] = sum_n in[c][n] in[c'][n] (c <= c', 36)}
+// in fp64 (fp32 products are exact in fp64).
+constexpr int MOM = 8 + 36;
+__global__ __launch_bounds__(256) void xin_moments_kernel(const float* __restrict__ in, int64_t ps, int64_t ld, int ci,
+                                                          int N, double* __restrict__ mom) {
+  __shared__ double red[4][MOM];
+  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float* x = in + (int64_t)p * ps;
+  double s1[8], s2[36];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) s1[c] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 36; ++c) s2[c] = 0.0;
+  for (int n = tid; n < N; n += 256) {
+    double v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < ci ? (double)x[(int64_t)c * ld + n] : 0.0;
+    int k = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      s1[c] += v[c];
+#pragma unroll
+      for (int d = c; d < 8; ++d) s2[k++] += v[c] * v[d];
+    }
+  }
+  auto wsum = [&](double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const double v = wsum(s1[c]);
+    if (lane == 0) red[w][c] = v;
+  }
+#pragma unroll
+  for (int c = 0; c < 36; ++c) {
+    const double v = wsum(s2[c]);
+    if (lane == 0) red[w][8 + c] = v;
+  }
+  __syncthreads();
+  if (tid < MOM) mom[(int64_t)p * MOM + tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+}
+
+// IN(eps)+BN fold of x = W1 . in + b1 per (pair, channel k) from the moments (same outputs as
+// in_finalize_kernel: sc / sh in eval mode, (mean, var) into mv in train mode).  W1 [C][8] zero-padded.
+__global__ void in_fold_moments_kernel(const double* __restrict__ mom, int N, const float* __restrict__ w1,
+                                       const float* __restrict__ b1, int C, float eps_in, mvr_bn_p bn, int train,
+                                       float* sc, float* sh, float2* mv) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (k >= C) return;
+  const double* m = mom + (int64_t)p * MOM;
+  const double inv = 1.0 / (double)N;
+  double wk[8], mu[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    wk[c] = (double)w1[k * 8 + c];
+    mu[c] = m[c] * inv;
+  }
+  double mean = b1 ? (double)b1[k] : 0.0, var = 0.0;
+  int q = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    mean += wk[c] * mu[c];
+#pragma unroll
+    for (int d = c; d < 8; ++d) {
+      const double cov = m[8 + q++] * inv - mu[c] * mu[d];
+      var += (c == d ? 1.0 : 2.0) * wk[c] * wk[d] * cov;
+    }
+  }
+  var = fmax(var, 0.0);
+  if (train) {
+    mv[(int64_t)p * C + k] = make_float2((float)mean, (float)var);
+    return;
+  }
+  const float rin = (float)(1.0 / sqrt(var + (double)eps_in));
+  float g = 1.f, b = 0.f, rm = 0.f, rs = 1.f;
+  if (bn.gamma) {
+    g = bn.gamma[k];
+    b = bn.beta[k];
+    rm = bn.mean[k];
+    rs = 1.f / sqrtf(bn.var[k] + 1e-5f);
+  }
+  const float gs = g * rs;
+  sc[(int64_t)p * C + k] = rin * gs;
+  sh[(int64_t)p * C + k] = (float)((double)b - (mean * (double)rin + (double)rm) * (double)gs);
+}
+
 // BatchNorm(points) of OAFilter.conv2 (oanet.py:72-76): per-cluster affine.
 __global__ void bn_fold_eval_kernel(mvr_bn_p bn, int C, float* sc, float* sh) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -192,7 +284,8 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
-int g_oan_fused = 1;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 1 PointCN (off: not faster yet)
+int g_oan_fused = 5;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 1 PointCN (off: not faster yet),
+                       // bit 2 conv1 folded into the first PointCN (point-conv XI variants)
 int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B timing)
 
 namespace {
@@ -232,7 +325,8 @@ struct Plan {
   char* uimg;            // their split-bf16 operand images
   size_t uimg_bytes;
   size_t bytes;
-  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *sc2, *sh2, *scK, *shK, *fac, *W1;
+  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *sc2, *sh2, *scK, *shK, *fac, *W1, *W8;
+  double* mom;           // input moments of the folded conv1 [P][MOM]
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
 };
 
@@ -269,6 +363,8 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   if ((size_t)P * MK * pl.Np > nf) nf = (size_t)P * MK * pl.Np;
   pl.fac = pl.fused ? nullptr : w.take<float>(nf);
   pl.W1 = w.take<float>((size_t)C * pl.Cinp);
+  pl.W8 = w.take<float>((size_t)C * 8);
+  pl.mom = w.take<double>((size_t)P * MOM);
   pl.st11 = w.take<float2>((size_t)P * TS * 2 * C);
   pl.stA = w.take<float2>((size_t)P * TS * C);
   pl.stT = w.take<float2>((size_t)P * TN * C);
@@ -428,7 +524,7 @@ extern "C" int mvr_set_pool_split(int on) {
 
 extern "C" int mvr_set_oan_fused(int on) {
   const int prev = g_oan_fused;
-  g_oan_fused = on & 3;
+  g_oan_fused = on & 7;
   return prev;
 }
 
@@ -466,10 +562,56 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   }
   Act in{const_cast<float*>(input), in_pstride, ld, Cin, N, nullptr, 0, 0};
   Act xa{pl.XA, CN, Np, C, N, pl.stA, C, 0};
-  cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW, w1);
-  // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C))
   Act x11top{pl.X11, 2 * CN, Np, C, N, pl.st11, 2 * C, 0};
-  for (int i = 0; i < H; ++i) cx.pointcn(blk->l1_1[i], xa, (i == H - 1) ? x11top : xa);
+  // conv1 folded into the first l1_1 PointCN when the point-conv kernel takes it: x = conv1(input) is
+  // recomputed by that PointCN's conv3 (B operand) and conv7 (residual) from the input's <= 8 rows,
+  // its InstanceNorm statistics come from the input's moments
+  GemmArgs f3{};
+  f3.math = g_default_math; f3.M = C; f3.N = N; f3.K = C; f3.batch = P;
+  f3.A = blk->l1_1[0].conv3.weight; f3.lda = C;
+  f3.B = input; f3.sBb = in_pstride; f3.ldb = ld;
+  f3.C = pl.T1; f3.sCb = CN; f3.ldc = Np;
+  f3.bias = blk->l1_1[0].conv3.bias; f3.bias_mode = f3.bias ? BIAS_M : BIAS_NONE;
+  f3.pro = PRO_B_K; f3.psc = pl.sc; f3.psh = pl.sh; f3.sPb = C;
+  f3.stats_mode = ST_ROW; f3.stats = pl.stT; f3.st_ld = C; f3.st_off = 0;
+  f3.xin = 1; f3.xci = Cin; f3.xw = pl.W8; f3.xb = blk->conv1.bias; f3.xld = ld;
+  f3.prof_kind = PK_CONV_PTS;
+  const bool fold1 = (g_oan_fused & 4) && !pl.fused_pcn && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
+                     pconv_covers(f3);
+  if (fold1) {
+    const int n8 = C * 8;
+    hipLaunchKernelGGL(pad_cols_kernel, dim3((n8 + 255) / 256), dim3(256), 0, s, blk->conv1.weight, C, Cin, 8, pl.W8);
+    hipLaunchKernelGGL(xin_moments_kernel, dim3(P), dim3(256), 0, s, input, in_pstride, ld, Cin, N, pl.mom);
+    const mvr_bn_p& bn1 = blk->l1_1[0].bn1;
+    hipLaunchKernelGGL(in_fold_moments_kernel, dim3((C + 127) / 128, P), dim3(128), 0, s, pl.mom, N, pl.W8,
+                       blk->conv1.bias, C, 1e-5f, bn1, bn_train, pl.sc, pl.sh, pl.mv);
+    cx.chk_launch();
+    if (bn_train) {
+      hipLaunchKernelGGL(in_bn_train_kernel, dim3((C + 255) / 256), dim3(256), 0, s, pl.mv, P, C, 1e-5f, bn1, pl.sc,
+                         pl.sh, (int64_t)C);
+      cx.chk_launch();
+    }
+    cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
+    Act t{pl.T1, CN, Np, C, N, pl.stT, C, 0};
+    cx.finalize_in(t, 1e-5f, blk->l1_1[0].bn5);
+    Act& y = (H == 1) ? x11top : xa;
+    GemmArgs f7{};
+    f7.math = g_default_math; f7.M = C; f7.N = N; f7.K = C; f7.batch = P;
+    f7.A = blk->l1_1[0].conv7.weight; f7.lda = C;
+    f7.B = pl.T1; f7.sBb = CN; f7.ldb = Np;
+    f7.C = y.p; f7.sCb = y.ps; f7.ldc = y.ld;
+    f7.R = input; f7.sRb = in_pstride; f7.has_res = 1;
+    f7.bias = blk->l1_1[0].conv7.bias; f7.bias_mode = f7.bias ? BIAS_M : BIAS_NONE;
+    f7.pro = PRO_B_K; f7.psc = pl.sc; f7.psh = pl.sh; f7.sPb = C;
+    f7.stats_mode = ST_ROW; f7.stats = y.st; f7.st_ld = y.st_ld; f7.st_off = y.st_off;
+    f7.xin = 2; f7.xci = Cin; f7.xw = pl.W8; f7.xb = blk->conv1.bias; f7.xld = ld;
+    f7.prof_kind = PK_CONV_PTS;
+    cx.chk(launch_gemm(f7, s));   // conv7 of l1_1[0] + x (recomputed)
+  } else {
+    cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW, w1);
+  }
+  // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C))
+  for (int i = fold1 ? 1 : 0; i < H; ++i) cx.pointcn(blk->l1_1[i], xa, (i == H - 1) ? x11top : xa);
 
   // diff_pool (oanet.py:96-110): E = exp(embed - tile max) over points, x_down = x . softmax(E)^T
   cx.finalize_in(x11top, 1e-3f, blk->down_bn);

@@ -61,6 +61,8 @@ struct PcArgs {
   int64_t groups;                       // P * ngrp
   const float* hw; const float* hb;     // HEAD: output conv 128 -> 1 (oanet.py:163)
   float* logits; float* scores; int32_t* pos;   // [P][N], [P][N], [P]
+  int xci; const float* xw; const float* xb;    // XI: x(k, n) = xb[k] + xw[k][:xci] . in(:, n) (xw [128][8])
+  int64_t rld;                                  // XI & 2: row stride of the block input R
 };
 
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_base + 16 l.
@@ -88,12 +90,17 @@ __device__ __forceinline__ float sum8(float v) {
 // 256 -> 128 convs of the first PointCN after diff_unpool (oanet.py:155), one workgroup per CU
 // (weights 192 VGPRs, chunk images 2 x 48 KB).  HEAD = 2: output head only, Y not stored (the
 // block's last conv when its activation is not returned).
-template <int KS, int PRO, int RES, int STATS, int HEAD>
+// XI: the block's conv1 (oanet.py:144-145, Cin = 6 or 8 -> 128) folded into its first PointCN, so its
+// 128-channel output x is never stored: XI = 1, the B operand rows are recomputed from the block input
+// (8 loads per point instead of 128 rows); XI = 2, the residual (RES) is recomputed from it.  Both use
+// the same fma order, so the two recomputations of x are bit-identical.
+template <int KS, int PRO, int RES, int STATS, int HEAD, int XI = 0>
 __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   constexpr int CIN = 16 * KS;   // input channels
   constexpr int NT = KS / 4;     // 16-row k-steps each wave loads and splits per chunk
   constexpr int RW = CIN / 4;    // input rows per wave
-  constexpr int NX = 8 * NT;     // activation registers per chunk
+  constexpr int NX = (XI & 1) ? 8 : 8 * NT;   // activation registers per chunk
+  static_assert(!XI || KS == 8, "conv1 folding: 128-channel convs");
   __shared__ __attribute__((aligned(16))) char xi[2][KS * FRB];      // chunk images (B fragments)
   __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
   __shared__ __attribute__((aligned(16))) float fold[2][2][CIN];   // (sc, sh) by pair parity
@@ -101,6 +108,12 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   __shared__ __attribute__((aligned(16))) float skl[STATS ? 4 : 1][STATS ? 32 : 4];   // row shifts [wave][erow][q]
   __shared__ float shw[HEAD ? PC : 1];
   __shared__ __attribute__((aligned(16))) float hpart[HEAD ? 2 : 1][4][CH];   // HEAD: per-wave partial logits by step parity
+  __shared__ __attribute__((aligned(16))) float xws[XI ? PC : 1][8];   // XI: conv1 weights, bias
+  __shared__ float xbs[XI ? PC : 1];
+  // XI & 2: the same weights as float4 over an epilogue lane's 4 rows 32w + erow + 8q: [ci][w][erow][q], bias [w][erow][q]
+  __shared__ __attribute__((aligned(16))) float xwe[(XI & 2) ? 8 : 1][(XI & 2) ? PC : 4];
+  __shared__ __attribute__((aligned(16))) float xbe[(XI & 2) ? PC : 4];
+  __shared__ __attribute__((aligned(16))) float xib[(XI & 2) ? 4 : 1][(XI & 2) ? 256 : 4];   // per wave: input chunk
 
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -132,6 +145,16 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   const int erow = lane >> 3, ec0 = 4 * (lane & 7);
   if (tid < PC) sbias[tid] = a.bias ? a.bias[tid] : 0.f;   // published by the prologue barriers
   if (HEAD && tid < PC) shw[tid] = a.hw[tid];
+  if (XI && tid < PC) {
+    const int k = tid, ke = (k & ~31) + 4 * (k & 7) + ((k >> 3) & 3);   // (w, erow, q) slot of row k
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      xws[k][c] = a.xw[k * 8 + c];
+      if (XI & 2) xwe[c][ke] = a.xw[k * 8 + c];
+    }
+    xbs[k] = a.xb ? a.xb[k] : 0.f;
+    if (XI & 2) xbe[ke] = xbs[k];
+  }
 
   // chunk cursor (pair, chunk in pair); cursors past the range stay on the last chunk (clamped
   // re-reads keep the issue unconditional, hence every s_waitcnt the compiler derives exact)
@@ -160,6 +183,15 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     const float* base = a.X + (int64_t)c.p * a.xps + (int64_t)(RW * w) * a.xld;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
+    if (XI & 1) {   // the block input's rows 0 .. xci-1 (clamped: weight columns past xci are zero)
+      const float* ib = a.X + (int64_t)c.p * a.xps;
+      const __amdgpu_buffer_rsrc_t ri =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ib), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NX; ++i)
+        r[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, 4 * n, min(i, a.xci - 1) * xld4, 0));
+      return;
+    }
     const int vo = 8 * h * xld4 + 4 * n;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -172,6 +204,21 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   // normalise + split half t of a chunk's registers -> its k-step fragment in image slot
   auto split_half = [&](const Cur& c, const float (&r)[NX], int slot, int t) {
     float v[8];
+    float xr[8];   // the B rows of this half as loaded, or (XI & 1) recomputed from the block input
+    if (XI & 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = RW * w + 16 * t + 8 * h + i;
+        const float4 w0 = *reinterpret_cast<const float4*>(&xws[k][0]), w1 = *reinterpret_cast<const float4*>(&xws[k][4]);
+        float acc = xbs[k];
+        acc = fmaf(w0.x, r[0], acc); acc = fmaf(w0.y, r[1], acc); acc = fmaf(w0.z, r[2], acc); acc = fmaf(w0.w, r[3], acc);
+        acc = fmaf(w1.x, r[4], acc); acc = fmaf(w1.y, r[5], acc); acc = fmaf(w1.z, r[6], acc); acc = fmaf(w1.w, r[7], acc);
+        xr[i] = acc;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xr[i] = r[8 * t + i];
+    }
     if (PRO) {
       const float* f = &fold[c.p & 1][0][RW * w + 16 * t + 8 * h];
       const float4 sa = *reinterpret_cast<const float4*>(f), sb = *reinterpret_cast<const float4*>(f + 4);
@@ -179,10 +226,10 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
       const float s1[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
       const float h1[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(r[8 * t + i], s1[i], h1[i]), 0.f);
+      for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(xr[i], s1[i], h1[i]), 0.f);
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = r[8 * t + i];
+      for (int i = 0; i < 8; ++i) v[i] = xr[i];
     }
     Frag f;
     if (PCONV_ABL & 2) {
@@ -203,6 +250,11 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   float* yb = ys[w];
   auto dma_r = [&](const Cur& c) {
     if (!RES) return;
+    if (XI & 2) {   // the block input's 8 rows x 32 columns (1 KB): lane -> row lane / 8, columns 4 (lane & 7)
+      const int n = min(c.kc * CH + 4 * (lane & 7), N4 - 4);
+      glds16(a.R + (int64_t)c.p * a.rps + (int64_t)min(lane >> 3, a.xci - 1) * a.rld + n, xib[w]);
+      return;
+    }
     const int n = min(c.kc * CH + 4 * (lane & 7), N4 - 4);
     const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + (lane >> 3)) * a.yld + n;
 #pragma unroll
@@ -246,13 +298,14 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     }
     // value (q, e) of this lane: row erow + 8q of the wave's 32, column n0 + ec0 + e
     float4 ev[4];
-    if (RES) {   // the residual DMA (issued one step ago; NX younger activation loads since)
+    if (RES && !(XI & 2)) {   // the residual DMA (issued one step ago; NX younger activation loads since)
       static_assert(!RES || NX == 16, "residual wait count");
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < 4; ++q) ev[q] = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // residual read before the transpose overwrites it
     } else {
+      if (XI & 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the block input's chunk (xib)
 #pragma unroll
       for (int q = 0; q < 4; ++q) ev[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -264,6 +317,26 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
       const float4 v = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
       const float bq = sbias[32 * w + erow + 8 * q];
       ev[q].x += v.x + bq; ev[q].y += v.y + bq; ev[q].z += v.z + bq; ev[q].w += v.w + bq;
+    }
+    if (XI & 2) {   // + x, recomputed for the lane's 4 rows x 4 columns in split_half's fma order
+      int e0 = 32 * w + 4 * erow;   // this lane's (w, erow) slot of xwe / xbe
+      asm volatile("" : "+v"(e0));   // opaque per chunk: the weight reads stay here (hoisted out of the chunk
+                                     // loop they would occupy registers across it and spill)
+      const float* xi = xib[w];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // one row at a time (register pressure)
+        const float b = xbe[e0 + q];
+        float4 xq = make_float4(b, b, b, b);
+#pragma unroll
+        for (int ci = 0; ci < 8; ++ci) {
+          const float4 v = *reinterpret_cast<const float4*>(xi + ci * 32 + ec0);
+          const float wq = xwe[ci][e0 + q];
+          xq.x = fmaf(wq, v.x, xq.x); xq.y = fmaf(wq, v.y, xq.y); xq.z = fmaf(wq, v.z, xq.z); xq.w = fmaf(wq, v.w, xq.w);
+        }
+        // x + conv7 output (fp32 addition commutes: the reference's x + out)
+        ev[q].x += xq.x; ev[q].y += xq.y; ev[q].z += xq.z; ev[q].w += xq.w;
+        PC_FENCE();
+      }
     }
     float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + n0 + ec0;
     const bool full = n0 + CH <= N;   // uniform: every column of the chunk is valid
@@ -352,7 +425,10 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   //   slot (j + 1) & 1) and the load of chunk j + 4 into the freed registers interleaved between
   //   the MFMA groups; epilogue of chunk j; residual DMA of chunk j + 1; fold of chunk j + 2's pair
   //   when it starts one; one barrier.
-  float x0[NX], x1[NX], x2[NX];
+  // NSET register sets (3; 2 for the residual-recomputing conv7, whose epilogue needs the registers): a
+  // chunk's loads are issued NSET steps before its MFMAs
+  constexpr int NSET = (XI & 2) ? 2 : 3;
+  float x0[NX], x1[NX], x2[NSET == 3 ? NX : 1];
   Cur cc = cstart, cs = cstart, ci = cstart, cf = cstart, cr = cstart;   // compute, split, issue, fold, residual
   stage_fold(cf.p);
   adv(cf);
@@ -361,8 +437,10 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   adv(ci);
   issue_x(ci, x1);
   adv(ci);
-  issue_x(ci, x2);
-  adv(ci);
+  if constexpr (NSET == 3) {
+    issue_x(ci, x2);
+    adv(ci);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
   for (int t = 0; t < NT; ++t) split_half(cs, x0, 0, t);
@@ -395,7 +473,7 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     if (lane == 0 && np) atomicAdd(a.pos + c.p, np);
   };
   Cur ch = cstart;   // head cursor (one step behind compute)
-  auto step = [&](int j, float (&xs)[NX]) {
+  auto step = [&](int j, auto& xs) {
     if (HEAD && j > 0) {
       head_finish(ch);
       adv(ch);
@@ -415,13 +493,21 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
   int j = 0;
-  for (; j + 2 < nloc; j += 3) {
-    step(j, x1);
-    step(j + 1, x2);
-    step(j + 2, x0);
+  if constexpr (NSET == 3) {
+    for (; j + 2 < nloc; j += 3) {
+      step(j, x1);
+      step(j + 1, x2);
+      step(j + 2, x0);
+    }
+    if (j < nloc) step(j, x1);
+    if (j + 1 < nloc) step(j + 1, x2);
+  } else {
+    for (; j + 1 < nloc; j += 2) {
+      step(j, x1);
+      step(j + 1, x0);
+    }
+    if (j < nloc) step(j, x1);
   }
-  if (j < nloc) step(j, x1);
-  if (j + 1 < nloc) step(j + 1, x2);
   if (HEAD) head_finish(ch);   // the last chunk (published by the last step's barrier)
 }
 
@@ -432,6 +518,12 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
 // land in the slot another wave still reads while splitting chunk j + 1 (pairs j + 1 and j + 3 then
 // differ by 2, same parity); with >= 2 chunks per pair consecutive staged pairs always alternate.
 bool pconv_covers(const GemmArgs& g) {
+  if (g.xin) {   // folded conv1: only the two shapes the OANet schedule uses
+    const bool ok = g_pconv && g.math == MATH_BF16X3 && g.M == PC && g.K == PC && !g.bkc && g.sAb == 0 &&
+                    g.pro == PRO_B_K && g.stats_mode == ST_ROW && !g.head_w && !g.no_store && g.bias_mode != BIAS_N &&
+                    g.N > CH && g.xw && g.xci >= 1 && g.xci <= 8 && (g.xin != 2 || (g.xld % 4 == 0 && g.xld >= round4(g.N)));
+    return ok && ((g.xin == 1 && !g.has_res) || (g.xin == 2 && g.has_res));
+  }
   if (g.head_w && g.stats_mode != ST_NONE) return false;
   if (g.no_store && !g.head_w) return false;   // statistics-only passes stay on gemm_kernel
   if (g.K == 2 * PC && (g.has_res || g.head_w)) return false;   // KS = 16 runs the 256 -> 128 convs only
@@ -454,12 +546,23 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   a.ngrp = (a.nch + GRP - 1) / GRP;
   a.groups = (int64_t)g.batch * a.ngrp;
   a.hw = g.head_w; a.hb = g.head_bp; a.logits = g.logits; a.scores = g.scores; a.pos = g.pos;
+  a.xci = g.xci; a.xw = g.xw; a.xb = g.xb; a.rld = g.xld;
   const int ks = g.K / 16;
   const int64_t slots = ks == 8 ? 512 : 256;   // resident workgroups (2 / 1 per CU)
   const int grid = (int)(a.groups < slots ? a.groups : slots);
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
   const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
   if (head && (!g.logits || !g.scores || !g.pos)) return MVR_EINVAL;
+  if (g.xin == 1) {   // folded conv1 -> conv3 of the block's first PointCN
+    hipLaunchKernelGGL((pconv_kernel<8, 1, 0, 1, 0, 1>), dim3(grid), dim3(256), 0, s, a);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
+  if (g.xin == 2) {   // ... and its conv7 with the residual x recomputed
+    hipLaunchKernelGGL((pconv_kernel<8, 1, 1, 1, 0, 2>), dim3(grid), dim3(256), 0, s, a);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
 #define MVR_PC(K_, P_, R_, S_, H_)                                                          \
   if (ks == K_ && pro == P_ && res == R_ && st == S_ && head == H_) {                       \
     hipLaunchKernelGGL((pconv_kernel<K_, P_, R_, S_, H_>), dim3(grid), dim3(256), 0, s, a); \

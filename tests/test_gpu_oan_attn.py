@@ -134,10 +134,10 @@ def test_diff_pool_rejects_bad_layout(gpu):
     assert L.mvr_oan_diff_unpool_workspace_bytes(1, 64, 16) == 0
 
 
-@pytest.mark.parametrize("fused", [1, 2, 3])
+@pytest.mark.parametrize("fused", [1, 2, 3, 4, 5])
 def test_oanet_fused_vs_gemm_path(gpu, fused):
-    """Whole filter with the fused kernels (bit 0: diff_pool/diff_unpool, bit 1: PointCN) vs the plain
-    GEMM path: same R, t (1e-4) and inlier masks."""
+    """Whole filter with the fused kernels (bit 0: diff_pool/diff_unpool, bit 1: PointCN, bit 2: conv1
+    folded into the first PointCN) vs the plain GEMM path: same R, t (1e-4) and inlier masks."""
     import torch
     from lib import _native as NV
     from test_gpu_oanet import _oanet
@@ -146,13 +146,14 @@ def test_oanet_fused_vs_gemm_path(gpu, fused):
     net = _oanet(128, 500, 7, gpu, which="full")
     outs = []
     L = NV.lib()
+    prev = L.mvr_set_oan_fused(fused)
     try:
         for f in (fused, 0):
             L.mvr_set_oan_fused(f)
             with torch.no_grad():
                 outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
     finally:
-        L.mvr_set_oan_fused(1)
+        L.mvr_set_oan_fused(prev)
     a, b = outs
     for i in range(2):
         np.testing.assert_allclose(a["logits"][i].cpu().numpy(), b["logits"][i].cpu().numpy(), atol=2e-3, rtol=1e-4)
@@ -161,3 +162,41 @@ def test_oanet_fused_vs_gemm_path(gpu, fused):
         sa, sb = a["scores"][i].cpu().numpy(), b["scores"][i].cpu().numpy()
         near = np.abs(sb - 0.5) < 1e-4
         assert np.array_equal((sa > 0.5)[~near], (sb > 0.5)[~near])
+
+
+@pytest.mark.parametrize("npts,train", [(2000, False), (517, False), (33, False), (65, False), (1200, True)])
+def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
+    """conv1 folded into the first PointCN (x recomputed from the block input, IN statistics from the
+    input's moments) vs conv1 materialised: same logits, R, t and masks; eval and train-mode BatchNorm,
+    ragged point counts.  Below ~100 points the weighted Procrustes of these random networks is
+    ill-conditioned (every path, the plain GEMM one included, is 1e-2..1 away from the fp64 oracle in R
+    at 33 points: tools/diag_fold.py), so there only block 0's logits are compared."""
+    import torch
+    from lib import _native as NV
+    from test_gpu_oanet import _oanet
+    from synth import synth_correspondences
+    xs, _, _ = synth_correspondences(5, npts, seed=23)
+    net = _oanet(128, 500, 9, gpu, train=train, which="full")
+    outs = []
+    L = NV.lib()
+    prev = L.mvr_set_oan_fused(5)
+    try:
+        for f in (5, 1):
+            L.mvr_set_oan_fused(f)
+            with torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    finally:
+        L.mvr_set_oan_fused(prev)
+    a, b = outs
+    np.testing.assert_allclose(a["logits"][0].cpu().numpy(), b["logits"][0].cpu().numpy(), atol=5e-4, rtol=1e-4)
+    if npts < 100:
+        return
+    for i in range(2):
+        np.testing.assert_allclose(a["logits"][i].cpu().numpy(), b["logits"][i].cpu().numpy(), atol=2e-3, rtol=1e-4)
+        np.testing.assert_allclose(a["rot_est"][i].cpu().numpy(), b["rot_est"][i].cpu().numpy(), atol=1e-4)
+        np.testing.assert_allclose(a["trans_est"][i].cpu().numpy(), b["trans_est"][i].cpu().numpy(), atol=1e-4)
+        sa, sb = a["scores"][i].cpu().numpy(), b["scores"][i].cpu().numpy()
+        near = np.abs(sb - 0.5) < 1e-4
+        assert np.array_equal((sa > 0.5)[~near], (sb > 0.5)[~near])
+    np.testing.assert_allclose(a["latent features"].cpu().numpy(), b["latent features"].cpu().numpy(),
+                               atol=2e-3, rtol=2e-3)
