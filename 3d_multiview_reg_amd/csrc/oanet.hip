@@ -104,96 +104,43 @@ __global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int C, 
   }
 }
 
-// The block's conv1 folded into its first PointCN (pconv XI): the InstanceNorm statistics of
-// x = W1 . in + b1 (oanet.py:144-145 conv1, then PointCN's IN, :27) follow exactly from the first and
-// second moments of the block input over the points, so x itself is never stored.
-// Per pair: mom[p] = {S1[c] = sum_n in[c][n] (c < 8), S2[c][c'] = sum_n in[c][n] in[c'][n] (c <= c', 36)}
-// in fp64 (fp32 products are exact in fp64).
-constexpr int MOM = 8 + 36;
-__global__ __launch_bounds__(256) void xin_moments_kernel(const float* __restrict__ in, int64_t ps, int64_t ld, int ci,
-                                                          int N, double* __restrict__ mom) {
-  __shared__ double red[4][MOM];
-  const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// The block's conv1 folded into its first PointCN (pconv XI): x = conv1(input) (oanet.py:144-145) is
+// never stored, so its InstanceNorm statistics (PointCN's first IN, oanet.py:27) are taken here from x
+// recomputed exactly as the point-conv kernel recomputes it (x = xb[k] + xw[k][0..7] . in[0..7][n], the
+// same fma order, hence the same fp32 values), as per-(pair, 128-point tile, channel) (sum, squared
+// deviations from the tile mean) partials — the GEMM epilogue's ST_ROW layout, finished by
+// in_finalize_kernel.  Reads only the <= 8 input rows.
+__global__ __launch_bounds__(128) void xin_stats_kernel(const float* __restrict__ in, int64_t ps, int64_t ld, int ci,
+                                                        int N, const float* __restrict__ xw,
+                                                        const float* __restrict__ xb, float2* __restrict__ st) {
+  __shared__ float tile[8][128];
+  const int k = threadIdx.x, t = blockIdx.x, p = blockIdx.y, T = gridDim.x;
+  const int n0 = 128 * t, nv = min(128, N - n0);
   const float* x = in + (int64_t)p * ps;
-  double s1[8], s2[36];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) s1[c] = 0.0;
-#pragma unroll
-  for (int c = 0; c < 36; ++c) s2[c] = 0.0;
-  for (int n = tid; n < N; n += 256) {
-    double v[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) v[c] = c < ci ? (double)x[(int64_t)c * ld + n] : 0.0;
-    int k = 0;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      s1[c] += v[c];
-#pragma unroll
-      for (int d = c; d < 8; ++d) s2[k++] += v[c] * v[d];
-    }
-  }
-  auto wsum = [&](double v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-  };
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const double v = wsum(s1[c]);
-    if (lane == 0) red[w][c] = v;
-  }
-#pragma unroll
-  for (int c = 0; c < 36; ++c) {
-    const double v = wsum(s2[c]);
-    if (lane == 0) red[w][8 + c] = v;
+  for (int e = k; e < 8 * 128; e += 128) {
+    const int c = e >> 7, n = e & 127;
+    tile[c][n] = (n < nv) ? x[(int64_t)min(c, ci - 1) * ld + n0 + n] : 0.f;
   }
   __syncthreads();
-  if (tid < MOM) mom[(int64_t)p * MOM + tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
-}
-
-// IN(eps)+BN fold of x = W1 . in + b1 per (pair, channel k) from the moments (same outputs as
-// in_finalize_kernel: sc / sh in eval mode, (mean, var) into mv in train mode).  W1 [C][8] zero-padded.
-__global__ void in_fold_moments_kernel(const double* __restrict__ mom, int N, const float* __restrict__ w1,
-                                       const float* __restrict__ b1, int C, float eps_in, mvr_bn_p bn, int train,
-                                       float* sc, float* sh, float2* mv) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  const int p = blockIdx.y;
-  if (k >= C) return;
-  const double* m = mom + (int64_t)p * MOM;
-  const double inv = 1.0 / (double)N;
-  double wk[8], mu[8];
+  float w[8];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    wk[c] = (double)w1[k * 8 + c];
-    mu[c] = m[c] * inv;
-  }
-  double mean = b1 ? (double)b1[k] : 0.0, var = 0.0;
-  int q = 0;
+  for (int c = 0; c < 8; ++c) w[c] = xw[k * 8 + c];
+  const float b = xb ? xb[k] : 0.f;
+  auto xval = [&](int n) {
+    float acc = b;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    mean += wk[c] * mu[c];
-#pragma unroll
-    for (int d = c; d < 8; ++d) {
-      const double cov = m[8 + q++] * inv - mu[c] * mu[d];
-      var += (c == d ? 1.0 : 2.0) * wk[c] * wk[d] * cov;
-    }
+    for (int c = 0; c < 8; ++c) acc = fmaf(w[c], tile[c][n], acc);
+    return acc;
+  };
+  float s = 0.f;
+  for (int n = 0; n < nv; ++n) s += xval(n);
+  const float mu = s / (float)nv;
+  float m2 = 0.f;
+  for (int n = 0; n < nv; ++n) {
+    const float d = xval(n) - mu;
+    m2 = fmaf(d, d, m2);
   }
-  var = fmax(var, 0.0);
-  if (train) {
-    mv[(int64_t)p * C + k] = make_float2((float)mean, (float)var);
-    return;
-  }
-  const float rin = (float)(1.0 / sqrt(var + (double)eps_in));
-  float g = 1.f, b = 0.f, rm = 0.f, rs = 1.f;
-  if (bn.gamma) {
-    g = bn.gamma[k];
-    b = bn.beta[k];
-    rm = bn.mean[k];
-    rs = 1.f / sqrtf(bn.var[k] + 1e-5f);
-  }
-  const float gs = g * rs;
-  sc[(int64_t)p * C + k] = rin * gs;
-  sh[(int64_t)p * C + k] = (float)((double)b - (mean * (double)rin + (double)rm) * (double)gs);
+  st[((int64_t)p * T + t) * 128 + k] = make_float2(s, m2);
 }
 
 // BatchNorm(points) of OAFilter.conv2 (oanet.py:72-76): per-cluster affine.
@@ -326,7 +273,6 @@ struct Plan {
   size_t uimg_bytes;
   size_t bytes;
   float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *sc2, *sh2, *scK, *shK, *fac, *W1, *W8;
-  double* mom;           // input moments of the folded conv1 [P][MOM]
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
 };
 
@@ -364,7 +310,6 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.fac = pl.fused ? nullptr : w.take<float>(nf);
   pl.W1 = w.take<float>((size_t)C * pl.Cinp);
   pl.W8 = w.take<float>((size_t)C * 8);
-  pl.mom = w.take<double>((size_t)P * MOM);
   pl.st11 = w.take<float2>((size_t)P * TS * 2 * C);
   pl.stA = w.take<float2>((size_t)P * TS * C);
   pl.stT = w.take<float2>((size_t)P * TN * C);
@@ -564,8 +509,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   Act xa{pl.XA, CN, Np, C, N, pl.stA, C, 0};
   Act x11top{pl.X11, 2 * CN, Np, C, N, pl.st11, 2 * C, 0};
   // conv1 folded into the first l1_1 PointCN when the point-conv kernel takes it: x = conv1(input) is
-  // recomputed by that PointCN's conv3 (B operand) and conv7 (residual) from the input's <= 8 rows,
-  // its InstanceNorm statistics come from the input's moments
+  // recomputed by that PointCN's conv3 (B operand) and conv7 (residual) from the input's <= 8 rows, and
+  // for its InstanceNorm statistics (xin_stats_kernel)
   GemmArgs f3{};
   f3.math = g_default_math; f3.M = C; f3.N = N; f3.K = C; f3.batch = P;
   f3.A = blk->l1_1[0].conv3.weight; f3.lda = C;
@@ -581,16 +526,10 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (fold1) {
     const int n8 = C * 8;
     hipLaunchKernelGGL(pad_cols_kernel, dim3((n8 + 255) / 256), dim3(256), 0, s, blk->conv1.weight, C, Cin, 8, pl.W8);
-    hipLaunchKernelGGL(xin_moments_kernel, dim3(P), dim3(256), 0, s, input, in_pstride, ld, Cin, N, pl.mom);
-    const mvr_bn_p& bn1 = blk->l1_1[0].bn1;
-    hipLaunchKernelGGL(in_fold_moments_kernel, dim3((C + 127) / 128, P), dim3(128), 0, s, pl.mom, N, pl.W8,
-                       blk->conv1.bias, C, 1e-5f, bn1, bn_train, pl.sc, pl.sh, pl.mv);
+    hipLaunchKernelGGL(xin_stats_kernel, dim3(TN, P), dim3(128), 0, s, input, in_pstride, ld, Cin, N, pl.W8,
+                       blk->conv1.bias, pl.stA);
     cx.chk_launch();
-    if (bn_train) {
-      hipLaunchKernelGGL(in_bn_train_kernel, dim3((C + 255) / 256), dim3(256), 0, s, pl.mv, P, C, 1e-5f, bn1, pl.sc,
-                         pl.sh, (int64_t)C);
-      cx.chk_launch();
-    }
+    cx.finalize_in(xa, 1e-5f, blk->l1_1[0].bn1);   // xa.st = pl.stA: the partials just written
     cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
     Act t{pl.T1, CN, Np, C, N, pl.stT, C, 0};
     cx.finalize_in(t, 1e-5f, blk->l1_1[0].bn5);

@@ -94,13 +94,21 @@ __device__ __forceinline__ float sum8(float v) {
 // 128-channel output x is never stored: XI = 1, the B operand rows are recomputed from the block input
 // (8 loads per point instead of 128 rows); XI = 2, the residual (RES) is recomputed from it.  Both use
 // the same fma order, so the two recomputations of x are bit-identical.
-template <int KS, int PRO, int RES, int STATS, int HEAD, int XI = 0>
-__global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
+// KW = 2 (KS = 16 only): 8 waves, the reduction split in two halves — wave w multiplies row block
+// w & 3 over input channels 128 (w >> 2) .. +127 (96 weight VGPRs, two waves per SIMD, where the 4-wave
+// KS = 16 form has one wave per SIMD and cannot overlap its MFMA chain with its own memory waits); the
+// upper half's partial sums reach the lower half's waves through LDS one step later, which then run the
+// epilogue for both (no residual / head there).
+template <int KS, int PRO, int RES, int STATS, int HEAD, int XI = 0, int KW = 1>
+__global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   constexpr int CIN = 16 * KS;   // input channels
-  constexpr int NT = KS / 4;     // 16-row k-steps each wave loads and splits per chunk
-  constexpr int RW = CIN / 4;    // input rows per wave
+  constexpr int NWV = 4 * KW;    // waves
+  constexpr int KSW = KS / KW;   // k-steps each wave multiplies
+  constexpr int NT = KS / NWV;   // 16-row k-steps each wave loads and splits per chunk
+  constexpr int RW = CIN / NWV;  // input rows per wave
   constexpr int NX = (XI & 1) ? 8 : 8 * NT;   // activation registers per chunk
   static_assert(!XI || KS == 8, "conv1 folding: 128-channel convs");
+  static_assert(KW == 1 || (KS == 16 && KW == 2 && !RES && !HEAD && !XI), "k-split: the 256 -> 128 convs");
   __shared__ __attribute__((aligned(16))) char xi[2][KS * FRB];      // chunk images (B fragments)
   __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
   __shared__ __attribute__((aligned(16))) float fold[2][2][CIN];   // (sc, sh) by pair parity
@@ -114,9 +122,13 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   __shared__ __attribute__((aligned(16))) float xwe[(XI & 2) ? 8 : 1][(XI & 2) ? PC : 4];
   __shared__ __attribute__((aligned(16))) float xbe[(XI & 2) ? PC : 4];
   __shared__ __attribute__((aligned(16))) float xib[(XI & 2) ? 4 : 1][(XI & 2) ? 256 : 4];   // per wave: input chunk
+  // KW = 2: the upper half's partial accumulators by chunk parity, [slot][row block][q][lane] float4 planes
+  __shared__ __attribute__((aligned(16))) float4 xch[KW == 2 ? 2 : 1][KW == 2 ? 4 : 1][KW == 2 ? 4 : 1][KW == 2 ? 64 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave (loads / splits input rows RW wv ..)
+  const int w = wv & 3;                                      // output row block
+  const int kh = wv >> 2;                                    // KW = 2: reduction half
   const int N = a.N, N4 = (N + 3) & ~3, nch = a.nch;
 
   // contiguous range of statistics groups -> chunk range [c0, c1) in (pair, chunk) order
@@ -128,12 +140,12 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   const int64_t c1 = (int64_t)p1 * nch + min(GRP * (int)(g1 - (int64_t)p1 * a.ngrp), nch);
   const int nloc = (int)(c1 - c0);
 
-  // weights -> split A fragments: row 32w + l32, k = 16q + 8h + 0..7
-  Frag wf[KS];
+  // weights -> split A fragments: row 32w + l32, k = 128 kh + 16q + 8h + 0..7
+  Frag wf[KSW];
   {
-    const float* wr = a.W + (int64_t)(32 * w + l32) * a.wld + 8 * h;
+    const float* wr = a.W + (int64_t)(32 * w + l32) * a.wld + 128 * kh * (KW - 1) + 8 * h;
 #pragma unroll
-    for (int q = 0; q < KS; ++q) {
+    for (int q = 0; q < KSW; ++q) {
       const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * q);
       const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * q + 4);
       const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
@@ -180,7 +192,7 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   const int xld4 = (int)a.xld * 4;
   auto issue_x = [&](const Cur& c, float (&r)[NX]) {
     const int n = min(c.kc * CH + l32, N - 1);
-    const float* base = a.X + (int64_t)c.p * a.xps + (int64_t)(RW * w) * a.xld;
+    const float* base = a.X + (int64_t)c.p * a.xps + (int64_t)(RW * wv) * a.xld;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
     if (XI & 1) {   // the block input's rows 0 .. xci-1 (clamped: weight columns past xci are zero)
@@ -220,7 +232,7 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
       for (int i = 0; i < 8; ++i) xr[i] = r[8 * t + i];
     }
     if (PRO) {
-      const float* f = &fold[c.p & 1][0][RW * w + 16 * t + 8 * h];
+      const float* f = &fold[c.p & 1][0][RW * wv + 16 * t + 8 * h];
       const float4 sa = *reinterpret_cast<const float4*>(f), sb = *reinterpret_cast<const float4*>(f + 4);
       const float4 ha = *reinterpret_cast<const float4*>(f + CIN), hb = *reinterpret_cast<const float4*>(f + CIN + 4);
       const float s1[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     } else {
       split8(v, f.h, f.m, f.l);
     }
-    char* dst = xi[slot] + (NT * w + t) * FRB + lane * 16;
+    char* dst = xi[slot] + (NT * wv + t) * FRB + lane * 16;
     *reinterpret_cast<bf16x8*>(dst) = f.h;
     *reinterpret_cast<bf16x8*>(dst + 1024) = f.m;
     *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
@@ -267,20 +279,20 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   int rn = 0;
   float ls[4], lss[4];
   // multiply chunk c (image slot) with hook(ks) after each k-step's MFMA group, then the epilogue
-  auto compute = [&](const Cur& c, int slot, auto&& hook) {
-    const int n0 = c.kc * CH;
+  // multiply chunk (image slot) with hook(ks) after each k-step's MFMA group
+  auto mfma = [&](int slot, auto&& hook) {
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const char* img = xi[slot] + lane * 16;
+    const char* img = xi[slot] + KSW * kh * (KW - 1) * FRB + lane * 16;
     Frag cur;
     cur.h = *reinterpret_cast<const bf16x8*>(img);
     cur.m = *reinterpret_cast<const bf16x8*>(img + 1024);
     cur.l = *reinterpret_cast<const bf16x8*>(img + 2048);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+    for (int ks = 0; ks < KSW; ++ks) {
       Frag nxt;
-      if (ks < KS - 1) {
+      if (ks < KSW - 1) {
         nxt.h = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB);
         nxt.m = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 1024);
         nxt.l = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 2048);
@@ -290,8 +302,13 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
       else acc = mfma6(wf[ks], cur, acc);
       hook(ks);
       PC_FENCE();
-      if (ks < KS - 1) cur = nxt;
+      if (ks < KSW - 1) cur = nxt;
     }
+    return acc;
+  };
+  // epilogue of chunk c (accumulator acc): bias (+ residual), stores, head, statistics
+  auto epilogue = [&](const Cur& c, const floatx16& acc) {
+    const int n0 = c.kc * CH;
     if (PCONV_ABL & 4) {
       asm volatile("" ::"v"(acc));
       return;
@@ -427,7 +444,7 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   //   when it starts one; one barrier.
   // NSET register sets (3; 2 for the residual-recomputing conv7, whose epilogue needs the registers): a
   // chunk's loads are issued NSET steps before its MFMAs
-  constexpr int NSET = (XI & 2) ? 2 : 3;
+  constexpr int NSET = ((XI & 2) || KW == 2) ? 2 : 3;
   float x0[NX], x1[NX], x2[NSET == 3 ? NX : 1];
   Cur cc = cstart, cs = cstart, ci = cstart, cf = cstart, cr = cstart;   // compute, split, issue, fold, residual
   stage_fold(cf.p);
@@ -473,15 +490,34 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     if (lane == 0 && np) atomicAdd(a.pos + c.p, np);
   };
   Cur ch = cstart;   // head cursor (one step behind compute)
+  Cur cp = cstart;     // KW = 2: chunk whose epilogue is pending (lower half), one step behind
+  floatx16 accp;       // ... and its lower-half accumulator
   auto step = [&](int j, auto& xs) {
     if (HEAD && j > 0) {
       head_finish(ch);
       adv(ch);
     }
-    compute(cc, j & 1, [&](int ks) {
+    floatx16 acc = mfma(j & 1, [&](int ks) {
       if ((ks & 1) && ks < 2 * NT) split_half(cs, xs, (j + 1) & 1, ks >> 1);
       if (ks == 2 * NT) issue_x(ci, xs);
     });
+    if constexpr (KW == 1) {
+      epilogue(cc, acc);
+    } else if (kh) {   // upper half: publish the partial sums (read by the lower half after the step barrier)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xch[j & 1][w][q][lane] = make_float4(acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]);
+    } else {
+      if (j > 0) {   // the previous chunk: its upper-half partials were published by the last step barrier
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 u = xch[(j - 1) & 1][w][q][lane];
+          accp[4 * q] += u.x; accp[4 * q + 1] += u.y; accp[4 * q + 2] += u.z; accp[4 * q + 3] += u.w;
+        }
+        epilogue(cp, accp);
+        adv(cp);
+      }
+      accp = acc;
+    }
     adv(cc);
     adv(cs);
     adv(ci);
@@ -509,6 +545,17 @@ __global__ __launch_bounds__(256, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
     if (j < nloc) step(j, x1);
   }
   if (HEAD) head_finish(ch);   // the last chunk (published by the last step's barrier)
+  if constexpr (KW == 2) {
+    if (!kh) {   // the last chunk's epilogue (its upper-half partials: published by the last step barrier)
+      const int jl = nloc - 1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 u = xch[jl & 1][w][q][lane];
+        accp[4 * q] += u.x; accp[4 * q + 1] += u.y; accp[4 * q + 2] += u.z; accp[4 * q + 3] += u.w;
+      }
+      epilogue(cp, accp);
+    }
+  }
 }
 
 }  // namespace
@@ -579,11 +626,19 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   MVR_PC(8, 0, 1, 0, 0)
   MVR_PC(8, 1, 1, 0, 1)    // the last PointCN conv of a block with the output head (oanet.py:174-175)
   MVR_PC(8, 1, 1, 0, 2)    // ... when the block's output activation is not returned (head only)
-  MVR_PC(16, 1, 0, 1, 0)   // PointCN(2C -> C) conv3 (IN/BN/ReLU prologue, statistics)
-  MVR_PC(16, 0, 0, 0, 0)   // PointCN(2C -> C) shortcut (raw input)
-  MVR_PC(16, 1, 0, 0, 0)
-  MVR_PC(16, 0, 0, 1, 0)
 #undef MVR_PC
+  // 256 -> 128 (PointCN(2C -> C) after diff_unpool, oanet.py:155): the k-split 8-wave form, one workgroup per CU
+#define MVR_PC16(P_, S_)                                                                                \
+  if (ks == 16 && pro == P_ && res == 0 && st == S_ && head == 0) {                                    \
+    hipLaunchKernelGGL((pconv_kernel<16, P_, 0, S_, 0, 0, 2>), dim3(grid), dim3(512), 0, s, a);         \
+    MVR_CHECK_LAUNCH();                                                                                 \
+    return MVR_OK;                                                                                      \
+  }
+  MVR_PC16(1, 1)   // conv3 (IN/BN/ReLU prologue, statistics)
+  MVR_PC16(0, 0)   // shortcut (raw input)
+  MVR_PC16(1, 0)
+  MVR_PC16(0, 1)
+#undef MVR_PC16
   return MVR_EINVAL;
 }
 
