@@ -105,42 +105,69 @@ __global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int C, 
 }
 
 // The block's conv1 folded into its first PointCN (pconv XI): x = conv1(input) (oanet.py:144-145) is
-// never stored, so its InstanceNorm statistics (PointCN's first IN, oanet.py:27) are taken here from x
-// recomputed exactly as the point-conv kernel recomputes it (x = xb[k] + xw[k][0..7] . in[0..7][n], the
-// same fma order, hence the same fp32 values), as per-(pair, 128-point tile, channel) (sum, squared
-// deviations from the tile mean) partials — the GEMM epilogue's ST_ROW layout, finished by
-// in_finalize_kernel.  Reads only the <= 8 input rows.
-__global__ __launch_bounds__(128) void xin_stats_kernel(const float* __restrict__ in, int64_t ps, int64_t ld, int ci,
-                                                        int N, const float* __restrict__ xw,
+// never stored, so its InstanceNorm statistics (PointCN's first IN, oanet.py:27) follow from the block
+// input: per 128-point tile, x_k = b_k + w_k . in is affine in the <= 8 input rows, so the tile's
+// (sum, squared deviations) of x_k are nv (b_k + w_k . mean) and w_k^T C w_k with the tile's input mean
+// and centred co-moment matrix C (fp32 tree sums over the tile, combined in fp64).  Written as the GEMM
+// epilogue's ST_ROW partials [P][tile][128], merged across tiles by in_finalize_kernel.  One wave per
+// (pair, tile).
+__global__ __launch_bounds__(256) void xin_stats_kernel(const float* __restrict__ in, int64_t ps, int64_t ld, int ci,
+                                                        int N, int T, const float* __restrict__ xw,
                                                         const float* __restrict__ xb, float2* __restrict__ st) {
-  __shared__ float tile[8][128];
-  const int k = threadIdx.x, t = blockIdx.x, p = blockIdx.y, T = gridDim.x;
+  __shared__ float mom[4][8 + 36];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, p = blockIdx.y;
+  const int t = 4 * blockIdx.x + wv;   // one wave per tile
+  if (t >= T) return;                  // (no block-wide synchronisation below)
   const int n0 = 128 * t, nv = min(128, N - n0);
-  const float* x = in + (int64_t)p * ps;
-  for (int e = k; e < 8 * 128; e += 128) {
-    const int c = e >> 7, n = e & 127;
-    tile[c][n] = (n < nv) ? x[(int64_t)min(c, ci - 1) * ld + n0 + n] : 0.f;
+  const float* x = in + (int64_t)p * ps + n0;
+  float v[2][8];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = lane + 64 * j;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[j][c] = (n < nv && c < ci) ? x[(int64_t)c * ld + n] : 0.f;
   }
-  __syncthreads();
-  float w[8];
+  auto wsum = [](float a) {
 #pragma unroll
-  for (int c = 0; c < 8; ++c) w[c] = xw[k * 8 + c];
-  const float b = xb ? xb[k] : 0.f;
-  auto xval = [&](int n) {
-    float acc = b;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) acc = fmaf(w[c], tile[c][n], acc);
-    return acc;
+    for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o, 64);
+    return a;
   };
-  float s = 0.f;
-  for (int n = 0; n < nv; ++n) s += xval(n);
-  const float mu = s / (float)nv;
-  float m2 = 0.f;
-  for (int n = 0; n < nv; ++n) {
-    const float d = xval(n) - mu;
-    m2 = fmaf(d, d, m2);
+  const float rn = 1.f / (float)nv;
+  float mu[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) mu[c] = wsum(v[0][c] + v[1][c]) * rn;
+  float* m = mom[wv];
+  int q = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int d = c; d < 8; ++d, ++q) {
+      float a = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (lane + 64 * j < nv) a = fmaf(v[j][c] - mu[c], v[j][d] - mu[d], a);
+      a = wsum(a);
+      if (lane == 0) m[8 + q] = a;
+    }
+  if (lane < 8) m[lane] = mu[lane];
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // the wave's own LDS writes (lgkmcnt(0)) before its reads below
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = lane + 64 * j;
+    float wk[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) wk[c] = xw[k * 8 + c];
+    double mean = xb ? (double)xb[k] : 0.0, m2 = 0.0;
+    int r = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      mean += (double)wk[c] * m[c];
+#pragma unroll
+      for (int d = c; d < 8; ++d, ++r) m2 += (c == d ? 1.0 : 2.0) * wk[c] * wk[d] * m[8 + r];
+    }
+    st[((int64_t)p * T + t) * 128 + k] = make_float2((float)(mean * nv), (float)fmax(m2, 0.0));
   }
-  st[((int64_t)p * T + t) * 128 + k] = make_float2(s, m2);
 }
 
 // BatchNorm(points) of OAFilter.conv2 (oanet.py:72-76): per-cluster affine.
@@ -526,8 +553,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (fold1) {
     const int n8 = C * 8;
     hipLaunchKernelGGL(pad_cols_kernel, dim3((n8 + 255) / 256), dim3(256), 0, s, blk->conv1.weight, C, Cin, 8, pl.W8);
-    hipLaunchKernelGGL(xin_stats_kernel, dim3(TN, P), dim3(128), 0, s, input, in_pstride, ld, Cin, N, pl.W8,
-                       blk->conv1.bias, pl.stA);
+    hipLaunchKernelGGL(xin_stats_kernel, dim3((TN + 3) / 4, P), dim3(256), 0, s, input, in_pstride, ld, Cin, N, TN,
+                       pl.W8, blk->conv1.bias, pl.stA);
     cx.chk_launch();
     cx.finalize_in(xa, 1e-5f, blk->l1_1[0].bn1);   // xa.st = pl.stA: the partials just written
     cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
