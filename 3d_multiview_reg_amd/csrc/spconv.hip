@@ -204,43 +204,36 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
 
 
 // ---------------------------------------------------------------------------------------------
-// Split-bf16 variant (the default): the same output-stationary gather-GEMM on
-// v_mfma_f32_32x32x16_bf16 with both operands as three bf16 terms (fp32-level accuracy, see
-// mfma_bf16.hpp) — 2.7x the fp32 MFMA rate.  32 input channels per step; the gathered input rows
-// are staged as fp32 [row][32] (144-byte rows: conflict-free 16-byte row reads) and split per
-// fragment; the weights come pre-split (mvr_spconv_wimage) as [k][32-channel block][plane][Cout]
-// rows of 32 bf16 padded to 80 bytes, staged by LDS-DMA.
+// Split-bf16 variant: the same output-stationary gather-GEMM on v_mfma_f32_32x32x16_bf16 with both
+// operands as three bf16 terms (fp32-level accuracy, see mfma_bf16.hpp) — 2.7x the fp32 MFMA rate.
+// 128 output rows per workgroup, one 32-row slab per wave over all TN output channels (NJ = TN / 32
+// accumulator tiles), so a wave's gathered rows are its own A operand: each lane gathers its row's 8
+// channels of each k-step straight into registers (three steps in flight), splits them itself — no LDS
+// for A, no duplicated gathers.  A step is 32 input channels of one active stencil offset.  The weights
+// come pre-split (mvr_spconv_wimage: [k][32-channel block][plane][Cout][32 + 8 pad] bf16, 80-byte rows)
+// and reach LDS through registers one step ahead (shared by the 4 waves).  All loads are compiler-tracked:
+// the gathers of step s + 3 stay in flight while step s + 1's weights are awaited.
 constexpr int SB_K = 32;     // input channels per step
-constexpr int SB_AST = 36;   // fp32 row stride of the gathered tile
 constexpr int SB_BST = 40;   // bf16 row stride of the weight image (80 B)
 constexpr int SB_CP = 128;   // output-channel padding of the weight image (largest TN)
+constexpr int SB_NS = 3;     // gathered steps in flight
 
-__device__ __forceinline__ void sp_glds16(const char* src, char* lds_base) {
-  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
-
-template <int TM, int TN, int WM, int WN>
-__global__ __launch_bounds__(256) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP) {
+template <int TN>
+__global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP) {
   using namespace bx;
-  constexpr int WTN = TN / WN;
-  constexpr int NJ = WTN / 32;
-  static_assert(TM / WM == 32, "wave tile rows must be 32");
-  constexpr int BPL = TN * SB_BST;          // bf16 elements of one plane of a B stage
-  constexpr int BG = 3 * BPL * 2 / 16;      // 16-byte granules of a B stage
-  __shared__ __attribute__((aligned(16))) float As[2][TM * SB_AST];
+  constexpr int NS = TN > 64 ? 2 : SB_NS;       // steps in flight (register sets: gathered rows + weights)
+  constexpr int TM = 128;                       // output rows per workgroup (4 waves x 32)
+  constexpr int NJ = TN / 32;                   // accumulator tiles per wave
+  constexpr int BPL = TN * SB_BST;              // bf16 elements of one plane of a weight stage
+  constexpr int BG = 3 * BPL * 2 / 16;          // 16-byte granules of a weight stage
+  constexpr int GPT = (BG + 255) / 256;         // ... per thread
   __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * BPL];
   __shared__ int32_t nb[TM][SP_KMAX + 1];
   __shared__ int kact[SP_KMAX];
   __shared__ int klist[SP_KMAX];
   __shared__ int nk;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
   const int64_t o0 = (int64_t)blockIdx.x * TM;
   const int c0 = blockIdx.y * TN;
@@ -270,38 +263,55 @@ __global__ __launch_bounds__(256) void spconv_bx_kernel(SpArgs a, const uint16_t
 
   const int nci = (a.Cin + SB_K - 1) / SB_K;
   const int steps = nk * nci;
-  constexpr int AV = TM * (SB_K / 4) / 256;   // float4 of the gathered tile per thread
-  float4 ra[AV];
+  const int row = 32 * w + l32;   // this lane's tile row
 
-  auto load_a = [&](int s) {
+  // gathered A of one step: k-step st, channels ci0 + 16 st + 8h + (0..7) of the lane's row, as two
+  // float4 each (clamped addresses; validity bits applied at the split)
+  struct ASet {
+    float4 v[4];
+    uint32_t m;
+    float4 bq[GPT];   // the step's weight stage granules (this thread's share)
+  };
+  auto load_a = [&](int s, ASet& A) {
+    if (s >= steps) s = steps - 1;   // clamped re-read past the end
     const int k = klist[s / nci];
     const int ci0 = (s % nci) * SB_K;
+    const int src = nb[row][k];
+    const float* base = a.in + (int64_t)(src >= 0 ? src : 0) * a.ldin;
+    uint32_t m = 0;
 #pragma unroll
-    for (int r = 0; r < AV; ++r) {
-      const int idx = tid + 256 * r;
-      const int row = idx >> 3, ci = ci0 + 4 * (idx & 7);
-      const int src = nb[row][k];
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (src >= 0 && ci < a.Cin) v = *reinterpret_cast<const float4*>(a.in + (int64_t)src * a.ldin + ci);
-      ra[r] = v;
+    for (int q = 0; q < 4; ++q) {
+      const int ci = ci0 + 16 * (q >> 1) + 8 * h + 4 * (q & 1);
+      m |= (src >= 0 && ci < a.Cin) ? (1u << q) : 0u;
+      A.v[q] = *reinterpret_cast<const float4*>(base + min(ci, a.Cin - 4));
     }
-  };
-  auto store_a = [&](int buf) {
+    A.m = m;
+    const int cb = s % nci;
+    const char* wb = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * 3 * CoutP + c0) * SB_BST * 2;
 #pragma unroll
-    for (int r = 0; r < AV; ++r) {
-      const int idx = tid + 256 * r;
-      *reinterpret_cast<float4*>(&As[buf][(idx >> 3) * SB_AST + 4 * (idx & 7)]) = ra[r];
-    }
-  };
-  // weight stage: granule g of [plane][TN rows][40] <- image row block (k, channel block) at column c0
-  auto dma_b = [&](int s, int buf) {
-    const int k = klist[s / nci], cb = s % nci;
-    const char* base = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * 3 * CoutP + c0) * SB_BST * 2;
-    char* dst = reinterpret_cast<char*>(Bs[buf]);
-    for (int g0 = wid * 64; g0 < BG; g0 += 256) {
-      const int g = g0 + lane;
+    for (int i = 0; i < GPT; ++i) {
+      const int g = min(tid + 256 * i, BG - 1);
       const int pl = g / (TN * 5), wi = g - pl * (TN * 5);
-      if (g < BG) sp_glds16(base + ((int64_t)pl * CoutP * SB_BST * 2) + wi * 16, dst + g0 * 16);
+      A.bq[i] = *reinterpret_cast<const float4*>(wb + (int64_t)pl * CoutP * SB_BST * 2 + wi * 16);
+    }
+  };
+  auto frag_a = [&](const ASet& A, int st) {
+    float v[8];
+    const float4 x0 = A.v[2 * st], x1 = A.v[2 * st + 1];
+    const bool k0 = (A.m >> (2 * st)) & 1, k1 = (A.m >> (2 * st + 1)) & 1;
+    v[0] = k0 ? x0.x : 0.f; v[1] = k0 ? x0.y : 0.f; v[2] = k0 ? x0.z : 0.f; v[3] = k0 ? x0.w : 0.f;
+    v[4] = k1 ? x1.x : 0.f; v[5] = k1 ? x1.y : 0.f; v[6] = k1 ? x1.z : 0.f; v[7] = k1 ? x1.w : 0.f;
+    Frag f;
+    split8(v, f.h, f.m, f.l);
+    return f;
+  };
+  // weight stage of a step: granule g of [plane][TN rows][80 B] <- image rows (k, channel block) at column c0
+  auto store_b = [&](const ASet& A, int buf) {
+    char* dst = reinterpret_cast<char*>(Bs[buf]);
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+      const int g = tid + 256 * i;
+      if (g < BG) *reinterpret_cast<float4*>(dst + g * 16) = A.bq[i];
     }
   };
 
@@ -312,46 +322,56 @@ __global__ __launch_bounds__(256) void spconv_bx_kernel(SpArgs a, const uint16_t
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
 
   if (steps > 0) {
-    load_a(0);
-    dma_b(0, 0);
-    store_a(0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int cur = 0;
-  for (int s = 0; s < steps; ++s) {
-    if (s + 1 < steps) {
-      load_a(s + 1);
-      dma_b(s + 1, cur ^ 1);
-    }
-    const float* A = As[cur];
-    const uint16_t* Bq = Bs[cur];
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const float* ap = A + (wm * 32 + l32) * SB_AST + 16 * st + 8 * h;
-      const float4 a0 = *reinterpret_cast<const float4*>(ap), a1 = *reinterpret_cast<const float4*>(ap + 4);
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      Frag fa;
-      split8(av, fa.h, fa.m, fa.l);
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const uint16_t* bp = Bq + (wn * WTN + 32 * j + l32) * SB_BST + 16 * st + 8 * h;
-        Frag fb;
-        fb.h = *reinterpret_cast<const bf16x8*>(bp);
-        fb.m = *reinterpret_cast<const bf16x8*>(bp + BPL);
-        fb.l = *reinterpret_cast<const bf16x8*>(bp + 2 * BPL);
-        acc[j] = mfma6(fa, fb, acc[j]);
-      }
-    }
-    if (s + 1 < steps) store_a(cur ^ 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // step s: the weights of step s + 1 (loaded NS steps ago) -> the other LDS stage, the split of step s's
+    // gathered rows, its set refilled with step s + NS, the MFMAs; one barrier
+    ASet A0, A1, A2;
+    load_a(0, A0);
+    load_a(1, A1);
+    if constexpr (NS == 3) load_a(2, A2);
+    store_b(A0, 0);
     __syncthreads();
-    cur ^= 1;
+    auto step = [&](int s, ASet& A, const ASet& An) {
+      const int cur = s & 1;
+      if (s + 1 < steps) store_b(An, cur ^ 1);
+      const Frag fa0 = frag_a(A, 0), fa1 = frag_a(A, 1);
+      load_a(s + NS, A);
+      const uint16_t* Bq = Bs[cur];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const Frag& fa = st ? fa1 : fa0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const uint16_t* bp = Bq + (32 * j + l32) * SB_BST + 16 * st + 8 * h;
+          Frag fb;
+          fb.h = *reinterpret_cast<const bf16x8*>(bp);
+          fb.m = *reinterpret_cast<const bf16x8*>(bp + BPL);
+          fb.l = *reinterpret_cast<const bf16x8*>(bp + 2 * BPL);
+          acc[j] = mfma6(fa, fb, acc[j]);
+        }
+      }
+      __syncthreads();
+    };
+    int s = 0;
+    if constexpr (NS == 3) {
+      for (; s + 2 < steps; s += 3) {
+        step(s, A0, A1);
+        step(s + 1, A1, A2);
+        step(s + 2, A2, A0);
+      }
+      if (s < steps) step(s, A0, A1);
+      if (s + 1 < steps) step(s + 1, A1, A2);
+    } else {
+      for (; s + 1 < steps; s += 2) {
+        step(s, A0, A1);
+        step(s + 1, A1, A0);
+      }
+      if (s < steps) step(s, A0, A1);
+    }
   }
 
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int c = c0 + wn * WTN + j * 32 + l32;
+    const int c = c0 + j * 32 + l32;
     if (c >= a.Cout) continue;
     float bsc = 1.f, bsh = 0.f;
     if (a.bn.gamma) {
@@ -361,7 +381,7 @@ __global__ __launch_bounds__(256) void spconv_bx_kernel(SpArgs a, const uint16_t
     const float bias = a.bias ? a.bias[c] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t ot = o0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t ot = o0 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (ot >= a.Mout) continue;
       const int64_t o = a.perm ? a.perm[ot] : ot;
       float v = acc[j][r] + bias;
@@ -440,16 +460,13 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
   if (wimg) {   // split-bf16 path (weights pre-split by mvr_spconv_wimage)
     const uint16_t* wi = reinterpret_cast<const uint16_t*>(wimg);
     const int64_t CoutP = sp_coutp(Cout);
-    if (Cout <= 32) {
-      hipLaunchKernelGGL((spconv_bx_kernel<128, 32, 4, 1>), dim3((unsigned)((Mout + 127) / 128), (Cout + 31) / 32),
-                         dim3(256), 0, s, a, wi, CoutP);
-    } else if (Cout <= 64) {
-      hipLaunchKernelGGL((spconv_bx_kernel<64, 64, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 63) / 64),
-                         dim3(256), 0, s, a, wi, CoutP);
-    } else {
-      hipLaunchKernelGGL((spconv_bx_kernel<64, 128, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 127) / 128),
-                         dim3(256), 0, s, a, wi, CoutP);
-    }
+    const unsigned gx = (unsigned)((Mout + 127) / 128);
+    if (Cout <= 32)
+      hipLaunchKernelGGL(spconv_bx_kernel<32>, dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
+    else if (Cout <= 64)
+      hipLaunchKernelGGL(spconv_bx_kernel<64>, dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
+    else
+      hipLaunchKernelGGL(spconv_bx_kernel<128>, dim3(gx, (Cout + 127) / 128), dim3(256), 0, s, a, wi, CoutP);
     MVR_CHECK_LAUNCH();
     return MVR_OK;
   }

@@ -19,10 +19,10 @@ from lib import _native as N
 from lib.sparse import SparseTensor
 
 
-# split-bf16 sparse convs (csrc/spconv.hip spconv_bx_kernel): correct but slower than the exact-fp32
-# MFMA kernel here (the convs are gather-latency bound and the bf16 staging lowers occupancy), so off
-# unless MVR_SPCONV_BF16=1
-SPLIT_BF16 = os.environ.get("MVR_SPCONV_BF16", "0") == "1"
+# split-bf16 sparse convs (csrc/spconv.hip spconv_bx_kernel, weights pre-split once per weight version):
+# the default (scene step: 9.0 -> 8.3 ms of sparse convs); MVR_SPCONV_BF16=0 selects the exact-fp32 MFMA
+# kernel (A/B timing)
+SPLIT_BF16 = os.environ.get("MVR_SPCONV_BF16", "1") == "1"
 # conv1 (7^3) as brick-tiled dense windows on split-bf16 MFMA (csrc/sparse.hip spconv_c1_brick_kernel);
 # MVR_CONV1_BRICKS=0 selects the per-row gather kernel (A/B timing)
 CONV1_BRICKS = os.environ.get("MVR_CONV1_BRICKS", "1") == "1"

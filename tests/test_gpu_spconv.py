@@ -1,0 +1,81 @@
+"""Sparse convolution kernels (csrc/spconv.hip, the MinkowskiConvolution forward of
+lib/descriptor/fcgf.py:118-227) against an fp64 gather-GEMM restatement: both arithmetic paths (exact
+fp32 MFMA, split-bf16 with pre-split weight images), every channel shape FCGF uses, partial stencils
+(-1 neighbours), the row order of mvr_kernel_map_order, the identity map (1x1x1 conv) and the fused
+bias / BatchNorm / residual / ReLU epilogue."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(gpu, Cin, Cout, K, Mout, Min, split, perm=False, epi=True, seed=0):
+    import torch
+    from lib import _native as NV
+    rng = np.random.default_rng(seed)
+    feat = rng.standard_normal((Min, Cin)).astype(np.float32)
+    if K == 1:
+        nbr = None
+        Mout = Min
+    else:
+        nbr = rng.integers(0, Min, size=(Mout, K)).astype(np.int32)
+        nbr[rng.random((Mout, K)) < 0.5] = -1   # partial stencils
+        nbr[rng.random(Mout) < 0.05] = -1       # a few rows with no neighbour at all
+    W = (rng.standard_normal((K, Cin, Cout)) / np.sqrt(K * Cin)).astype(np.float32)
+    bias = rng.standard_normal(Cout).astype(np.float32) if epi else None
+    g, b = rng.random(Cout).astype(np.float32) + 0.5, rng.standard_normal(Cout).astype(np.float32)
+    m, v = rng.standard_normal(Cout).astype(np.float32), rng.random(Cout).astype(np.float32) + 0.5
+    res = rng.standard_normal((Mout, Cout)).astype(np.float32) if epi else None
+    # fp64 reference
+    ref = np.zeros((Mout, Cout))
+    nb = np.arange(Min)[:, None] if nbr is None else nbr
+    for k in range(nb.shape[1]):
+        ok = nb[:, k] >= 0
+        ref[ok] += feat[nb[ok, k]].astype(np.float64) @ W[k].astype(np.float64)
+    if epi:
+        ref = ((ref + bias - m) / np.sqrt(v.astype(np.float64) + 1e-5) * g + b) + res
+        ref = np.maximum(ref, 0)
+    d = lambda x: torch.from_numpy(x).to(gpu) if x is not None else None
+    F, Wt, nbr_t, bias_t, res_t = d(feat), d(W), d(nbr), d(bias), d(res)
+    gb, bb, mb, vb = d(g), d(b), d(m), d(v)
+    L = NV.lib()
+    perm_t = None
+    if perm and nbr is not None:
+        ws = torch.empty(L.mvr_kernel_map_order_bytes(Mout), dtype=torch.uint8, device=gpu)
+        perm_t = torch.empty(Mout, dtype=torch.int32, device=gpu)
+        NV.check(L.mvr_kernel_map_order(NV.ptr(nbr_t), Mout, K, NV.ptr(perm_t), NV.ptr(ws), ws.numel(), NV.stream()),
+                 "order")
+    wimg = None
+    if split:
+        nbytes = L.mvr_spconv_wimage_bytes(K, Cin, Cout)
+        wimg = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
+        NV.check(L.mvr_spconv_wimage(NV.ptr(Wt), K, Cin, Cout, NV.ptr(wimg), nbytes, NV.stream()), "wimage")
+    out = torch.full((Mout, Cout), float("nan"), device=gpu)
+    bn = NV.BnP(gb.data_ptr(), bb.data_ptr(), mb.data_ptr(), vb.data_ptr()) if epi else NV.BnP(None, None, None, None)
+    rc = L.mvr_spconv(NV.ptr(F), Cin, Cin, NV.ptr(nbr_t), NV.ptr(perm_t), K, Mout, NV.ptr(Wt), Cout, NV.ptr(bias_t), bn,
+                      1e-5, NV.ptr(res_t), Cout, int(epi), NV.ptr(out), Cout, NV.ptr(wimg), NV.stream())
+    assert rc == 0
+    got = out.cpu().numpy()
+    scale = np.abs(ref).max() + 1e-30
+    err = np.abs(got - ref).max() / scale
+    assert np.isfinite(got).all() and err < 2e-6, (Cin, Cout, K, split, err)
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("cin,cout", [(32, 32), (32, 64), (64, 64), (64, 128), (128, 128), (128, 256), (256, 256),
+                                      (256, 128), (256, 64), (128, 64), (96, 64)])
+def test_spconv_3x3x3(gpu, cin, cout, split):
+    _run(gpu, cin, cout, 27, 1000, 900, split, perm=True, seed=cin + cout)
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("cin,cout,mout", [(96, 64, 777), (64, 32, 300), (32, 32, 129)])
+def test_spconv_identity_map(gpu, cin, cout, mout, split):
+    """1x1x1 convs (conv1_tr, final: fcgf.py:209-227) run with the identity map (nbr NULL)"""
+    _run(gpu, cin, cout, 1, mout, mout, split, epi=cout != 32, seed=cin)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_spconv_ragged_rows_no_perm(gpu, split):
+    """a row count far from the tile size, natural row order, no epilogue, 8 offsets (transposed-conv size)"""
+    _run(gpu, 64, 64, 8, 130, 2000, split, perm=False, epi=False, seed=9)
