@@ -388,16 +388,28 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     }
     __syncthreads();
     if (!flag[0]) return;   // uniform
+    // merge the splits in split order (whichever arrived last: the result does not depend on arrival order)
+    const floatx16 own[4] = {O[0], O[1], O[2], O[3]};
+    const float mown = m, lown = l;
     for (int o = 0; o < a.nks; ++o) {
-      if (o == ks) continue;
       const float* th = a.part + (slot * a.nks + o) * PSLAB + tid;
-      const float m2 = th[64 * ATHREADS], l2 = th[65 * ATHREADS];
+      const float m2 = o == ks ? mown : th[64 * ATHREADS], l2 = o == ks ? lown : th[65 * ATHREADS];
+      if (o == 0) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) O[cb][r] = o == ks ? own[cb][r] : th[(16 * cb + r) * ATHREADS];
+        m = m2;
+        l = l2;
+        continue;
+      }
       const float mn = fmaxf(m, m2);
       const float f1 = __builtin_amdgcn_exp2f(m - mn), f2 = __builtin_amdgcn_exp2f(m2 - mn);
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) O[cb][r] = O[cb][r] * f1 + th[(16 * cb + r) * ATHREADS] * f2;
+        for (int r = 0; r < 16; ++r)
+          O[cb][r] = O[cb][r] * f1 + (o == ks ? own[cb][r] : th[(16 * cb + r) * ATHREADS]) * f2;
       l = l * f1 + l2 * f2;
       m = mn;
     }
