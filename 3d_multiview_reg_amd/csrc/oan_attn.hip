@@ -57,6 +57,19 @@ constexpr float A_NEG = -3.0e38f;
 static_assert(64 * ATL * 4 <= 2 * STAGE_B, "epilogue half tile must fit the stage ring");
 
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// one MFMA, then a share of the VALU and LDS writes placed in the same scheduling region, six times
+#define ATTN_INTERLEAVE6()                          \
+  do {                                              \
+    _Pragma("unroll") for (int u_ = 0; u_ < 6; ++u_) { \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); \
+      __builtin_amdgcn_sched_group_barrier(0x002, 5, 0); \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0); \
+    }                                               \
+  } while (0)
+#ifndef ATTN_ABL
+#define ATTN_ABL 0   // pool timing ablations (wrong results; tools/build_variant.sh): 1 no softmax, 2 no
+                     // tile split, 4 no P.V MFMAs, 8 no S MFMAs
+#endif
 
 // Byte offset of the 4 keys 4q .. 4q+3 (q = 0..7) of row `row` in a [row][32 keys] bf16 image
 // whose 16-byte chunk (s, h) holds the 8 keys of k-step s, lane half h in the C-register k order
@@ -258,6 +271,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   // 4 (tid & 7) .. +3
   const int sq = tid & 7;
   auto store_tile = [&](int kb, int st) {
+    if (ATTN_ABL & 2) return;
     char* K = smem + st * STAGE_B;
     char* V = K + IMG;
     const char* xt = xraw + (kb & 1) * XT;
@@ -282,6 +296,42 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       *reinterpret_cast<u32x2*>(K + PLANE + ko) = M;
       *reinterpret_cast<u32x2*>(K + 2 * PLANE + ko) = L;
     }
+  };
+
+  // the same split in four parts placed between the MFMAs of a stage (the 8 waves run their stages in
+  // step, so a split phase of its own leaves the matrix pipes idle): load_x reads a thread's two raw
+  // key groups, store_v / store_k write one of them to the V / K image of stage st
+  auto load_x = [&](int kb, int i) {
+    const int c = (tid >> 3) + 64 * i;
+    float4 x = *reinterpret_cast<const float4*>(xraw + (kb & 1) * XT + c * 128 + 16 * sq);
+    if (kb * AKB + 4 * sq >= N) x = make_float4(0.f, 0.f, 0.f, 0.f);
+    return x;
+  };
+  auto store_v = [&](int st, int i, float4 x) {
+    if (ATTN_ABL & 2) return;
+    asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));   // keep the split at its placement
+    char* V = smem + st * STAGE_B + IMG;
+    const int c = (tid >> 3) + 64 * i;
+    u32x2 H, M, L;
+    split4(x, H, M, L);
+    const int vo = kord_off(c, sq);
+    *reinterpret_cast<u32x2*>(V + vo) = H;
+    *reinterpret_cast<u32x2*>(V + PLANE + vo) = M;
+    *reinterpret_cast<u32x2*>(V + 2 * PLANE + vo) = L;
+  };
+  auto store_k = [&](int st, int i, float4 x, const float2& f) {
+    if (ATTN_ABL & 2) return;
+    asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
+    char* K = smem + st * STAGE_B;
+    const int c = (tid >> 3) + 64 * i;
+    const float4 xn = make_float4(fmaxf(fmaf(x.x, f.x, f.y), 0.f), fmaxf(fmaf(x.y, f.x, f.y), 0.f),
+                                  fmaxf(fmaf(x.z, f.x, f.y), 0.f), fmaxf(fmaf(x.w, f.x, f.y), 0.f));
+    u32x2 H, M, L;
+    split4(xn, H, M, L);
+    const int ko = c * 64 + 8 * sq;
+    *reinterpret_cast<u32x2*>(K + ko) = H;
+    *reinterpret_cast<u32x2*>(K + PLANE + ko) = M;
+    *reinterpret_cast<u32x2*>(K + 2 * PLANE + ko) = L;
   };
 
   floatx16 O[4];
@@ -317,7 +367,9 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   __syncthreads();
   for (int kb = kb0; kb < kb1; ++kb) {
     const int st = kb & 1;
-    store_tile(kb + 1, st ^ 1);   // zeros past the end
+    // tile kb + 1 (zeros past the end) -> stage st ^ 1, split between the MFMAs below
+    const float4 x0 = load_x(kb + 1, 0);
+    float4 x1;
     dma_tile(kb + 2);             // into the buffer of tile kb, split one iteration ago
     const char* K = smem + st * STAGE_B;
     const char* V = K + IMG;
@@ -331,7 +383,14 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       Frag nxt;
       if (ks < 7) nxt = read_k(K, ks + 1);
       SCHED_FENCE();
-      S = mfma6(cur, q[ks], S);
+      if (ks == 2) store_v(st ^ 1, 0, x0);
+      if (ks == 5) store_k(st ^ 1, 0, x0, ssh[tid >> 3]);
+      if (ks == 6) x1 = load_x(kb + 1, 1);
+      if (ATTN_ABL & 8)
+        asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l));
+      else
+        S = mfma6(cur, q[ks], S);
+      if (ks == 2 || ks == 5) ATTN_INTERLEAVE6();
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
@@ -344,7 +403,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       for (int r = 0; r < 16; ++r)
         if (kb * AKB + (r & 3) + 8 * (r >> 2) + 4 * h >= N) v[r] = -__builtin_inff();
     }
-    online_softmax(v, m, l, O);
+    if (!(ATTN_ABL & 1)) online_softmax(v, m, l, O);
     Frag pf[2];
     split8(v, pf[0].h, pf[0].m, pf[0].l);
     split8(v + 8, pf[1].h, pf[1].m, pf[1].l);
@@ -355,7 +414,13 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       Frag nxt;
       if (i < 7) nxt = kord_frag(V, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2, h);
       SCHED_FENCE();
-      O[cb] = mfma6(vf, pf[s], O[cb]);
+      if (i == 2) store_v(st ^ 1, 1, x1);
+      if (i == 5) store_k(st ^ 1, 1, x1, ssh[(tid >> 3) + 64]);
+      if (ATTN_ABL & 4)
+        asm volatile("" ::"v"(vf.h), "v"(vf.m), "v"(vf.l), "v"(pf[s].h), "v"(pf[s].m), "v"(pf[s].l));
+      else
+        O[cb] = mfma6(vf, pf[s], O[cb]);
+      if (i == 2 || i == 5) ATTN_INTERLEAVE6();
       SCHED_FENCE();
       if (i < 7) vf = nxt;
     }
@@ -563,7 +628,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
+  for (int kb = 0; kb < ((ATTN_ABL & 16) ? 0 : nkb); ++kb) {
     const int st = kb & 1;
     if (kb + 1 < nkb) issue(kb + 1, st ^ 1);
     const char* Wi = smem + st * USTAGE;
@@ -585,7 +650,10 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
       Frag nxt;
       if (ks < 7) nxt = read_w(Wi, ks + 1);
       SCHED_FENCE();
-      S = mfma6(cur, q[ks], S);
+      if (ATTN_ABL & 8)
+        asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l));
+      else
+        S = mfma6(cur, q[ks], S);
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
@@ -593,7 +661,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = S[r];
-    online_softmax(v, m, l, O);
+    if (!(ATTN_ABL & 1)) online_softmax(v, m, l, O);
     Frag pf[2];
     split8(v, pf[0].h, pf[0].m, pf[0].l);
     split8(v + 8, pf[1].h, pf[1].m, pf[1].l);

@@ -216,12 +216,20 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
 constexpr int SB_K = 32;     // input channels per step
 constexpr int SB_BST = 40;   // bf16 row stride of the weight image (80 B)
 constexpr int SB_CP = 128;   // output-channel padding of the weight image (largest TN)
-constexpr int SB_NS = 3;     // gathered steps in flight
+#ifndef SPBX_NS32   // gathered steps in flight per output-channel tile width (register budget)
+#define SPBX_NS32 3
+#endif
+#ifndef SPBX_NS64
+#define SPBX_NS64 3
+#endif
+#ifndef SPBX_NS128
+#define SPBX_NS128 3
+#endif
 
-template <int TN>
+template <int TN, int NS>
 __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP) {
   using namespace bx;
-  constexpr int NS = TN > 64 ? 2 : SB_NS;       // steps in flight (register sets: gathered rows + weights)
+  // NS: steps in flight (register sets: gathered rows + weights)
   constexpr int TM = 128;                       // output rows per workgroup (4 waves x 32)
   constexpr int NJ = TN / 32;                   // accumulator tiles per wave
   constexpr int BPL = TN * SB_BST;              // bf16 elements of one plane of a weight stage
@@ -324,11 +332,10 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   if (steps > 0) {
     // step s: the weights of step s + 1 (loaded NS steps ago) -> the other LDS stage, the split of step s's
     // gathered rows, its set refilled with step s + NS, the MFMAs; one barrier
-    ASet A0, A1, A2;
-    load_a(0, A0);
-    load_a(1, A1);
-    if constexpr (NS == 3) load_a(2, A2);
-    store_b(A0, 0);
+    ASet A[NS];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) load_a(u, A[u]);
+    store_b(A[0], 0);
     __syncthreads();
     auto step = [&](int s, ASet& A, const ASet& An) {
       const int cur = s & 1;
@@ -352,21 +359,13 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
       __syncthreads();
     };
     int s = 0;
-    if constexpr (NS == 3) {
-      for (; s + 2 < steps; s += 3) {
-        step(s, A0, A1);
-        step(s + 1, A1, A2);
-        step(s + 2, A2, A0);
-      }
-      if (s < steps) step(s, A0, A1);
-      if (s + 1 < steps) step(s + 1, A1, A2);
-    } else {
-      for (; s + 1 < steps; s += 2) {
-        step(s, A0, A1);
-        step(s + 1, A1, A0);
-      }
-      if (s < steps) step(s, A0, A1);
+    for (; s + NS - 1 < steps; s += NS) {
+#pragma unroll
+      for (int u = 0; u < NS; ++u) step(s + u, A[u], A[(u + 1) % NS]);
     }
+#pragma unroll
+    for (int u = 0; u < NS - 1; ++u)
+      if (s + u < steps) step(s + u, A[u], A[(u + 1) % NS]);
   }
 
 #pragma unroll
@@ -462,11 +461,12 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
     const int64_t CoutP = sp_coutp(Cout);
     const unsigned gx = (unsigned)((Mout + 127) / 128);
     if (Cout <= 32)
-      hipLaunchKernelGGL(spconv_bx_kernel<32>, dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
+      hipLaunchKernelGGL((spconv_bx_kernel<32, SPBX_NS32>), dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
     else if (Cout <= 64)
-      hipLaunchKernelGGL(spconv_bx_kernel<64>, dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
+      hipLaunchKernelGGL((spconv_bx_kernel<64, SPBX_NS64>), dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
     else
-      hipLaunchKernelGGL(spconv_bx_kernel<128>, dim3(gx, (Cout + 127) / 128), dim3(256), 0, s, a, wi, CoutP);
+      hipLaunchKernelGGL((spconv_bx_kernel<128, SPBX_NS128>), dim3(gx, (Cout + 127) / 128), dim3(256), 0, s, a, wi,
+                         CoutP);
     MVR_CHECK_LAUNCH();
     return MVR_OK;
   }

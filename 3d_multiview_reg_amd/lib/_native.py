@@ -198,8 +198,10 @@ _ws_cache = {}
 
 
 def workspace(nbytes, device):
-    """Reusable per-device scratch buffer (grown on demand)."""
-    key = (device.index if device.index is not None else torch.cuda.current_device())
+    """Reusable scratch buffer per (device, current stream), grown on demand: launches on one stream are
+    ordered, so consecutive calls can share it; a second stream gets its own."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)

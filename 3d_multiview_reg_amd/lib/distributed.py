@@ -50,6 +50,7 @@ def pack_records(first_pair, R, t, scores, flag=None):
     rec[:, 10:13] = t.reshape(n, 3).float()
     rec[:, 13] = (scores > 0.5).float().mean(dim=1)
     if flag is not None:
+        flag = getattr(flag, "tensor", flag)   # lib.filtering.oanet.DeviceFlag: stays on the device
         rec[:, 14] = torch.as_tensor(flag, device=R.device).float().reshape(-1).expand(n)
     return rec
 

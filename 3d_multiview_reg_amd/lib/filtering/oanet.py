@@ -34,6 +34,34 @@ class _Slots(nn.Module):
         return len(self._modules)
 
 
+class DeviceFlag:
+    """The SVD-fallback flag of the forward pass (oanet.py:265 returns a Python bool) as a bool-like view of a
+    device tensor: building it enqueues nothing that waits, reading it (bool(), ==, repr) synchronises once.
+    A forward pass therefore never blocks the host, so consecutive passes on different streams can overlap."""
+    __slots__ = ("_t", "_v")
+
+    def __init__(self, t):
+        self._t, self._v = t, None
+
+    @property
+    def tensor(self):
+        return self._t
+
+    def __bool__(self):
+        if self._v is None:
+            self._v = bool(self._t.item())
+        return self._v
+
+    def __eq__(self, other):
+        return bool(self) == other
+
+    def __hash__(self):
+        return hash(bool(self))
+
+    def __repr__(self):
+        return repr(bool(self))
+
+
 def _bn(c):
     return nn.BatchNorm2d(c)
 
@@ -196,5 +224,5 @@ class OANet(nn.Module):
             for k, v in zip(("logits", "scores", "rot_est", "trans_est"), (logits, scores, R, t)):
                 out[k].append(v)
         out["latent features"] = latent[:, :, :Npts].unsqueeze(3)
-        out["gradient_flag"] = bool(status.any().item())
+        out["gradient_flag"] = DeviceFlag(status.any())
         return out

@@ -49,6 +49,10 @@ class PairwiseReg(nn.Module):
     def compute_descriptors(self, input_dict):
         if self.precomputed_desc:
             return input_dict, None, None
+        return self.match_samples(input_dict, *self.sample_descriptors(input_dict))
+
+    def sample_descriptors(self, input_dict):
+        """First stage of compute_descriptors: FCGF + Sampler -> (xyz_b [B,n,3], f_b [B,n,32], F0, F1)."""
         dev = next(self.descriptor_module.parameters()).device
         xyz_down = input_dict["pcd0"].to(dev).float().contiguous()
         pts_list = input_dict["pts_list"]
@@ -61,6 +65,11 @@ class PairwiseReg(nn.Module):
         else:
             F1 = torch.empty(F0.shape[0], 0, device=dev)
         xyz_b, f_b = self.sampler(xyz_down, F0, pts_list)                      # [B, n, 3], [B, n, 32]
+        return xyz_b, f_b, F0, F1
+
+    def match_samples(self, input_dict, xyz_b, f_b, F0, F1):
+        """Second stage of compute_descriptors: feature NN over the pair list -> filtering input."""
+        dev = xyz_b.device
         B, n = xyz_b.shape[0], xyz_b.shape[1]
         if self.connectivity_info is not None:
             pairs = torch.as_tensor(self.connectivity_info, dtype=torch.int64, device=dev).reshape(-1, 2)

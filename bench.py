@@ -42,7 +42,7 @@ PEAK_BF16_TFLOPS = 16 * PEAK_FP32_TFLOPS   # dense bf16 MFMA (fp32 MFMA is 1/16 
 PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
 GEMM_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter")
-MFMA_PEAKS = {"feat_nn": PEAK_SPLIT_TFLOPS, "spconv": PEAK_FP32_TFLOPS}
+MFMA_PEAKS = {"feat_nn": PEAK_SPLIT_TFLOPS, "spconv": PEAK_SPLIT_TFLOPS}   # split-bf16 sparse convs (spconv_bx_kernel)
 
 
 def log(*a):
@@ -127,18 +127,50 @@ class SceneWorkload:
         self.pairs = n_frag * (n_frag - 1) // 2
         self.vox_counts = None
 
-    def step(self):
+    def describe(self):
+        """voxelise -> FCGF -> Sampler (first stage of compute_descriptors)"""
         from lib.sparse import voxelize
         coords, sel, counts, xyz_down = voxelize(self.raw, self.voxel, self.dev)   # prepare_data on the GPU
         self.vox_counts = counts
         data = {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
                 "pts_list": torch.tensor(counts)}
         np.random.seed(self.rng_seed)
-        fin, _, _ = self.model.compute_descriptors(data)
+        return data, self.model.sample_descriptors(data)
+
+    def finish(self, data, samples):
+        """feature NN over all pairs -> OANet -> Procrustes -> per-pair records (R, t, inlier fraction)"""
+        fin, _, _ = self.model.match_samples(data, *samples)
         out = self.model.filter_correspondences(fin)
         R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
         conf = (s > 0.5).float().mean(dim=1, keepdim=True)
         return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)
+
+    def step(self):
+        return self.finish(*self.describe())
+
+    def step_pipelined(self, world):
+        """Two-stage software pipeline over consecutive scenes on two HIP streams: the matching + filtering
+        of scene k-1 (stream B, enqueued first) runs while scene k is voxelised and described (stream A,
+        whose host-side steps — the voxel counts, the numpy sample draw — then overlap B's device work).
+        Returns the gathered records of scene k-1 (None on the first call)."""
+        if not hasattr(self, "streams"):
+            self.streams = (torch.cuda.Stream(self.dev), torch.cuda.Stream(self.dev))
+            self.pending = None
+        sA, sB = self.streams
+        rec = None
+        if self.pending is not None:
+            data, samples, ev = self.pending
+            with torch.cuda.stream(sB):
+                sB.wait_event(ev)
+                for x in samples[:2]:
+                    x.record_stream(sB)
+                rec = records_allgather(self.finish(data, samples), world)
+        with torch.cuda.stream(sA):
+            data, samples = self.describe()
+            ev = torch.cuda.Event()
+            ev.record(sA)
+        self.pending = (data, samples, ev)
+        return rec
 
     def config(self):
         return {"workload": "one synthetic 3DMatch-scale scene per GPU (configs[2]): %d fragments x ~%d voxels "
@@ -202,6 +234,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events in the timed region (A/B timing)")
+    ap.add_argument("--no-pipeline", action="store_true", help="scene workload: run the stages of a step back to "
+                    "back on one stream (default: two-stage pipeline over consecutive scenes, SceneWorkload.step_pipelined)")
     ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
                     "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -228,9 +262,16 @@ def main():
     else:
         wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
 
+    pipelined = args.workload == "scene" and not args.no_pipeline
+
+    def run_step():
+        if pipelined:
+            return wl.step_pipelined(world)
+        return records_allgather(wl.step(), world)
+
     with torch.no_grad():
-        for _ in range(args.warmup):
-            records_allgather(wl.step(), world)
+        for _ in range(max(args.warmup, 1 if pipelined else 0)):   # the pipeline is filled before timing
+            run_step()
         # one untimed step with events on every launch: the per-class breakdown and the dominant class;
         # the timed region then records events only around the dominant class's launches (events on
         # every launch cost ~1 ms per step).  --prof-seq (PMC attribution of exactly the timed steps'
@@ -240,7 +281,7 @@ def main():
         _native.prof_mask(None)
         if not args.prof_seq:
             _native.prof_set(1)
-            records_allgather(wl.step(), world)
+            run_step()
             torch.cuda.synchronize()
             prof_all = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
             _native.prof_set(0)
@@ -251,7 +292,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            rec = records_allgather(wl.step(), world)
+            rec = run_step()
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
@@ -320,7 +361,10 @@ def main():
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32(bf16x3)", "data": "synthetic",
-            "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world),
+            "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
+                           schedule=("2-stage stream pipeline over consecutive scenes: FCGF of scene k beside "
+                                     "matching+OANet of scene k-1; every timed step runs both stages in full"
+                                     if pipelined else "stages back to back on one stream")),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
         print(json.dumps(line), flush=True)
