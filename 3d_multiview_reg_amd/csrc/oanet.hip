@@ -264,6 +264,52 @@ int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B 
 
 namespace {
 
+// Debugging aid (mvr_debug_stage_hash): a position-weighted 64-bit sum of the bit patterns of each stage's
+// activation (valid columns only), accumulated into consecutive slots of a caller buffer — comparing runs
+// names the first stage whose output differs.
+static unsigned long long* g_dbg = nullptr;
+static int g_dbg_cap = 0, g_dbg_n = 0;
+
+__global__ void dbg_hash_kernel(const float* __restrict__ p, int rows, int L, int64_t ps, int64_t ld, int64_t total,
+                                unsigned long long* out) {
+  unsigned long long acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = i % L, r = (i / L) % rows, b = i / ((int64_t)L * rows);
+    acc += (unsigned long long)__float_as_uint(p[b * ps + r * ld + n]) * (unsigned long long)(2 * i + 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
+}
+
+static void dbg_hash(const float* p, int P, int rows, int L, int64_t ps, int64_t ld, hipStream_t s) {
+  if (!g_dbg || g_dbg_n >= g_dbg_cap) return;
+  hipLaunchKernelGGL(dbg_hash_kernel, dim3(1024), dim3(256), 0, s, p, rows, L, ps, ld, (int64_t)P * rows * L,
+                     g_dbg + g_dbg_n++);
+}
+
+// and a copy of one chosen stage's statistics partials (mvr_debug_stage_dump)
+static void* g_dump = nullptr;
+static size_t g_dump_bytes = 0;
+static int g_dump_stage = -1;
+static void dbg_dump(const void* p, size_t bytes, hipStream_t s) {
+  if (g_dump && g_dbg && g_dbg_n - 1 == g_dump_stage)
+    (void)hipMemcpyAsync(g_dump, p, bytes < g_dump_bytes ? bytes : g_dump_bytes, hipMemcpyDeviceToDevice, s);
+}
+
+extern "C" int mvr_debug_stage_dump(int stage, void* dst, size_t bytes) {
+  g_dump = dst;
+  g_dump_bytes = bytes;
+  g_dump_stage = stage;
+  return MVR_OK;
+}
+
+extern "C" int mvr_debug_stage_hash(unsigned long long* buf, int cap) {
+  g_dbg = buf;
+  g_dbg_cap = buf ? cap : 0;
+  g_dbg_n = 0;
+  return MVR_OK;
+}
+
 struct Act {
   float* p;      // base
   int64_t ps;    // pair stride
@@ -436,12 +482,24 @@ struct Ctx {
     y.csplit = 1 << 30;
     const mvr_conv_p* hd = head;   // the head goes with conv7 only
     head = nullptr;
+    dbg_hash(pl.sc, pl.P, 1, x.C, x.C, 0, s);
+    dbg_hash(pl.sh, pl.P, 1, x.C, x.C, 0, s);
     if (sc) conv(pc.shortcut, x, false, y, nullptr, ST_NONE);
     conv(pc.conv3, x, true, t, nullptr, ST_ROW);
+    const int TNn = (pl.N + 127) / 128;
+    dbg_hash(reinterpret_cast<const float*>(pl.stT), pl.P, 1, TNn * y.C * 2, (int64_t)TNn * y.C * 2, 0, s);
     finalize_in(t, 1e-5f, pc.bn5);
+    dbg_hash(pl.sc, pl.P, 1, y.C, y.C, 0, s);
+    dbg_hash(pl.sh, pl.P, 1, y.C, y.C, 0, s);
     head = hd;
     conv(pc.conv7, t, true, y, sc ? &y : &x, hd ? ST_NONE : ST_ROW, nullptr, hd && head_only);
     head = nullptr;
+    if (!hd) {
+      dbg_hash(y.p, pl.P, y.C, pl.N, y.ps, y.ld, s);
+      // rows [st_off, st_off + C) of each tile's partials (the rest of st_ld may belong to another producer)
+      dbg_hash(reinterpret_cast<const float*>(y.st + y.st_off), pl.P * TNn, 1, 2 * y.C, y.st_ld * 2, 0, s);
+      dbg_dump(y.st, (size_t)pl.P * TNn * y.st_ld * sizeof(float2), s);
+    }
   }
 
   void oafilter(const mvr_oafilter_p& f, const Act& xd) {
@@ -556,10 +614,16 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     hipLaunchKernelGGL(xin_stats_kernel, dim3((TN + 3) / 4, P), dim3(256), 0, s, input, in_pstride, ld, Cin, N, TN,
                        pl.W8, blk->conv1.bias, pl.stA);
     cx.chk_launch();
+    dbg_hash(reinterpret_cast<const float*>(pl.stA), P, 1, TN * C * 2, (int64_t)TN * C * 2, 0, s);
     cx.finalize_in(xa, 1e-5f, blk->l1_1[0].bn1);   // xa.st = pl.stA: the partials just written
+    dbg_hash(pl.sc, P, 1, C, C, 0, s);
+    dbg_hash(pl.sh, P, 1, C, C, 0, s);
     cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
     Act t{pl.T1, CN, Np, C, N, pl.stT, C, 0};
+    dbg_hash(reinterpret_cast<const float*>(pl.stT), P, 1, TN * C * 2, (int64_t)TN * C * 2, 0, s);
     cx.finalize_in(t, 1e-5f, blk->l1_1[0].bn5);
+    dbg_hash(pl.sc, P, 1, C, C, 0, s);
+    dbg_hash(pl.sh, P, 1, C, C, 0, s);
     Act& y = (H == 1) ? x11top : xa;
     GemmArgs f7{};
     f7.math = g_default_math; f7.M = C; f7.N = N; f7.K = C; f7.batch = P;
@@ -573,11 +637,18 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     f7.xin = 2; f7.xci = Cin; f7.xw = pl.W8; f7.xb = blk->conv1.bias; f7.xld = ld;
     f7.prof_kind = PK_CONV_PTS;
     cx.chk(launch_gemm(f7, s));   // conv7 of l1_1[0] + x (recomputed)
+    dbg_hash(pl.T1, P, C, N, CN, Np, s);
+    dbg_hash(y.p, P, C, N, y.ps, y.ld, s);
   } else {
     cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW, w1);
   }
   // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C))
-  for (int i = fold1 ? 1 : 0; i < H; ++i) cx.pointcn(blk->l1_1[i], xa, (i == H - 1) ? x11top : xa);
+  for (int i = fold1 ? 1 : 0; i < H; ++i) {
+    Act& yo = (i == H - 1) ? x11top : xa;
+    cx.pointcn(blk->l1_1[i], xa, yo);
+    dbg_hash(pl.T1, P, C, N, CN, Np, s);
+    dbg_hash(yo.p, P, C, N, yo.ps, yo.ld, s);
+  }
 
   // diff_pool (oanet.py:96-110): E = exp(embed - tile max) over points, x_down = x . softmax(E)^T
   cx.finalize_in(x11top, 1e-3f, blk->down_bn);
@@ -601,8 +672,12 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.prof_kind = PK_POOL;
     cx.chk(launch_gemm(g, s));
   }
+  dbg_hash(pl.XD, P, C, Kc, (int64_t)C * Kp, Kp, s);
   // l2: OAFilter x H (in place on XD)
-  for (int i = 0; i < H; ++i) cx.oafilter(blk->l2[i], xd);
+  for (int i = 0; i < H; ++i) {
+    cx.oafilter(blk->l2[i], xd);
+    dbg_hash(pl.XD, P, C, Kc, (int64_t)C * Kp, Kp, s);
+  }
 
   // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C): softmax over clusters
   cx.finalize_in(x11top, 1e-3f, blk->up_bn);
@@ -626,6 +701,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.prof_kind = PK_UNPOOL;
     cx.chk(launch_gemm(g, s));
   }
+  dbg_hash(pl.X11 + CN, P, C, N, 2 * CN, Np, s);
   // l1_2: PointCN(2C -> C, shortcut) + (H-1) PointCN(C)
   Act x11{pl.X11, 2 * CN, Np, 2 * C, N, pl.st11, 2 * C, 0};
   x11.tw0 = x11top.tw0;   // rows [0, C): the last l1_1 PointCN; rows [C, 2C): diff_unpool (128)
@@ -647,7 +723,10 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
       cx.h_logits = logits; cx.h_scores = scores; cx.h_pos = guard_pos;
     }
     cx.pointcn(blk->l1_2[i], i == 0 ? x11 : out, out);
+    dbg_hash(pl.T1, P, C, N, CN, Np, s);
+    if (latent || i < H - 1) dbg_hash(out.p, P, C, N, out.ps, out.ld, s);
   }
+  dbg_hash(logits, P, 1, N, N, N, s);
   if (!fuse_head) {
     hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, out.ps, out.ld, C, N,
                        blk->output.weight, blk->output.bias, logits, scores, guard_pos);

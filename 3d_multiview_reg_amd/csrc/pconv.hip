@@ -32,6 +32,9 @@
 
 namespace mvr {
 
+#ifndef PCONV_POISON
+#define PCONV_POISON 0
+#endif
 #ifndef PCONV_ABL
 #define PCONV_ABL 0   // timing ablations (wrong results; tools/build_variant.sh): 1 no MFMA, 2 no split,
                       // 4 no epilogue, 8 no activation loads
@@ -64,17 +67,6 @@ struct PcArgs {
   int xci; const float* xw; const float* xb;    // XI: x(k, n) = xb[k] + xw[k][:xci] . in(:, n) (xw [128][8])
   int64_t rld;                                  // XI & 2: row stride of the block input R
 };
-
-// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_base + 16 l.
-// Not tracked by the compiler: completion is awaited with an explicit s_waitcnt vmcnt.
-__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
-  const uint32_t lds = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_base;
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
 
 #define PC_FENCE() __builtin_amdgcn_sched_barrier(0)
 
@@ -113,7 +105,6 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
   __shared__ __attribute__((aligned(16))) float fold[2][2][CIN];   // (sc, sh) by pair parity
   __shared__ float sbias[PC];
-  __shared__ __attribute__((aligned(16))) float skl[STATS ? 4 : 1][STATS ? 32 : 4];   // row shifts [wave][erow][q]
   __shared__ float shw[HEAD ? PC : 1];
   __shared__ __attribute__((aligned(16))) float hpart[HEAD ? 2 : 1][4][CH];   // HEAD: per-wave partial logits by step parity
   __shared__ __attribute__((aligned(16))) float xws[XI ? PC : 1][8];   // XI: conv1 weights, bias
@@ -126,6 +117,19 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   __shared__ __attribute__((aligned(16))) float4 xch[KW == 2 ? 2 : 1][KW == 2 ? 4 : 1][KW == 2 ? 4 : 1][KW == 2 ? 64 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+#if PCONV_POISON   // debugging: NaN in every LDS array before use (finds reads of data never written)
+  {
+    auto poison = [&](void* p, size_t bytes) {
+      float* f = reinterpret_cast<float*>(p);
+      for (size_t i = tid; i < bytes / 4; i += blockDim.x) f[i] = __builtin_nanf("");
+    };
+    poison(xi, sizeof(xi)); poison(ys, sizeof(ys)); poison(fold, sizeof(fold)); poison(sbias, sizeof(sbias));
+    poison(shw, sizeof(shw)); poison(hpart, sizeof(hpart)); poison(xws, sizeof(xws));
+    poison(xbs, sizeof(xbs)); poison(xwe, sizeof(xwe)); poison(xbe, sizeof(xbe)); poison(xib, sizeof(xib));
+    poison(xch, sizeof(xch));
+    __syncthreads();
+  }
+#endif
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave (loads / splits input rows RW wv ..)
   const int w = wv & 3;                                      // output row block
   const int kh = wv >> 2;                                    // KW = 2: reduction half
@@ -257,20 +261,25 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
   };
 
-  // residual of chunk c, rows 32w .. 32w+31 x 32 columns, by LDS-DMA into the wave's scratch as
-  // [row][32] (lane: row 8i + lane/8, columns 4 (lane & 7)); columns clamped into the padded row
+  // residual of chunk c, loaded one step ahead into registers: this lane's rows 32w + erow + 8q (q = 0..3)
+  // x columns ec0 .. ec0 + 3 of the chunk, exactly the values its epilogue owns (no LDS trip); XI & 2: the
+  // lane's 16 bytes of the block input's 8 rows x 32 columns (row lane / 8, columns 4 (lane & 7)), which
+  // the epilogue publishes to the wave's xib for the recomputation.  Columns clamped into the padded row.
+  // (These were LDS-DMAs once: an LDS-DMA does not complete in order with loads into registers, so the
+  // vmcnt counts that were meant to cover it did not — run-to-run differences under load.)
   float* yb = ys[w];
-  auto dma_r = [&](const Cur& c) {
+  float4 rres[(RES && !(XI & 2)) ? 4 : 1];
+  float4 rxi;
+  auto load_r = [&](const Cur& c) {
     if (!RES) return;
-    if (XI & 2) {   // the block input's 8 rows x 32 columns (1 KB): lane -> row lane / 8, columns 4 (lane & 7)
-      const int n = min(c.kc * CH + 4 * (lane & 7), N4 - 4);
-      glds16(a.R + (int64_t)c.p * a.rps + (int64_t)min(lane >> 3, a.xci - 1) * a.rld + n, xib[w]);
+    const int n = min(c.kc * CH + ec0, N4 - 4);
+    if (XI & 2) {
+      rxi = *reinterpret_cast<const float4*>(a.R + (int64_t)c.p * a.rps + (int64_t)min(lane >> 3, a.xci - 1) * a.rld + n);
       return;
     }
-    const int n = min(c.kc * CH + 4 * (lane & 7), N4 - 4);
-    const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + (lane >> 3)) * a.yld + n;
+    const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + erow) * a.yld + n;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(src + (int64_t)(8 * i) * a.yld, yb + 256 * i);
+    for (int q = 0; q < 4; ++q) rres[(RES && !(XI & 2)) ? q : 0] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.yld);
   };
 
   // running statistics of the current 128-point group, per lane (its 4 rows x 4 columns of each chunk):
@@ -315,14 +324,11 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
     // value (q, e) of this lane: row erow + 8q of the wave's 32, column n0 + ec0 + e
     float4 ev[4];
-    if (RES && !(XI & 2)) {   // the residual DMA (issued one step ago; NX younger activation loads since)
-      static_assert(!RES || NX == 16, "residual wait count");
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    if (RES && !(XI & 2)) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ev[q] = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // residual read before the transpose overwrites it
+      for (int q = 0; q < 4; ++q) ev[q] = rres[(RES && !(XI & 2)) ? q : 0];
     } else {
-      if (XI & 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the block input's chunk (xib)
+      if (XI & 2) *reinterpret_cast<float4*>(xib[w] + 32 * (lane >> 3) + 4 * (lane & 7)) = rxi;   // read below by this wave
 #pragma unroll
       for (int q = 0; q < 4; ++q) ev[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -390,20 +396,16 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
           if (nv < 1) ev[q].x = 0.f;
         }
       }
-      float4* skp = reinterpret_cast<float4*>(&skl[w][4 * erow]);   // (kept in LDS: registers are full)
+      // row shift of the running sums: the row's bias (a constant, so no state crosses chunks — a shift kept
+      // in LDS from the group's first chunk gave run-to-run differences; y - bias is the conv (+ residual)
+      // term, O(its spread), so SS - S^2 / n keeps fp32 accuracy)
       float sK[4];
-      if (c.kc % GRP == 0) {   // the group's first chunk: row shifts
-        const float rc = __builtin_amdgcn_rcpf((float)cnt);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          sK[q] = sum8(ev[q].x + ev[q].y + ev[q].z + ev[q].w) * rc;
-          ls[q] = lss[q] = 0.f;
-        }
-        *skp = make_float4(sK[0], sK[1], sK[2], sK[3]);   // the 8 lanes of a row write the same values
+      for (int q = 0; q < 4; ++q) sK[q] = sbias[32 * w + erow + 8 * q];
+      if (c.kc % GRP == 0) {   // the group's first chunk
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ls[q] = lss[q] = 0.f;
         rn = 0;
-      } else {
-        const float4 k4 = *skp;
-        sK[0] = k4.x; sK[1] = k4.y; sK[2] = k4.z; sK[3] = k4.w;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -434,7 +436,6 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
         }
       }
     }
-    if (RES) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // scratch reads done before the next DMA
   };
 
   // Software pipeline (chunk j of this workgroup's range; register set (j % 3)):
@@ -442,9 +443,9 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   //   slot (j + 1) & 1) and the load of chunk j + 4 into the freed registers interleaved between
   //   the MFMA groups; epilogue of chunk j; residual DMA of chunk j + 1; fold of chunk j + 2's pair
   //   when it starts one; one barrier.
-  // NSET register sets (3; 2 for the residual-recomputing conv7, whose epilogue needs the registers): a
-  // chunk's loads are issued NSET steps before its MFMAs
-  constexpr int NSET = ((XI & 2) || KW == 2) ? 2 : 3;
+  // NSET register sets (3; 2 where the residual's registers or the k-split take the room): a chunk's loads
+  // are issued NSET steps before its MFMAs
+  constexpr int NSET = (RES || KW == 2) ? 2 : 3;
   float x0[NX], x1[NX], x2[NSET == 3 ? NX : 1];
   Cur cc = cstart, cs = cstart, ci = cstart, cf = cstart, cr = cstart;   // compute, split, issue, fold, residual
   stage_fold(cf.p);
@@ -464,7 +465,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   adv(cs);
   issue_x(ci, x0);
   adv(ci);
-  dma_r(cr);
+  load_r(cr);
   adv(cr);
   {
     const Cur prev = cf;
@@ -521,7 +522,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     adv(cc);
     adv(cs);
     adv(ci);
-    dma_r(cr);
+    load_r(cr);
     adv(cr);
     const Cur prev = cf;
     adv(cf);
@@ -564,7 +565,15 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
 // N > CH: with one chunk per pair the fold of chunk j + 3's pair (staged at the end of step j) could
 // land in the slot another wave still reads while splitting chunk j + 1 (pairs j + 1 and j + 3 then
 // differ by 2, same parity); with >= 2 chunks per pair consecutive staged pairs always alternate.
+#ifndef PCONV_OFF
+#define PCONV_OFF 0   // diagnosis builds: route classes of convs to gemm_kernel (1 plain 128-channel, 8 the 256 ->
+                      // 128 k-split, 16 head epilogue)
+#endif
+
 bool pconv_covers(const GemmArgs& g) {
+  if ((PCONV_OFF & 16) && g.head_w) return false;
+  if ((PCONV_OFF & 8) && g.K == 2 * PC) return false;
+  if ((PCONV_OFF & 1) && !g.xin && !g.head_w && g.K == PC) return false;
   if (g.xin) {   // folded conv1: only the two shapes the OANet schedule uses
     const bool ok = g_pconv && g.math == MATH_BF16X3 && g.M == PC && g.K == PC && !g.bkc && g.sAb == 0 &&
                     g.pro == PRO_B_K && g.stats_mode == ST_ROW && !g.head_w && !g.no_store && g.bias_mode != BIAS_N &&

@@ -60,6 +60,8 @@ _SIGS = {
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),
     "mvr_set_pool_split": (c_int, [c_int]),
+    "mvr_debug_stage_hash": (c_int, [c_vp, c_int]),
+    "mvr_debug_stage_dump": (c_int, [c_int, c_vp, c_size]),
     "mvr_pointcn_fused": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_vp, c_int, c_int, c_int, c_vp, c_i64, c_int, c_vp]),
     "mvr_oan_diff_pool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
@@ -206,4 +208,9 @@ def workspace(nbytes, device):
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
         _ws_cache[key] = buf
+    if _WS_POISON:   # debugging: 0x7f bytes (3.4e38) in every handed-out workspace (finds reads before writes)
+        buf[:int(nbytes)].fill_(0x7F)
     return buf
+
+
+_WS_POISON = os.environ.get("MVR_WS_POISON") == "1"

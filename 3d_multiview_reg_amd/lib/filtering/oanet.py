@@ -210,6 +210,9 @@ class OANet(nn.Module):
             R = torch.empty(P, 3, 3, device=dev)
             t = torch.empty(P, 3, 1, device=dev)
             res = torch.empty(P, Npts, device=dev)
+            if N._WS_POISON:   # debugging: NaN in every output buffer before the block writes it
+                for x in (logits, scores, R, t, res, latent):
+                    x.fill_(3.0e38)
             last = bi == len(blocks) - 1
             rc = L.mvr_oan_block_forward(
                 ctypes.byref(params), N.ptr(inp), rows * ld, ld, N.ptr(xs), Npts * Cxs, Cxs, P, Npts, int(self.training),

@@ -127,6 +127,12 @@ int mvr_set_pool_split(int on);
  * row pointers with pair stride row_pstride (the next block's input rows 6,7).
  * guard_pos: int32 [P] scratch (zeroed here).  status: int32 [P] (may be NULL).
  * bn_train: BatchNorm layers normalise with batch statistics (module.train()). */
+/* Debugging: while buf is non-NULL, every mvr_oan_block_forward launch sequence adds a position-weighted
+ * 64-bit hash of each stage's activation to the next of cap device slots (zeroed by the caller);
+ * NULL disables.  Not for concurrent use from two streams. */
+int mvr_debug_stage_hash(unsigned long long* buf, int cap);
+/* Debugging: copy the statistics partials hashed as stage `stage` into dst (bytes); NULL disables. */
+int mvr_debug_stage_dump(int stage, void* dst, size_t bytes);
 int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride, int64_t ld,
                           const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N, int bn_train,
                           float* logits,
