@@ -128,31 +128,31 @@ class SceneWorkload:
         self.vox_counts = None
 
     def describe(self):
-        """voxelise -> FCGF -> Sampler (first stage of compute_descriptors)"""
+        """voxelise -> FCGF -> Sampler -> feature NN over all pairs (compute_descriptors)"""
         from lib.sparse import voxelize
         coords, sel, counts, xyz_down = voxelize(self.raw, self.voxel, self.dev)   # prepare_data on the GPU
         self.vox_counts = counts
         data = {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
                 "pts_list": torch.tensor(counts)}
         np.random.seed(self.rng_seed)
-        return data, self.model.sample_descriptors(data)
+        fin, _, _ = self.model.compute_descriptors(data)
+        return fin
 
-    def finish(self, data, samples):
-        """feature NN over all pairs -> OANet -> Procrustes -> per-pair records (R, t, inlier fraction)"""
-        fin, _, _ = self.model.match_samples(data, *samples)
+    def finish(self, fin):
+        """OANet -> Procrustes -> per-pair records (R, t, inlier fraction)"""
         out = self.model.filter_correspondences(fin)
         R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
         conf = (s > 0.5).float().mean(dim=1, keepdim=True)
         return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)
 
     def step(self):
-        return self.finish(*self.describe())
+        return self.finish(self.describe())
 
     def step_pipelined(self, world):
-        """Two-stage software pipeline over consecutive scenes on two HIP streams: the matching + filtering
-        of scene k-1 (stream B, enqueued first) runs while scene k is voxelised and described (stream A,
-        whose host-side steps — the voxel counts, the numpy sample draw — then overlap B's device work).
-        Returns the gathered records of scene k-1 (None on the first call)."""
+        """Two-stage software pipeline over consecutive scenes on two HIP streams: the filtering (OANet +
+        Procrustes) of scene k-1 (stream B, enqueued first) runs while scene k is voxelised, described and
+        matched (stream A, whose host-side steps — the voxel counts, the numpy sample draw — then overlap B's
+        device work).  Returns the gathered records of scene k-1 (None on the first call)."""
         if not hasattr(self, "streams"):
             # B (matching + OANet, the longer stage) at high priority: its kernels take the CUs first and the
             # FCGF stage fills what they leave free
@@ -161,17 +161,16 @@ class SceneWorkload:
         sA, sB = self.streams
         rec = None
         if self.pending is not None:
-            data, samples, ev = self.pending
+            fin, ev = self.pending
             with torch.cuda.stream(sB):
                 sB.wait_event(ev)
-                for x in samples[:2]:
-                    x.record_stream(sB)
-                rec = records_allgather(self.finish(data, samples), world)
+                fin["xs"].record_stream(sB)
+                rec = records_allgather(self.finish(fin), world)
         with torch.cuda.stream(sA):
-            data, samples = self.describe()
+            fin = self.describe()
             ev = torch.cuda.Event()
             ev.record(sA)
-        self.pending = (data, samples, ev)
+        self.pending = (fin, ev)
         return rec
 
     def config(self):
@@ -373,8 +372,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32(bf16x3)", "data": "synthetic",
             "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
-                           schedule=("2-stage stream pipeline over consecutive scenes: FCGF of scene k beside "
-                                     "matching+OANet of scene k-1; every timed step runs both stages in full"
+                           schedule=("2-stage stream pipeline over consecutive scenes: FCGF + feature NN of scene k "
+                                     "beside OANet + Procrustes of scene k-1; every timed step runs both stages in full"
                                      if pipelined else "stages back to back on one stream")),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:

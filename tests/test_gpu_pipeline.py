@@ -1,5 +1,5 @@
-"""The bench's two-stage stream pipeline (bench.py SceneWorkload.step_pipelined: feature NN + OANet of
-scene k-1 on one HIP stream while scene k is voxelised and described by FCGF on another) returns the same
+"""The bench's two-stage stream pipeline (bench.py SceneWorkload.step_pipelined: OANet + Procrustes of
+scene k-1 on one HIP stream while scene k is voxelised, described by FCGF and matched on another) returns the same
 per-pair records as the stages run back to back on one stream — bit for bit, every kernel on the path is
 run-to-run deterministic — and no forward pass blocks the host (the SVD-fallback flag stays on the device
 until read)."""

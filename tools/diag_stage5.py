@@ -19,15 +19,15 @@ def main():
 
     def run(tag, stream=None):
         with torch.no_grad():
-            data, smp = wl.describe()
+            fin = wl.describe()
             torch.cuda.synchronize()
             buf = torch.zeros(256, dtype=torch.int64, device=dev)
             L.mvr_debug_stage_hash(NV.ptr(buf), 256)
             if stream is None:
-                wl.finish(data, smp)
+                wl.finish(fin)
             else:
                 with torch.cuda.stream(stream):
-                    wl.finish(data, smp)
+                    wl.finish(fin)
             torch.cuda.synchronize()
             L.mvr_debug_stage_hash(None, 0)
         res.setdefault(tag, []).append(buf.tolist())
