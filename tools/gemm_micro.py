@@ -20,6 +20,7 @@ CASES = {
     "embed_rowsmx": (K, N, C, 2, 0, 1, 2, 0),
     "pool": (C, K, N, 3, 1, 0, 1, 0),
     "unpool": (C, N, K, 3, 0, 0, 1, 0),
+    "oaf_conv2": (C, K, K, 1, 1, 2, 1, 1),    # OAFilter conv2 (oanet.hip oafilter): W2 shared, bias per n, residual
 }
 
 
@@ -33,6 +34,9 @@ def run(name, iters, math, pconv=1):
     sAb = 0 if A.dim() == 2 else M * Kk
     Nl = (Nn + 31) // 32 * 32   # 128-byte rows, as the OANet activations (csrc/oanet.hip plan)
     Bt = torch.randn(P, Nn, Kk, device=d) if bkc else torch.randn(P, Kk, Nl, device=d)
+    sBb = (Nn * Kk if bkc else Kk * Nl)
+    if name.startswith("oaf"):   # the weight operand is shared by all pairs
+        Bt, sBb = torch.randn(Nn, Kk, device=d) * 0.05, 0
     Cout = torch.empty(P, M, Nl, device=d)
     R = torch.randn(P, M, Nl, device=d) if res else None
     bvec = torch.randn(M if bias == 1 else Nn, device=d) if bias else None
@@ -52,7 +56,7 @@ def run(name, iters, math, pconv=1):
     L.mvr_set_pconv(pconv)
 
     def go():
-        rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Nn * Kk if bkc else Kk * Nl, Kk if bkc else Nl, bkc,
+        rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), sBb, Kk if bkc else Nl, bkc,
                             NV.ptr(Cout), M * Nl, Nl, NV.ptr(R), M * Nl, NV.ptr(bvec), bias, NV.ptr(sc),
                             NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, math, NV.stream())
         assert rc == 0
