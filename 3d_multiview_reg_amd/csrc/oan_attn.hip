@@ -686,6 +686,215 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
            a.stats ? a.stats + ((int64_t)p * ntile + 2 * nb) * a.st_ld + a.st_off : nullptr, a.st_ld);
 }
 
+// ---------------------------------------------------------------------------------------------
+// diff_unpool, 4-wave form: 128 queries per 256-thread workgroup, two workgroups per CU.  The 8-wave
+// kernel above owns a CU alone, so its per-workgroup prologue (x_up columns in) and epilogue (output
+// and statistics out) leave the matrix pipes idle; here the two co-resident workgroups drift out of
+// phase and cover each other's prologue, epilogue and LDS-DMA waits.  LDS (76.8 KB + 2.5 KB): the W
+// image double-buffered (26112 B each, unpadded) and one x_down image (24 KB): W(kb+1) lands during
+// stage kb, x_down(kb+1) during the S MFMAs of stage kb+1.  Requires clusters <= 512.
+// ---------------------------------------------------------------------------------------------
+constexpr int U4T = 256;                 // threads
+constexpr int U4Q = 128;                 // queries per workgroup
+constexpr int WIMG4 = 3 * WPLANE;        // 26112 B: W image block as it lands in LDS
+constexpr int U4XD = 2 * WIMG4;          // x_down image offset
+constexpr int U4L = 2 * WIMG4 + IMG;     // 76800 B
+constexpr int U4QB = 32 * U4Q * 4;       // a prologue quarter: 32 channels x 128 points fp32 (16 KB)
+constexpr int U4TL = U4Q + 4;            // fp32 row stride of the epilogue tile
+static_assert(WIMG4 + 2 * U4QB <= U4L, "prologue quarters (at WIMG4) fit");
+static_assert(64 * U4TL * 4 <= U4L, "epilogue half tile fits");
+
+__global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[U4L];
+  __shared__ float bsh[512];
+  __shared__ float2 ssh[AC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  int p, nb;
+  pair_block(a.nqb, p, nb);
+  if (p >= a.P) return;   // uniform over the workgroup
+  const int N = a.N, nkb = a.nkb;
+  const char* dimg = a.dimg + (int64_t)p * nkb * IMG;
+
+  // W image block kb -> smem + (kb & 1) WIMG4 (26 DMAs of up to 1 KB dealt over the 4 waves; the last is
+  // half a DMA); x_down image block kb -> smem + U4XD (24 DMAs)
+  auto issue_w = [&](int kb) {
+    char* dst = smem + (kb & 1) * WIMG4;
+    const char* src = a.wimg + (int64_t)kb * WIMG;
+    for (int off = w * 1024; off < WIMG4; off += 4 * 1024)
+      if (off + 16 * lane < WIMG4) glds16b(src + off + 16 * lane, dst + off);
+  };
+  auto issue_xd = [&](int kb) {
+    const char* src = dimg + (int64_t)kb * IMG;
+    for (int off = w * 1024; off < IMG; off += 4 * 1024) glds16b(src + off + 16 * lane, smem + U4XD + off);
+  };
+  issue_w(0);
+
+  for (int i = tid; i < nkb * AKB; i += U4T)
+    bsh[i] = i < a.Kc ? (a.bias ? a.bias[i] * LOG2E : 0.f) : -__builtin_inff();
+  if (tid < AC) ssh[tid] = make_float2(a.sc[(int64_t)p * a.sps + tid], a.sh[(int64_t)p * a.sps + tid]);
+
+  // queries: this lane's point n = nb 128 + 32 w + l32; xn[c][n] for c = 16 ks + 8h + i as split B
+  // fragments.  The 128 x 128 x_up block comes through LDS in quarters of 32 channels (a DMA moves two
+  // 512-byte row segments: lane -> row 2i + h, points 4 l32 .. +3), double-buffered at [WIMG4, WIMG4 +
+  // 32 KB); points past the end read a clamped column and are zeroed.
+  const int n = nb * U4Q + 32 * w + l32;
+  const bool nok = n < N;
+  const int nlast = ((N + 3) & ~3) - 4;
+  const float* xb = a.X + (int64_t)p * a.xps + min(nb * U4Q + 4 * l32, nlast);
+  auto qdma = [&](int qt) {
+    char* dst = smem + WIMG4 + (qt & 1) * U4QB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r2 = 4 * w + i;   // row pair (2 r2, 2 r2 + 1) of the quarter
+      glds16b(reinterpret_cast<const char*>(xb + (int64_t)(32 * qt + 2 * r2 + h) * a.xld), dst + r2 * 1024);
+    }
+  };
+  qdma(0);
+  Frag q[8];
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {
+    if (qt < 3) qdma(qt + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the W(0) DMAs are older: waited with them)
+    __syncthreads();
+    const float* xt = reinterpret_cast<const float*>(smem + WIMG4 + (qt & 1) * U4QB) + 32 * w + l32;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ks = 2 * qt + kk;
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int c = 16 * ks + 8 * h + i;
+        const float2 f = ssh[c];
+        const float x = fmaxf(fmaf(xt[(c - 32 * qt) * U4Q], f.x, f.y), 0.f);
+        v[i] = nok ? x : 0.f;
+      }
+      split8(v, q[ks].h, q[ks].m, q[ks].l);
+    }
+    __syncthreads();
+  }
+  issue_xd(0);
+
+  floatx16 O[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[cb][r] = 0.f;
+  float m = A_NEG, l = 0.f;
+
+  const int wbase = l32 * WROW + 16 * h;
+  auto read_w = [&](const char* Wi, int ks) {
+    const int off = wbase + 32 * ks;
+    Frag f;
+    f.h = *reinterpret_cast<const bf16x8*>(Wi + off);
+    f.m = *reinterpret_cast<const bf16x8*>(Wi + WPLANE + off);
+    f.l = *reinterpret_cast<const bf16x8*>(Wi + 2 * WPLANE + off);
+    return f;
+  };
+
+  // stage kb: W(kb) landed (waited before the barrier that ended stage kb - 1 / the prologue);
+  // x_down(kb) in flight
+  for (int kb = 0; kb < nkb; ++kb) {
+    if (kb + 1 < nkb) issue_w(kb + 1);   // the other W buffer: last read by stage kb - 1
+    const char* Wi = smem + (kb & 1) * WIMG4;
+    const char* D = smem + U4XD;
+    floatx16 S;
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const float4 b = *reinterpret_cast<const float4*>(bsh + kb * AKB + 8 * r4 + 4 * h);
+      S[4 * r4 + 0] = b.x;
+      S[4 * r4 + 1] = b.y;
+      S[4 * r4 + 2] = b.z;
+      S[4 * r4 + 3] = b.w;
+    }
+    Frag cur = read_w(Wi, 0);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      Frag nxt;
+      if (ks < 7) nxt = read_w(Wi, ks + 1);
+      SCHED_FENCE();
+      S = mfma6(cur, q[ks], S);
+      SCHED_FENCE();
+      if (ks < 7) cur = nxt;
+    }
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = S[r];
+    online_softmax(v, m, l, O);
+    Frag pf[2];
+    split8(v, pf[0].h, pf[0].m, pf[0].l);
+    split8(v + 8, pf[1].h, pf[1].m, pf[1].l);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // x_down(kb) (and W(kb + 1))
+    __syncthreads();
+    Frag df = kord_frag(D, l32, 0, h);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int s = i >> 2, cb = i & 3;
+      Frag nxt;
+      if (i < 7) nxt = kord_frag(D, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2, h);
+      SCHED_FENCE();
+      O[cb] = mfma6(df, pf[s], O[cb]);
+      SCHED_FENCE();
+      if (i < 7) df = nxt;
+    }
+    __syncthreads();   // every wave is done with x_down(kb) and W(kb)
+    if (kb + 1 < nkb) issue_xd(kb + 1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // epilogue: O (rows c = 32 cb + (q & 3) + 8 (q >> 2) + 4h, column 32 w + l32) / l -> out[c][nb 128 + col]
+  // through an LDS tile in two passes of 64 rows; a wave stores two rows per step (lane half h: row
+  // 2 it + h, columns 4 l32 .. +3) and forms the rows' (sum, squared deviations) over the tile's valid
+  // columns (the workgroup's 128 columns are one statistics tile)
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = lt > 0.f ? 1.f / lt : 0.f;
+  float* T = reinterpret_cast<float*>(smem);
+  const int col0 = nb * U4Q;
+  const int nv = min(max(N - col0, 0), U4Q);
+  const float rnv = nv > 0 ? 1.f / (float)nv : 0.f;
+  bool ok[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ok[u] = 4 * l32 + u < nv;
+  const int Lp = (N + 3) & ~3;
+  const bool sok = col0 + 4 * l32 < Lp;
+  float* out = a.out + (int64_t)p * a.ops;
+  float2* st = a.stats ? a.stats + ((int64_t)p * ((N + 127) / 128) + nb) * a.st_ld + a.st_off : nullptr;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int q2 = 0; q2 < 16; ++q2) {
+        const int c = 32 * cc + (q2 & 3) + 8 * (q2 >> 2) + 4 * h;
+        T[c * U4TL + 32 * w + l32] = nok ? O[2 * hf + cc][q2] * inv : 0.f;
+      }
+    __syncthreads();
+    for (int it = 0; it < 8; ++it) {
+      const int cl = 16 * w + 2 * it + h, c = 64 * hf + cl;
+      float4 x = *reinterpret_cast<const float4*>(T + cl * U4TL + 4 * l32);
+      if (!ok[0]) x.x = 0.f;
+      if (!ok[1]) x.y = 0.f;
+      if (!ok[2]) x.z = 0.f;
+      if (!ok[3]) x.w = 0.f;
+      if (st) {
+        const float sm = half_sum((x.x + x.y) + (x.z + x.w));
+        const float mu = sm * rnv;
+        const float d0 = ok[0] ? x.x - mu : 0.f, d1 = ok[1] ? x.y - mu : 0.f, d2 = ok[2] ? x.z - mu : 0.f,
+                    d3 = ok[3] ? x.w - mu : 0.f;
+        const float m2 = half_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
+        if (l32 == 0 && nv > 0) st[c] = make_float2(sm, m2);
+      }
+      if (sok) *reinterpret_cast<float4*>(out + (int64_t)c * a.old + col0 + 4 * l32) = x;
+    }
+    __syncthreads();
+  }
+}
+
+#ifndef UNPOOL4_DEFAULT
+#define UNPOOL4_DEFAULT 1
+#endif
+int g_unpool4 = UNPOOL4_DEFAULT;   // mvr_set_unpool4: the 4-wave diff_unpool kernel (0: the 8-wave one, A/B timing)
+
 }  // namespace mvr
 
 using namespace mvr;
@@ -819,8 +1028,20 @@ extern "C" int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t
   a.P = P; a.N = N; a.Kc = clusters; a.nkb = nkb; a.nqb = (N + AQ - 1) / AQ;
   a.out = out; a.ops = out_pstride; a.old = out_ld;
   a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
-  const int grid = ((P + 7) / 8) * 8 * a.nqb;
-  hipLaunchKernelGGL(oan_unpool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
+  if (g_unpool4 && clusters <= 512) {
+    a.nqb = (N + U4Q - 1) / U4Q;
+    const int grid = ((P + 7) / 8) * 8 * a.nqb;
+    hipLaunchKernelGGL(oan_unpool4_kernel, dim3(grid), dim3(U4T), 0, stream, a);
+  } else {
+    const int grid = ((P + 7) / 8) * 8 * a.nqb;
+    hipLaunchKernelGGL(oan_unpool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
+  }
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_set_unpool4(int on) {
+  const int prev = mvr::g_unpool4;
+  mvr::g_unpool4 = on ? 1 : 0;
+  return prev;
 }

@@ -60,6 +60,7 @@ _SIGS = {
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),
     "mvr_set_pool_split": (c_int, [c_int]),
+    "mvr_set_unpool4": (c_int, [c_int]),
     "mvr_debug_stage_hash": (c_int, [c_vp, c_int]),
     "mvr_debug_stage_dump": (c_int, [c_int, c_vp, c_size]),
     "mvr_pointcn_fused": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -127,6 +127,9 @@ int mvr_set_pool_split(int on);
  * row pointers with pair stride row_pstride (the next block's input rows 6,7).
  * guard_pos: int32 [P] scratch (zeroed here).  status: int32 [P] (may be NULL).
  * bn_train: BatchNorm layers normalise with batch statistics (module.train()). */
+/* diff_unpool kernel choice (process-wide): 1 (default) the 4-wave, two-per-CU kernel when clusters <= 512,
+ * 0 the 8-wave kernel (A/B timing).  Returns the previous setting. */
+int mvr_set_unpool4(int on);
 /* Debugging: while buf is non-NULL, every mvr_oan_block_forward launch sequence adds a position-weighted
  * 64-bit hash of each stage's activation to the next of cap device slots (zeroed by the caller);
  * NULL disables.  Not for concurrent use from two streams. */

@@ -81,8 +81,18 @@ def test_diff_pool_matches_fp64(gpu, P, N, Kc, split):
     np.testing.assert_allclose(st.cpu().numpy()[..., 1], sref[..., 1], rtol=1e-4, atol=1e-6 * scale ** 2 * 128)
 
 
-@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33)])
-def test_diff_unpool_matches_fp64(gpu, P, N, Kc):
+@pytest.mark.parametrize("kern", [1, 0])   # mvr_set_unpool4: 4-wave two-per-CU kernel / 8-wave kernel
+@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (2, 300, 700)])
+def test_diff_unpool_matches_fp64(gpu, P, N, Kc, kern):
+    from lib import _native as NV
+    prev = NV.lib().mvr_set_unpool4(kern)
+    try:
+        _unpool_case(gpu, P, N, Kc)
+    finally:
+        NV.lib().mvr_set_unpool4(prev)
+
+
+def _unpool_case(gpu, P, N, Kc):
     import torch
     from lib import _native as NV
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 7 + N)
