@@ -71,6 +71,24 @@ __device__ __forceinline__ void hash_insert_min(HashView h, uint64_t key, int32_
   }
 }
 
+// the same with at most `maxp` probes; a key that finds no slot sets *overflow (the caller re-runs with a
+// table sized for every key)
+__device__ __forceinline__ void hash_insert_min_bounded(HashView h, uint64_t key, int32_t v, int maxp, int* overflow) {
+  uint64_t s = mix64(key) & (h.cap - 1);
+  for (int probe = 0; probe < maxp; ++probe) {
+    unsigned long long cur = h.keys[s];
+    if (cur == EMPTY_KEY)
+      cur = atomicCAS(reinterpret_cast<unsigned long long*>(&h.keys[s]), (unsigned long long)EMPTY_KEY,
+                      (unsigned long long)key);
+    if (cur == EMPTY_KEY || cur == key) {
+      if (h.vals[s] > v) atomicMin(&h.vals[s], v);
+      return;
+    }
+    s = (s + 1) & (h.cap - 1);
+  }
+  atomicOr(overflow, 1);
+}
+
 __device__ __forceinline__ int64_t hash_slot(const HashView& h, uint64_t key) {
   uint64_t s = mix64(key) & (h.cap - 1);
   for (uint64_t probe = 0; probe < h.cap; ++probe) {
@@ -124,6 +142,11 @@ __global__ void coarse_keys_kernel(const int4* __restrict__ c, int64_t M, int s,
 __global__ void insert_min_kernel(const uint64_t* __restrict__ keys, int64_t n, HashView h) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) hash_insert_min(h, keys[i], (int32_t)i);
+}
+
+__global__ void insert_min_bounded_kernel(const uint64_t* __restrict__ keys, int64_t n, HashView h, int* overflow) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) hash_insert_min_bounded(h, keys[i], (int32_t)i, 64, overflow);
 }
 
 __global__ void first_flag_kernel(const uint64_t* __restrict__ keys, int64_t n, HashView h, int32_t* flags) {
@@ -516,12 +539,13 @@ struct DedupWs {
   uint64_t* keys; int4* cc; int32_t* flags; int32_t* pos; int32_t* bsum; void* table; size_t table_bytes;
 };
 
-static size_t dedup_ws_bytes(int64_t n) {
+// table sized for `keys` distinct keys (<= n)
+static size_t dedup_ws_bytes(int64_t n, int64_t keys = -1) {
   const int64_t nb = (n + SCAN_B - 1) / SCAN_B;
-  return (size_t)n * (8 + 16 + 4 + 4) + (size_t)nb * 4 + hash_table_bytes(n) + 8 * 256;
+  return (size_t)n * (8 + 16 + 4 + 4) + (size_t)nb * 4 + hash_table_bytes(keys < 0 ? n : keys) + 8 * 256;
 }
 
-static DedupWs dedup_ws(void* ws, int64_t n) {
+static DedupWs dedup_ws(void* ws, int64_t n, int64_t keys = -1) {
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
   DedupWs d{};
@@ -531,16 +555,19 @@ static DedupWs dedup_ws(void* ws, int64_t n) {
   d.flags = reinterpret_cast<int32_t*>(take((size_t)n * 4));
   d.pos = reinterpret_cast<int32_t*>(take((size_t)n * 4));
   d.bsum = reinterpret_cast<int32_t*>(take((size_t)nb * 4 + 4));
-  d.table_bytes = hash_table_bytes(n);
+  d.table_bytes = hash_table_bytes(keys < 0 ? n : keys);
   d.table = take(d.table_bytes);
   return d;
 }
 
 static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel_out, int64_t* counts, int B,
-                     hipStream_t s) {
+                     hipStream_t s, int* overflow = nullptr) {
   HashView h = hash_view(d.table, d.table_bytes);
   hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)h.cap)), dim3(256), 0, s, h);
-  hipLaunchKernelGGL(insert_min_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h);
+  if (overflow)
+    hipLaunchKernelGGL(insert_min_bounded_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h, overflow);
+  else
+    hipLaunchKernelGGL(insert_min_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h);
   hipLaunchKernelGGL(first_flag_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h, d.flags);
   const int nb = (int)((n + SCAN_B - 1) / SCAN_B);
   (void)hipMemsetAsync(counts, 0, sizeof(int64_t) * (1 + B), s);
@@ -584,6 +611,32 @@ extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, in
   hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, 1.0 / (double)voxel,
                      d.keys, d.cc);
   return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s);
+}
+
+// The raw-point table sized for distinct_hint voxels instead of n points (the raw cloud holds ~12 points per
+// voxel: a table for all of them is ~200 MB of clears and cache-missing probes per scene).  Inserts probe at most
+// 64 slots; a key that finds none sets counts_out[B + 1] (counts_out: B + 2 entries), and the caller re-runs
+// mvr_voxelize.  Same outputs as mvr_voxelize otherwise.
+extern "C" size_t mvr_voxelize_hint_workspace_bytes(int64_t n, int64_t distinct_hint) {
+  return dedup_ws_bytes(n, distinct_hint > 0 && distinct_hint < n ? distinct_hint : n);
+}
+
+extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel,
+                                 int64_t distinct_hint, void* ws, size_t ws_bytes, int32_t* coords_out,
+                                 int64_t* sel_out, int64_t* counts_out, hipStream_t s) {
+  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.f) || !ws || !coords_out || !counts_out ||
+      distinct_hint <= 0)
+    return MVR_EINVAL;
+  const int64_t keys = distinct_hint < n ? distinct_hint : n;
+  if (ws_bytes < dedup_ws_bytes(n, keys)) return MVR_EINVAL;
+  if (hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (2 + B), s) != hipSuccess) return MVR_ELAUNCH;
+  if (n == 0) return MVR_OK;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
+  DedupWs d = dedup_ws(ws, n, keys);
+  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, 1.0 / (double)voxel,
+                     d.keys, d.cc);
+  return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s,
+                   reinterpret_cast<int*>(counts_out + 1 + B));
 }
 
 extern "C" size_t mvr_coords_downsample_workspace_bytes(int64_t M) { return dedup_ws_bytes(M); }

@@ -126,7 +126,7 @@ class SparseTensor:
         return self.coords_man.coords_at(self.coords_key)
 
 
-def voxelize(points_list, voxel_size, device):
+def voxelize(points_list, voxel_size, device, distinct_hint=None):
     """Batched sparse_quantize of raw fragments (scripts/pairwise_demo.py:74-96).
     points_list: list of float arrays/tensors [n_b, 3].  Returns (coords int32 [M,4],
     sel int64 [M] (global point index), counts list, xyz_down float32 [M,3])."""
@@ -137,15 +137,30 @@ def voxelize(points_list, voxel_size, device):
     off = torch.tensor(np.concatenate([[0], np.cumsum(n)]), dtype=torch.int64, device=device)
     total = int(sum(n))
     L = N.lib()
-    ws = N.workspace(L.mvr_voxelize_workspace_bytes(total), device)
     coords = torch.empty(total, 4, dtype=torch.int32, device=device)
     sel = torch.empty(total, dtype=torch.int64, device=device)
-    cnt = torch.empty(1 + B, dtype=torch.int64, device=device)
-    N.check(L.mvr_voxelize(N.ptr(xyz), N.ptr(off), B, total, float(voxel_size), N.ptr(ws), ws.numel(), N.ptr(coords),
-                           N.ptr(sel), N.ptr(cnt), N.stream()), "mvr_voxelize")
-    c = cnt.cpu().numpy()
+    cnt = torch.empty(2 + B, dtype=torch.int64, device=device)
+    dev_key = device.index if device.index is not None else torch.cuda.current_device()
+    hint = _VOX_HINT.get(dev_key) if distinct_hint is None else distinct_hint
+    c = None
+    if hint:   # hash table sized for the expected voxel count; a key that finds no slot -> full-size re-run
+        ws = N.workspace(L.mvr_voxelize_hint_workspace_bytes(total, int(hint)), device)
+        N.check(L.mvr_voxelize_hint(N.ptr(xyz), N.ptr(off), B, total, float(voxel_size), int(hint), N.ptr(ws),
+                                    ws.numel(), N.ptr(coords), N.ptr(sel), N.ptr(cnt), N.stream()), "mvr_voxelize_hint")
+        c = cnt.cpu().numpy()
+        if c[1 + B]:
+            c = None
+    if c is None:
+        ws = N.workspace(L.mvr_voxelize_workspace_bytes(total), device)
+        N.check(L.mvr_voxelize(N.ptr(xyz), N.ptr(off), B, total, float(voxel_size), N.ptr(ws), ws.numel(),
+                               N.ptr(coords), N.ptr(sel), N.ptr(cnt), N.stream()), "mvr_voxelize")
+        c = cnt.cpu().numpy()
     M = int(c[0])
+    _VOX_HINT[dev_key] = max(3 * M // 2, 1024)   # the next call's table: this cloud's voxels + 50 %
     coords, sel = coords[:M], sel[:M]
     xyz_down = torch.empty(M, 3, device=device)
     N.check(L.mvr_gather_rows(N.ptr(xyz), 3, N.ptr(sel), M, N.ptr(xyz_down), N.stream()), "mvr_gather_rows")
-    return coords, sel, [int(v) for v in c[1:]], xyz_down
+    return coords, sel, [int(v) for v in c[1:1 + B]], xyz_down
+
+
+_VOX_HINT = {}   # per device: voxel-count estimate for the next voxelize() table (the last call's count + 50 %)

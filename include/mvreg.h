@@ -277,6 +277,13 @@ size_t mvr_voxelize_workspace_bytes(int64_t n);
 int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel, void* workspace,
                  size_t workspace_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                  mvr_stream_t stream);
+/* mvr_voxelize with the dedup hash table sized for distinct_hint voxels instead of n raw points (the raw
+ * cloud holds ~12 points per voxel); inserts probe at most 64 slots and a key that finds none sets
+ * counts_out[B + 1] (counts_out has B + 2 entries): the caller then re-runs mvr_voxelize. */
+size_t mvr_voxelize_hint_workspace_bytes(int64_t n, int64_t distinct_hint);
+int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel,
+                      int64_t distinct_hint, void* ws, size_t ws_bytes, int32_t* coords_out, int64_t* sel_out,
+                      int64_t* counts_out, mvr_stream_t stream);
 size_t mvr_coords_downsample_workspace_bytes(int64_t M);
 /* strided coordinate set floor(c/s)*s (first-occurrence order); counts_out as above */
 int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, int stride_out, void* workspace,

@@ -27,6 +27,26 @@ def test_voxelize_matches_oracle(gpu, frags):
     np.testing.assert_array_equal(xyz.cpu().numpy(), np.concatenate(frags)[osel])
 
 
+@pytest.mark.parametrize("hint", [None, 1000, 10 ** 6, "exact"])
+def test_voxelize_hint_sized_table_matches_oracle(gpu, frags, hint):
+    """mvr_voxelize_hint: the hash table sized for the expected voxel count (lib.sparse keeps the last
+    count + 50 %); a hint far too small overflows the bounded probing and re-runs at full size; every
+    hint gives the oracle's voxels bit for bit."""
+    from lib import sparse
+    from oracle.fcgf import voxelize as ovox
+    oc, osel, ocnt = ovox(frags, 0.025)
+    h = len(oc) if hint == "exact" else hint
+    sparse._VOX_HINT.clear()
+    c, sel, counts, _ = sparse.voxelize(frags, 0.025, gpu, distinct_hint=h)
+    assert counts == list(ocnt)
+    np.testing.assert_array_equal(c.cpu().numpy(), oc)
+    np.testing.assert_array_equal(sel.cpu().numpy(), osel)
+    # the next call without an explicit hint uses the recorded one
+    c2, sel2, counts2, _ = sparse.voxelize(frags, 0.025, gpu)
+    assert counts2 == list(ocnt)
+    np.testing.assert_array_equal(sel2.cpu().numpy(), osel)
+
+
 def test_strided_sets_and_kernel_maps_match_oracle(gpu, frags):
     from lib.sparse import voxelize, CoordinateManager
     from oracle.fcgf import Levels
