@@ -56,6 +56,98 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float A_NEG = -3.0e38f;
 static_assert(64 * ATL * 4 <= 2 * STAGE_B, "epilogue half tile must fit the stage ring");
 
+// ---------------------------------------------------------------------------------------------
+// Operand math.  H = 0: split-bf16, three bf16 terms per fp32 operand, 6 MFMAs per product (mfma_bf16.hpp).
+// H = 1: split-fp16, x = h + l with h = fp16(x), l = fp16(x - h) (RNE; x - h exact in fp32): 22 significant
+// bits, |x - h - l| <= 2^-22 |x| for |x| >= 2^-3 and <= 2^-25 absolute below; the products hh, hl, lh on
+// v_mfma_f32_32x32x16_f16 (3 MFMAs; the dropped ll <= 2^-22 relative).  The H = 1 kernels keep every
+// operand where that holds, or hand the launch to H = 0:
+//  * weight rows are scaled by a power of two to <= 2^14 (undone on the logits): relative 2^-22 per term;
+//  * probabilities are formed as exp2(v - m + 7) <= 2^15 (the same factor is in the softmax sum);
+//  * the logit side's activations (K / query operand) are checked against the fp16 range (< 65504); their
+//    absolute floor (2^-25 per term below 2^-3) bounds the logit error by 2^-25 sum_c |W[j][c] log2 e|,
+//    so a weight row with that sum > 128 (a floor above 2^-18 in log2 units) sends the launch to H = 0;
+//  * the value side (V operand: pool's raw x, unpool's x_down) is checked per row (channel), whose
+//    relative precision the next InstanceNorm exposes: a row with max |v| >= 65504 or in (0, 2^-3) too.
+// A launch that trips a check sets its flag word and is re-run with H = 0 (guarded launches that return
+// at once when the flag is clear), so results are within ~4x fp32 rounding of exact or are split-bf16's.
+// ---------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ int g_attn_reruns;           // guarded split-bf16 re-runs that ran (mvr_attn_reruns, diagnostics)
+constexpr float F16_RANGE = 65504.f;
+constexpr float F16_FLOOR = 0.125f;     // below: the low term is subnormal (absolute 2^-25)
+constexpr float W_SUM_MAX = 128.f;      // max sum_c |W[j][c] log2 e| of a weight row (logit floor <= 2^-18)
+// value-side row check: out of range, or nonzero and below the full-precision floor
+__device__ __forceinline__ bool v_row_bad(float rmax) { return !(rmax < F16_RANGE) || (rmax > 0.f && rmax < F16_FLOOR); }
+
+template <int H> struct FragT;
+template <> struct FragT<0> { typedef bf16x8 V; V p[3]; };
+template <> struct FragT<1> { typedef f16x8 V; V p[2]; };
+template <int H> constexpr int planes() { return H ? 2 : 3; }
+
+template <int H> __device__ __forceinline__ void split_pair(f32x2 x, unsigned* o);
+template <> __device__ __forceinline__ void split_pair<0>(f32x2 x, unsigned* o) {
+  o[0] = cvt_pk(x);
+  const f32x2 r = x - unpack(o[0]);
+  o[1] = cvt_pk(r);
+  o[2] = cvt_pk(r - unpack(o[1]));
+}
+template <> __device__ __forceinline__ void split_pair<1>(f32x2 x, unsigned* o) {
+  const f16x2 hh = __builtin_convertvector(x, f16x2);
+  o[0] = __builtin_bit_cast(unsigned, hh);
+  const f32x2 r = x - __builtin_convertvector(hh, f32x2);
+  o[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2));
+}
+// 4 fp32 -> one u32x2 (4 packed 16-bit terms) per plane
+template <int H> __device__ __forceinline__ void split4t(const float4& a, u32x2* o) {
+  unsigned lo[3], hi[3];
+  split_pair<H>(f32x2{a.x, a.y}, lo);
+  split_pair<H>(f32x2{a.z, a.w}, hi);
+#pragma unroll
+  for (int i = 0; i < planes<H>(); ++i) o[i] = u32x2{lo[i], hi[i]};
+}
+template <int H> __device__ __forceinline__ FragT<H> split8t(const float* v) {
+  unsigned t[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split_pair<H>(f32x2{v[2 * i], v[2 * i + 1]}, t[i]);
+  FragT<H> f;
+#pragma unroll
+  for (int pl = 0; pl < planes<H>(); ++pl)
+    f.p[pl] = __builtin_bit_cast(typename FragT<H>::V, u32x4{t[0][pl], t[1][pl], t[2][pl], t[3][pl]});
+  return f;
+}
+// acc += A . B, small terms first
+template <int H> __device__ __forceinline__ floatx16 mma(const FragT<H>& a, const FragT<H>& b, floatx16 acc);
+template <> __device__ __forceinline__ floatx16 mma<0>(const FragT<0>& a, const FragT<0>& b, floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
+  return acc;
+}
+template <> __device__ __forceinline__ floatx16 mma<1>(const FragT<1>& a, const FragT<1>& b, floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.p[0], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.p[0], b.p[0], acc, 0, 0, 0);
+  return acc;
+}
+// a fragment whose planes sit `ps` bytes apart
+template <int H> __device__ __forceinline__ FragT<H> ld_frag(const char* p, int ps) {
+  FragT<H> f;
+#pragma unroll
+  for (int pl = 0; pl < planes<H>(); ++pl) f.p[pl] = *reinterpret_cast<const typename FragT<H>::V*>(p + pl * ps);
+  return f;
+}
+// power-of-two scale bringing |x| <= amax to <= 2^14 (amax = 0: 2^14)
+__device__ __forceinline__ float range_scale(float amax) {
+  int e;
+  (void)frexpf(amax, &e);   // amax < 2^e
+  return ldexpf(1.f, min(max(14 - e, -64), 64));
+}
+
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 // one MFMA, then a share of the VALU and LDS writes placed in the same scheduling region, six times
 #define ATTN_INTERLEAVE6()                          \
@@ -63,6 +155,15 @@ static_assert(64 * ATL * 4 <= 2 * STAGE_B, "epilogue half tile must fit the stag
     _Pragma("unroll") for (int u_ = 0; u_ < 6; ++u_) { \
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); \
       __builtin_amdgcn_sched_group_barrier(0x002, 5, 0); \
+      __builtin_amdgcn_sched_group_barrier(0x200, 1, 0); \
+    }                                               \
+  } while (0)
+// the same for the 3 MFMAs of a split-fp16 product (the split itself is shorter: ~2/3 of the VALU)
+#define ATTN_INTERLEAVE3()                          \
+  do {                                              \
+    _Pragma("unroll") for (int u_ = 0; u_ < 3; ++u_) { \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); \
+      __builtin_amdgcn_sched_group_barrier(0x002, 7, 0); \
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0); \
     }                                               \
   } while (0)
@@ -115,8 +216,9 @@ __device__ __forceinline__ void pair_block(int nblk, int& p, int& blk) {
 // Lazy rescaling: the running max m moves only when a block exceeds it by more than RESCALE (log2
 // units), so the probabilities exp2(v - m) stay <= 2^RESCALE and O, l are rescaled a few times per
 // query instead of every block; O / l is the softmax-weighted sum whichever m was used.
-// Leaves the probabilities in v.
+// Leaves the probabilities in v, times 2^PSH (the sum l carries the same factor).
 constexpr float RESCALE = 8.f;
+template <int PSH = 0>
 __device__ __forceinline__ void online_softmax(float (&v)[16], float& m, float& l, floatx16 (&O)[4]) {
   float bm = __builtin_fmaxf(__builtin_fmaxf(v[0], v[1]), v[2]);
 #pragma unroll
@@ -131,10 +233,11 @@ __device__ __forceinline__ void online_softmax(float (&v)[16], float& m, float& 
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) O[cb] *= alpha;
   }
+  const float ms = m - (float)PSH;
   float ps = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    v[r] = __builtin_amdgcn_exp2f(v[r] - m);
+    v[r] = __builtin_amdgcn_exp2f(v[r] - ms);
     ps += v[r];
   }
   l += ps;
@@ -198,6 +301,8 @@ struct PoolArgs {
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(Kc/128)][st_ld] (+ st_off + c), nullable
   int nks;                                         // key splits per (pair, query block); 1: none
   float* part; int* cnt;                           // nks > 1: per-split (O, m, l) slabs, arrival tickets
+  int* range;                                      // H = 1: set when an operand is outside the fp16 range
+  const int* guard;                                // H = 0 re-run: return unless *guard is set
 };
 
 constexpr int PSLAB = 66 * ATHREADS;               // floats of one split's slab: O (64 / thread), m, l
@@ -212,11 +317,22 @@ __device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
 }
 
 constexpr int XT = AC * AKB * 4;   // raw fp32 key tile [128 c][32 n] (16 KB)
+template <int H> constexpr int pool_smem() {
+  return 4 * planes<H>() * PLANE > 64 * ATL * 4 ? 4 * planes<H>() * PLANE : 64 * ATL * 4;
+}
 
+template <int H>
 __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_B];
-  __shared__ __attribute__((aligned(16))) char xraw[2 * XT];   // LDS-DMA ring of raw key tiles
-  __shared__ float2 ssh[AC];                                  // (sc, sh) of this pair
+  constexpr int NP = planes<H>();
+  constexpr int IMGT = NP * PLANE;         // one stage image (K or V)
+  constexpr int STAGET = 2 * IMGT;         // one stage: K image, V image
+  __shared__ __attribute__((aligned(16))) char smem[pool_smem<H>()];   // stage ring; epilogue tile
+  __shared__ __attribute__((aligned(16))) char xraw[2 * XT];           // LDS-DMA ring of raw key tiles
+  __shared__ float2 ssh[AC];                                          // (sc, sh) of this pair
+  if (a.guard) {
+    if (*a.guard == 0) return;   // uniform: the fp16 launch before this one stayed in range
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_attn_reruns, 1);
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   int p, jb, ks = 0;
   if (a.nks > 1) {   // the splits of one (pair, query block) are blocks b, b + 8, ..: one XCD, adjacent
@@ -252,55 +368,49 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   if (tid < AC) ssh[tid] = make_float2(a.sc[(int64_t)p * a.sps + tid], a.sh[(int64_t)p * a.sps + tid]);
 
   // queries: this lane's W row (column j of S^T) as split B fragments, one per 16-channel k-step
+  // (H = 1: the row scaled to <= 2^14, the scale undone on the logits)
   const int j = jb * AQ + 32 * w + l32;
   const bool jok = j < a.Kc;
   const float* wr = a.W + (int64_t)min(j, a.Kc - 1) * AC + 8 * h;
-  Frag q[8];
+  FragT<H> q[8];
+  float wsc = 1.f;
+  bool wbad = false;
+  {
+    float v[8][8];
+    float amax = 0.f, asum = 0.f;
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * ks);
-    const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * ks + 4);
-    float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+    for (int ks = 0; ks < 8; ++ks) {
+      const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * ks);
+      const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * ks + 4);
+      const float t[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = jok ? v[i] * LOG2E : 0.f;   // logits in log2 units
-    split8(v, q[ks].h, q[ks].m, q[ks].l);
-  }
-  const float bj = (jok && a.bias) ? a.bias[j] * LOG2E : 0.f;
-
-  // split raw tile kb (xraw[kb & 1]) into stage st: thread -> channel c = tid / 8 + 64 i, keys
-  // 4 (tid & 7) .. +3
-  const int sq = tid & 7;
-  auto store_tile = [&](int kb, int st) {
-    if (ATTN_ABL & 2) return;
-    char* K = smem + st * STAGE_B;
-    char* V = K + IMG;
-    const char* xt = xraw + (kb & 1) * XT;
-    const bool nok = kb * AKB + 4 * sq < N;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = (tid >> 3) + 64 * i;
-      float4 x = *reinterpret_cast<const float4*>(xt + c * 128 + 16 * sq);
-      if (!nok) x = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float2 f = ssh[c];
-      u32x2 H, M, L;
-      split4(x, H, M, L);
-      const int vo = kord_off(c, sq);
-      *reinterpret_cast<u32x2*>(V + vo) = H;
-      *reinterpret_cast<u32x2*>(V + PLANE + vo) = M;
-      *reinterpret_cast<u32x2*>(V + 2 * PLANE + vo) = L;
-      const float4 xn = make_float4(fmaxf(fmaf(x.x, f.x, f.y), 0.f), fmaxf(fmaf(x.y, f.x, f.y), 0.f),
-                                    fmaxf(fmaf(x.z, f.x, f.y), 0.f), fmaxf(fmaf(x.w, f.x, f.y), 0.f));
-      split4(xn, H, M, L);
-      const int ko = c * 64 + 8 * sq;
-      *reinterpret_cast<u32x2*>(K + ko) = H;
-      *reinterpret_cast<u32x2*>(K + PLANE + ko) = M;
-      *reinterpret_cast<u32x2*>(K + 2 * PLANE + ko) = L;
+      for (int i = 0; i < 8; ++i) {
+        v[ks][i] = jok ? t[i] * LOG2E : 0.f;   // logits in log2 units
+        amax = fmaxf(amax, fabsf(v[ks][i]));
+        asum += fabsf(v[ks][i]);
+      }
     }
-  };
+    if (H) {
+      wbad = asum + __shfl_xor(asum, 32, 64) > W_SUM_MAX;
+      wsc = range_scale(fmaxf(amax, __shfl_xor(amax, 32, 64)));
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[ks][i] *= wsc;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) q[ks] = split8t<H>(v[ks]);
+  }
+  const float wisc = 1.f / wsc;   // exact: a power of two
+  const float bj = ((jok && a.bias) ? a.bias[j] * LOG2E : 0.f) * wsc;
+  float kmax = 0.f;               // H = 1: max xn split so far (K operand range check)
+  float vmax[2] = {0.f, 0.f};     // H = 1: max |x| of this thread's two channel rows so far (V operand)
 
-  // the same split in four parts placed between the MFMAs of a stage (the 8 waves run their stages in
-  // step, so a split phase of its own leaves the matrix pipes idle): load_x reads a thread's two raw
-  // key groups, store_v / store_k write one of them to the V / K image of stage st
+  const int sq = tid & 7;
+  // the split of raw tile kb + 1 in four parts placed between the MFMAs of a stage (the 8 waves run
+  // their stages in step, so a split phase of its own leaves the matrix pipes idle): load_x reads a
+  // thread's two raw key groups (thread -> channel c = tid / 8 + 64 i, keys 4 (tid & 7) .. +3),
+  // store_v / store_k write one of them to the V / K image of stage st
   auto load_x = [&](int kb, int i) {
     const int c = (tid >> 3) + 64 * i;
     float4 x = *reinterpret_cast<const float4*>(xraw + (kb & 1) * XT + c * 128 + 16 * sq);
@@ -310,28 +420,28 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   auto store_v = [&](int st, int i, float4 x) {
     if (ATTN_ABL & 2) return;
     asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));   // keep the split at its placement
-    char* V = smem + st * STAGE_B + IMG;
+    char* V = smem + st * STAGET + IMGT;
     const int c = (tid >> 3) + 64 * i;
-    u32x2 H, M, L;
-    split4(x, H, M, L);
+    u32x2 o[3];
+    split4t<H>(x, o);
     const int vo = kord_off(c, sq);
-    *reinterpret_cast<u32x2*>(V + vo) = H;
-    *reinterpret_cast<u32x2*>(V + PLANE + vo) = M;
-    *reinterpret_cast<u32x2*>(V + 2 * PLANE + vo) = L;
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) *reinterpret_cast<u32x2*>(V + pl * PLANE + vo) = o[pl];
+    if (H) vmax[i] = fmaxf(fmaxf(vmax[i], fmaxf(fabsf(x.x), fabsf(x.y))), fmaxf(fabsf(x.z), fabsf(x.w)));
   };
   auto store_k = [&](int st, int i, float4 x, const float2& f) {
     if (ATTN_ABL & 2) return;
     asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
-    char* K = smem + st * STAGE_B;
+    char* K = smem + st * STAGET;
     const int c = (tid >> 3) + 64 * i;
     const float4 xn = make_float4(fmaxf(fmaf(x.x, f.x, f.y), 0.f), fmaxf(fmaf(x.y, f.x, f.y), 0.f),
                                   fmaxf(fmaf(x.z, f.x, f.y), 0.f), fmaxf(fmaf(x.w, f.x, f.y), 0.f));
-    u32x2 H, M, L;
-    split4(xn, H, M, L);
+    u32x2 o[3];
+    split4t<H>(xn, o);
     const int ko = c * 64 + 8 * sq;
-    *reinterpret_cast<u32x2*>(K + ko) = H;
-    *reinterpret_cast<u32x2*>(K + PLANE + ko) = M;
-    *reinterpret_cast<u32x2*>(K + 2 * PLANE + ko) = L;
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) *reinterpret_cast<u32x2*>(K + pl * PLANE + ko) = o[pl];
+    if (H) kmax = fmaxf(fmaxf(kmax, fmaxf(xn.x, xn.y)), fmaxf(xn.z, xn.w));
   };
 
   floatx16 O[4];
@@ -346,23 +456,30 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   const int tr_off = ((lane & 15) >> 2) * 64 + 32 * (g & 1) + 8 * (lane & 3);
   auto read_k = [&](const char* K, int ks) {
     const int o0 = (16 * ks + 8 * h) * 64 + tr_off, o1 = o0 + 4 * 64;
-    Frag f;
-    u32x2 t0 = ds_read_tr(K + o0), t1 = ds_read_tr(K + o1);
-    f.h = __builtin_bit_cast(bf16x8, u32x4{t0[0], t0[1], t1[0], t1[1]});
-    t0 = ds_read_tr(K + PLANE + o0);
-    t1 = ds_read_tr(K + PLANE + o1);
-    f.m = __builtin_bit_cast(bf16x8, u32x4{t0[0], t0[1], t1[0], t1[1]});
-    t0 = ds_read_tr(K + 2 * PLANE + o0);
-    t1 = ds_read_tr(K + 2 * PLANE + o1);
-    f.l = __builtin_bit_cast(bf16x8, u32x4{t0[0], t0[1], t1[0], t1[1]});
+    FragT<H> f;
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+      const u32x2 t0 = ds_read_tr(K + pl * PLANE + o0), t1 = ds_read_tr(K + pl * PLANE + o1);
+      f.p[pl] = __builtin_bit_cast(typename FragT<H>::V, u32x4{t0[0], t0[1], t1[0], t1[1]});
+    }
     return f;
+  };
+  // A fragment (row = 32 cb + lane row, k-step s) of a V image
+  auto v_frag = [&](const char* V, int row, int s) {
+    return ld_frag<H>(V + row * 64 + 16 * ((2 * s + h) ^ ((row >> 2) & 3)), PLANE);
   };
 
   // ring: raw tile kb + 2 lands while stage kb & 1 is consumed and tile kb + 1 is split into the other
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   dma_tile(kb0 + 1);
-  store_tile(kb0, kb0 & 1);
+  {
+    const float4 x0 = load_x(kb0, 0), x1 = load_x(kb0, 1);
+    store_v(kb0 & 1, 0, x0);
+    store_k(kb0 & 1, 0, x0, ssh[tid >> 3]);
+    store_v(kb0 & 1, 1, x1);
+    store_k(kb0 & 1, 1, x1, ssh[(tid >> 3) + 64]);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kb = kb0; kb < kb1; ++kb) {
@@ -371,61 +488,76 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     const float4 x0 = load_x(kb + 1, 0);
     float4 x1;
     dma_tile(kb + 2);             // into the buffer of tile kb, split one iteration ago
-    const char* K = smem + st * STAGE_B;
-    const char* V = K + IMG;
-    // S^T[n][j] = b[j] + sum_c xn[c][n] W[j][c] (log2 units), fragments one k-step ahead
+    const char* K = smem + st * STAGET;
+    const char* V = K + IMGT;
+    // S^T[n][j] = b[j] + sum_c xn[c][n] W[j][c] (log2 units; H = 1: times wsc), fragments one k-step ahead
     floatx16 S;
 #pragma unroll
     for (int r = 0; r < 16; ++r) S[r] = bj;
-    Frag cur = read_k(K, 0);
+    FragT<H> cur = read_k(K, 0);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      Frag nxt;
+      FragT<H> nxt;
       if (ks < 7) nxt = read_k(K, ks + 1);
       SCHED_FENCE();
       if (ks == 2) store_v(st ^ 1, 0, x0);
       if (ks == 5) store_k(st ^ 1, 0, x0, ssh[tid >> 3]);
       if (ks == 6) x1 = load_x(kb + 1, 1);
       if (ATTN_ABL & 8)
-        asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l));
+        asm volatile("" ::"v"(cur.p[0]), "v"(cur.p[1]));
       else
-        S = mfma6(cur, q[ks], S);
-      if (ks == 2 || ks == 5) ATTN_INTERLEAVE6();
+        S = mma<H>(cur, q[ks], S);
+      if (ks == 2 || ks == 5) {
+        if (H) ATTN_INTERLEAVE3(); else ATTN_INTERLEAVE6();
+      }
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
-    Frag vf = kord_frag(V, l32, 0, h);   // first V fragment, in flight during the softmax
+    FragT<H> vf = v_frag(V, l32, 0);   // first V fragment, in flight during the softmax
     float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = S[r];
+    for (int r = 0; r < 16; ++r) v[r] = H ? S[r] * wisc : S[r];
     if (kb * AKB + AKB > N) {   // ragged last block
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         if (kb * AKB + (r & 3) + 8 * (r >> 2) + 4 * h >= N) v[r] = -__builtin_inff();
     }
-    if (!(ATTN_ABL & 1)) online_softmax(v, m, l, O);
-    Frag pf[2];
-    split8(v, pf[0].h, pf[0].m, pf[0].l);
-    split8(v + 8, pf[1].h, pf[1].m, pf[1].l);
+    if (!(ATTN_ABL & 1)) online_softmax<H ? 7 : 0>(v, m, l, O);
+    FragT<H> pf[2] = {split8t<H>(v), split8t<H>(v + 8)};
     // O[c][j] += sum_n x[c][n] P[n][j]
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int s = i >> 2, cb = i & 3;
-      Frag nxt;
-      if (i < 7) nxt = kord_frag(V, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2, h);
+      FragT<H> nxt;
+      if (i < 7) nxt = v_frag(V, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2);
       SCHED_FENCE();
       if (i == 2) store_v(st ^ 1, 1, x1);
       if (i == 5) store_k(st ^ 1, 1, x1, ssh[(tid >> 3) + 64]);
       if (ATTN_ABL & 4)
-        asm volatile("" ::"v"(vf.h), "v"(vf.m), "v"(vf.l), "v"(pf[s].h), "v"(pf[s].m), "v"(pf[s].l));
+        asm volatile("" ::"v"(vf.p[0]), "v"(vf.p[1]), "v"(pf[s].p[0]), "v"(pf[s].p[1]));
       else
-        O[cb] = mfma6(vf, pf[s], O[cb]);
-      if (i == 2 || i == 5) ATTN_INTERLEAVE6();
+        O[cb] = mma<H>(vf, pf[s], O[cb]);
+      if (i == 2 || i == 5) {
+        if (H) ATTN_INTERLEAVE3(); else ATTN_INTERLEAVE6();
+      }
       SCHED_FENCE();
       if (i < 7) vf = nxt;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+  }
+  if (H) {
+    // rows: the 8 threads of a channel (tid & 7) saw all of this split's keys of it
+    bool bad = wbad || !(kmax < F16_RANGE);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float r = vmax[i];
+      r = fmaxf(r, __shfl_xor(r, 1, 64));
+      r = fmaxf(r, __shfl_xor(r, 2, 64));
+      r = fmaxf(r, __shfl_xor(r, 4, 64));
+      bad |= v_row_bad(r);
+    }
+    if (__any(bad) && lane == 0) atomicOr(a.range, 1);
   }
   if (a.nks > 1) {
     // publish this split's (O, m, l); the last split to arrive merges all of them (counter hand-off:
@@ -445,8 +577,11 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int tk = __hip_atomic_fetch_add(a.cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = tk == a.nks - 1;
-      if (tk == a.nks - 1) {
+      // tickets are not reset between the fp16 launch and its guarded re-run: the last split of a slot
+      // draws nks - 1 modulo nks
+      const bool last = tk % a.nks == a.nks - 1;
+      flag[0] = last;
+      if (last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -489,26 +624,53 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
 // ---------------------------------------------------------------------------------------------
 // diff_unpool
 // ---------------------------------------------------------------------------------------------
-// W [Kc][128] -> image [nkb][3 planes][32 j][WROW bytes] bf16 (WIMG bytes per block); rows j >= Kc zero.
-__global__ void split_w_kernel(const float* __restrict__ W, int Kc, int nkb, char* img) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// W [Kc][128] -> image [nkb][planes][32 j][WROW bytes] (wimg_stride<H> bytes per block); rows j >= Kc zero.
+// A row is 16 adjacent threads (8 channels each).  bs[j] = (b[j] log2e, 1) with H = 0; with H = 1 the row is
+// scaled by s = range_scale(max |row|) and bs[j] = (b[j] log2e s, 1 / s); rows j >= Kc: (-inf, 1).
+template <int H> constexpr int wimg_stride() { return H ? 17 * 1024 : WIMG; }
+template <int H> constexpr int ximg_bytes() { return planes<H>() * PLANE; }
+static_assert(2 * WPLANE <= 17 * 1024, "fp16 W image block");
+
+template <int H>
+__global__ void split_w_kernel(const float* __restrict__ W, const float* __restrict__ bias, int Kc, int nkb, char* img,
+                               float2* bs, int* range, const int* guard) {
+  if (guard && *guard == 0) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;   // nkb * 512 threads: a multiple of 16
   if (i >= nkb * 512) return;
   const int ch = i & 15, jj = (i >> 4) & 31, kb = i >> 9;
   const int j = kb * AKB + jj;
   float v[8];
+  float amax = 0.f, asum = 0.f;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = j < Kc ? W[(int64_t)j * AC + 8 * ch + e] * LOG2E : 0.f;   // log2 units
-  Frag f;
-  split8(v, f.h, f.m, f.l);
-  char* base = img + (int64_t)kb * WIMG + jj * WROW + 16 * ch;
-  *reinterpret_cast<bf16x8*>(base) = f.h;
-  *reinterpret_cast<bf16x8*>(base + WPLANE) = f.m;
-  *reinterpret_cast<bf16x8*>(base + 2 * WPLANE) = f.l;
+  for (int e = 0; e < 8; ++e) {
+    v[e] = j < Kc ? W[(int64_t)j * AC + 8 * ch + e] * LOG2E : 0.f;   // log2 units
+    amax = fmaxf(amax, fabsf(v[e]));
+    asum += fabsf(v[e]);
+  }
+  float s = 1.f;
+  if (H) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+      asum += __shfl_xor(asum, o, 64);
+    }
+    if (__any(asum > W_SUM_MAX) && (threadIdx.x & 63) == 0) atomicOr(range, 1);
+    s = range_scale(amax);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= s;
+  }
+  const FragT<H> f = split8t<H>(v);
+  char* base = img + (int64_t)kb * wimg_stride<H>() + jj * WROW + 16 * ch;
+#pragma unroll
+  for (int pl = 0; pl < planes<H>(); ++pl) *reinterpret_cast<typename FragT<H>::V*>(base + pl * WPLANE) = f.p[pl];
+  if (ch == 0)
+    bs[j] = j < Kc ? make_float2((bias ? bias[j] * LOG2E : 0.f) * s, 1.f / s) : make_float2(-__builtin_inff(), 1.f);
 }
 
-// x_down [P][128][ld] (Kc valid columns) -> image [P][nkb][3 planes][128 c][32 j] (kord_off order)
+// x_down [P][128][ld] (Kc valid columns) -> split-bf16 image [P][nkb][3 planes][128 c][32 j] (kord_off order)
 __global__ void split_xd_kernel(const float* __restrict__ XD, int64_t ps, int64_t ld, int P, int Kc, int nkb,
-                                char* img) {
+                                char* img, const int* guard) {
+  if (guard && *guard == 0) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)P * nkb * 1024) return;
   const int q = (int)(i & 7), c = (int)((i >> 3) & 127);
@@ -519,23 +681,58 @@ __global__ void split_xd_kernel(const float* __restrict__ XD, int64_t ps, int64_
   const float* src = XD + p * ps + (int64_t)c * ld;
   const float4 x = make_float4(j0 < Kc ? src[j0] : 0.f, j0 + 1 < Kc ? src[j0 + 1] : 0.f,
                                j0 + 2 < Kc ? src[j0 + 2] : 0.f, j0 + 3 < Kc ? src[j0 + 3] : 0.f);
-  u32x2 H, M, L;
-  split4(x, H, M, L);
-  char* base = img + pk * IMG + kord_off(c, q);
-  *reinterpret_cast<u32x2*>(base) = H;
-  *reinterpret_cast<u32x2*>(base + PLANE) = M;
-  *reinterpret_cast<u32x2*>(base + 2 * PLANE) = L;
+  u32x2 o[3];
+  split4t<0>(x, o);
+  char* base = img + pk * ximg_bytes<0>() + kord_off(c, q);
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x2*>(base + pl * PLANE) = o[pl];
+}
+
+// the split-fp16 image [P][nkb][2 planes][128 c][32 j], one wave per row (p, c) of x_down (Kc <= 512: lane l
+// holds clusters 8 l .. 8 l + 7), with the value-side row check
+__global__ void split_xd16_kernel(const float* __restrict__ XD, int64_t ps, int64_t ld, int P, int Kc, int nkb,
+                                  char* img, int* range) {
+  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // p * 128 + c
+  const int lane = threadIdx.x & 63;
+  if (row >= (int64_t)P * AC) return;   // whole waves
+  const int c = (int)(row & 127);
+  const int64_t p = row >> 7;
+  const float* src = XD + p * ps + (int64_t)c * ld;
+  float v[8];
+  float rmax = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int j = 8 * lane + e;
+    v[e] = j < Kc ? src[j] : 0.f;
+    rmax = fmaxf(rmax, fabsf(v[e]));
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) rmax = fmaxf(rmax, __shfl_xor(rmax, o, 64));
+  if (lane == 0 && v_row_bad(rmax)) atomicOr(range, 1);
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int j0 = 8 * lane + 4 * g, kb = j0 >> 5, q = (j0 & 31) >> 2;
+    if (kb >= nkb) break;
+    u32x2 o[3];
+    split4t<1>(make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]), o);
+    char* base = img + (p * nkb + kb) * ximg_bytes<1>() + kord_off(c, q);
+    *reinterpret_cast<u32x2*>(base) = o[0];
+    *reinterpret_cast<u32x2*>(base + PLANE) = o[1];
+  }
 }
 
 struct UnpoolArgs {
   const float* X; int64_t xps, xld;                // x_up [P][128][xld] (raw)
   const float* sc; const float* sh; int64_t sps;   // folded IN+BN of the embedding input
-  const char* wimg;                                // split_w_kernel image [nkb][WIMG]
-  const float* bias;                               // [Kc], nullable
-  const char* dimg;                                // split_xd_kernel image [P][nkb][IMG]
-  int P, N, Kc, nkb, nqb;                          // nqb = ceil(N / 256) query blocks
+  const char* wimg;                                // split_w_kernel image [nkb][wimg_stride]
+  const float* bias;                               // [Kc], nullable (the 8-wave kernel)
+  const float2* bs;                                // split_w_kernel (bias, 1 / row scale) [nkb * 32]
+  const char* dimg;                                // split_xd_kernel image [P][nkb][ximg_bytes]
+  int P, N, Kc, nkb, nqb;                          // nqb = ceil(N / queries per workgroup)
   float* out; int64_t ops, old;                    // [P][128][old]
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(N/128)][st_ld] (+ st_off + c), nullable
+  int* range;                                      // H = 1: set when an operand is outside the fp16 range
+  const int* guard;                                // H = 0 re-run: return unless *guard is set
 };
 
 
@@ -696,53 +893,66 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
 // ---------------------------------------------------------------------------------------------
 constexpr int U4T = 256;                 // threads
 constexpr int U4Q = 128;                 // queries per workgroup
-constexpr int WIMG4 = 3 * WPLANE;        // 26112 B: W image block as it lands in LDS
-constexpr int U4XD = 2 * WIMG4;          // x_down image offset
-constexpr int U4L = 2 * WIMG4 + IMG;     // 76800 B
 constexpr int U4QB = 32 * U4Q * 4;       // a prologue quarter: 32 channels x 128 points fp32 (16 KB)
 constexpr int U4TL = U4Q + 4;            // fp32 row stride of the epilogue tile
-static_assert(WIMG4 + 2 * U4QB <= U4L, "prologue quarters (at WIMG4) fit");
-static_assert(64 * U4TL * 4 <= U4L, "epilogue half tile fits");
+template <int H> constexpr int u4_wimg() { return planes<H>() * WPLANE; }   // W image block as it lands in LDS
+template <int H> constexpr int u4_lds() { return 2 * u4_wimg<H>() + ximg_bytes<H>(); }   // 76800 / 51200 B
+static_assert(u4_wimg<0>() + 2 * U4QB <= u4_lds<0>() && u4_wimg<1>() + 2 * U4QB <= u4_lds<1>(),
+              "prologue quarters (at the second W buffer) fit");
+static_assert(64 * U4TL * 4 <= u4_lds<1>(), "epilogue half tile fits");
 
+template <int H>
 __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[U4L];
-  __shared__ float bsh[512];
+  constexpr int WI4 = u4_wimg<H>();
+  constexpr int XDO = 2 * WI4;             // x_down image offset
+  constexpr int XIMG = ximg_bytes<H>();
+  constexpr int WSTR = wimg_stride<H>();
+  __shared__ __attribute__((aligned(16))) char smem[u4_lds<H>()];
+  __shared__ __attribute__((aligned(16))) float bsh[512];
+  __shared__ __attribute__((aligned(16))) float ish[H ? 512 : 4];
   __shared__ float2 ssh[AC];
+  if (a.guard) {
+    if (*a.guard == 0) return;   // uniform: the fp16 launch before this one stayed in range
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_attn_reruns, 1);
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   int p, nb;
   pair_block(a.nqb, p, nb);
   if (p >= a.P) return;   // uniform over the workgroup
   const int N = a.N, nkb = a.nkb;
-  const char* dimg = a.dimg + (int64_t)p * nkb * IMG;
+  const char* dimg = a.dimg + (int64_t)p * nkb * XIMG;
 
-  // W image block kb -> smem + (kb & 1) WIMG4 (26 DMAs of up to 1 KB dealt over the 4 waves; the last is
-  // half a DMA); x_down image block kb -> smem + U4XD (24 DMAs)
+  // W image block kb -> smem + (kb & 1) WI4 (1 KB DMAs dealt over the 4 waves; the last may be partial);
+  // x_down image block kb -> smem + XDO
   auto issue_w = [&](int kb) {
-    char* dst = smem + (kb & 1) * WIMG4;
-    const char* src = a.wimg + (int64_t)kb * WIMG;
-    for (int off = w * 1024; off < WIMG4; off += 4 * 1024)
-      if (off + 16 * lane < WIMG4) glds16b(src + off + 16 * lane, dst + off);
+    char* dst = smem + (kb & 1) * WI4;
+    const char* src = a.wimg + (int64_t)kb * WSTR;
+    for (int off = w * 1024; off < WI4; off += 4 * 1024)
+      if (off + 16 * lane < WI4) glds16b(src + off + 16 * lane, dst + off);
   };
   auto issue_xd = [&](int kb) {
-    const char* src = dimg + (int64_t)kb * IMG;
-    for (int off = w * 1024; off < IMG; off += 4 * 1024) glds16b(src + off + 16 * lane, smem + U4XD + off);
+    const char* src = dimg + (int64_t)kb * XIMG;
+    for (int off = w * 1024; off < XIMG; off += 4 * 1024) glds16b(src + off + 16 * lane, smem + XDO + off);
   };
   issue_w(0);
 
-  for (int i = tid; i < nkb * AKB; i += U4T)
-    bsh[i] = i < a.Kc ? (a.bias ? a.bias[i] * LOG2E : 0.f) : -__builtin_inff();
+  for (int i = tid; i < nkb * AKB; i += U4T) {
+    const float2 b = a.bs[i];
+    bsh[i] = b.x;
+    if (H) ish[i] = b.y;
+  }
   if (tid < AC) ssh[tid] = make_float2(a.sc[(int64_t)p * a.sps + tid], a.sh[(int64_t)p * a.sps + tid]);
 
   // queries: this lane's point n = nb 128 + 32 w + l32; xn[c][n] for c = 16 ks + 8h + i as split B
   // fragments.  The 128 x 128 x_up block comes through LDS in quarters of 32 channels (a DMA moves two
-  // 512-byte row segments: lane -> row 2i + h, points 4 l32 .. +3), double-buffered at [WIMG4, WIMG4 +
+  // 512-byte row segments: lane -> row 2i + h, points 4 l32 .. +3), double-buffered at [WI4, WI4 +
   // 32 KB); points past the end read a clamped column and are zeroed.
   const int n = nb * U4Q + 32 * w + l32;
   const bool nok = n < N;
   const int nlast = ((N + 3) & ~3) - 4;
   const float* xb = a.X + (int64_t)p * a.xps + min(nb * U4Q + 4 * l32, nlast);
   auto qdma = [&](int qt) {
-    char* dst = smem + WIMG4 + (qt & 1) * U4QB;
+    char* dst = smem + WI4 + (qt & 1) * U4QB;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r2 = 4 * w + i;   // row pair (2 r2, 2 r2 + 1) of the quarter
@@ -750,13 +960,14 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
     }
   };
   qdma(0);
-  Frag q[8];
+  FragT<H> q[8];
+  float xmax = 0.f;
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
     if (qt < 3) qdma(qt + 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the W(0) DMAs are older: waited with them)
     __syncthreads();
-    const float* xt = reinterpret_cast<const float*>(smem + WIMG4 + (qt & 1) * U4QB) + 32 * w + l32;
+    const float* xt = reinterpret_cast<const float*>(smem + WI4 + (qt & 1) * U4QB) + 32 * w + l32;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int ks = 2 * qt + kk;
@@ -767,11 +978,13 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
         const float2 f = ssh[c];
         const float x = fmaxf(fmaf(xt[(c - 32 * qt) * U4Q], f.x, f.y), 0.f);
         v[i] = nok ? x : 0.f;
+        if (H) xmax = fmaxf(xmax, v[i]);
       }
-      split8(v, q[ks].h, q[ks].m, q[ks].l);
+      q[ks] = split8t<H>(v);
     }
     __syncthreads();
   }
+  if (H && __any(!(xmax < F16_RANGE)) && lane == 0) atomicOr(a.range, 1);
   issue_xd(0);
 
   floatx16 O[4];
@@ -782,21 +995,19 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
   float m = A_NEG, l = 0.f;
 
   const int wbase = l32 * WROW + 16 * h;
-  auto read_w = [&](const char* Wi, int ks) {
-    const int off = wbase + 32 * ks;
-    Frag f;
-    f.h = *reinterpret_cast<const bf16x8*>(Wi + off);
-    f.m = *reinterpret_cast<const bf16x8*>(Wi + WPLANE + off);
-    f.l = *reinterpret_cast<const bf16x8*>(Wi + 2 * WPLANE + off);
-    return f;
+  auto read_w = [&](const char* Wi, int ks) { return ld_frag<H>(Wi + wbase + 32 * ks, WPLANE); };
+  auto d_frag = [&](const char* D, int row, int s) {
+    return ld_frag<H>(D + row * 64 + 16 * ((2 * s + h) ^ ((row >> 2) & 3)), PLANE);
   };
 
   // stage kb: W(kb) landed (waited before the barrier that ended stage kb - 1 / the prologue);
   // x_down(kb) in flight
   for (int kb = 0; kb < nkb; ++kb) {
     if (kb + 1 < nkb) issue_w(kb + 1);   // the other W buffer: last read by stage kb - 1
-    const char* Wi = smem + (kb & 1) * WIMG4;
-    const char* D = smem + U4XD;
+    const char* Wi = smem + (kb & 1) * WI4;
+    const char* D = smem + XDO;
+    // S[j][n] = b[j] + sum_c W[j][c] xn[c][n] (log2 units, H = 1: row j times its scale; -inf rows past
+    // the clusters)
     floatx16 S;
 #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4) {
@@ -806,33 +1017,42 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
       S[4 * r4 + 2] = b.z;
       S[4 * r4 + 3] = b.w;
     }
-    Frag cur = read_w(Wi, 0);
+    FragT<H> cur = read_w(Wi, 0);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
-      Frag nxt;
+      FragT<H> nxt;
       if (ks < 7) nxt = read_w(Wi, ks + 1);
       SCHED_FENCE();
-      S = mfma6(cur, q[ks], S);
+      S = mma<H>(cur, q[ks], S);
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
     float v[16];
+    if (H) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = S[r];
-    online_softmax(v, m, l, O);
-    Frag pf[2];
-    split8(v, pf[0].h, pf[0].m, pf[0].l);
-    split8(v + 8, pf[1].h, pf[1].m, pf[1].l);
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 is = *reinterpret_cast<const float4*>(ish + kb * AKB + 8 * r4 + 4 * h);
+        v[4 * r4 + 0] = S[4 * r4 + 0] * is.x;
+        v[4 * r4 + 1] = S[4 * r4 + 1] * is.y;
+        v[4 * r4 + 2] = S[4 * r4 + 2] * is.z;
+        v[4 * r4 + 3] = S[4 * r4 + 3] * is.w;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = S[r];
+    }
+    online_softmax<H ? 7 : 0>(v, m, l, O);
+    FragT<H> pf[2] = {split8t<H>(v), split8t<H>(v + 8)};
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // x_down(kb) (and W(kb + 1))
     __syncthreads();
-    Frag df = kord_frag(D, l32, 0, h);
+    FragT<H> df = d_frag(D, l32, 0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int s = i >> 2, cb = i & 3;
-      Frag nxt;
-      if (i < 7) nxt = kord_frag(D, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2, h);
+      FragT<H> nxt;
+      if (i < 7) nxt = d_frag(D, 32 * ((i + 1) & 3) + l32, (i + 1) >> 2);
       SCHED_FENCE();
-      O[cb] = mfma6(df, pf[s], O[cb]);
+      O[cb] = mma<H>(df, pf[s], O[cb]);
       SCHED_FENCE();
       if (i < 7) df = nxt;
     }
@@ -894,6 +1114,10 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
 #define UNPOOL4_DEFAULT 1
 #endif
 int g_unpool4 = UNPOOL4_DEFAULT;   // mvr_set_unpool4: the 4-wave diff_unpool kernel (0: the 8-wave one, A/B timing)
+#ifndef ATTN_MATH_DEFAULT
+#define ATTN_MATH_DEFAULT 1
+#endif
+int g_attn_h = ATTN_MATH_DEFAULT;  // mvr_set_attn_math: split-fp16 (1) or split-bf16 (0) pool / 4-wave unpool
 
 }  // namespace mvr
 
@@ -905,7 +1129,7 @@ static int64_t round_up4(int64_t x) { return (x + 3) & ~(int64_t)3; }
 extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int clusters) {
   if (P <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return 0;
   const size_t nkb = (size_t)(clusters + AKB - 1) / AKB;
-  return nkb * (WIMG + (size_t)P * IMG) + 256;
+  return nkb * (WIMG + (size_t)P * IMG + AKB * sizeof(float2)) + 512;   // W image, x_down images, bs, flag
 }
 
 // Key splits of the pool launch: with one 512-thread workgroup per CU, P x ceil(Kc / 256) workgroups
@@ -932,9 +1156,10 @@ static int pool_splits(int P, int nqb, int N) {
   return best;
 }
 
+// pool workspace: [nks > 1: per-split slabs, slot tickets] [range flag]
 static size_t pool_ws_bytes(int P, int clusters, int nks) {
   const size_t slots = (size_t)P * ((clusters + AQ - 1) / AQ);
-  return nks > 1 ? slots * ((size_t)nks * PSLAB * 4 + 4) + 512 : 0;
+  return (nks > 1 ? slots * ((size_t)nks * PSLAB * 4 + 4) : 0) + 512;
 }
 
 extern "C" size_t mvr_oan_diff_pool_workspace_bytes(int P, int channels, int clusters) {
@@ -976,21 +1201,37 @@ extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x
   a.out = out; a.ops = out_pstride; a.old = out_ld;
   a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
   a.nks = 1;
+  const size_t slots = (size_t)P * a.nqb;
+  int* range = nullptr;   // split-fp16 needs the workspace's flag word
   if (workspace && al16(workspace)) {
     const int k = pool_splits(P, a.nqb, N);
     if (k > 1 && workspace_bytes >= pool_ws_bytes(P, clusters, k)) {
-      const size_t slots = (size_t)P * a.nqb;
       a.nks = k;
       a.part = reinterpret_cast<float*>(workspace);
       a.cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + slots * (size_t)k * PSLAB * 4);
-      if (hipMemsetAsync(a.cnt, 0, slots * sizeof(int), stream) != hipSuccess) return MVR_ELAUNCH;
     }
+    if (g_attn_h && workspace_bytes >= pool_ws_bytes(P, clusters, a.nks))
+      range = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
+                                     (a.nks > 1 ? slots * ((size_t)a.nks * PSLAB * 4 + 4) : 0));
+  }
+  // the tickets and the flag word are adjacent: one memset
+  if (a.nks > 1 || range) {
+    void* z = a.nks > 1 ? (void*)a.cnt : (void*)range;
+    const size_t zb = (a.nks > 1 ? slots * sizeof(int) : 0) + (range ? sizeof(int) : 0);
+    if (hipMemsetAsync(z, 0, zb, stream) != hipSuccess) return MVR_ELAUNCH;
   }
   const double fl = 4.0 * AC * clusters * (double)N * P;
   const double by = 4.0 * AC * ((double)N + clusters) * P;
   ProfScope prof(PK_POOL, fl, by, stream);
   const int grid = ((P + 7) / 8) * 8 * a.nqb * a.nks;
-  hipLaunchKernelGGL(oan_pool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
+  if (range) {   // split-fp16, then the split-bf16 re-run that returns at once unless an operand was out of range
+    a.range = range;
+    hipLaunchKernelGGL(oan_pool_kernel<1>, dim3(grid), dim3(ATHREADS), 0, stream, a);
+    MVR_CHECK_LAUNCH();
+    a.range = nullptr;
+    a.guard = range;
+  }
+  hipLaunchKernelGGL(oan_pool_kernel<0>, dim3(grid), dim3(ATHREADS), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }
@@ -1012,32 +1253,74 @@ extern "C" int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t
   const int nkb = (clusters + AKB - 1) / AKB;
   char* wimg = reinterpret_cast<char*>(workspace);
   char* dimg = wimg + (size_t)nkb * WIMG;
+  float2* bs = reinterpret_cast<float2*>(dimg + (size_t)P * nkb * IMG);
+  int* range = reinterpret_cast<int*>(bs + (size_t)nkb * AKB);
   const double fl = 4.0 * AC * clusters * (double)N * P;
   const double by = 4.0 * AC * (2.0 * N + clusters) * P;
   ProfScope prof(PK_UNPOOL, fl, by, stream);
-  hipLaunchKernelGGL(split_w_kernel, dim3((nkb * 512 + 255) / 256), dim3(256), 0, stream, weight, clusters, nkb, wimg);
-  MVR_CHECK_LAUNCH();
-  const int64_t nx = (int64_t)P * nkb * 1024;
-  hipLaunchKernelGGL(split_xd_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, stream, x_down, xd_pstride,
-                     xd_ld, P, clusters, nkb, dimg);
-  MVR_CHECK_LAUNCH();
   UnpoolArgs a{};
   a.X = x_up; a.xps = x_pstride; a.xld = x_ld;
   a.sc = sc; a.sh = sh; a.sps = s_pstride;
-  a.wimg = wimg; a.bias = bias; a.dimg = dimg;
+  a.wimg = wimg; a.bias = bias; a.bs = bs; a.dimg = dimg;
   a.P = P; a.N = N; a.Kc = clusters; a.nkb = nkb; a.nqb = (N + AQ - 1) / AQ;
   a.out = out; a.ops = out_pstride; a.old = out_ld;
   a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
+  const int64_t nx = (int64_t)P * nkb * 1024;
+  const dim3 gw((nkb * 512 + 255) / 256), gx((unsigned)((nx + 255) / 256));
   if (g_unpool4 && clusters <= 512) {
     a.nqb = (N + U4Q - 1) / U4Q;
     const int grid = ((P + 7) / 8) * 8 * a.nqb;
-    hipLaunchKernelGGL(oan_unpool4_kernel, dim3(grid), dim3(U4T), 0, stream, a);
+    const int* guard = nullptr;
+    if (g_attn_h) {   // split-fp16, then the split-bf16 re-run that returns at once unless an operand was out of range
+      if (hipMemsetAsync(range, 0, sizeof(int), stream) != hipSuccess) return MVR_ELAUNCH;
+      hipLaunchKernelGGL(split_w_kernel<1>, gw, dim3(256), 0, stream, weight, bias, clusters, nkb, wimg, bs, range,
+                         nullptr);
+      MVR_CHECK_LAUNCH();
+      hipLaunchKernelGGL(split_xd16_kernel, dim3((unsigned)(((int64_t)P * AC * 64 + 255) / 256)), dim3(256), 0, stream,
+                         x_down, xd_pstride, xd_ld, P, clusters, nkb, dimg, range);
+      MVR_CHECK_LAUNCH();
+      a.range = range;
+      hipLaunchKernelGGL(oan_unpool4_kernel<1>, dim3(grid), dim3(U4T), 0, stream, a);
+      MVR_CHECK_LAUNCH();
+      a.range = nullptr;
+      a.guard = guard = range;
+    }
+    hipLaunchKernelGGL(split_w_kernel<0>, gw, dim3(256), 0, stream, weight, bias, clusters, nkb, wimg, bs, nullptr,
+                       guard);
+    MVR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(split_xd_kernel, gx, dim3(256), 0, stream, x_down, xd_pstride, xd_ld, P, clusters, nkb, dimg,
+                       guard);
+    MVR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(oan_unpool4_kernel<0>, dim3(grid), dim3(U4T), 0, stream, a);
   } else {
+    hipLaunchKernelGGL(split_w_kernel<0>, gw, dim3(256), 0, stream, weight, bias, clusters, nkb, wimg, bs, nullptr,
+                       nullptr);
+    MVR_CHECK_LAUNCH();
+    hipLaunchKernelGGL(split_xd_kernel, gx, dim3(256), 0, stream, x_down, xd_pstride, xd_ld, P, clusters, nkb, dimg,
+                       nullptr);
+    MVR_CHECK_LAUNCH();
     const int grid = ((P + 7) / 8) * 8 * a.nqb;
     hipLaunchKernelGGL(oan_unpool_kernel, dim3(grid), dim3(ATHREADS), 0, stream, a);
   }
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_attn_reruns(int reset) {
+  int v = 0;
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_attn_reruns), sizeof(int)) != hipSuccess)
+    return -1;
+  if (reset) {
+    const int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_attn_reruns), &z, sizeof(int)) != hipSuccess) return -1;
+  }
+  return v;
+}
+
+extern "C" int mvr_set_attn_math(int h) {
+  const int prev = mvr::g_attn_h;
+  mvr::g_attn_h = h ? 1 : 0;
+  return prev;
 }
 
 extern "C" int mvr_set_unpool4(int on) {

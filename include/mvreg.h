@@ -130,6 +130,13 @@ int mvr_set_pool_split(int on);
 /* diff_unpool kernel choice (process-wide): 1 (default) the 4-wave, two-per-CU kernel when clusters <= 512,
  * 0 the 8-wave kernel (A/B timing).  Returns the previous setting. */
 int mvr_set_unpool4(int on);
+/* operand math of diff_pool and the 4-wave diff_unpool: 1 (default) split-fp16 (3 MFMAs per product, weight
+   rows range-scaled, activations range-checked with a split-bf16 re-run when one exceeds the fp16 range),
+   0 split-bf16 (6 MFMAs).  Returns the previous setting. */
+int mvr_set_attn_math(int h);
+/* Diagnostics: how many split-bf16 re-runs of split-fp16 attention launches ran on the current device since
+   the last reset (synchronises the device); -1 on error. */
+int mvr_attn_reruns(int reset);
 /* Debugging: while buf is non-NULL, every mvr_oan_block_forward launch sequence adds a position-weighted
  * 64-bit hash of each stage's activation to the next of cap device slots (zeroed by the caller);
  * NULL disables.  Not for concurrent use from two streams. */

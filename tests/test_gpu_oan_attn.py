@@ -3,8 +3,10 @@ lib/filtering/oanet.py:96-129 on the same inputs, including ragged sizes (N and 
 multiples, pair counts not a multiple of the 8-pair XCD group), the per-tile InstanceNorm
 partials, and the whole OANet block with the fused path on vs off.
 
-Tolerance: the kernels compute in fp32 with split-bf16 MFMA products (fp32-level accuracy), so
-outputs are compared to fp64 at 2e-5 relative to the output scale."""
+Tolerance: the kernels compute in fp32 with split MFMA products — split-bf16 (three bf16 terms, 6 MFMAs) or the
+default split-fp16 (two fp16 terms, 22 significant bits, 3 MFMAs; mvr_set_attn_math) — so outputs are compared to
+fp64 at 2e-5 relative to the output scale.  Operands outside the fp16 range send a split-fp16 launch to its
+split-bf16 re-run: the outputs are then bit-identical to a split-bf16 launch."""
 import numpy as np
 import pytest
 
@@ -43,11 +45,20 @@ def _tile_stats(y, L):
     return out
 
 
+@pytest.fixture(params=[1, 0], ids=["fp16x2", "bf16x3"])
+def math(request):
+    from lib import _native as NV
+    prev = NV.lib().mvr_set_attn_math(request.param)
+    yield request.param
+    NV.lib().mvr_set_attn_math(prev)
+
+
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (41, 700, 300)])
-def test_diff_pool_matches_fp64(gpu, P, N, Kc, split):
+def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
     """split: mvr_oan_diff_pool_ws with a workspace (points split over 2-4 workgroups per (pair, cluster
-    block) and merged by the last one; N >= 256 here always splits on a 256-CU part)"""
+    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  The split-fp16 math
+    needs the workspace's flag word: without one the launch is split-bf16."""
     import torch
     from lib import _native as NV
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 1000 + N)
@@ -81,9 +92,9 @@ def test_diff_pool_matches_fp64(gpu, P, N, Kc, split):
     np.testing.assert_allclose(st.cpu().numpy()[..., 1], sref[..., 1], rtol=1e-4, atol=1e-6 * scale ** 2 * 128)
 
 
-@pytest.mark.parametrize("kern", [1, 0])   # mvr_set_unpool4: 4-wave two-per-CU kernel / 8-wave kernel
+@pytest.mark.parametrize("kern", [1, 0])   # mvr_set_unpool4: 4-wave two-per-CU kernel / 8-wave kernel (bf16x3)
 @pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (2, 300, 700)])
-def test_diff_unpool_matches_fp64(gpu, P, N, Kc, kern):
+def test_diff_unpool_matches_fp64(gpu, P, N, Kc, kern, math):
     from lib import _native as NV
     prev = NV.lib().mvr_set_unpool4(kern)
     try:
@@ -92,7 +103,7 @@ def test_diff_unpool_matches_fp64(gpu, P, N, Kc, kern):
         NV.lib().mvr_set_unpool4(prev)
 
 
-def _unpool_case(gpu, P, N, Kc):
+def _unpool_case(gpu, P, N, Kc, edit=None, check=True):
     import torch
     from lib import _native as NV
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 7 + N)
@@ -101,6 +112,8 @@ def _unpool_case(gpu, P, N, Kc):
     xdn = np.zeros((P, C, Kp), np.float32)
     xdn[:, :, :Kc] = r.standard_normal((P, C, Kc))
     xdn[:, :, Kc:] = 123.0   # padding columns must not enter
+    if edit:
+        edit(x, sc, sh, W, b, xdn)
     _, e = _embed(x, sc, sh, W, b, N)
     ref = (torch.from_numpy(xdn[:, :, :Kc]).double() @ torch.softmax(e, dim=1)).numpy()   # oanet.py:124-128
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
@@ -117,6 +130,8 @@ def _unpool_case(gpu, P, N, Kc):
                                  NV.ptr(st), 2 * C, C, NV.ptr(wbuf), ws, NV.stream()) == 0
     torch.cuda.synchronize()
     o = out.cpu().numpy()
+    if not check:
+        return o, st.cpu().numpy()
     assert np.isnan(o[:, :C]).all()
     scale = np.abs(ref).max()
     np.testing.assert_allclose(o[:, C:, :N], ref, atol=2e-5 * scale, rtol=0)
@@ -126,6 +141,153 @@ def _unpool_case(gpu, P, N, Kc):
     assert np.all(s[:, :, :C] == 0)
     np.testing.assert_allclose(s[:, :, C:, 0], sref[..., 0], atol=2e-5 * scale * 128, rtol=0)
     np.testing.assert_allclose(s[:, :, C:, 1], sref[..., 1], rtol=1e-4, atol=1e-6 * scale ** 2 * 128)
+
+
+def _pool_run(gpu, P, N, Kc, edit):
+    import torch
+    from lib import _native as NV
+    x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=5 * P + N)
+    edit(x, sc, sh, W, b)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu)
+    Kp = (Kc + 3) // 4 * 4
+    out = torch.full((P, C, Kp), float("nan"), device=gpu)
+    st = torch.zeros((P, (Kc + 127) // 128, C, 2), device=gpu)
+    L = NV.lib()
+    nb = L.mvr_oan_diff_pool_workspace_bytes(P, C, Kc)
+    wbuf = torch.full((nb,), 0xAB, dtype=torch.uint8, device=gpu)
+    gx, gsc, gsh, gW, gb = t(x), t(sc), t(sh), t(W), t(b)
+    assert L.mvr_oan_diff_pool_ws(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb), P, C, N,
+                                  Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.ptr(wbuf), nb, NV.stream()) == 0
+    torch.cuda.synchronize()
+    xd, e = _embed(x, sc, sh, W, b, N)
+    ref = (xd @ torch.softmax(e, dim=2).transpose(1, 2)).numpy()
+    return out.cpu().numpy(), st.cpu().numpy(), ref
+
+
+def _big_x(x, sc, sh, W, b, *rest):
+    x[1, 7, 11] = 7.0e4          # a raw value past the fp16 range (pool: the V operand), normalised into it
+    sc[1, 7] = 1.0e-3            # (unpool: queries in range, no re-run)
+
+
+def _big_xn(x, sc, sh, W, b, *rest):
+    sc[0, 3] = 3.0e4             # normalised values past it (pool: K operand; unpool: the queries)
+
+
+def _big_w(x, sc, sh, W, b, *rest):
+    W *= 2.0e5                   # weights far past it, activations far below: the logit floor bound
+    sc *= 1.0e-5                 # (sum_c |W[j][c]| > 128) re-runs
+    sh *= 1.0e-5
+
+
+def _mid_w(x, sc, sh, W, b, *rest):
+    W[5] *= 6.0                  # sum_c |W[j][c]| ~ 130 on one row: re-runs
+    W[:5] *= 3.0                 # ~ 65 on others: not on its own
+
+
+def _small_v(x, sc, sh, W, b, *rest):
+    x[2, 40] *= 1.0e-3           # one raw row (pool's V operand) below 2^-3: re-runs
+
+
+def _tiny_w(x, sc, sh, W, b, *rest):
+    W *= 1.0e-6                  # and far below (fp16 subnormals without the row scale)
+
+
+POOL_RERUN = ("_big_x", "_big_xn", "_big_w", "_mid_w", "_small_v")
+
+
+@pytest.mark.parametrize("edit", [_big_x, _big_xn, _big_w, _mid_w, _small_v, _tiny_w])
+def test_diff_pool_fp16_range(gpu, edit):
+    """split-fp16 pool: weight rows are scaled into range (results as close to fp64 as in range); an operand
+    outside the split-fp16 precision window (oan_attn.hip: activations past 65504, a weight row with
+    sum |W| log2 e > 128, a V row in (0, 2^-3)) re-runs the launch in split-bf16 (output and statistics
+    bit-identical to it)"""
+    from lib import _native as NV
+    L = NV.lib()
+    prev = L.mvr_set_attn_math(0)
+    try:
+        o0, s0, ref = _pool_run(gpu, 3, 1234, 500, edit)
+        L.mvr_set_attn_math(1)
+        L.mvr_attn_reruns(1)
+        o1, s1, _ = _pool_run(gpu, 3, 1234, 500, edit)
+    finally:
+        L.mvr_set_attn_math(prev)
+    assert (L.mvr_attn_reruns(1) > 0) == (edit.__name__ in POOL_RERUN)
+    if edit.__name__ in POOL_RERUN:   # re-run (fp64 agreement is then the split-bf16 kernel's, at logits ~1e4)
+        assert np.array_equal(o0, o1) and np.array_equal(s0, s1)
+        return
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(o1[:, :, :500], ref, atol=2e-5 * scale, rtol=0)
+    if edit is _tiny_w:
+        assert not np.array_equal(o0, o1)   # the fp16 launch's own result
+
+
+def _big_xd(x, sc, sh, W, b, xdn):
+    xdn[1, 9, 17] = -9.0e4       # unpool V operand past the fp16 range
+
+
+def _small_xd(x, sc, sh, W, b, xdn):
+    xdn[0, 100] *= 1.0e-4        # one x_down row below 2^-3
+
+
+UNPOOL_RERUN = ("_big_xd", "_small_xd", "_big_xn", "_big_w", "_mid_w")
+
+
+@pytest.mark.parametrize("edit", [_big_xd, _small_xd, _big_xn, _big_w, _mid_w, _big_x, _tiny_w])
+def test_diff_unpool_fp16_range(gpu, edit):
+    from lib import _native as NV
+    L = NV.lib()
+    prev = L.mvr_set_attn_math(0)
+    try:
+        o0, s0 = _unpool_case(gpu, 3, 1234, 500, edit, check=False)
+        L.mvr_set_attn_math(1)
+        L.mvr_attn_reruns(1)
+        o1, s1 = _unpool_case(gpu, 3, 1234, 500, edit, check=False)
+        assert (L.mvr_attn_reruns(1) > 0) == (edit.__name__ in UNPOOL_RERUN)
+        if edit.__name__ not in UNPOOL_RERUN:
+            _unpool_case(gpu, 3, 1234, 500, edit)   # vs fp64
+    finally:
+        L.mvr_set_attn_math(prev)
+    if edit.__name__ in UNPOOL_RERUN:
+        assert np.array_equal(o0, o1, equal_nan=True) and np.array_equal(s0, s1)
+    elif edit is _tiny_w:
+        assert not np.array_equal(o0, o1, equal_nan=True)
+
+
+def test_oanet_default_init_runs_fp16_attention(gpu):
+    """The RegBlock OANet (128 channels, 500 clusters, PyTorch default initialisation as in bench.py) on
+    synthetic correspondences: no diff_pool / diff_unpool launch leaves the split-fp16 window, and the outputs
+    stay within the fused-path tolerances of the split-bf16 run."""
+    import torch
+    from lib import _native as NV
+    from lib.filtering.oanet import OANet
+    from synth import synth_correspondences
+    torch.manual_seed(0)
+    cfg = {"misc": {"iter_num": 1, "net_depth": 12, "net_channel": 128, "clusters": 500, "normalize_weights": True,
+                    "use_gpu": True}, "data": {"use_mutuals": 0}}
+    net = OANet(cfg).to(gpu).eval()
+    xs, _, _ = synth_correspondences(8, 3000, seed=4)
+    L = NV.lib()
+    outs = []
+    prev = L.mvr_set_attn_math(1)
+    try:
+        for mth in (1, 0):
+            L.mvr_set_attn_math(mth)
+            L.mvr_attn_reruns(1)
+            with torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1).to(gpu)}))
+            assert L.mvr_attn_reruns(1) == 0
+    finally:
+        L.mvr_set_attn_math(prev)
+    a, b = outs
+    for i in range(2):
+        la, lb = a["logits"][i].cpu().numpy(), b["logits"][i].cpu().numpy()
+        assert not np.array_equal(la, lb)
+        np.testing.assert_allclose(la, lb, atol=2e-3, rtol=1e-4)
+        np.testing.assert_allclose(a["rot_est"][i].cpu().numpy(), b["rot_est"][i].cpu().numpy(), atol=1e-4)
+        np.testing.assert_allclose(a["trans_est"][i].cpu().numpy(), b["trans_est"][i].cpu().numpy(), atol=1e-4)
+        sa, sb = a["scores"][i].cpu().numpy(), b["scores"][i].cpu().numpy()
+        near = np.abs(sb - 0.5) < 1e-4
+        assert np.array_equal((sa > 0.5)[~near], (sb > 0.5)[~near])
 
 
 def test_diff_pool_rejects_bad_layout(gpu):
@@ -183,7 +345,9 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
     (fp32 itself lands up to 2e-4 from exact arithmetic, and either GPU path up to ~1.6e-4 from the fp32
     oracle on pairs where fp32 and fp64 happen to agree: tools/diag_fold2.py; the two GPU paths differ
     only by fp32 rounding of x and its statistics), so the folded path must be as close to the fp64 oracle
-    as the materialised path or the fp32 oracle is (within 3x), or within 1e-4 of it.  (The materialised path's own parity: the golden and oracle tests of test_gpu_oanet.py.)  Below ~100 points the Procrustes is
+    as the materialised path or the fp32 oracle is (within 3x), or within 2e-4 of it (the split-fp16 attention
+    carries 22-bit operands: on the most sensitive pair (1200 points, train mode) the folded path lands 1.7e-4
+    from fp64 where the fp32 oracle is 1.7e-5 away and the materialised path 5e-5).  (The materialised path's own parity: the golden and oracle tests of test_gpu_oanet.py.)  Below ~100 points the Procrustes is
     ill-conditioned for every path (1e-2..1 from fp64 at 33 points: tools/diag_fold.py): block-0 logits
     only.  Eval and train-mode BatchNorm, ragged point counts."""
     import torch
@@ -221,5 +385,5 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
         for k in ("rot_est", "trans_est"):
             f, m = a[k][i].cpu().numpy(), b[k][i].cpu().numpy()
             r32, r64 = o32[k][i], o64[k][i]
-            bound = np.maximum(1e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
+            bound = np.maximum(2e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
             assert (dist(f, r64) <= bound).all(), (i, k, dist(f, r64), dist(m, r64), dist(r32, r64))

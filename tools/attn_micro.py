@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--clusters", type=int, default=K)
     ap.add_argument("--points", type=int, default=N)
+    ap.add_argument("--math", type=int, default=-1, help="1 split-fp16, 0 split-bf16, -1 both (+ max difference)")
     a = ap.parse_args()
     run(a, a.clusters, a.points)
 
@@ -38,13 +39,13 @@ def run(a, K, N):
     st_d = torch.empty(P, (K + 127) // 128, C, 2, device=d)
     st_u = torch.empty(P, (N + 127) // 128, C, 2, device=d)
     L = NV.lib()
-    ws = L.mvr_oan_diff_unpool_workspace_bytes(P, C, K)
+    ws = max(L.mvr_oan_diff_unpool_workspace_bytes(P, C, K), L.mvr_oan_diff_pool_workspace_bytes(P, C, K))
     wbuf = torch.empty(ws, dtype=torch.uint8, device=d)
     s = NV.stream()
 
     def pool():
-        assert L.mvr_oan_diff_pool(NV.ptr(x), C * N, N, NV.ptr(sc), NV.ptr(sh), C, NV.ptr(W), NV.ptr(b), P, C, N, K,
-                                   NV.ptr(out_d), C * K, K, NV.ptr(st_d), C, 0, s) == 0
+        assert L.mvr_oan_diff_pool_ws(NV.ptr(x), C * N, N, NV.ptr(sc), NV.ptr(sh), C, NV.ptr(W), NV.ptr(b), P, C, N,
+                                      K, NV.ptr(out_d), C * K, K, NV.ptr(st_d), C, 0, NV.ptr(wbuf), ws, s) == 0
 
     def unpool():
         assert L.mvr_oan_diff_unpool(NV.ptr(x), C * N, N, NV.ptr(sc), NV.ptr(sh), C, NV.ptr(W), NV.ptr(b), NV.ptr(xd),
@@ -53,9 +54,25 @@ def run(a, K, N):
 
     flops = 4.0 * C * K * N * P
     print("P=%d N=%d clusters=%d" % (P, N, K))
-    for name, fn in (("pool", pool), ("unpool", unpool)):
+    maths = [a.math] if a.math >= 0 else [0, 1]
+    for name, fn, o in (("pool", pool, out_d), ("unpool", unpool, out_u)):
         if a.only and a.only != name:
             continue
+        res = {}
+        for mth in maths:
+            L.mvr_set_attn_math(mth)
+            fn()
+            torch.cuda.synchronize()
+            res[mth] = o.clone()
+            time_it(a, name + "/h%d" % mth, fn, flops)
+        if len(res) == 2:
+            d = (res[0] - res[1]).abs().max().item()
+            print("%-7s max |h1 - h0| %.3e (max |out| %.3e)" % (name, d, res[0].abs().max().item()), flush=True)
+        L.mvr_set_attn_math(1)
+
+
+def time_it(a, name, fn, flops):
+    if True:
         for _ in range(2):
             fn()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
