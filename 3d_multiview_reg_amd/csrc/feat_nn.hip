@@ -29,6 +29,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int NN_STAGE = 128;      // targets per LDS stage
 constexpr int NN_ROW = 32;         // bf16 per LDS plane row; 16-byte chunk c of row r sits at slot
@@ -72,6 +74,18 @@ __device__ __forceinline__ void nn_split8(const float4& a, const float4& b, u32x
     H[i] = hp;
     Mm[i] = mp;
     L[i] = nn_cvt_pk(r - nn_unpack(mp));
+  }
+}
+// 8 fp32 -> two fp16x8 terms of 2^8 x (x 2^8 = h + l to 2^-22 relative, 2^-25 absolute), as u32x4; the
+// fp16 form of the fast path (feat_nn_fast<1>): |x| < 2^7 keeps x 2^8 inside the fp16 range
+__device__ __forceinline__ void nn_split8h(const float4& a, const float4& b, u32x4& H, u32x4& L) {
+  const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = x[i] * 256.f;
+    const f16x2 hh = __builtin_convertvector(v, f16x2);
+    H[i] = __builtin_bit_cast(unsigned, hh);
+    L[i] = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(hh, f32x2), f16x2));
   }
 }
 __device__ __forceinline__ float nn_max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
@@ -328,6 +342,12 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
 //    chunk, and each lane keeps per-query partial sums over the targets it saw (4 x 16 registers),
 //    reduced across the 32 lanes once at the end.
 // Per (query, target): one fma, one exp2, one add, three fmas.
+// H = 0: the distance MFMAs on three-term split-bf16 (6 per k-step); H = 1: on two-term split-fp16 of the
+// features scaled by 2^8 (3 per k-step; the accumulator is in 2^16 units, undone in the logit's fma).  H = 1
+// needs |f|^2 < 2^14 for every query and target (|f_i| < 2^7: in range); a workgroup that sees a larger norm
+// falls back to the online path like an underflowed one.  Unit-norm descriptors: |f_i| <= 1, so the
+// absolute floor of the low term (2^-25 of the scaled value) is 2^-33 of a component.
+template <int H>
 __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   auto& Fp = sm.Fp;
   auto& Xf = sm.Xf;
@@ -343,6 +363,7 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
 
   // queries = A operand rows: lane row l32, dims 16s + 8kh + (0..7)
   bf16x8 qh[2], qm[2], ql[2];
+  f16x8 q16h[2], q16l[2];
   float q2 = 0.f;
   {
     const int jq = q0 + l32;
@@ -354,17 +375,25 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      u32x4 H, Mm, L;
-      nn_split8(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], H, Mm, L);
-      qh[s] = __builtin_bit_cast(bf16x8, H);
-      qm[s] = __builtin_bit_cast(bf16x8, Mm);
-      ql[s] = __builtin_bit_cast(bf16x8, L);
+      u32x4 Hh, Mm, L;
+      if (H) {
+        nn_split8h(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], Hh, L);
+        q16h[s] = __builtin_bit_cast(f16x8, Hh);
+        q16l[s] = __builtin_bit_cast(f16x8, L);
+      } else {
+        nn_split8(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], Hh, Mm, L);
+        qh[s] = __builtin_bit_cast(bf16x8, Hh);
+        qm[s] = __builtin_bit_cast(bf16x8, Mm);
+        ql[s] = __builtin_bit_cast(bf16x8, L);
+      }
     }
   }
+  constexpr float ACC_UNIT = H ? 65536.f : 1.f;   // accumulator units (2^8 x 2^8 with H = 1)
+  bool bad = H && !(q2 < 16384.f);                 // H = 1 range (NaN included)
   // accumulator register r holds query row 8 (r >> 2) + 4 kh + (r & 3): its start value -|fs|^2 / 2
   floatx16 init;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) init[r] = -0.5f * __shfl(q2, 8 * (r >> 2) + 4 * kh + (r & 3), 64);
+  for (int r = 0; r < 16; ++r) init[r] = -0.5f * ACC_UNIT * __shfl(q2, 8 * (r >> 2) + 4 * kh + (r & 3), 64);
 
   const int srow = tid >> 1, shalf = tid & 1;
   float4 fr[4];
@@ -385,17 +414,24 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   auto store_lds = [&](int buf, int t0) {
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      u32x4 H, Mm, L;
-      nn_split8(fr[2 * g], fr[2 * g + 1], H, Mm, L);
+      u32x4 Hh, Mm, L;
       const int c = 8 * ((2 * shalf + g) ^ ((srow >> 2) & 3));
-      *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = H;
-      *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = Mm;
-      *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
+      if (H) {
+        nn_split8h(fr[2 * g], fr[2 * g + 1], Hh, L);
+        *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = Hh;
+        *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = L;
+      } else {
+        nn_split8(fr[2 * g], fr[2 * g + 1], Hh, Mm, L);
+        *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = Hh;
+        *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = Mm;
+        *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
+      }
     }
     float n2 = 0.f;
 #pragma unroll
     for (int v = 0; v < 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
     n2 += __shfl_xor(n2, 1, 64);
+    if (H) bad |= !(n2 < 16384.f);   // rows past Mt are zeros
     if (tid < NN_STAGE) {
       Xf[buf][tid].x = xr0;
       Xf[buf][tid].y = xr1;
@@ -408,7 +444,7 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   float S[16], AX[16], AY[16], AZ[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) S[r] = AX[r] = AY[r] = AZ[r] = 0.f;
-  const float kk2 = 2.f * a.k2;
+  const float kk2 = 2.f * a.k2 / ACC_UNIT;
   const int nst = (Mt + NN_STAGE - 1) / NN_STAGE;
   load_regs(0);
   store_lds(0, 0);
@@ -420,6 +456,19 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = 8 * ((2 * s + kh) ^ ((row >> 2) & 3));
+      if (H) {
+        const f16x8 th = *reinterpret_cast<const f16x8*>(&Fp[cur][0][row][c]);
+        const f16x8 tl = *reinterpret_cast<const f16x8*>(&Fp[cur][1][row][c]);
+        if (NN_ABL & 1) {
+          asm volatile("" ::"v"(th), "v"(tl));
+          acc[s] += 1.f;
+          continue;
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(q16l[s], th, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(q16h[s], tl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(q16h[s], th, acc, 0, 0, 0);
+        continue;
+      }
       const bf16x8 th = *reinterpret_cast<const bf16x8*>(&Fp[cur][0][row][c]);
       const bf16x8 tm = *reinterpret_cast<const bf16x8*>(&Fp[cur][1][row][c]);
       const bf16x8 tl = *reinterpret_cast<const bf16x8*>(&Fp[cur][2][row][c]);
@@ -475,7 +524,6 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       AZ[r] += __shfl_xor(AZ[r], o, 64);
     }
   }
-  bool bad = false;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int jq = q0 + 8 * (r >> 2) + 4 * kh + (r & 3);
@@ -503,7 +551,7 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   return true;
 }
 
-int g_nn_fast = 1;   // mvr_set_feat_nn_fast
+int g_nn_fast = 2;   // mvr_set_feat_nn_fast: 0 online path only, 1 fast path split-bf16, 2 fast path split-fp16
 
 // MODE 0 (soft) with a.fast: the bounded-shift path, falling back to the online path for a workgroup
 // whose softmax sums underflowed; otherwise the online path (MODE 1 argmax, 2 two nearest).
@@ -511,7 +559,7 @@ template <int MODE>
 __global__ __launch_bounds__(256, MODE == 0 ? 2 : 3) void feat_nn_kernel(NNArgs a) {
   __shared__ __attribute__((aligned(16))) NNSmem sm;
   if (MODE == 0 && a.fast) {
-    if (feat_nn_fast(a, sm)) return;
+    if (a.fast == 2 ? feat_nn_fast<1>(a, sm) : feat_nn_fast<0>(a, sm)) return;
     __syncthreads();
   }
   feat_nn_online<MODE>(a, sm);
@@ -607,6 +655,6 @@ extern "C" int mvr_gather_rows(const float* src, int C, const int64_t* idx, int 
 
 extern "C" int mvr_set_feat_nn_fast(int on) {
   const int prev = mvr::g_nn_fast;
-  mvr::g_nn_fast = on ? 1 : 0;
+  mvr::g_nn_fast = on < 0 ? 0 : on > 2 ? 2 : on;
   return prev;
 }

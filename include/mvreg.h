@@ -254,7 +254,9 @@ int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft
                 int32_t* idx_out, mvr_stream_t stream);
 /* Soft mode runs a bounded-shift softmax first (shift k2 |fs|^2 per query instead of a running maximum:
  * no max tracking or rescaling) and falls back to the online softmax per 128-query workgroup where a
- * softmax sum underflows (< 2^-60).  1 (default) on, 0 online only.  Returns the previous setting. */
+ * softmax sum underflows (< 2^-60).  2 (default) on, its distance MFMAs on two-term split-fp16 of the features
+ * scaled by 2^8 (3 MFMAs per k-step; a workgroup with a descriptor norm^2 >= 2^14 falls back too), 1 on with
+ * three-term split-bf16 (6 MFMAs), 0 online only.  Returns the previous setting. */
 int mvr_set_feat_nn_fast(int on);
 
 /* Two nearest neighbours in feature space (scripts/extract_data.py:178-184, sklearn NearestNeighbors

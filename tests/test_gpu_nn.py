@@ -51,22 +51,26 @@ def test_feat_nn_pairs_vs_oracle(gpu, n, m):
             assert bad.mean() < 1e-3, bad.mean()
 
 
-@pytest.mark.parametrize("scale", [1.0, 2.5])
-def test_feat_nn_fast_path_matches_online(gpu, scale):
-    """Soft mode: the bounded-shift path (feat_nn_fast) against the online-softmax path; at scale 2.5
-    some queries' softmax sums underflow the fast path and their workgroups fall back."""
+@pytest.mark.parametrize("scale,offset", [(1.0, 0.0), (2.5, 0.0), (0.05, 130.0)])
+def test_feat_nn_fast_path_matches_online(gpu, scale, offset):
+    """Soft mode: the bounded-shift path (feat_nn_fast, split-fp16 and split-bf16 distance MFMAs) against the
+    online-softmax path; at scale 2.5 some queries' softmax sums underflow the fast path and their workgroups
+    fall back; with a common offset of 150 the descriptors are close together (no underflow) but their norms
+    are past the split-fp16 range (|f|^2 >= 2^14): the fp16 form falls back."""
     import torch
     from lib import _native as NV
     from oracle.soft_nn import soft_nn
     B, n = 3, 2000
     f = unit_features(B, n, 32, seed=7)
-    f[1] *= np.float32(scale)           # fragment 1 farther from everything in feature space
+    f[1] *= np.float32(scale if offset == 0 else 1.0)   # fragment 1 farther from everything in feature space
+    if offset:
+        f = (f * np.float32(scale) + np.float32(offset / np.sqrt(32))).astype(np.float32)
     x = np.random.RandomState(6).uniform(-2, 2, (B, n, 3)).astype(np.float32)
     pairs = np.array([[0, 1], [1, 2], [2, 0]], dtype=np.int64)
     tf, tx, tp = (torch.from_numpy(a).to(gpu) for a in (f, x, pairs))
     L = NV.lib()
     outs = []
-    for fast in (1, 0):
+    for fast in (2, 1, 0):
         prev = L.mvr_set_feat_nn_fast(fast)
         out = torch.empty(len(pairs), n, 6, device=gpu)
         rc = L.mvr_feat_nn(NV.ptr(tf), n * 32, NV.ptr(tf), n * 32, NV.ptr(tx), n * 3, NV.ptr(tx), n * 3, NV.ptr(tp),
@@ -74,10 +78,17 @@ def test_feat_nn_fast_path_matches_online(gpu, scale):
         L.mvr_set_feat_nn_fast(prev)
         assert rc == 0
         outs.append(out.cpu().numpy())
-    ref = soft_nn(f[pairs[:, 0]], f[pairs[:, 1]], x[pairs[:, 1]], "soft", st=False)
-    assert np.all(np.isfinite(outs[0]))
-    np.testing.assert_allclose(outs[0][..., 3:], ref, atol=3e-5)
-    np.testing.assert_allclose(outs[0], outs[1], atol=3e-5)
+    for o in outs:
+        assert np.all(np.isfinite(o))
+    if offset:   # (|f|^2 ~ 2^14: fp32 distances themselves are off by ~1e-3 here, no oracle comparison)
+        assert np.array_equal(outs[0], outs[2])   # every fp16 workgroup fell back to the online path
+        return
+    ref = soft_nn(f[pairs[:, 0]].astype(np.float64), f[pairs[:, 1]].astype(np.float64),
+                  x[pairs[:, 1]].astype(np.float64), "soft", st=False)
+    for o in outs:
+        np.testing.assert_allclose(o[..., 3:], ref, atol=3e-5)
+    np.testing.assert_allclose(outs[0], outs[2], atol=3e-5)
+    np.testing.assert_allclose(outs[1], outs[2], atol=3e-5)
 
 
 def test_sampler_indices_and_gather(gpu):
