@@ -216,6 +216,9 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
 constexpr int SB_K = 32;     // input channels per step
 constexpr int SB_BST = 40;   // bf16 row stride of the weight image (80 B)
 constexpr int SB_CP = 128;   // output-channel padding of the weight image (largest TN)
+#ifndef SPBX_ABL
+#define SPBX_ABL 0   // timing ablation (wrong results; tools/build_variant.sh): 1 no MFMAs
+#endif
 #ifndef SPBX_NS32   // gathered steps in flight per output-channel tile width (register budget)
 #define SPBX_NS32 3
 #endif
@@ -353,7 +356,11 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
           fb.h = *reinterpret_cast<const bf16x8*>(bp);
           fb.m = *reinterpret_cast<const bf16x8*>(bp + BPL);
           fb.l = *reinterpret_cast<const bf16x8*>(bp + 2 * BPL);
+#if SPBX_ABL & 1
+          asm volatile("" ::"v"(fa.h), "v"(fa.m), "v"(fa.l), "v"(fb.h), "v"(fb.m), "v"(fb.l));
+#else
           acc[j] = mfma6(fa, fb, acc[j]);
+#endif
         }
       }
       __syncthreads();
