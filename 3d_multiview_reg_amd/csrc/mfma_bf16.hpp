@@ -83,5 +83,82 @@ __device__ __forceinline__ u32x2 ds_read_tr(const char* lds) {
   return __builtin_bit_cast(u32x2, r);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-math generic forms.  H = 0: the three-term split-bf16 above (6 MFMAs per product); H = 1: two-term
+// split-fp16, x = h + l, h = fp16(x), l = fp16(x - h) (RNE, x - h exact in fp32): 22 significant bits
+// (2^-22 relative for |x| >= 2^-3, 2^-25 absolute below, overflow at 65504), products hh, hl, lh on
+// v_mfma_f32_32x32x16_f16 (3 MFMAs).  Callers keep operands inside that window (see oan_attn.hip, pconv.hip).
+// ---------------------------------------------------------------------------------------------
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+constexpr float F16_RANGE = 65504.f;
+
+template <int H> struct FragT;
+template <> struct FragT<0> { typedef bf16x8 V; V p[3]; };
+template <> struct FragT<1> { typedef f16x8 V; V p[2]; };
+template <int H> constexpr int planes() { return H ? 2 : 3; }
+
+template <int H> __device__ __forceinline__ void split_pair(f32x2 x, unsigned* o);
+template <> __device__ __forceinline__ void split_pair<0>(f32x2 x, unsigned* o) {
+  o[0] = cvt_pk(x);
+  const f32x2 r = x - unpack(o[0]);
+  o[1] = cvt_pk(r);
+  o[2] = cvt_pk(r - unpack(o[1]));
+}
+template <> __device__ __forceinline__ void split_pair<1>(f32x2 x, unsigned* o) {
+  const f16x2 hh = __builtin_convertvector(x, f16x2);
+  o[0] = __builtin_bit_cast(unsigned, hh);
+  const f32x2 r = x - __builtin_convertvector(hh, f32x2);
+  o[1] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, f16x2));
+}
+// 4 fp32 -> one u32x2 (4 packed 16-bit terms) per plane
+template <int H> __device__ __forceinline__ void split4t(const float4& a, u32x2* o) {
+  unsigned lo[3], hi[3];
+  split_pair<H>(f32x2{a.x, a.y}, lo);
+  split_pair<H>(f32x2{a.z, a.w}, hi);
+#pragma unroll
+  for (int i = 0; i < planes<H>(); ++i) o[i] = u32x2{lo[i], hi[i]};
+}
+template <int H> __device__ __forceinline__ FragT<H> split8t(const float* v) {
+  unsigned t[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) split_pair<H>(f32x2{v[2 * i], v[2 * i + 1]}, t[i]);
+  FragT<H> f;
+#pragma unroll
+  for (int pl = 0; pl < planes<H>(); ++pl)
+    f.p[pl] = __builtin_bit_cast(typename FragT<H>::V, u32x4{t[0][pl], t[1][pl], t[2][pl], t[3][pl]});
+  return f;
+}
+// acc += A . B, small terms first
+template <int H> __device__ __forceinline__ floatx16 mma(const FragT<H>& a, const FragT<H>& b, floatx16 acc);
+template <> __device__ __forceinline__ floatx16 mma<0>(const FragT<0>& a, const FragT<0>& b, floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
+  return acc;
+}
+template <> __device__ __forceinline__ floatx16 mma<1>(const FragT<1>& a, const FragT<1>& b, floatx16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.p[0], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.p[0], b.p[0], acc, 0, 0, 0);
+  return acc;
+}
+// a fragment whose planes sit `ps` bytes apart
+template <int H> __device__ __forceinline__ FragT<H> ld_frag(const char* p, int ps) {
+  FragT<H> f;
+#pragma unroll
+  for (int pl = 0; pl < planes<H>(); ++pl) f.p[pl] = *reinterpret_cast<const typename FragT<H>::V*>(p + pl * ps);
+  return f;
+}
+// power-of-two scale bringing |x| <= amax to <= 2^14 (amax = 0: 2^14)
+__device__ __forceinline__ float range_scale(float amax) {
+  int e;
+  (void)frexpf(amax, &e);   // amax < 2^e
+  return ldexpf(1.f, min(max(14 - e, -64), 64));
+}
+
 }  // namespace bx
 }  // namespace mvr

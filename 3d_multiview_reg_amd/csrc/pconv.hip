@@ -25,6 +25,9 @@
 // a group come from one workgroup and consecutive chunks of a workgroup share cache lines.
 // Roofline: 2*128*128 flops per point-pair column against (128 + 128 (+128 residual)) * 4 bytes:
 // AI = 32 (21 with the residual) flop/B < the split-MFMA ridge -> HBM-bound.
+#include <atomic>
+#include <utility>
+
 #include "common.hpp"
 #include "gemm.hpp"
 #include "mfma_bf16.hpp"
@@ -41,6 +44,14 @@ namespace mvr {
 #endif
 
 int g_pconv = 1;   // mvr_set_pconv: 0 routes these convs to gemm_kernel (A/B timing)
+#ifndef PCONV_MATH_DEFAULT
+#define PCONV_MATH_DEFAULT 1
+#endif
+int g_pconv_h = PCONV_MATH_DEFAULT;   // mvr_set_pconv_math: 1 split-fp16 (re-run in split-bf16 when out of range)
+
+// flag words of split-fp16 launches: launch i uses slot i % 1024 and marks it with its own epoch i + 1, so
+// slots need no clearing (a stale mark is another launch's epoch)
+__device__ int g_pc_flags[1024];
 
 namespace {
 
@@ -66,6 +77,8 @@ struct PcArgs {
   float* logits; float* scores; int32_t* pos;   // [P][N], [P][N], [P]
   int xci; const float* xw; const float* xb;    // XI: x(k, n) = xb[k] + xw[k][:xci] . in(:, n) (xw [128][8])
   int64_t rld;                                  // XI & 2: row stride of the block input R
+  int* range; const int* guard; int epoch;      // split-fp16: flag word set to epoch when an activation is out
+                                                // of range; split-bf16 re-run: return unless *guard == epoch
 };
 
 #define PC_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -91,9 +104,19 @@ __device__ __forceinline__ float sum8(float v) {
 // KS = 16 form has one wave per SIMD and cannot overlap its MFMA chain with its own memory waits); the
 // upper half's partial sums reach the lower half's waves through LDS one step later, which then run the
 // epilogue for both (no residual / head there).
-template <int KS, int PRO, int RES, int STATS, int HEAD, int XI = 0, int KW = 1>
+// H = 1: split-fp16 operands (mfma_bf16.hpp: 3 MFMAs per product instead of 6, 2-plane images).  Each
+// weight row is scaled by a power of two to <= 2^14 and the activations by XS = 2^6 as they are split
+// (activations are O(1) — IN + BN + ReLU outputs, or the block's residual stream —: 22-bit precision down to
+// 2^-9, below 65504 up to 1023); the epilogue undoes both per row.  A lane that splits an activation of
+// 1023.5 or more, or whose activations (8 input rows over all its chunks) are all below 2^-9 without being
+// all zero, marks the launch, whose split-bf16 re-run then replaces every output.
+template <int KS, int PRO, int RES, int STATS, int HEAD, int XI = 0, int KW = 1, int H = 0>
 __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs a) {
   constexpr int CIN = 16 * KS;   // input channels
+  constexpr int FRBT = planes<H>() * 1024;     // one k-step's fragment set: planes x 64 lanes x 16 B
+  constexpr float XS = H ? 64.f : 1.f;
+  static_assert(!H || HEAD == 0, "the head's positive counts are not re-runnable");
+  if (a.guard && *a.guard != a.epoch) return;   // uniform: the split-fp16 launch stayed in range
   constexpr int NWV = 4 * KW;    // waves
   constexpr int KSW = KS / KW;   // k-steps each wave multiplies
   constexpr int NT = KS / NWV;   // 16-row k-steps each wave loads and splits per chunk
@@ -101,7 +124,8 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   constexpr int NX = (XI & 1) ? 8 : 8 * NT;   // activation registers per chunk
   static_assert(!XI || KS == 8, "conv1 folding: 128-channel convs");
   static_assert(KW == 1 || (KS == 16 && KW == 2 && !RES && !HEAD && !XI), "k-split: the 256 -> 128 convs");
-  __shared__ __attribute__((aligned(16))) char xi[2][KS * FRB];      // chunk images (B fragments)
+  __shared__ __attribute__((aligned(16))) char xi[2][KS * FRBT];     // chunk images (B fragments)
+  __shared__ float srisc[H ? PC : 1];                                // H = 1: 1 / (row scale XS)
   __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];   // per wave: residual DMA / transpose
   __shared__ __attribute__((aligned(16))) float fold[2][2][CIN];   // (sc, sh) by pair parity
   __shared__ float sbias[PC];
@@ -144,18 +168,31 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   const int64_t c1 = (int64_t)p1 * nch + min(GRP * (int)(g1 - (int64_t)p1 * a.ngrp), nch);
   const int nloc = (int)(c1 - c0);
 
-  // weights -> split A fragments: row 32w + l32, k = 128 kh + 16q + 8h + 0..7
-  Frag wf[KSW];
+  // weights -> split A fragments: row 32w + l32, k = 128 kh + 16q + 8h + 0..7 (H = 1: the row scaled)
+  FragT<H> wf[KSW];
   {
-    const float* wr = a.W + (int64_t)(32 * w + l32) * a.wld + 128 * kh * (KW - 1) + 8 * h;
+    const float* wrow = a.W + (int64_t)(32 * w + l32) * a.wld;
+    float wsc = 1.f;
+    if (H) {   // the whole row (every lane of the row's waves / halves derives the same scale)
+      float amax = 0.f;
+      for (int k = 0; k < CIN; k += 4) {
+        const float4 u = *reinterpret_cast<const float4*>(wrow + k);
+        amax = fmaxf(fmaxf(amax, fmaxf(fabsf(u.x), fabsf(u.y))), fmaxf(fabsf(u.z), fabsf(u.w)));
+      }
+      wsc = range_scale(amax);
+      if (kh == 0 && h == 0) srisc[32 * w + l32] = 1.f / (wsc * XS);   // published by the prologue barriers
+    }
+    const float* wr = wrow + 128 * kh * (KW - 1) + 8 * h;
 #pragma unroll
     for (int q = 0; q < KSW; ++q) {
       const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * q);
       const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * q + 4);
-      const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      split8(v, wf[q].h, wf[q].m, wf[q].l);
+      const float v[8] = {u0.x * wsc, u0.y * wsc, u0.z * wsc, u0.w * wsc, u1.x * wsc, u1.y * wsc, u1.z * wsc, u1.w * wsc};
+      wf[q] = split8t<H>(v);
     }
   }
+  bool xbad = false;   // H = 1: an activation of this lane's splits past the fp16 range
+  float xmx = 0.f;     // H = 1: max |activation| x XS of this lane's splits
   // epilogue ownership: rows 32w + erow + 8q (q = 0..3), columns ec0 .. ec0 + 3 of the chunk — each
   // float4 store instruction of the wave then writes 8 whole 128-byte row segments
   const int erow = lane >> 3, ec0 = 4 * (lane & 7);
@@ -247,6 +284,21 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = xr[i];
     }
+    char* dst = xi[slot] + (NT * wv + t) * FRBT + lane * 16;
+    if (H) {
+      float mx = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[i] *= XS;
+        mx = fmaxf(mx, fabsf(v[i]));
+      }
+      xbad |= !(mx < F16_RANGE);
+      xmx = fmaxf(xmx, mx);
+      const FragT<H> f = split8t<H>(v);
+#pragma unroll
+      for (int pl = 0; pl < planes<H>(); ++pl) *reinterpret_cast<typename FragT<H>::V*>(dst + 1024 * pl) = f.p[pl];
+      return;
+    }
     Frag f;
     if (PCONV_ABL & 2) {
       f.h = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
@@ -255,7 +307,6 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     } else {
       split8(v, f.h, f.m, f.l);
     }
-    char* dst = xi[slot] + (NT * wv + t) * FRB + lane * 16;
     *reinterpret_cast<bf16x8*>(dst) = f.h;
     *reinterpret_cast<bf16x8*>(dst + 1024) = f.m;
     *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
@@ -293,22 +344,15 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const char* img = xi[slot] + KSW * kh * (KW - 1) * FRB + lane * 16;
-    Frag cur;
-    cur.h = *reinterpret_cast<const bf16x8*>(img);
-    cur.m = *reinterpret_cast<const bf16x8*>(img + 1024);
-    cur.l = *reinterpret_cast<const bf16x8*>(img + 2048);
+    const char* img = xi[slot] + KSW * kh * (KW - 1) * FRBT + lane * 16;
+    FragT<H> cur = ld_frag<H>(img, 1024);
 #pragma unroll
     for (int ks = 0; ks < KSW; ++ks) {
-      Frag nxt;
-      if (ks < KSW - 1) {
-        nxt.h = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB);
-        nxt.m = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 1024);
-        nxt.l = *reinterpret_cast<const bf16x8*>(img + (ks + 1) * FRB + 2048);
-      }
+      FragT<H> nxt;
+      if (ks < KSW - 1) nxt = ld_frag<H>(img + (ks + 1) * FRBT, 1024);
       PC_FENCE();
-      if (PCONV_ABL & 1) asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l), "v"(wf[ks].h));
-      else acc = mfma6(wf[ks], cur, acc);
+      if (PCONV_ABL & 1) asm volatile("" ::"v"(cur.p[0]), "v"(cur.p[1]), "v"(wf[ks].p[0]));
+      else acc = mma<H>(wf[ks], cur, acc);
       hook(ks);
       PC_FENCE();
       if (ks < KSW - 1) cur = nxt;
@@ -337,7 +381,11 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     for (int r = 0; r < 16; ++r) yb[((r & 3) + 8 * (r >> 2) + 4 * h) * YLD + l32] = acc[r];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
+      float4 v = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
+      if (H) {
+        const float is = srisc[32 * w + erow + 8 * q];
+        v.x *= is; v.y *= is; v.z *= is; v.w *= is;
+      }
       const float bq = sbias[32 * w + erow + 8 * q];
       ev[q].x += v.x + bq; ev[q].y += v.y + bq; ev[q].z += v.z + bq; ev[q].w += v.w + bq;
     }
@@ -557,6 +605,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       epilogue(cp, accp);
     }
   }
+  if (H && __any(xbad || (xmx > 0.f && xmx < 0.125f)) && lane == 0) atomicExch(a.range, a.epoch);
 }
 
 }  // namespace
@@ -609,22 +658,43 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
   const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
   if (head && (!g.logits || !g.scores || !g.pos)) return MVR_EINVAL;
-  if (g.xin == 1) {   // folded conv1 -> conv3 of the block's first PointCN
-    hipLaunchKernelGGL((pconv_kernel<8, 1, 0, 1, 0, 1>), dim3(grid), dim3(256), 0, s, a);
-    MVR_CHECK_LAUNCH();
-    return MVR_OK;
+  // split-fp16, then its guarded split-bf16 re-run — not for the head launches (their positive counts are
+  // atomics) nor where the output overwrites the residual in place (the re-run needs the residual intact)
+  auto span = [&](const float* p, int64_t ps) {
+    const char* b = reinterpret_cast<const char*>(p);
+    return std::make_pair(b, b + ((int64_t)(g.batch - 1) * ps + (int64_t)g.M * g.ldc) * 4);
+  };
+  bool alias = false;
+  if (g.has_res && g.R) {
+    const auto c = span(g.C, g.sCb), r = span(g.R, g.sRb);
+    alias = c.first < r.second && r.first < c.second;
   }
-  if (g.xin == 2) {   // ... and its conv7 with the residual x recomputed
-    hipLaunchKernelGGL((pconv_kernel<8, 1, 1, 1, 0, 2>), dim3(grid), dim3(256), 0, s, a);
-    MVR_CHECK_LAUNCH();
-    return MVR_OK;
+  const bool h1 = g_pconv_h && !head && !alias;
+  if (h1) {
+    static int* flags = nullptr;
+    static std::atomic<unsigned> launches{0};
+    if (!flags && hipGetSymbolAddress(reinterpret_cast<void**>(&flags), HIP_SYMBOL(g_pc_flags)) != hipSuccess)
+      return MVR_ELAUNCH;
+    const unsigned id = launches.fetch_add(1, std::memory_order_relaxed);
+    a.range = flags + id % 1024;
+    a.epoch = (int)(id & 0x3fffffffu) + 1;
   }
-#define MVR_PC(K_, P_, R_, S_, H_)                                                          \
-  if (ks == K_ && pro == P_ && res == R_ && st == S_ && head == H_) {                       \
-    hipLaunchKernelGGL((pconv_kernel<K_, P_, R_, S_, H_>), dim3(grid), dim3(256), 0, s, a); \
-    MVR_CHECK_LAUNCH();                                                                     \
-    return MVR_OK;                                                                          \
-  }
+#define MVR_PCL(THREADS, ...)                                                   \
+  do {                                                                          \
+    if (h1) {                                                                   \
+      hipLaunchKernelGGL((__VA_ARGS__, 1>), dim3(grid), dim3(THREADS), 0, s, a); \
+      MVR_CHECK_LAUNCH();                                                       \
+      a.guard = a.range;                                                        \
+      a.range = nullptr;                                                        \
+    }                                                                           \
+    hipLaunchKernelGGL((__VA_ARGS__, 0>), dim3(grid), dim3(THREADS), 0, s, a);   \
+    MVR_CHECK_LAUNCH();                                                         \
+    return MVR_OK;                                                              \
+  } while (0)
+  if (g.xin == 1) MVR_PCL(256, pconv_kernel<8, 1, 0, 1, 0, 1, 1);   // folded conv1 -> conv3 of the block's first PointCN
+  if (g.xin == 2) MVR_PCL(256, pconv_kernel<8, 1, 1, 1, 0, 2, 1);   // ... and its conv7 with the residual x recomputed
+#define MVR_PC(K_, P_, R_, S_, H_) \
+  if (ks == K_ && pro == P_ && res == R_ && st == S_ && head == H_) MVR_PCL(256, pconv_kernel<K_, P_, R_, S_, H_, 0, 1);
   MVR_PC(8, 1, 0, 1, 0)
   MVR_PC(8, 1, 1, 1, 0)
   MVR_PC(8, 1, 0, 0, 0)
@@ -633,25 +703,38 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   MVR_PC(8, 0, 1, 1, 0)
   MVR_PC(8, 0, 0, 0, 0)
   MVR_PC(8, 0, 1, 0, 0)
-  MVR_PC(8, 1, 1, 0, 1)    // the last PointCN conv of a block with the output head (oanet.py:174-175)
-  MVR_PC(8, 1, 1, 0, 2)    // ... when the block's output activation is not returned (head only)
 #undef MVR_PC
-  // 256 -> 128 (PointCN(2C -> C) after diff_unpool, oanet.py:155): the k-split 8-wave form, one workgroup per CU
-#define MVR_PC16(P_, S_)                                                                                \
-  if (ks == 16 && pro == P_ && res == 0 && st == S_ && head == 0) {                                    \
-    hipLaunchKernelGGL((pconv_kernel<16, P_, 0, S_, 0, 0, 2>), dim3(grid), dim3(512), 0, s, a);         \
-    MVR_CHECK_LAUNCH();                                                                                 \
-    return MVR_OK;                                                                                      \
+  // the last PointCN conv of a block with the output head (oanet.py:174-175), and the same when the block's
+  // output activation is not returned (head only): split-bf16 only
+  if (ks == 8 && pro == 1 && res == 1 && st == 0 && head == 1) {
+    hipLaunchKernelGGL((pconv_kernel<8, 1, 1, 0, 1>), dim3(grid), dim3(256), 0, s, a);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
   }
+  if (ks == 8 && pro == 1 && res == 1 && st == 0 && head == 2) {
+    hipLaunchKernelGGL((pconv_kernel<8, 1, 1, 0, 2>), dim3(grid), dim3(256), 0, s, a);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
+  // 256 -> 128 (PointCN(2C -> C) after diff_unpool, oanet.py:155): the k-split 8-wave form, one workgroup per CU
+#define MVR_PC16(P_, S_) \
+  if (ks == 16 && pro == P_ && res == 0 && st == S_ && head == 0) MVR_PCL(512, pconv_kernel<16, P_, 0, S_, 0, 0, 2);
   MVR_PC16(1, 1)   // conv3 (IN/BN/ReLU prologue, statistics)
   MVR_PC16(0, 0)   // shortcut (raw input)
   MVR_PC16(1, 0)
   MVR_PC16(0, 1)
 #undef MVR_PC16
+#undef MVR_PCL
   return MVR_EINVAL;
 }
 
 }  // namespace mvr
+
+extern "C" int mvr_set_pconv_math(int h) {
+  const int prev = mvr::g_pconv_h;
+  mvr::g_pconv_h = h ? 1 : 0;
+  return prev;
+}
 
 extern "C" int mvr_set_pconv(int on) {
   const int prev = mvr::g_pconv;

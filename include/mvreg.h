@@ -77,6 +77,10 @@ int mvr_set_gemm_math(int math);
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */
 int mvr_set_pconv(int on);
+/* operand math of the point convs (not the output-head launches): 1 (default) split-fp16 (3 MFMAs per
+   product, weight rows range-scaled, activations x 2^6 after the prologue and range-checked, with a guarded
+   split-bf16 re-run of a launch that saw one past the fp16 range), 0 split-bf16.  Returns the previous setting. */
+int mvr_set_pconv_math(int h);
 
 /* ------------------------------------------------------------------------
  * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters

@@ -18,7 +18,8 @@ def _pad(a, width):
     return out
 
 
-def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shared_a=False, math=1):
+def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shared_a=False, math=1, edit=None,
+         raw=False):
     import torch
     from lib import _native as NV
     r = np.random.RandomState(seed)
@@ -27,6 +28,8 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shar
     Bm = r.standard_normal((batch, K, N)).astype(np.float32)       # logical B(k, n)
     if pro == 3:
         Bm = np.abs(Bm)
+    if edit:
+        edit(A, Bm)
     Bstore = _pad(np.swapaxes(Bm, 1, 2), K4) if bkc else _pad(Bm, N4)
     Rm = r.standard_normal((batch, M, N)).astype(np.float32) if res else None
     bias = r.standard_normal(M if bias_mode == 1 else N).astype(np.float32) if bias_mode else None
@@ -80,6 +83,8 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shar
                         NV.ptr(pv[1]), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats_mode, math, NV.stream())
     assert rc == 0
     torch.cuda.synchronize()
+    if raw:
+        return C.cpu().numpy(), None if st is None else st.cpu().numpy()
     Cg = C.cpu().numpy().astype(np.float64)
     assert np.all(np.isfinite(Cg)), "padding columns must be written with finite values"
     Cg = Cg[..., :N]
@@ -156,6 +161,114 @@ def test_gemm_ragged_k(gpu, math):
     _run(gpu, 128, 999, 7, 2, 0, 0, 1, 1, 0, shared_a=True, math=math)
     _run(gpu, 70, 333, 45, 2, 0, 1, 0, 0, 0, math=math)
     _run(gpu, 70, 333, 45, 2, 3, 1, 0, 1, 0, math=math)
+
+
+PCONV_COMBOS = [(2, 0, 1, 1, 0), (2, 0, 1, 1, 1), (2, 0, 1, 0, 0), (0, 0, 1, 0, 0), (0, 0, 1, 1, 0), (2, 0, 1, 0, 1)]
+
+
+@pytest.fixture(params=[1, 0], ids=["pc_fp16x2", "pc_bf16x3"])
+def pmath(request):
+    from lib import _native as NV
+    prev = NV.lib().mvr_set_pconv_math(request.param)
+    yield request.param
+    NV.lib().mvr_set_pconv_math(prev)
+
+
+@pytest.mark.parametrize("combo", PCONV_COMBOS)
+@pytest.mark.parametrize("shape", [(128, 5000, 128, 3), (128, 517, 256, 3), (128, 5000, 256, 2), (128, 500, 128, 5),
+                                   (128, 33, 128, 1100)])
+def test_pconv_maths(gpu, combo, shape, pmath):
+    """the point-conv shapes (csrc/pconv.hip) on split-fp16 (weight rows range-scaled, activations x 2^6 after
+    the prologue) and split-bf16: both within 1e-5 of the float64 result at its |A| |B| scale"""
+    M, N, K, b = shape
+    pro, bkc, bias, stats, res = combo
+    if K == 256 and res:
+        pytest.skip("the 256-channel convs have no residual form")
+    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=True, math=1)
+
+
+def _big_b(A, B):
+    B[1, 5, 7] = 7.0e4      # an activation past the fp16 range
+
+
+def _big_b_pro(A, B):
+    B[0, 9, 100] = 4.0e3    # ... past it after the prologue's x 2^6 (and sc <= 1.5)
+
+
+def _tiny_b(A, B):
+    B *= 1.0e-5             # raw activations all below 2^-9: re-run (the prologue lifts them: not there)
+
+
+def _big_a(A, B):
+    A *= 3.0e5              # weights: row-scaled, no re-run
+
+
+@pytest.mark.parametrize("edit", [_big_b, _big_b_pro, _tiny_b, _big_a])
+@pytest.mark.parametrize("combo", [(2, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 1)])
+@pytest.mark.parametrize("K", [128, 256])
+def test_pconv_fp16_range(gpu, edit, combo, K):
+    """an activation outside the split-fp16 window re-runs the launch in split-bf16: outputs and statistics
+    bit-identical to a split-bf16 launch; weights far past the fp16 range are scaled, not re-run"""
+    from lib import _native as NV
+    pro, bkc, bias, stats, res = combo
+    if K == 256 and res:
+        pytest.skip("the 256-channel convs have no residual form")
+    if (edit is _big_b_pro and not pro) or (edit is _tiny_b and pro):
+        pytest.skip("prologue case")
+    L = NV.lib()
+    outs = []
+    prev = L.mvr_set_pconv_math(0)
+    try:
+        for m in (0, 1):
+            L.mvr_set_pconv_math(m)
+            outs.append(_run(gpu, 128, 700, K, 3, pro, bkc, bias, stats, res, seed=7, shared_a=True, edit=edit,
+                             raw=True))
+        if edit is not _big_a:   # (outputs ~1e8 there: the statistics' cancellation exceeds their fp64 tolerance)
+            _run(gpu, 128, 700, K, 3, pro, bkc, bias, stats, res, seed=7, shared_a=True, edit=edit)   # vs float64
+    finally:
+        L.mvr_set_pconv_math(prev)
+    (c0, s0), (c1, s1) = outs
+    if edit is _big_a:
+        assert not np.array_equal(c0, c1)
+        np.testing.assert_allclose(c1, c0, rtol=1e-5, atol=1e-5 * np.abs(c0).max())
+    else:
+        assert np.array_equal(c0, c1, equal_nan=True)
+        assert s0 is None or np.array_equal(s0, s1)
+
+
+def test_pconv_in_place_residual(gpu):
+    """out = conv(x) + out in place (the OANet PointCN / OAFilter form): the launch cannot be re-run once it has
+    overwritten its residual, so it runs split-bf16 directly — with an out-of-range activation too, the result
+    is the split-bf16 one bit for bit"""
+    import torch
+    from lib import _native as NV
+    r = np.random.RandomState(11)
+    P, M, N, K = 3, 128, 700, 128
+    N4 = r4(N)
+    A = (0.1 * r.standard_normal((M, K))).astype(np.float32)
+    B = _pad(r.standard_normal((P, K, N)).astype(np.float32), N4)
+    B[1, 3, 9] = 8.0e4
+    R = _pad(r.standard_normal((P, M, N)).astype(np.float32), N4)
+    bias = r.standard_normal(M).astype(np.float32)
+    L = NV.lib()
+    outs = []
+    prev = L.mvr_set_pconv_math(0)
+    try:
+        for m in (0, 1):
+            L.mvr_set_pconv_math(m)
+            tA, tB, tb = (torch.from_numpy(x).to(gpu) for x in (A, B, bias))
+            C = torch.from_numpy(R.copy()).to(gpu)
+            assert L.mvr_gemm_f32(M, N, K, P, NV.ptr(tA), 0, K, NV.ptr(tB), K * N4, N4, 0, NV.ptr(C), M * N4, N4,
+                                  NV.ptr(C), M * N4, NV.ptr(tb), 1, None, None, 0, 0, 0, None, 0, 0, 0, 1,
+                                  NV.stream()) == 0
+            torch.cuda.synchronize()
+            outs.append(C.cpu().numpy())
+    finally:
+        L.mvr_set_pconv_math(prev)
+    assert np.array_equal(outs[0], outs[1])
+    ref = A.astype(np.float64) @ B[..., :N].astype(np.float64) + bias[None, :, None] + R[..., :N]
+    scale = np.abs(A).astype(np.float64) @ np.abs(B[..., :N]).astype(np.float64) + 1.0
+    assert np.all(np.abs(outs[1][..., :N] - ref) <= 1e-5 * scale)
 
 
 def test_gemm_bf16x3_accuracy_vs_fp32(gpu):
