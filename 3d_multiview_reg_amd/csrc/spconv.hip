@@ -12,6 +12,8 @@
 // gathers 16 input channels of the tile's neighbour rows (16-byte row loads) and the
 // matching W[k] slice into LDS, then runs v_mfma_f32_32x32x2_f32.  No atomics: every
 // output row is owned by exactly one workgroup (deterministic results).
+#include <atomic>
+
 #include "common.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
@@ -31,6 +33,7 @@ struct SpArgs {
   const float* res; int64_t ldres;
   int relu;
   float* out; int64_t ldout;
+  int* range; const int* guard; int epoch;   // split-fp16 flag slot / split-bf16 re-run guard (pconv.hip scheme)
 };
 
 constexpr int SP_BK = 16;
@@ -229,16 +232,24 @@ constexpr int SB_CP = 128;   // output-channel padding of the weight image (larg
 #define SPBX_NS128 3
 #endif
 
-template <int TN, int NS>
-__global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP) {
+// H = 1: split-fp16 (mfma_bf16.hpp, 3 MFMAs per product): the image's fp16 section (each output channel's
+// weights scaled by a power of two to <= 2^14), the gathered features x XS = 2^6 as they are split, both undone
+// per column in the epilogue (isc); a lane that splits a value of 1023.5 or more, or whose values are all below
+// 2^-9 without being zero, marks the launch for its guarded split-bf16 re-run (pconv.hip's flag slots).
+template <int TN, int NS, int H>
+__global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP,
+                                                           const float* __restrict__ isc) {
   using namespace bx;
   // NS: steps in flight (register sets: gathered rows + weights)
+  constexpr int NPL = planes<H>();
+  constexpr float XS = H ? 64.f : 1.f;
   constexpr int TM = 128;                       // output rows per workgroup (4 waves x 32)
   constexpr int NJ = TN / 32;                   // accumulator tiles per wave
-  constexpr int BPL = TN * SB_BST;              // bf16 elements of one plane of a weight stage
-  constexpr int BG = 3 * BPL * 2 / 16;          // 16-byte granules of a weight stage
+  constexpr int BPL = TN * SB_BST;              // 16-bit elements of one plane of a weight stage
+  constexpr int BG = NPL * BPL * 2 / 16;        // 16-byte granules of a weight stage
   constexpr int GPT = (BG + 255) / 256;         // ... per thread
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][3 * BPL];
+  if (a.guard && *a.guard != a.epoch) return;   // uniform: the split-fp16 launch stayed in range
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][NPL * BPL];
   __shared__ int32_t nb[TM][SP_KMAX + 1];
   __shared__ int kact[SP_KMAX];
   __shared__ int klist[SP_KMAX];
@@ -298,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     }
     A.m = m;
     const int cb = s % nci;
-    const char* wb = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * 3 * CoutP + c0) * SB_BST * 2;
+    const char* wb = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * NPL * CoutP + c0) * SB_BST * 2;
 #pragma unroll
     for (int i = 0; i < GPT; ++i) {
       const int g = min(tid + 256 * i, BG - 1);
@@ -306,15 +317,25 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
       A.bq[i] = *reinterpret_cast<const float4*>(wb + (int64_t)pl * CoutP * SB_BST * 2 + wi * 16);
     }
   };
+  bool xbad = false;   // H = 1: a gathered value past the fp16 window
+  float xmx = 0.f;     // H = 1: max |value| x XS of this lane's splits
   auto frag_a = [&](const ASet& A, int st) {
     float v[8];
     const float4 x0 = A.v[2 * st], x1 = A.v[2 * st + 1];
     const bool k0 = (A.m >> (2 * st)) & 1, k1 = (A.m >> (2 * st + 1)) & 1;
     v[0] = k0 ? x0.x : 0.f; v[1] = k0 ? x0.y : 0.f; v[2] = k0 ? x0.z : 0.f; v[3] = k0 ? x0.w : 0.f;
     v[4] = k1 ? x1.x : 0.f; v[5] = k1 ? x1.y : 0.f; v[6] = k1 ? x1.z : 0.f; v[7] = k1 ? x1.w : 0.f;
-    Frag f;
-    split8(v, f.h, f.m, f.l);
-    return f;
+    if (H) {
+      float mx = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[i] *= XS;
+        mx = fmaxf(mx, fabsf(v[i]));
+      }
+      xbad |= !(mx < F16_RANGE);
+      xmx = fmaxf(xmx, mx);
+    }
+    return split8t<H>(v);
   };
   // weight stage of a step: granule g of [plane][TN rows][80 B] <- image rows (k, channel block) at column c0
   auto store_b = [&](const ASet& A, int buf) {
@@ -343,23 +364,20 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     auto step = [&](int s, ASet& A, const ASet& An) {
       const int cur = s & 1;
       if (s + 1 < steps) store_b(An, cur ^ 1);
-      const Frag fa0 = frag_a(A, 0), fa1 = frag_a(A, 1);
+      const FragT<H> fa0 = frag_a(A, 0), fa1 = frag_a(A, 1);
       load_a(s + NS, A);
       const uint16_t* Bq = Bs[cur];
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-        const Frag& fa = st ? fa1 : fa0;
+        const FragT<H>& fa = st ? fa1 : fa0;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const uint16_t* bp = Bq + (32 * j + l32) * SB_BST + 16 * st + 8 * h;
-          Frag fb;
-          fb.h = *reinterpret_cast<const bf16x8*>(bp);
-          fb.m = *reinterpret_cast<const bf16x8*>(bp + BPL);
-          fb.l = *reinterpret_cast<const bf16x8*>(bp + 2 * BPL);
+          const FragT<H> fb = ld_frag<H>(reinterpret_cast<const char*>(bp), 2 * BPL);
 #if SPBX_ABL & 1
-          asm volatile("" ::"v"(fa.h), "v"(fa.m), "v"(fa.l), "v"(fb.h), "v"(fb.m), "v"(fb.l));
+          asm volatile("" ::"v"(fa.p[0]), "v"(fa.p[1]), "v"(fb.p[0]), "v"(fb.p[1]));
 #else
-          acc[j] = mfma6(fa, fb, acc[j]);
+          acc[j] = mma<H>(fa, fb, acc[j]);
 #endif
         }
       }
@@ -385,23 +403,45 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
       bsh = a.bn.beta[c] - a.bn.mean[c] * bsc;
     }
     const float bias = a.bias ? a.bias[c] : 0.f;
+    const float is = H ? isc[c] : 1.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int64_t ot = o0 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
       if (ot >= a.Mout) continue;
       const int64_t o = a.perm ? a.perm[ot] : ot;
-      float v = acc[j][r] + bias;
+      float v = (H ? acc[j][r] * is : acc[j][r]) + bias;
       v = fmaf(v, bsc, bsh);
       if (a.res) v += a.res[o * a.ldres + c];
       if (a.relu) v = fmaxf(v, 0.f);
       a.out[o * a.ldout + c] = v;
     }
   }
+  if (H && __any(xbad || (xmx > 0.f && xmx < 0.125f)) && lane == 0) atomicExch(a.range, a.epoch);
 }
 
-// W [K][Cin][Cout] fp32 -> image [K][nci][3][CoutP][40] bf16 (h, m, l planes; zero padding)
+// per output channel c: s_c = range_scale(max_{k, ci} |W[k][ci][c]|) -> wsc[c], isc[c] = 1 / (s_c 2^6); one wave
+// per channel
+__global__ void spconv_wscale_kernel(const float* __restrict__ W, int K, int Cin, int Cout, int64_t CoutP, float* wsc,
+                                     float* isc) {
+  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (c >= CoutP) return;   // whole waves
+  float amax = 0.f;
+  if (c < Cout)
+    for (int64_t e = lane; e < (int64_t)K * Cin; e += 64) amax = fmaxf(amax, fabsf(W[e * Cout + c]));
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+  if (lane == 0) {
+    const float s = bx::range_scale(amax);
+    wsc[c] = s;
+    isc[c] = 1.f / (s * 64.f);
+  }
+}
+
+// W [K][Cin][Cout] fp32 -> image: [K][nci][3][CoutP][40] bf16 (h, m, l planes; zero padding), then
+// [K][nci][2][CoutP][40] fp16 (h, l of W[.][.][c] wsc[c]), then wsc[CoutP], isc[CoutP]
 __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin, int Cout, int nci, int64_t CoutP,
-                                     uint16_t* img) {
+                                     uint16_t* img, uint16_t* img16, const float* __restrict__ wsc) {
   using namespace bx;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // (k, cb, c, 4 groups of 8 channels)
   const int64_t total = (int64_t)K * nci * CoutP * 4;
@@ -423,7 +463,20 @@ __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin
   *reinterpret_cast<bf16x8*>(row) = f.h;
   *reinterpret_cast<bf16x8*>(row + CoutP * SB_BST) = f.m;
   *reinterpret_cast<bf16x8*>(row + 2 * CoutP * SB_BST) = f.l;
+  const float sc = wsc[c];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] *= sc;
+  const FragT<1> g = split8t<1>(v);
+  uint16_t* row16 = img16 + ((kb * 2) * CoutP + c) * SB_BST + 8 * q;
+  *reinterpret_cast<f16x8*>(row16) = g.p[0];
+  *reinterpret_cast<f16x8*>(row16 + CoutP * SB_BST) = g.p[1];
 }
+
+#ifndef SPCONV_MATH_DEFAULT
+#define SPCONV_MATH_DEFAULT 1
+#endif
+int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_spconv_math
+__device__ int g_sp_flags[1024];         // flag slots (pconv.hip scheme: slot i % 1024, epoch i + 1)
 
 }  // namespace mvr
 
@@ -431,10 +484,21 @@ using namespace mvr;
 
 static int64_t sp_coutp(int Cout) { return ((int64_t)Cout + SB_CP - 1) / SB_CP * SB_CP; }
 
+// image sections (bytes): bf16 planes, fp16 planes, wsc, isc
+static size_t sp_bf16_bytes(int K, int Cin, int Cout) {
+  return (size_t)K * ((Cin + SB_K - 1) / SB_K) * 3 * sp_coutp(Cout) * SB_BST * 2;
+}
+static size_t sp_f16_bytes(int K, int Cin, int Cout) { return sp_bf16_bytes(K, Cin, Cout) / 3 * 2; }
+
 extern "C" size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout) {
   if (K <= 0 || Cin <= 0 || Cout <= 0) return 0;
-  const int64_t nci = (Cin + SB_K - 1) / SB_K;
-  return (size_t)(K * nci * 3 * sp_coutp(Cout) * SB_BST * 2);
+  return sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout) + 2 * sp_coutp(Cout) * sizeof(float);
+}
+
+extern "C" int mvr_set_spconv_math(int h) {
+  const int prev = g_spconv_h;
+  g_spconv_h = h ? 1 : 0;
+  return prev;
 }
 
 extern "C" int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, hipStream_t s) {
@@ -444,8 +508,14 @@ extern "C" int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void*
   const int nci = (Cin + SB_K - 1) / SB_K;
   const int64_t CoutP = sp_coutp(Cout);
   const int64_t total = (int64_t)K * nci * CoutP * 4;
+  char* base = reinterpret_cast<char*>(img);
+  uint16_t* img16 = reinterpret_cast<uint16_t*>(base + sp_bf16_bytes(K, Cin, Cout));
+  float* wsc = reinterpret_cast<float*>(base + sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout));
+  hipLaunchKernelGGL(spconv_wscale_kernel, dim3((unsigned)((CoutP * 64 + 255) / 256)), dim3(256), 0, s, W, K, Cin, Cout,
+                     CoutP, wsc, wsc + CoutP);
+  MVR_CHECK_LAUNCH();
   hipLaunchKernelGGL(spconv_wimage_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, W, K, Cin, Cout, nci,
-                     CoutP, reinterpret_cast<uint16_t*>(img));
+                     CoutP, reinterpret_cast<uint16_t*>(img), img16, wsc);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }
@@ -461,19 +531,55 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
       (reinterpret_cast<uintptr_t>(W) & 15))
     return MVR_EINVAL;
   if (Mout == 0) return MVR_OK;
-  SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout};
+  SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout,
+           nullptr, nullptr, 0};
   ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
-  if (wimg) {   // split-bf16 path (weights pre-split by mvr_spconv_wimage)
+  if (wimg) {   // split paths (weights pre-split by mvr_spconv_wimage)
+    const char* base = reinterpret_cast<const char*>(wimg);
     const uint16_t* wi = reinterpret_cast<const uint16_t*>(wimg);
+    const uint16_t* wi16 = reinterpret_cast<const uint16_t*>(base + sp_bf16_bytes(K, Cin, Cout));
     const int64_t CoutP = sp_coutp(Cout);
+    const float* isc = reinterpret_cast<const float*>(base + sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout)) +
+                       CoutP;
     const unsigned gx = (unsigned)((Mout + 127) / 128);
+    // split-fp16 then its guarded split-bf16 re-run, unless the output overwrites the residual (the re-run reads it)
+    auto overlap = [&](const float* p, int64_t ld, int64_t rows, int cols) {
+      if (!p) return false;
+      const char *o0 = reinterpret_cast<const char*>(out), *o1 = o0 + ((Mout - 1) * ldout + Cout) * 4;
+      const char *p0 = reinterpret_cast<const char*>(p), *p1 = p0 + ((rows - 1) * ld + cols) * 4;
+      return o0 < p1 && p0 < o1;
+    };
+    // (in / out never alias: rows are gathered).  Output tiles of 32 / 64 channels stay split-bf16: there the
+    // split-fp16 kernel holds more VGPRs (155 vs 125 at TN = 32), one workgroup per CU fewer for a gather-latency
+    // bound loop — measured slower (tools/spconv_micro.py: s1:1:32:32 0.378 -> 0.384 ms, up:1:128:64 0.403 ->
+    // 0.453), where the 128-channel tiles gain (s1:4:128:128 0.304 -> 0.217, s1:8:256:256 0.437 -> 0.346)
+    const bool h1 = g_spconv_h && Cout > 64 && !overlap(res, ldres, Mout, Cout);
+    if (h1) {
+      static int* flags = nullptr;
+      static std::atomic<unsigned> launches{0};
+      if (!flags && hipGetSymbolAddress(reinterpret_cast<void**>(&flags), HIP_SYMBOL(g_sp_flags)) != hipSuccess)
+        return MVR_ELAUNCH;
+      const unsigned id = launches.fetch_add(1, std::memory_order_relaxed);
+      a.range = flags + id % 1024;
+      a.epoch = (int)(id & 0x3fffffffu) + 1;
+    }
+#define MVR_SPL(TN_, NS_, GY)                                                                                   \
+  do {                                                                                                          \
+    if (h1) {                                                                                                   \
+      hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 1>), dim3(gx, GY), dim3(256), 0, s, a, wi16, CoutP, isc);  \
+      MVR_CHECK_LAUNCH();                                                                                       \
+      a.guard = a.range;                                                                                        \
+      a.range = nullptr;                                                                                        \
+    }                                                                                                           \
+    hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx, GY), dim3(256), 0, s, a, wi, CoutP, isc);      \
+  } while (0)
     if (Cout <= 32)
-      hipLaunchKernelGGL((spconv_bx_kernel<32, SPBX_NS32>), dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
+      MVR_SPL(32, SPBX_NS32, 1);
     else if (Cout <= 64)
-      hipLaunchKernelGGL((spconv_bx_kernel<64, SPBX_NS64>), dim3(gx, 1), dim3(256), 0, s, a, wi, CoutP);
+      MVR_SPL(64, SPBX_NS64, 1);
     else
-      hipLaunchKernelGGL((spconv_bx_kernel<128, SPBX_NS128>), dim3(gx, (Cout + 127) / 128), dim3(256), 0, s, a, wi,
-                         CoutP);
+      MVR_SPL(128, SPBX_NS128, (Cout + 127) / 128);
+#undef MVR_SPL
     MVR_CHECK_LAUNCH();
     return MVR_OK;
   }

@@ -321,10 +321,16 @@ int mvr_kernel_map_order(const int32_t* nbr, int64_t Mout, int K, int32_t* perm,
 int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K, int64_t Mout,
                const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
                int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg, mvr_stream_t stream);
-/* Weight image of mvr_spconv's split-bf16 path: W [K][Cin][Cout] fp32 -> three bf16 planes in
- * [K][ceil(Cin/32)][plane][round_up(Cout,128)][40] rows (80-byte rows, zero padded). */
+/* Weight image of mvr_spconv's split paths: W [K][Cin][Cout] fp32 -> three bf16 planes in
+ * [K][ceil(Cin/32)][plane][round_up(Cout,128)][40] rows (80-byte rows, zero padded), then the same rows as two
+ * fp16 planes of W[.][.][c] s_c (s_c: a power of two bringing output channel c's weights to <= 2^14), then
+ * s_c and 1 / (s_c 2^6) per channel. */
 size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout);
 int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, mvr_stream_t stream);
+/* operand math of mvr_spconv with a weight image: 1 (default) split-fp16 (3 MFMAs per product; gathered
+   features x 2^6 and window-checked, a guarded split-bf16 re-run of a launch that saw one outside it; split-bf16
+   directly when the output overlaps the residual), 0 split-bf16.  Returns the previous setting. */
+int mvr_set_spconv_math(int h);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
 size_t mvr_brick_map_bytes(int64_t M);
