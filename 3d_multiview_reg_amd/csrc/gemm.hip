@@ -25,8 +25,12 @@
 //     lane owns 4 consecutive columns of a row: float4 residual loads and stores, row statistics
 //     reduced with 3 swizzles, column statistics with 2 DPP moves and one cross-half shuffle.
 // Roofline: 2*M*N*K flops per GEMM against the 157.3 TF/s fp32 MFMA peak.
+#include <atomic>
+#include <utility>
+
 #include "common.hpp"
 #include "gemm.hpp"
+#include "mfma_bf16.hpp"
 #include "prof.hpp"
 
 #ifndef GEMM_EARLY
@@ -81,6 +85,7 @@ struct KArgs {
   GemmArgs g;
   int persist;  // number of persistent workgroups
   int m_fast;   // tile order: m-tiles fastest (see tile_of)
+  int* range; const int* guard; int epoch;   // MATH_F16X2 flag slot / MATH_BF16X3 re-run guard (pconv.hip scheme)
 };
 
 __device__ __forceinline__ float& f4(float4& v, int i) { return reinterpret_cast<float*>(&v)[i]; }
@@ -620,6 +625,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   float* fac = vec + 4 * KV;                  // [2 stages][128] softmax factors (PRO_B_SMX)
   float2* red = reinterpret_cast<float2*>(fac + 2 * BN);    // [2][128] partial statistics
   float* redm = fac + 2 * BN + 4 * BM;                      // [2][128] tile maxima (softmax)
+  if (ka.guard && *ka.guard != ka.epoch) return;   // uniform: the split-fp16 launch stayed in its window
+  float amx = 0.f, bmx = 0.f;   // MATH_F16X2: max |A| x 2^6, |B| x 2^6 this lane split
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -867,6 +874,37 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
             for (int j = 0; j < 2; ++j)
               acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4(a4[ii][s4], e), f4(b4[j][s4], e), acc[ii][j], 0,
                                                                 0, 0);
+    } else if (MATH == MATH_F16X2) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bx::FragT<1> fa[2], fb[2];
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          const float4 u0 = a4[ii][2 * st], u1 = a4[ii][2 * st + 1];
+          float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] *= 64.f;
+            amx = fmaxf(amx, fabsf(v[e]));
+          }
+          fa[ii] = bx::split8t<1>(v);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 u0 = b4[j][2 * st], u1 = b4[j][2 * st + 1];
+          float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] *= 64.f;
+            bmx = fmaxf(bmx, fabsf(v[e]));
+          }
+          fb[j] = bx::split8t<1>(v);
+        }
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[ii][j] = bx::mma<1>(fa[ii], fb[j], acc[ii][j]);
+      }
     } else {
       // two k16 steps; lane half h holds k = 16s + 8h + (0..7) = chunks (2s, 2s+1) of its registers
 #pragma unroll
@@ -908,6 +946,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     int b, tm, tn;
     tile_of(i, b, tm, tn);
     TSTAMP(5);
+    if (MATH == MATH_F16X2) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[ii][j] *= 1.f / 4096.f;   // the operands' 2^6 x 2^6
+    }
     tile_epilogue<BIAS, STATS, RES>(g, acc, b, tm, tn, red, redm);
     TSTAMP(6);
     // (red / redm are next written in the next tile's epilogue, after at least one stage barrier)
@@ -917,15 +961,54 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   if (lane == 0)
     for (int q = 0; q < 8; ++q) atomicAdd(&g_gemm_trace[q], tr[q]);
 #endif
+  if (MATH == MATH_F16X2) {   // outside the window: past 65504 (1023.5 unscaled), or nonzero but all below 2^-9
+    const bool bad = !(amx < bx::F16_RANGE) || !(bmx < bx::F16_RANGE) || (amx > 0.f && amx < 0.125f) ||
+                     (bmx > 0.f && bmx < 0.125f);
+    if (__any(bad) && lane == 0) atomicExch(ka.range, ka.epoch);
+  }
 }
 
+#ifndef GEMM_F16_DEFAULT
+#define GEMM_F16_DEFAULT 1
+#endif
+int g_gemm_h = GEMM_F16_DEFAULT;   // mvr_set_gemm_f16: MATH_BF16X3 launches run split-fp16 first
+__device__ int g_gm_flags[1024];    // flag slots (pconv.hip scheme: slot i % 1024, epoch i + 1)
+
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
-static void launch_t(const KArgs& ka, long long tiles, hipStream_t s) {
+static void launch_t(const KArgs& ka0, long long tiles, hipStream_t s) {
+  KArgs ka = ka0;
   const unsigned wgs = (unsigned)(tiles < ka.persist ? tiles : ka.persist);
-  if (ka.g.math == MATH_F32)
+  if (ka.g.math == MATH_F32) {
     hipLaunchKernelGGL((gemm_kernel<MATH_F32, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
-  else
-    hipLaunchKernelGGL((gemm_kernel<MATH_BF16X3, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
+    return;
+  }
+  // split-fp16 first unless the output overlaps an operand or the residual (the re-run reads them)
+  const GemmArgs& g = ka.g;
+  auto span = [&](const void* p, int64_t sb, int64_t rows, int64_t ld, int64_t cols) {
+    const char* b = reinterpret_cast<const char*>(p);
+    return std::make_pair(b, b + ((int64_t)(g.batch - 1) * sb + (rows - 1) * ld + cols) * 4);
+  };
+  bool alias = false;
+  if (g.C) {
+    const auto c = span(g.C, g.sCb, g.M, g.ldc, g.N);
+    auto hit = [&](std::pair<const char*, const char*> o) { return c.first < o.second && o.first < c.second; };
+    alias = hit(span(g.A, g.sAb, g.M, g.lda, g.K)) ||
+            hit(g.bkc ? span(g.B, g.sBb, g.N, g.ldb, g.K) : span(g.B, g.sBb, g.K, g.ldb, g.N)) ||
+            (g.has_res && hit(span(g.R, g.sRb, g.M, g.ldc, g.N)));
+  }
+  if (g_gemm_h && !alias) {
+    static int* flags = nullptr;
+    static std::atomic<unsigned> launches{0};
+    if (flags || hipGetSymbolAddress(reinterpret_cast<void**>(&flags), HIP_SYMBOL(g_gm_flags)) == hipSuccess) {
+      const unsigned id = launches.fetch_add(1, std::memory_order_relaxed);
+      ka.range = flags + id % 1024;
+      ka.epoch = (int)(id & 0x3fffffffu) + 1;
+      hipLaunchKernelGGL((gemm_kernel<MATH_F16X2, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
+      ka.guard = ka.range;
+      ka.range = nullptr;
+    }
+  }
+  hipLaunchKernelGGL((gemm_kernel<MATH_BF16X3, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
 }
 
 static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -951,7 +1034,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
     ok = ok && al16(g.psc) && al16(g.psh) && g.sPb % 4 == 0 && g.K % 4 == 0 && g.K <= KV_MAX;
   if (g.pro == PRO_B_SMX) ok = ok && al16(g.psc) && g.sPb % 4 == 0 && g.pld % 4 == 0 && g.pld >= N4;
   if (!ok) return MVR_EINVAL;
-  KArgs ka;
+  KArgs ka{};
   ka.g = g;
   ka.persist = 2 * 256;  // 2 workgroups per CU (LDS-bound), 256 CUs
   ka.m_fast = (g.sAb == 0 && gemm_mtiles(g.M) > 1) ? 1 : 0;
@@ -1022,6 +1105,12 @@ extern "C" int mvr_gemm_trace(unsigned long long* out, int reset) {
   return 0;
 }
 #endif
+
+extern "C" int mvr_set_gemm_f16(int on) {
+  const int prev = mvr::g_gemm_h;
+  mvr::g_gemm_h = on ? 1 : 0;
+  return prev;
+}
 
 extern "C" int mvr_set_gemm_math(int math) {
   if (math != mvr::MATH_F32 && math != mvr::MATH_BF16X3) return MVR_EINVAL;

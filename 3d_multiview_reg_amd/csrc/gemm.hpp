@@ -32,7 +32,10 @@ enum Stats : int {
 // MATH_BF16X3: each fp32 operand split into three bf16 terms (x = h + m + l to 2^-25 |x|) and the
 // six products hh, hm, mh, mm, hl, lh accumulated in fp32 by v_mfma_f32_32x32x16_bf16 — fp32-level
 // accuracy (the dropped ml, lm, ll terms are <= 2^-23 relative) at 6/16 of the fp32 MFMA cycles.
-enum Math : int { MATH_F32 = 0, MATH_BF16X3 = 1 };
+// MATH_F16X2 (internal): two-term split-fp16 (mfma_bf16.hpp) of A x 2^6 and B x 2^6, 3 MFMAs per product; what a
+// MATH_BF16X3 launch runs first when mvr_set_gemm_f16 is on, with a guarded MATH_BF16X3 re-run when an operand
+// left the split-fp16 window (gemm.hip launch_t).
+enum Math : int { MATH_F32 = 0, MATH_BF16X3 = 1, MATH_F16X2 = 2 };
 extern int g_default_math;   // used by the OANet orchestrator (mvr_set_gemm_math)
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 32;

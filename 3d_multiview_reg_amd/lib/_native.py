@@ -64,6 +64,7 @@ _SIGS = {
     "mvr_set_attn_math": (c_int, [c_int]),
     "mvr_set_pconv_math": (c_int, [c_int]),
     "mvr_set_spconv_math": (c_int, [c_int]),
+    "mvr_set_gemm_f16": (c_int, [c_int]),
     "mvr_attn_reruns": (c_int, [c_int]),
     "mvr_debug_stage_hash": (c_int, [c_vp, c_int]),
     "mvr_debug_stage_dump": (c_int, [c_int, c_vp, c_size]),

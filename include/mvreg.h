@@ -73,6 +73,11 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
                  mvr_stream_t stream);
 /* GEMM arithmetic used by mvr_oan_block_forward (process-wide; default 1 = bf16 split). */
 int mvr_set_gemm_math(int math);
+/* With the split math (1), run each generic GEMM launch as two-term split-fp16 first (A and B x 2^6, 3 MFMAs per
+   product) with a guarded split-bf16 re-run when an operand left the window (|x| >= 1023.5, or a lane's values
+   nonzero but all below 2^-9) or when the output overlaps an input: 1 (default) on, 0 off.  Returns the previous
+   setting. */
+int mvr_set_gemm_f16(int on);
 /* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */

@@ -129,15 +129,26 @@ COMBOS = [(0, 0, 1, 1, 0), (0, 0, 1, 0, 0), (2, 0, 1, 1, 0), (2, 0, 1, 0, 0), (2
           (0, 1, 0, 0, 0)]
 
 
-@pytest.mark.parametrize("math", [0, 1])       # exact fp32 MFMA / 3-term bf16 split
+@pytest.fixture(params=[1, 0], ids=["g_fp16x2", "g_bf16x3"])
+def gf16(request):
+    """mvr_set_gemm_f16: split-math launches run split-fp16 first (guarded split-bf16 re-run) or split-bf16 only"""
+    from lib import _native as NV
+    prev = NV.lib().mvr_set_gemm_f16(request.param)
+    yield request.param
+    NV.lib().mvr_set_gemm_f16(prev)
+
+
+@pytest.mark.parametrize("math", [0, 1])       # exact fp32 MFMA / split (fp16 x2 first, or bf16 x3: gf16)
 @pytest.mark.parametrize("combo", COMBOS)
 @pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 36, 3), (500, 300, 64, 1), (1, 40, 8, 2),
                                    (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2),
                                    (128, 5000, 128, 3), (128, 517, 128, 2), (128, 500, 128, 5), (128, 31, 128, 2),
                                    (128, 517, 256, 3), (128, 5000, 256, 2)])
-def test_gemm_modes(gpu, combo, shape, math):
+def test_gemm_modes(gpu, combo, shape, math, gf16):
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo
+    if math == 0 and gf16 == 0:
+        pytest.skip("gf16 applies to the split math")
     if pro in (1, 2) and K % 4:
         pytest.skip("per-k prologue needs K % 4 == 0")
     _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1),
@@ -269,6 +280,36 @@ def test_pconv_in_place_residual(gpu):
     ref = A.astype(np.float64) @ B[..., :N].astype(np.float64) + bias[None, :, None] + R[..., :N]
     scale = np.abs(A).astype(np.float64) @ np.abs(B[..., :N]).astype(np.float64) + 1.0
     assert np.all(np.abs(outs[1][..., :N] - ref) <= 1e-5 * scale)
+
+
+def _big_a_gemm(A, B):
+    A[0, 3, 5] = 2.0e3     # x 2^6 past 65504
+
+
+def _tiny_gemm(A, B):
+    A *= 1.0e-7            # every lane's values nonzero but below 2^-9 (B's too: a prologue lifts A)
+    B *= 1.0e-7
+
+
+@pytest.mark.parametrize("edit", [_big_a_gemm, _tiny_gemm])
+@pytest.mark.parametrize("combo", [(1, 1, 2, 1, 1), (0, 0, 1, 1, 0), (2, 0, 1, 2, 0)])
+def test_gemm_f16_window(gpu, edit, combo):
+    """generic GEMM: an operand outside the split-fp16 window re-runs the launch in split-bf16 (bit-identical)"""
+    from lib import _native as NV
+    pro, bkc, bias, stats, res = combo
+    L = NV.lib()
+    outs = []
+    prev = L.mvr_set_gemm_f16(0)
+    try:
+        for f in (0, 1):
+            L.mvr_set_gemm_f16(f)
+            outs.append(_run(gpu, 130, 517, 260, 2, pro, bkc, bias, stats, res, seed=3, shared_a=(pro != 1),
+                             edit=edit, raw=True))
+    finally:
+        L.mvr_set_gemm_f16(prev)
+    (c0, s0), (c1, s1) = outs
+    assert np.array_equal(c0, c1, equal_nan=True)
+    assert s0 is None or np.array_equal(s0, s1, equal_nan=True)
 
 
 def test_gemm_bf16x3_accuracy_vs_fp32(gpu):
