@@ -6,7 +6,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 for c in conv_pro_stats conv_res; do
   echo "== $c"
   python3 "$R/tools/gemm_micro.py" --math 1 --only $c 2>&1 | grep pconv
-  for so in "$R"/tools/variants/pc_abl*.so; do
+  for so in "$R"/tools/vsp/pc_abl*.so; do
     echo -n "$(basename $so .so): "
     MVR_LIB=$so python3 "$R/tools/gemm_micro.py" --math 1 --only $c 2>&1 | grep pconv
   done
