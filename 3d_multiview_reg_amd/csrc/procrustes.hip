@@ -212,6 +212,174 @@ __global__ __launch_bounds__(256) void procrustes_kernel(ProcrustesArgs<T> a) {
   }
 }
 
+
+// ----------------------------------------------------------------------------------------------------
+// RANSAC over given correspondences: lib/utils.py:671-709 run_ransac ->
+// Open3D 0.9 registration_ransac_based_on_correspondence(TransformationEstimationPointToPoint(False),
+// ransac_n = 4, max_correspondence_distance = 0.05, RANSACConvergenceCriteria(50000, 2500)).
+// Open3D 0.9's loop (restated; oracle/ransac.py): min(max_iteration, max_validation) iterations; each draws
+// ransac_n correspondences with replacement, fits R, t by Umeyama without scaling (fp64), and scores the
+// fit over ALL correspondences: inlier iff |R x1 + t - x2|^2 < d^2, fitness = inliers / n,
+// rmse = sqrt(sum of inlier d^2 / inliers); the result is the first hypothesis that is best by (fitness
+// desc, rmse asc) among those with fitness > 0, identity when none (or n < ransac_n).  Open3D seeds
+// std::rand from the clock; here draw j of iteration i for pair p is splitmix64(seed + ctr * golden) % n with
+// ctr = (p << 40) | (i << 8) | j — reproducible, and the same on the host (oracle/ransac.py:draws).
+//
+// One thread per (pair, hypothesis): its 4 draws, the Umeyama fit (jacobi_svd3), then a sequential pass
+// over the pair's correspondences staged through LDS in 256-row tiles (every thread of the workgroup reads
+// the same row: LDS broadcast), in correspondence order and with rounded fp64 ops (no contraction), so the
+// counts and error sums equal the host restatement's bit for bit.  A second kernel picks each pair's best.
+// Work per pair: iters x n x ~15 fp64 ops (2500 x 5000: 0.19 GFLOP) — fp64 VALU-bound.
+// ----------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t ransac_draw(uint64_t seed, uint64_t ctr) {
+  uint64_t z = seed + ctr * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct RansacArgs {
+  const double* x1; const double* x2; int64_t ps;   // [P][ps] rows of 3 doubles
+  const int32_t* n;                                  // [P] correspondences per pair
+  int P, iters, rn;
+  double d2;                                         // max distance squared
+  uint64_t seed;
+  int32_t* cnt; double* err;                         // [P][iters]
+  double* hyp;                                       // [P][iters][12] (R row-major, t) or null
+};
+
+constexpr int RS_TILE = 256;
+
+__global__ __launch_bounds__(256) void ransac_eval_kernel(RansacArgs a) {
+#pragma clang fp contract(off)   // hipcc contracts a * b + c into fma by default; the evaluation rounds every op
+  __shared__ double tile[RS_TILE][6];
+  const int p = blockIdx.y, it = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.n[p];
+  if (n < a.rn) return;   // uniform: no hypotheses (selection returns identity)
+  const double* x1 = a.x1 + (int64_t)p * a.ps;
+  const double* x2 = a.x2 + (int64_t)p * a.ps;
+  const bool live = it < a.iters;
+  double R[3][3], t[3];
+  {
+    // Umeyama without scaling on the draws: sigma = sum (dst - mu_d)(src - mu_s)^T / k = U S V^T,
+    // R = U diag(1, 1, sign(det U det V)) V^T, t = mu_d - R mu_s
+    double s[8][3], d[8][3], ms[3] = {0, 0, 0}, md[3] = {0, 0, 0};
+    const int k = a.rn;
+    for (int j = 0; j < k; ++j) {
+      const uint64_t ctr = ((uint64_t)p << 40) | ((uint64_t)(live ? it : 0) << 8) | (uint64_t)j;
+      const int64_t c = (int64_t)(ransac_draw(a.seed, ctr) % (uint64_t)n);
+      for (int e = 0; e < 3; ++e) {
+        s[j][e] = x1[3 * c + e];
+        d[j][e] = x2[3 * c + e];
+        ms[e] = ms[e] + s[j][e];
+        md[e] = md[e] + d[j][e];
+      }
+    }
+    for (int e = 0; e < 3; ++e) {
+      ms[e] = ms[e] / k;
+      md[e] = md[e] / k;
+    }
+    double H[3][3];
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c) {
+        double acc = 0.0;
+        for (int j = 0; j < k; ++j) acc = acc + (d[j][r] - md[r]) * (s[j][c] - ms[c]);
+        H[r][c] = acc / k;
+      }
+    double U[3][3], S[3], V[3][3];
+    jacobi_svd3(H, U, S, V);
+    const double sg = (det3(U) * det3(V) < 0.0) ? -1.0 : 1.0;
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < 3; ++c)
+        R[r][c] = (U[r][0] * V[c][0] + U[r][1] * V[c][1]) + (sg * U[r][2]) * V[c][2];
+    for (int r = 0; r < 3; ++r)
+      t[r] = md[r] - ((R[r][0] * ms[0] + R[r][1] * ms[1]) + R[r][2] * ms[2]);
+  }
+  if (live && a.hyp) {
+    double* h = a.hyp + ((int64_t)p * a.iters + it) * 12;
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) h[3 * r + c] = R[r][c];
+      h[9 + r] = t[r];
+    }
+  }
+  int good = 0;
+  double e2 = 0.0;
+  for (int b0 = 0; b0 < n; b0 += RS_TILE) {
+    const int nb = min(RS_TILE, n - b0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nb * 6; i += blockDim.x) {
+      const int r = i / 6, e = i % 6;
+      tile[r][e] = e < 3 ? x1[3 * (int64_t)(b0 + r) + e] : x2[3 * (int64_t)(b0 + r) + e - 3];
+    }
+    __syncthreads();
+    for (int r = 0; r < nb; ++r) {
+      const double* q = tile[r];
+      double dd = 0.0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const double y = ((R[e][0] * q[0] + R[e][1] * q[1]) + R[e][2] * q[2]) + t[e];
+        const double df = y - q[3 + e];
+        dd = dd + df * df;
+      }
+      if (dd < a.d2) {
+        ++good;
+        e2 = e2 + dd;
+      }
+    }
+  }
+  if (live) {
+    a.cnt[(int64_t)p * a.iters + it] = good;
+    a.err[(int64_t)p * a.iters + it] = e2;
+  }
+}
+
+// best hypothesis per pair: fitness desc, rmse asc, iteration asc (= Open3D's strict-improvement loop)
+__global__ __launch_bounds__(256) void ransac_select_kernel(RansacArgs a, double* T, double* fitness, double* rmse,
+                                                            int32_t* best) {
+  __shared__ int bi[256];
+  const int p = blockIdx.x, tid = threadIdx.x;
+  const int n = a.n[p];
+  auto better = [&](int i, int j) {   // hypothesis i strictly before j in the order
+    if (j < 0) return i >= 0;
+    if (i < 0) return false;
+    const int ci = a.cnt[(int64_t)p * a.iters + i], cj = a.cnt[(int64_t)p * a.iters + j];
+    if (ci != cj) return ci > cj;
+    const double ri = sqrt(a.err[(int64_t)p * a.iters + i] / ci), rj = sqrt(a.err[(int64_t)p * a.iters + j] / cj);
+    if (ri != rj) return ri < rj;
+    return i < j;
+  };
+  int mine = -1;
+  if (n >= a.rn)
+    for (int i = tid; i < a.iters; i += blockDim.x)
+      if (a.cnt[(int64_t)p * a.iters + i] > 0 && better(i, mine)) mine = i;
+  bi[tid] = mine;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w && better(bi[tid + w], bi[tid])) bi[tid] = bi[tid + w];
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const int b = bi[0];
+  double* Tp = T + (int64_t)p * 16;
+  for (int i = 0; i < 16; ++i) Tp[i] = (i % 5 == 0) ? 1.0 : 0.0;
+  best[p] = b;
+  if (b < 0) {
+    fitness[p] = 0.0;
+    rmse[p] = 0.0;
+    return;
+  }
+  const int c = a.cnt[(int64_t)p * a.iters + b];
+  fitness[p] = (double)c / n;
+  rmse[p] = sqrt(a.err[(int64_t)p * a.iters + b] / c);
+  // the winner's transformation, recomputed by its own thread in ransac_eval_kernel: read it back from the
+  // hypothesis buffer (always allocated by the launcher)
+  const double* h = a.hyp + ((int64_t)p * a.iters + b) * 12;
+  for (int r = 0; r < 3; ++r) {
+    for (int cc = 0; cc < 3; ++cc) Tp[4 * r + cc] = h[3 * r + cc];
+    Tp[4 * r + 3] = h[9 + r];
+  }
+}
+
 }  // namespace mvr
 
 template <typename T>
@@ -248,4 +416,34 @@ extern "C" int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_
   return procrustes_launch<double>(x1, x2, x_pstride, x_nstride, w, w_pstride, guard_pos, w_copy, wc_pstride, P, N,
                                    normalize, eps, R, t, res, res_pstride, res_copy, rc_pstride, status, guard_group,
                                    stream);
+}
+
+extern "C" size_t mvr_ransac_workspace_bytes(int P, int iters) {
+  if (P <= 0 || iters <= 0) return 0;
+  return (size_t)P * iters * (sizeof(int32_t) + sizeof(double) + 12 * sizeof(double)) + 256;
+}
+
+extern "C" int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride, const int32_t* n, int P, int ransac_n,
+                          int iters, double max_dist, uint64_t seed, double* T, double* fitness, double* rmse,
+                          int32_t* best_iter, double* hyp_out, void* workspace, size_t workspace_bytes,
+                          hipStream_t stream) {
+  if (P < 0 || !x1 || !x2 || !n || !T || !fitness || !rmse || !best_iter || ransac_n < 3 || ransac_n > 8 ||
+      iters <= 0 || iters >= (1 << 30) || P >= (1 << 23) || !(max_dist > 0.0))
+    return MVR_EINVAL;
+  if (P == 0) return MVR_OK;
+  const size_t need = mvr_ransac_workspace_bytes(P, iters) - (hyp_out ? (size_t)P * iters * 12 * sizeof(double) : 0);
+  if (!workspace || workspace_bytes < need) return MVR_EINVAL;
+  mvr::RansacArgs a{};
+  a.x1 = x1; a.x2 = x2; a.ps = x_pstride; a.n = n;
+  a.P = P; a.iters = iters; a.rn = ransac_n; a.d2 = max_dist * max_dist; a.seed = seed;
+  char* w = static_cast<char*>(workspace);
+  a.err = reinterpret_cast<double*>(w);
+  a.cnt = reinterpret_cast<int32_t*>(w + (size_t)P * iters * sizeof(double));
+  a.hyp = hyp_out ? hyp_out
+                  : reinterpret_cast<double*>(w + (((size_t)P * iters * (sizeof(double) + sizeof(int32_t)) + 255) & ~(size_t)255));
+  hipLaunchKernelGGL(mvr::ransac_eval_kernel, dim3((iters + 255) / 256, P), dim3(256), 0, stream, a);
+  MVR_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mvr::ransac_select_kernel, dim3(P), dim3(256), 0, stream, a, T, fitness, rmse, best_iter);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
 }

@@ -51,6 +51,9 @@ _SIGS = {
                                c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_vp]),
     "mvr_procrustes_f64": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_i64, c_int, c_int, c_int,
                                    ctypes.c_double, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_vp]),
+    "mvr_ransac_workspace_bytes": (c_size, [c_int, c_int]),
+    "mvr_ransac": (c_int, [c_vp, c_vp, c_i64, c_vp, c_int, c_int, c_int, ctypes.c_double, ctypes.c_uint64, c_vp, c_vp,
+                           c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
                              c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int,
                              c_int, c_int, c_vp]),

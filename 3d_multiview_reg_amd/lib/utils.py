@@ -286,9 +286,53 @@ def evaluate_registration(num_fragment, result, result_pairs, gt_pairs, gt, gt_i
     return good * 1.0 / n_res, good * 1.0 / n_gt
 
 
-def run_ransac(xyz_i, xyz_j):
-    """utils.py:671-709 uses Open3D's RANSAC (a comparison baseline, out of scope here)."""
-    raise NotImplementedError("RANSAC baseline (open3d) is not part of the MI355X hot path")
+RANSAC_N, RANSAC_DIST, RANSAC_ITERS = 4, 0.05, 2500   # utils.py:688,701-705: min(50000, 2500) iterations
+
+
+def run_ransac_batch(xyz_i, xyz_j, counts=None, seed=0, ransac_n=RANSAC_N, max_dist=RANSAC_DIST,
+                     iters=RANSAC_ITERS, device=None, return_all=False):
+    """Batched RANSAC over correspondences (csrc/procrustes.hip mvr_ransac): xyz_i, xyz_j [P, n, 3]
+    (torch or numpy; computed in fp64 as Open3D's Vector3d), counts [P] valid rows per pair (default n).
+    Returns T [P, 4, 4] float64 numpy (x_j ~ T x_i), and with return_all also fitness, rmse, best_iter."""
+    from lib import _native as N
+    N.require_hip()
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    x1 = torch.as_tensor(xyz_i).to(dev, torch.float64).contiguous()
+    x2 = torch.as_tensor(xyz_j).to(dev, torch.float64).contiguous()
+    if x1.dim() != 3 or x1.shape != x2.shape or x1.shape[-1] != 3:
+        raise ValueError("xyz_i / xyz_j must both be [P, n, 3]")
+    P, n = x1.shape[0], x1.shape[1]
+    cnt = torch.full((P,), n, dtype=torch.int32) if counts is None else torch.as_tensor(counts).to(torch.int32)
+    if cnt.numel() != P or bool((cnt < 0).any()) or bool((cnt > n).any()):
+        raise ValueError("counts must be [P] with 0 <= counts <= n")
+    cnt = cnt.to(dev)
+    T = torch.empty(P, 4, 4, dtype=torch.float64, device=dev)
+    fit = torch.empty(P, dtype=torch.float64, device=dev)
+    rmse = torch.empty(P, dtype=torch.float64, device=dev)
+    best = torch.empty(P, dtype=torch.int32, device=dev)
+    L = N.lib()
+    ws = N.workspace(L.mvr_ransac_workspace_bytes(P, iters), dev)
+    N.check(L.mvr_ransac(N.ptr(x1), N.ptr(x2), n * 3, N.ptr(cnt), P, ransac_n, iters, float(max_dist),
+                         int(seed) & 0xFFFFFFFFFFFFFFFF, N.ptr(T), N.ptr(fit), N.ptr(rmse), N.ptr(best), None,
+                         N.ptr(ws), ws.numel(), N.stream()), "mvr_ransac")
+    if return_all:
+        return T.cpu().numpy(), fit.cpu().numpy(), rmse.cpu().numpy(), best.cpu().numpy()
+    return T.cpu().numpy()
+
+
+_ransac_calls = [0]
+
+
+def run_ransac(xyz_i, xyz_j, seed=None):
+    """utils.py:671-709: RANSAC-based estimate of the transformation mapping xyz_i [n,3] onto xyz_j [n,3]
+    (correspondences are row-aligned), returned as a 4x4 float64 array.  Open3D seeds its draws from the
+    clock; here each call draws from a counter-based stream (seed = call number unless given)."""
+    if seed is None:
+        seed = _ransac_calls[0]
+        _ransac_calls[0] += 1
+    x1 = np.asarray(xyz_i, dtype=np.float64).reshape(1, -1, 3)
+    x2 = np.asarray(xyz_j, dtype=np.float64).reshape(1, -1, 3)
+    return run_ransac_batch(x1, x2, seed=seed)[0]
 
 
 def compute_overlap_ratio(pc_i, pc_j, trans, method="3DMatch", voxel_size=0.025):

@@ -53,6 +53,24 @@ int mvr_procrustes_f64(const double* x1, const double* x2, int64_t x_pstride, in
                        mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * RANSAC over given correspondences, batched over pairs.
+ * Replaces lib/utils.py:671-709 run_ransac (Open3D 0.9
+ * registration_ransac_based_on_correspondence, point-to-point estimation without
+ * scaling, ransac_n = 4, max distance 0.05, RANSACConvergenceCriteria(50000, 2500):
+ * 2500 iterations) as called at scripts/benchmark_pairwise_registration.py:100,212.
+ *   x1(p,i,:) = x1[p*x_pstride + 3i + 0..2] (fp64), x2 likewise; n[p] correspondences of pair p.
+ *   Outputs: T [P,4,4] row-major (x2 ~ T x1; identity when no hypothesis has an inlier or
+ *   n[p] < ransac_n), fitness [P], rmse [P], best_iter [P] (-1: none).
+ *   Draw j of iteration i for pair p: splitmix64(seed + ((p<<40)|(i<<8)|j) * 0x9E3779B97F4A7C15) % n[p]
+ *   (Open3D draws std::rand() % n from a clock seed).  hyp_out [P,iters,12] (R row-major, t) may be
+ *   NULL; workspace >= mvr_ransac_workspace_bytes(P, iters).
+ * ---------------------------------------------------------------------- */
+size_t mvr_ransac_workspace_bytes(int P, int iters);
+int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride, const int32_t* n, int P, int ransac_n,
+               int iters, double max_dist, uint64_t seed, double* T, double* fitness, double* rmse,
+               int32_t* best_iter, double* hyp_out, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
+
+/* ------------------------------------------------------------------------
  * One fused fp32-MFMA batched GEMM of the OANet schedule (exposed for tests):
  *   C[b](m,n) = sum_k pro_A(A(m,k)) pro_B(B(k,n)) + bias + R[b](m,n)
  * pro: 0 none, 1 relu(A*sc[k]+sh[k]), 2 relu(B*sc[k]+sh[k]) (sc/sh at [b*sPb + k]),
