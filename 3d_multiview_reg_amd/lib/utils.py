@@ -258,7 +258,7 @@ def computeTransformationErr(trans, info):
     t = trans[:3, 3]
     q = mat2quat(trans[:3, :3])
     er = np.concatenate([t, q[1:]], axis=0)
-    return float(er.reshape(1, 6) @ info @ er.reshape(6, 1) / info[0, 0])
+    return float((er.reshape(1, 6) @ info @ er.reshape(6, 1))[0, 0] / info[0, 0])
 
 
 def evaluate_registration(num_fragment, result, result_pairs, gt_pairs, gt, gt_info, err2=0.2):
