@@ -76,3 +76,30 @@ def test_filter_method_plumbing(gpu, tmp_path, refine):
     s = main(argv)
     assert 0.0 <= s["recall"] <= 1.0 and "iclnuim-office1" in s["scenes"]
     assert os.path.exists(os.path.join(root, "redwood", "results", "RegBlock", "all", "iclnuim-office1", "traj.txt"))
+
+
+def test_pairwise_demo(gpu, tmp_path, monkeypatch):
+    """scripts/pairwise_demo.py mirror: two synthetic fragments (PLY) -> est_T.log in the reference's place"""
+    import yaml
+    from lib.ply import write_ply_xyz
+    from lib.utils import read_trajectory, load_config
+    from synth import synth_scene_fragments
+    from scripts.pairwise_demo import main, parser
+    frags, _ = synth_scene_fragments(n_frag=2, seed=5, n_pts=60000)
+    for k in range(2):
+        write_ply_xyz(str(tmp_path / ("cloud_bin_%d.ply" % k)), frags[k])
+    cfg = {"misc": {"voxel_size": 0.025, "net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128,
+                    "use_gpu": True, "normalize_weights": True},
+           "data": {"use_mutuals": 0, "max_num_points": 5000},
+           "method": {"task": "pairwise", "descriptor_module": "fcgf", "filter_module": "oanet"},
+           "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
+    with open(tmp_path / "config.yaml", "w") as f:
+        yaml.safe_dump(cfg, f)
+    monkeypatch.chdir(tmp_path)
+    a = parser().parse_args([str(tmp_path / "config.yaml"), "--source_pc", str(tmp_path / "cloud_bin_0.ply"),
+                             "--target_pc", str(tmp_path / "cloud_bin_1.ply"), "--verbose"])
+    T = main(load_config(a.config), a)
+    keys, traj = read_trajectory(str(tmp_path / "data/demo/pairwise/results/est_T.log"))
+    assert keys.tolist() == [["0", "1", "True"]]
+    np.testing.assert_allclose(traj[0], T, atol=1e-9)
+    np.testing.assert_allclose(T[:3, :3] @ T[:3, :3].T, np.eye(3), atol=1e-5)
