@@ -125,7 +125,12 @@ class Sampler(torch.nn.Module):
 
     def forward(self, input_C, input_F, pts_list):
         N.require_hip(input_F)
-        idx = self.indices(pts_list, input_C).to(input_F.device).reshape(-1).contiguous()
+        idx = self.indices(pts_list, input_C)
+        if idx.device.type == "cpu":
+            # the host draws reach the device through pinned memory without blocking the host (a pageable
+            # copy would wait for everything already queued on the stream, i.e. the whole FCGF pass)
+            idx = idx.pin_memory().to(input_F.device, non_blocking=True)
+        idx = idx.reshape(-1).contiguous()
         B = len(pts_list)
         C = input_F.float().contiguous()
         X = input_C.float().contiguous()

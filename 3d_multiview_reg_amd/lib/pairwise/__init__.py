@@ -56,8 +56,13 @@ class PairwiseReg(nn.Module):
         dev = next(self.descriptor_module.parameters()).device
         xyz_down = input_dict["pcd0"].to(dev).float().contiguous()
         pts_list = input_dict["pts_list"]
-        sinput0 = SparseTensor(input_dict["sinput0_F"], coords=input_dict["sinput0_C"],
-                               batch_size=len(pts_list)).to(dev)
+        if input_dict.get("sinput0_coords_manager") is not None:
+            # a prepared lib.sparse.CoordinateManager of sinput0_C (its strided coordinate sets already built,
+            # e.g. one scene ahead on another stream): the FCGF launches then need no host synchronisation
+            sinput0 = SparseTensor(input_dict["sinput0_F"], coords_manager=input_dict["sinput0_coords_manager"]).to(dev)
+        else:
+            sinput0 = SparseTensor(input_dict["sinput0_F"], coords=input_dict["sinput0_C"],
+                                   batch_size=len(pts_list)).to(dev)
         F0 = self.descriptor_module(sinput0).F
         if self.train_descriptor:
             sinput1 = SparseTensor(input_dict["sinput1_F"], coords=input_dict["sinput1_C"]).to(dev)

@@ -134,7 +134,7 @@ def voxelize(points_list, voxel_size, device, distinct_hint=None):
     B = len(pts)
     n = [int(p.shape[0]) for p in pts]
     xyz = torch.cat(pts, 0).to(device).contiguous()
-    off = torch.tensor(np.concatenate([[0], np.cumsum(n)]), dtype=torch.int64, device=device)
+    off = torch.tensor(np.concatenate([[0], np.cumsum(n)]), dtype=torch.int64).pin_memory().to(device, non_blocking=True)
     total = int(sum(n))
     L = N.lib()
     coords = torch.empty(total, 4, dtype=torch.int32, device=device)

@@ -138,8 +138,11 @@ def extract_mutuals(x1, x2, x1_soft_matches, x2_soft_matches, threshold=0.05):
 
 def pair_index(B, device=None):
     """All C(B,2) fragment pairs in lexicographic order (utils.py:873-876), int64 [P,2]."""
-    pairs = list(combinations(range(B), 2))
-    return torch.tensor(pairs, dtype=torch.long, device=device).reshape(-1, 2)
+    pairs = torch.tensor(list(combinations(range(B), 2)), dtype=torch.long).reshape(-1, 2)
+    if device is not None and torch.device(device).type == "cuda":
+        # pinned + non_blocking: a pageable upload would block the host until the stream's queued work is done
+        return pairs.pin_memory().to(device, non_blocking=True)
+    return pairs.to(device) if device is not None else pairs
 
 
 def extract_overlaping_pairs(xyz, feat, conectivity_info=None):

@@ -127,13 +127,22 @@ class SceneWorkload:
         self.pairs = n_frag * (n_frag - 1) // 2
         self.vox_counts = None
 
-    def describe(self):
-        """voxelise -> FCGF -> Sampler -> feature NN over all pairs (compute_descriptors)"""
-        from lib.sparse import voxelize
-        coords, sel, counts, xyz_down = voxelize(self.raw, self.voxel, self.dev)   # prepare_data on the GPU
+    def prepare(self):
+        """voxelise (prepare_data on the GPU) and build the strided coordinate sets of the sparse input: every
+        host synchronisation of the scene (voxel counts, the size of each coordinate level) happens here"""
+        from lib.sparse import voxelize, CoordinateManager
+        coords, sel, counts, xyz_down = voxelize(self.raw, self.voxel, self.dev)
+        cm = CoordinateManager(coords, len(counts))
+        for s in (2, 4, 8):   # FCGF's tensor strides (fcgf.py:118-227)
+            cm.coords_at(s)
         self.vox_counts = counts
-        data = {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
-                "pts_list": torch.tensor(counts)}
+        return {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
+                "pts_list": torch.tensor(counts), "sinput0_coords_manager": cm}
+
+    def describe(self, data=None):
+        """(voxelise ->) FCGF -> Sampler -> feature NN over all pairs (compute_descriptors)"""
+        if data is None:
+            data = self.prepare()
         np.random.seed(self.rng_seed)
         fin, _, _ = self.model.compute_descriptors(data)
         return fin
@@ -149,16 +158,20 @@ class SceneWorkload:
         return self.finish(self.describe())
 
     def step_pipelined(self, world):
-        """Two-stage software pipeline over consecutive scenes on two HIP streams: the filtering (OANet +
-        Procrustes) of scene k-1 (stream B, enqueued first) runs while scene k is voxelised, described and
-        matched (stream A, whose host-side steps — the voxel counts, the numpy sample draw — then overlap B's
-        device work).  Returns the gathered records of scene k-1 (None on the first call)."""
+        """Software pipeline over consecutive scenes on three HIP streams: the filtering (OANet + Procrustes)
+        of scene k-1 (stream B, enqueued first) runs while scene k is described by FCGF and matched (stream A),
+        and scene k+1 is voxelised with its coordinate levels built (stream C).  Every host synchronisation of
+        a scene (voxel counts, level sizes) waits only for stream C's short queue, so the host enqueues the FCGF
+        stage without stalls and streams A and B stay fed.  Returns the gathered records of scene k-1 (None on
+        the first call)."""
         if not hasattr(self, "streams"):
-            # B (matching + OANet, the longer stage) at high priority: its kernels take the CUs first and the
-            # FCGF stage fills what they leave free
-            self.streams = (torch.cuda.Stream(self.dev), torch.cuda.Stream(self.dev, priority=-1))
+            # B (OANet, the longer stage) at high priority: its kernels take the CUs first and the FCGF stage
+            # fills what they leave free; C (short voxelisation kernels the host waits for) high as well
+            self.streams = (torch.cuda.Stream(self.dev), torch.cuda.Stream(self.dev, priority=-1),
+                            torch.cuda.Stream(self.dev, priority=-1))
             self.pending = None
-        sA, sB = self.streams
+            self.prepared = None
+        sA, sB, sC = self.streams
         rec = None
         if self.pending is not None:
             fin, ev = self.pending
@@ -166,11 +179,23 @@ class SceneWorkload:
                 sB.wait_event(ev)
                 fin["xs"].record_stream(sB)
                 rec = records_allgather(self.finish(fin), world)
+        if self.prepared is None:
+            with torch.cuda.stream(sC):
+                self.prepared = (self.prepare(), torch.cuda.Event())
+                self.prepared[1].record(sC)
+        data, evc = self.prepared
         with torch.cuda.stream(sA):
-            fin = self.describe()
+            sA.wait_event(evc)
+            cm = data["sinput0_coords_manager"]
+            for t in [data["pcd0"], data["sinput0_C"], data["sinput0_F"]] + list(cm.coords.values()):
+                t.record_stream(sA)
+            fin = self.describe(data)
             ev = torch.cuda.Event()
             ev.record(sA)
         self.pending = (fin, ev)
+        with torch.cuda.stream(sC):   # the next scene (the same synthetic scene, re-voxelised each step)
+            self.prepared = (self.prepare(), torch.cuda.Event())
+            self.prepared[1].record(sC)
         return rec
 
     def config(self):
@@ -372,8 +397,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32(bf16x3)", "data": "synthetic",
             "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
-                           schedule=("2-stage stream pipeline over consecutive scenes: FCGF + feature NN of scene k "
-                                     "beside OANet + Procrustes of scene k-1; every timed step runs both stages in full"
+                           schedule=("3-stream pipeline over consecutive scenes: voxelisation + coordinate levels of "
+                                     "scene k+1, FCGF + feature NN of scene k, OANet + Procrustes of scene k-1; every "
+                                     "timed step runs every stage in full"
                                      if pipelined else "stages back to back on one stream")),
             "roofline": roof, "cpu_baseline": cpu}
     if rank == 0:
