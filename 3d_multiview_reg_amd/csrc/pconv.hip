@@ -38,6 +38,15 @@ namespace mvr {
 #ifndef PCONV_POISON
 #define PCONV_POISON 0
 #endif
+#ifndef PCONV_NTS
+#define PCONV_NTS 1   // nontemporal output stores (-2 % per launch, tools/jobs A/B)
+#endif
+#ifndef PCONV_NTR
+#define PCONV_NTR 0   // experiment: nontemporal residual loads
+#endif
+#ifndef PCONV_NTL
+#define PCONV_NTL 2   // cache-policy bits of the activation buffer loads: nt (streamed once; -3 % per step's point convs)
+#endif
 #ifndef PCONV_ABL
 #define PCONV_ABL 0   // timing ablations (wrong results; tools/build_variant.sh): 1 no MFMA, 2 no split,
                       // 4 no epilogue, 8 no activation loads
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       for (int i = 0; i < 8; ++i)
         r[8 * t + i] = (PCONV_ABL & 8) ? (float)(i + t)
                                        : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                       rs, vo, (16 * t + i) * xld4, 0));
+                                                                       rs, vo, (16 * t + i) * xld4, PCONV_NTL));
   };
   // normalise + split half t of a chunk's registers -> its k-step fragment in image slot
   auto split_half = [&](const Cur& c, const float (&r)[NX], int slot, int t) {
@@ -330,7 +339,15 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
     const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + erow) * a.yld + n;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) rres[(RES && !(XI & 2)) ? q : 0] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.yld);
+    for (int q = 0; q < 4; ++q) {
+      if (PCONV_NTR) {
+        const u32x4 u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + (int64_t)(8 * q) * a.yld));
+        rres[(RES && !(XI & 2)) ? q : 0] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                                                       __uint_as_float(u.w));
+      } else {
+        rres[(RES && !(XI & 2)) ? q : 0] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.yld);
+      }
+    }
   };
 
   // running statistics of the current 128-point group, per lane (its 4 rows x 4 columns of each chunk):
@@ -414,7 +431,15 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     if (HEAD != 2) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (full || n0 + ec0 < N4) *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
+        if (full || n0 + ec0 < N4) {
+          if (PCONV_NTS) {
+            const u32x4 u = {__float_as_uint(ev[q].x), __float_as_uint(ev[q].y), __float_as_uint(ev[q].z),
+                             __float_as_uint(ev[q].w)};
+            __builtin_nontemporal_store(u, reinterpret_cast<u32x4*>(ydst + (int64_t)(8 * q) * a.yld));
+          } else {
+            *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
+          }
+        }
     }
     if (HEAD) {   // partial logits of the wave's 32 rows for the chunk's columns, summed over lanes l ^ 8, 16, 32
       float hp[4] = {0.f, 0.f, 0.f, 0.f};
