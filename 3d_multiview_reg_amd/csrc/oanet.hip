@@ -43,49 +43,22 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
   const int T = (L + tw - 1) / tw;
   const float2* sp = st + (int64_t)p * T * st_ld + st_off + cc;
   // two passes over the tiles: the pooled mean, then M2 = sum_t (M2_t + n_t (mean_t - mean)^2)
-  // (tiles are full except the last, so one reciprocal serves all but one).  When a thread's tiles fit
-  // FIN_R registers (T <= G * FIN_R: every point launch), they are all loaded up front — one round trip
-  // to memory instead of a chain per pass — and kept for the second pass.
-  constexpr int FIN_R = 12;
-  const bool inreg = T <= G * FIN_R;
-  float2 v[FIN_R];
+  // (tiles are full except the last, so one reciprocal serves all but one)
   double tot = 0.0;
-  if (inreg) {
-#pragma unroll
-    for (int i = 0; i < FIN_R; ++i) {
-      const int t = tg + i * G;
-      v[i] = t < T ? sp[(int64_t)t * st_ld] : make_float2(0.f, 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < FIN_R; ++i) tot += (double)v[i].x;
-  } else {
 #pragma unroll 4
-    for (int t = tg; t < T; t += G) tot += (double)__builtin_nontemporal_load(&sp[(int64_t)t * st_ld].x);
-  }
+  for (int t = tg; t < T; t += G) tot += (double)__builtin_nontemporal_load(&sp[(int64_t)t * st_ld].x);
   red[tg * nb + lt] = tot;
   __syncthreads();
   tot = 0.0;
   for (int j = 0; j < G; ++j) tot += red[j * nb + lt];
   const double mean = tot / L, rtw = 1.0 / tw;
   double m2 = 0.0;
-  if (inreg) {
-#pragma unroll
-    for (int i = 0; i < FIN_R; ++i) {
-      const int t = tg + i * G;
-      if (t < T) {
-        const int nv = min(tw, L - tw * t);
-        const double d = (double)v[i].x * (nv == tw ? rtw : 1.0 / nv) - mean;
-        m2 += (double)v[i].y + d * d * nv;
-      }
-    }
-  } else {
 #pragma unroll 4
-    for (int t = tg; t < T; t += G) {
-      const float2 w = sp[(int64_t)t * st_ld];
-      const int nv = min(tw, L - tw * t);
-      const double d = (double)w.x * (nv == tw ? rtw : 1.0 / nv) - mean;
-      m2 += (double)w.y + d * d * nv;
-    }
+  for (int t = tg; t < T; t += G) {
+    const float2 v = sp[(int64_t)t * st_ld];
+    const int nv = min(tw, L - tw * t);
+    const double d = (double)v.x * (nv == tw ? rtw : 1.0 / nv) - mean;
+    m2 += (double)v.y + d * d * nv;
   }
   __syncthreads();   // every group has read the sums
   red[tg * nb + lt] = m2;
@@ -444,8 +417,8 @@ struct Ctx {
   // IN(eps)+BN fold of activation `a` -> sc / sh ([P][a.C], default pl.sc / pl.sh)
   void finalize_in(const Act& a, float eps, const mvr_bn_p& bn, float* sc = nullptr, float* sh = nullptr) {
     if (!sc) { sc = pl.sc; sh = pl.sh; }
-    // 64 channels x 8 tile groups per workgroup: 512 threads that fit beside the other stream's kernels
-    const int bs = 64, G = 8;
+    const int bs = a.C >= 256 ? 256 : (a.C + 63) & ~63;
+    const int G = 1024 / bs < 4 ? 1024 / bs : 4;   // tile groups per channel
     dim3 grid((a.C + bs - 1) / bs, pl.P);
     hipLaunchKernelGGL(in_finalize_kernel, grid, dim3(bs, G), sizeof(double) * bs * G, s, a.st, a.st_ld, a.st_off,
                        a.tw0, a.csplit, a.tw1, a.C, a.L, eps, bn, train, sc, sh, (int64_t)a.C, pl.mv);
