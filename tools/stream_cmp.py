@@ -1,5 +1,6 @@
-"""Per-kernel device time per step: the untimed sequential step (stream 0) vs the pipelined timed steps
-(streams 1, 2) of a `tools/prof_bench.sh` kernel trace.  usage: stream_cmp.py <trace_kernel_trace.csv> <steps>"""
+"""Per-kernel device time per step by HIP stream of a `tools/prof_bench.sh` kernel trace: stream 0 = the
+untimed sequential profiled step; the other streams = the pipelined steps (bench.py: C voxelisation, A FCGF +
+matching, B OANet, in creation order).  usage: stream_cmp.py <trace_kernel_trace.csv> <pipelined steps>"""
 import collections
 import csv
 import sys
@@ -8,14 +9,17 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 steps = int(sys.argv[2])
 tot = collections.defaultdict(float)
 for r in rows:
-    n = r["Kernel_Name"].split("(")[0].replace("void ", "")[:48]
+    n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mvr::", "")[:44]
     tot[(n, r["Stream_Id"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-names = sorted({k[0] for k in tot}, key=lambda n: -tot.get((n, "0"), 0))
-print(f"{'kernel':48s} {'seq ms':>8s} {'A ms/st':>8s} {'B ms/st':>8s}")
-s0 = s1 = s2 = 0.0
+sids = sorted({k[1] for k in tot}, key=int)
+names = sorted({k[0] for k in tot}, key=lambda n: -sum(tot.get((n, s), 0) for s in sids))
+print("%-44s %s" % ("kernel (ms; stream 0 = one sequential step, others per pipelined step)",
+                    " ".join("%9s" % ("s%s" % s) for s in sids)))
+sums = collections.Counter()
 for n in names:
-    a, b, c = tot.get((n, "0"), 0), tot.get((n, "1"), 0) / steps, tot.get((n, "2"), 0) / steps
-    s0 += a; s1 += b; s2 += c
-    if max(a, b, c) > 0.05:
-        print(f"{n:48s} {a:8.3f} {b:8.3f} {c:8.3f}")
-print(f"{'total':48s} {s0:8.3f} {s1:8.3f} {s2:8.3f}")
+    v = [tot.get((n, s), 0) / (1 if s == "0" else steps) for s in sids]
+    for s, x in zip(sids, v):
+        sums[s] += x
+    if max(v) > 0.05:
+        print("%-44s %s" % (n, " ".join("%9.3f" % x for x in v)))
+print("%-44s %s" % ("total", " ".join("%9.3f" % sums[s] for s in sids)))
