@@ -9,7 +9,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 steps = int(sys.argv[2])
 tot = collections.defaultdict(float)
 for r in rows:
-    n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("mvr::", "")[:44]
+    n = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("mvr::", "")[:44]
     tot[(n, r["Stream_Id"])] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
 sids = sorted({k[1] for k in tot}, key=int)
 names = sorted({k[0] for k in tot}, key=lambda n: -sum(tot.get((n, s), 0) for s in sids))
