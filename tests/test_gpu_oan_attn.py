@@ -361,6 +361,15 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
     net = _oanet(128, 500, 9, gpu, train=train, which="full")
     outs = []
     L = NV.lib()
+    if os.environ.get("MVR_TEST_DEBUG"):   # the library knobs as this test finds them
+        knobs = {}
+        for k in ("pconv", "feat_nn_fast", "oan_fused", "pool_split", "unpool4", "attn_math",
+                  "pconv_math", "spconv_math", "gemm_f16"):
+            f = getattr(L, "mvr_set_" + k)
+            v = f(0)
+            f(v)
+            knobs[k] = v
+        print("\nDEBUG knobs %s" % knobs, flush=True)
     prev = L.mvr_set_oan_fused(5)
     try:
         for f in (5, 1):
