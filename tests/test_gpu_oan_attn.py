@@ -369,7 +369,7 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
             v = f(0)
             f(v)
             knobs[k] = v
-        print("\nDEBUG knobs %s" % knobs, flush=True)
+        print("\nDEBUG knobs %s reruns before %d" % (knobs, L.mvr_attn_reruns(1)), flush=True)
     prev = L.mvr_set_oan_fused(5)
     try:
         for f in (5, 1):
@@ -388,8 +388,8 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
     if os.environ.get("MVR_TEST_DEBUG"):   # history-dependence diagnosis (open issue)
         import hashlib
         hx = lambda v: hashlib.sha1(np.ascontiguousarray(v).tobytes()).hexdigest()[:12]  # noqa: E731
-        print("\nDEBUG npts %d train %d: gpu5 %s gpu1 %s o64 %s xs %s" % (
-            npts, train, hx(outs[0]["logits"][1].cpu().numpy()), hx(outs[1]["logits"][1].cpu().numpy()),
+        print("\nDEBUG npts %d train %d: attention re-runs %d gpu5 %s gpu1 %s o64 %s xs %s" % (
+            npts, train, L.mvr_attn_reruns(0), hx(outs[0]["logits"][1].cpu().numpy()), hx(outs[1]["logits"][1].cpu().numpy()),
             hx(o64["logits"][1]), hx(xs)), flush=True)
     for out in outs:
         for i in range(2):
