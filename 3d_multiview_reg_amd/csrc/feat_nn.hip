@@ -551,7 +551,7 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   return true;
 }
 
-int g_nn_fast = 2;   // mvr_set_feat_nn_fast: 0 online path only, 1 fast path split-bf16, 2 fast path split-fp16
+int g_nn_fast = 1;   // mvr_set_feat_nn_fast: 0 online path only, 1 fast path split-bf16 (default), 2 fast path split-fp16
 
 // MODE 0 (soft) with a.fast: the bounded-shift path, falling back to the online path for a workgroup
 // whose softmax sums underflowed; otherwise the online path (MODE 1 argmax, 2 two nearest).

@@ -969,10 +969,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
 }
 
 #ifndef GEMM_F16_DEFAULT
-#define GEMM_F16_DEFAULT 1
+#define GEMM_F16_DEFAULT 0
 #endif
 int g_gemm_h = GEMM_F16_DEFAULT;   // mvr_set_gemm_f16: MATH_BF16X3 launches run split-fp16 first
-__device__ int g_gm_flags[1024];    // flag slots (pconv.hip scheme: slot i % 1024, epoch i + 1)
 
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
 static void launch_t(const KArgs& ka0, long long tiles, hipStream_t s) {
@@ -982,31 +981,17 @@ static void launch_t(const KArgs& ka0, long long tiles, hipStream_t s) {
     hipLaunchKernelGGL((gemm_kernel<MATH_F32, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
     return;
   }
-  // split-fp16 first unless the output overlaps an operand or the residual (the re-run reads them)
+  // split-fp16 first when the caller provides a zeroed flag word, unless the output is an operand or the residual
+  // (in place: the re-run reads them).  Outputs never partially overlap inputs (launch_gemm contract), so the test is
+  // pointer equality — a property of the call, not of where the allocator placed the buffers.
   const GemmArgs& g = ka.g;
-  auto span = [&](const void* p, int64_t sb, int64_t rows, int64_t ld, int64_t cols) {
-    const char* b = reinterpret_cast<const char*>(p);
-    return std::make_pair(b, b + ((int64_t)(g.batch - 1) * sb + (rows - 1) * ld + cols) * 4);
-  };
-  bool alias = false;
-  if (g.C) {
-    const auto c = span(g.C, g.sCb, g.M, g.ldc, g.N);
-    auto hit = [&](std::pair<const char*, const char*> o) { return c.first < o.second && o.first < c.second; };
-    alias = hit(span(g.A, g.sAb, g.M, g.lda, g.K)) ||
-            hit(g.bkc ? span(g.B, g.sBb, g.N, g.ldb, g.K) : span(g.B, g.sBb, g.K, g.ldb, g.N)) ||
-            (g.has_res && hit(span(g.R, g.sRb, g.M, g.ldc, g.N)));
-  }
-  if (g_gemm_h && !alias) {
-    static int* flags = nullptr;
-    static std::atomic<unsigned> launches{0};
-    if (flags || hipGetSymbolAddress(reinterpret_cast<void**>(&flags), HIP_SYMBOL(g_gm_flags)) == hipSuccess) {
-      const unsigned id = launches.fetch_add(1, std::memory_order_relaxed);
-      ka.range = flags + id % 1024;
-      ka.epoch = (int)(id & 0x3fffffffu) + 1;
-      hipLaunchKernelGGL((gemm_kernel<MATH_F16X2, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
-      ka.guard = ka.range;
-      ka.range = nullptr;
-    }
+  const bool alias = g.C && (g.C == g.A || g.C == g.B || (g.has_res && g.C == g.R));
+  if (g_gemm_h && g.flag && !alias) {
+    ka.range = g.flag;
+    ka.epoch = 1;
+    hipLaunchKernelGGL((gemm_kernel<MATH_F16X2, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
+    ka.guard = ka.range;
+    ka.range = nullptr;
   }
   hipLaunchKernelGGL((gemm_kernel<MATH_BF16X3, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
 }
@@ -1081,8 +1066,12 @@ extern "C" int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int6
                             int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc,
                             const float* R, int64_t sRb, const float* bias, int bias_mode, const float* psc,
                             const float* psh, int64_t sPb, int64_t pld, int pro, float* stats, int64_t st_ld,
-                            int st_off, int stats_mode, int math, hipStream_t stream) {
+                            int st_off, int stats_mode, int math, int32_t* range_flag, hipStream_t stream) {
   mvr::GemmArgs g{};
+  if (range_flag && math == mvr::MATH_BF16X3 && (mvr::g_gemm_h || mvr::g_pconv_h)) {
+    if (hipMemsetAsync(range_flag, 0, sizeof(int32_t), stream) != hipSuccess) return MVR_ELAUNCH;
+    g.flag = range_flag;
+  }
   g.math = math;
   g.M = M; g.N = N; g.K = K; g.batch = batch;
   g.A = A; g.sAb = sAb; g.lda = lda;

@@ -37,6 +37,8 @@ enum Stats : int {
 // left the split-fp16 window (gemm.hip launch_t).
 enum Math : int { MATH_F32 = 0, MATH_BF16X3 = 1, MATH_F16X2 = 2 };
 extern int g_default_math;   // used by the OANet orchestrator (mvr_set_gemm_math)
+extern int g_gemm_h;         // mvr_set_gemm_f16
+extern int g_pconv_h;        // mvr_set_pconv_math
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 32;
 
@@ -63,6 +65,10 @@ struct GemmArgs {
   // (columns >= xci zero), xb [128] (nullable)
   int xin; int xci; const float* xw; const float* xb;
   int64_t xld;   // row stride of the block input (xin = 2: R's rows; xin = 1 uses ldb)
+  // MATH_BF16X3 with mvr_set_gemm_f16 / mvr_set_pconv_math on: a zeroed int in device memory owned by this launch
+  // (stream-ordered); the split-fp16 pass sets it when an operand leaves the fp16 window and the guarded split-bf16
+  // pass then recomputes every output.  Null: split-bf16 only.
+  int* flag;
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the
@@ -72,7 +78,8 @@ struct GemmArgs {
 // Padding columns of C in [N, round_up(N, 4)) are written (finite values: 0 after a softmax
 // epilogue) and never enter results, statistics or the K tail.  PRO_A_K / PRO_B_K need K % 4 == 0
 // and K <= 512.  Launch on `stream`; returns 0 or a negative error (MVR_EINVAL on a violated
-// contract).
+// contract).  The output (C) is either disjoint from A, B and R or equal to R (in place, residual); it never
+// partially overlaps an input.
 int launch_gemm(const GemmArgs& g, hipStream_t stream);
 
 // 128 -> 128 point convolutions (pconv.hip): launch_gemm routes the shapes pconv_covers() accepts there

@@ -1046,7 +1046,7 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
 #endif
 int g_unpool4 = UNPOOL4_DEFAULT;   // mvr_set_unpool4: the 4-wave diff_unpool kernel (0: the 8-wave one, A/B timing)
 #ifndef ATTN_MATH_DEFAULT
-#define ATTN_MATH_DEFAULT 1
+#define ATTN_MATH_DEFAULT 0
 #endif
 int g_attn_h = ATTN_MATH_DEFAULT;  // mvr_set_attn_math: split-fp16 (1) or split-bf16 (0) pool / 4-wave unpool
 
@@ -1068,13 +1068,10 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
 // (points) of every (pair, query block) shortens the rounds.  Picks nks in {1, 2, 4} minimising
 // rounds / nks (ties: fewer splits), with >= 8 key blocks per split.
 static int pool_splits(int P, int nqb, int N) {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  int dev = 0, cus = 0;   // the current device's CU count (an attribute query, no process state)
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
   const int64_t wg = (int64_t)((P + 7) / 8) * 8 * nqb;
   const int nkb = (N + AKB - 1) / AKB;
   int best = 1;
@@ -1134,14 +1131,17 @@ extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x
   a.nks = 1;
   const size_t slots = (size_t)P * a.nqb;
   int* range = nullptr;   // split-fp16 needs the workspace's flag word
-  if (workspace && al16(workspace)) {
+  // with a workspace the key-split count is a function of the shape alone (pool_splits); a workspace smaller than
+  // mvr_oan_diff_pool_workspace_bytes is an error rather than a silently different split (and summation order)
+  if (workspace) {
+    if (!al16(workspace) || workspace_bytes < pool_ws_bytes(P, clusters, 4)) return MVR_EINVAL;
     const int k = pool_splits(P, a.nqb, N);
-    if (k > 1 && workspace_bytes >= pool_ws_bytes(P, clusters, k)) {
+    if (k > 1) {
       a.nks = k;
       a.part = reinterpret_cast<float*>(workspace);
       a.cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + slots * (size_t)k * PSLAB * 4);
     }
-    if (g_attn_h && workspace_bytes >= pool_ws_bytes(P, clusters, a.nks))
+    if (g_attn_h)
       range = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
                                      (a.nks > 1 ? slots * ((size_t)a.nks * PSLAB * 4 + 4) : 0));
   }

@@ -347,7 +347,11 @@ struct Plan {
   size_t bytes;
   float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *sc2, *sh2, *scK, *shK, *fac, *W1, *W8;
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
+  int* flags;            // FLAG_SLOTS range flags of the split-fp16 launches (zeroed at the block's start)
 };
+
+// one flag word per guarded split-fp16 launch of a block forward, assigned in launch order (a block issues ~30)
+constexpr int FLAG_SLOTS = 128;
 
 // Activations [P][C][Np] over points and [P][C][Kp] over clusters, rows padded to a multiple of 32
 // floats: 128-byte rows, so that row segments written by the epilogues cover whole cache lines
@@ -398,6 +402,7 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.uimg = pl.fused ? w.take<char>(pl.uimg_bytes) : nullptr;
   pl.mv = w.take<float2>((size_t)P * 2 * C);
   pl.stcol = w.take<float2>((size_t)P * MC * Kc);
+  pl.flags = w.take<int>(FLAG_SLOTS);
   pl.bytes = w.off + 256;
   return pl;
 }
@@ -406,7 +411,11 @@ struct Ctx {
   const Plan& pl;
   hipStream_t s;
   int train;
+  bool f16;   // split-fp16 launches enabled (flags zeroed)
   int err = 0;
+  int nflag = 0;
+  // the next launch's own zeroed flag word, or null (split-bf16 only) when split-fp16 is off or the slots are used up
+  int* flag() { return f16 && nflag < FLAG_SLOTS ? pl.flags + nflag++ : nullptr; }
   void chk(int e) {
     if (e && !err) err = e;
   }
@@ -457,6 +466,7 @@ struct Ctx {
     g.stats_mode = stats_mode;
     g.stats = out.st; g.st_ld = out.st_ld; g.st_off = out.st_off;
     g.prof_kind = (in.L == pl.Kc && out.L == pl.Kc) ? PK_OAFILTER : (out.C == pl.Kc ? PK_EMBED : PK_CONV_PTS);
+    g.flag = flag();
     chk(launch_gemm(g, s));
   }
 
@@ -528,6 +538,7 @@ struct Ctx {
     g.pro = PRO_A_K; g.psc = pl.scK; g.psh = pl.shK; g.sPb = 0;
     g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
     g.prof_kind = PK_OAFILTER;
+    g.flag = flag();
     chk(launch_gemm(g, s));
     finalize_in(o2, 1e-3f, f.bn3);
     conv(f.conv3, o2, true, xd, &xd, ST_ROW);  // in place: out = conv3(...) + x
@@ -576,7 +587,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (!blk->l1_2[0].shortcut.weight) return MVR_EINVAL;
   const Plan pl = plan(C, Kc, Cin, P, N, workspace);
   if (workspace_bytes < pl.bytes) return MVR_EINVAL;
-  Ctx cx{pl, s, bn_train};
+  Ctx cx{pl, s, bn_train, g_gemm_h || g_pconv_h};
+  if (cx.f16 && hipMemsetAsync(pl.flags, 0, sizeof(int) * FLAG_SLOTS, s) != hipSuccess) return MVR_ELAUNCH;
   const int64_t Np = pl.Np, Kp = pl.Kp;
   const int64_t CN = (int64_t)C * Np;
   const int TN = gemm_ntiles(N);
@@ -618,6 +630,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     cx.finalize_in(xa, 1e-5f, blk->l1_1[0].bn1);   // xa.st = pl.stA: the partials just written
     dbg_hash(pl.sc, P, 1, C, C, 0, s);
     dbg_hash(pl.sh, P, 1, C, C, 0, s);
+    f3.flag = cx.flag();
     cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
     Act t{pl.T1, CN, Np, C, N, pl.stT, C, 0};
     dbg_hash(reinterpret_cast<const float*>(pl.stT), P, 1, TN * C * 2, (int64_t)TN * C * 2, 0, s);
@@ -636,6 +649,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     f7.stats_mode = ST_ROW; f7.stats = y.st; f7.st_ld = y.st_ld; f7.st_off = y.st_off;
     f7.xin = 2; f7.xci = Cin; f7.xw = pl.W8; f7.xb = blk->conv1.bias; f7.xld = ld;
     f7.prof_kind = PK_CONV_PTS;
+    f7.flag = cx.flag();
     cx.chk(launch_gemm(f7, s));   // conv7 of l1_1[0] + x (recomputed)
     dbg_hash(pl.T1, P, C, N, CN, Np, s);
     dbg_hash(y.p, P, C, N, y.ps, y.ld, s);
@@ -670,6 +684,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.pro = PRO_B_SMX; g.psc = pl.fac; g.sPb = (int64_t)TN * Kp; g.pld = Kp;
     g.stats_mode = ST_ROW; g.stats = pl.stD; g.st_ld = C; g.st_off = 0;
     g.prof_kind = PK_POOL;
+    g.flag = cx.flag();
     cx.chk(launch_gemm(g, s));
   }
   dbg_hash(pl.XD, P, C, Kc, (int64_t)C * Kp, Kp, s);
@@ -699,6 +714,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.pro = PRO_B_SMX; g.psc = pl.fac; g.sPb = (int64_t)MK * Np; g.pld = Np;
     g.stats_mode = ST_ROW; g.stats = pl.st11; g.st_ld = 2 * C; g.st_off = C;
     g.prof_kind = PK_UNPOOL;
+    g.flag = cx.flag();
     cx.chk(launch_gemm(g, s));
   }
   dbg_hash(pl.X11 + CN, P, C, N, 2 * CN, Np, s);
@@ -710,7 +726,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   Act out{latent ? latent : pl.XA, latent ? (int64_t)C * ld : CN, latent ? ld : Np, C, N, pl.stA, C, 0};
   // the output head (oanet.py:163,174-178) runs in the epilogue of the last PointCN conv when the
   // point-conv kernel takes it; the guard counts start at zero either way
-  (void)hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s);
+  if (hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s) != hipSuccess) return MVR_ELAUNCH;
   GemmArgs probe{};
   probe.math = g_default_math; probe.M = C; probe.N = N; probe.K = C; probe.batch = P; probe.pro = PRO_B_K;
   probe.has_res = 1; probe.bias_mode = BIAS_M; probe.head_w = blk->output.weight;
@@ -739,8 +755,9 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
                           t, res, N, res_row, row_pstride, status, guard_group, s);
   if (e3) return e3;
   if (score_row) {  // next block's input row 7 = (guarded) scores (oanet.py:247-248)
-    (void)hipMemcpy2DAsync(score_row, row_pstride * sizeof(float), scores, N * sizeof(float), N * sizeof(float), P,
-                     hipMemcpyDeviceToDevice, s);
+    if (hipMemcpy2DAsync(score_row, row_pstride * sizeof(float), scores, N * sizeof(float), N * sizeof(float), P,
+                         hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return MVR_ELAUNCH;
   }
   return hipGetLastError() == hipSuccess ? MVR_OK : MVR_ELAUNCH;
 }

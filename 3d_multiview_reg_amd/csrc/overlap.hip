@@ -321,7 +321,7 @@ extern "C" int mvr_radius_overlap_count(const void* index, size_t bytes, const d
   if (!index || !xyz || !off || !pairs || !T || !counts || B <= 0 || M < 0 || P < 0 || max_points < 0 ||
       !(r > 0.0) || bytes < mvr_radius_index_bytes(M) || P > 32767)
     return MVR_EINVAL;
-  (void)hipMemsetAsync(counts, 0, sizeof(int32_t) * 2 * (size_t)P, s);
+  if (hipMemsetAsync(counts, 0, sizeof(int32_t) * 2 * (size_t)P, s) != hipSuccess) return MVR_ELAUNCH;
   if (P == 0 || max_points == 0) return hipGetLastError() == hipSuccess ? MVR_OK : MVR_ELAUNCH;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)P * 2.0 * (double)max_points * 200.0, s);
   RIndex ix = index_view(const_cast<void*>(index), M);

@@ -25,8 +25,6 @@
 // a group come from one workgroup and consecutive chunks of a workgroup share cache lines.
 // Roofline: 2*128*128 flops per point-pair column against (128 + 128 (+128 residual)) * 4 bytes:
 // AI = 32 (21 with the residual) flop/B < the split-MFMA ridge -> HBM-bound.
-#include <atomic>
-#include <utility>
 
 #include "common.hpp"
 #include "gemm.hpp"
@@ -54,13 +52,10 @@ namespace mvr {
 
 int g_pconv = 1;   // mvr_set_pconv: 0 routes these convs to gemm_kernel (A/B timing)
 #ifndef PCONV_MATH_DEFAULT
-#define PCONV_MATH_DEFAULT 1
+#define PCONV_MATH_DEFAULT 0
 #endif
-int g_pconv_h = PCONV_MATH_DEFAULT;   // mvr_set_pconv_math: 1 split-fp16 (re-run in split-bf16 when out of range)
-
-// flag words of split-fp16 launches: launch i uses slot i % 1024 and marks it with its own epoch i + 1, so
-// slots need no clearing (a stale mark is another launch's epoch)
-__device__ int g_pc_flags[1024];
+int g_pconv_h = PCONV_MATH_DEFAULT;   // mvr_set_pconv_math: 0 split-bf16 (fp32-equivalent, default), 1 split-fp16
+                                      // (re-run in split-bf16 when out of range)
 
 namespace {
 
@@ -86,8 +81,8 @@ struct PcArgs {
   float* logits; float* scores; int32_t* pos;   // [P][N], [P][N], [P]
   int xci; const float* xw; const float* xb;    // XI: x(k, n) = xb[k] + xw[k][:xci] . in(:, n) (xw [128][8])
   int64_t rld;                                  // XI & 2: row stride of the block input R
-  int* range; const int* guard; int epoch;      // split-fp16: flag word set to epoch when an activation is out
-                                                // of range; split-bf16 re-run: return unless *guard == epoch
+  int* range; const int* guard; int epoch;      // split-fp16: the caller's zeroed flag word, set to epoch (1) when an
+                                                // activation is out of range; split-bf16 re-run: return unless *guard == epoch
 };
 
 #define PC_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -683,26 +678,14 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
   const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
   if (head && (!g.logits || !g.scores || !g.pos)) return MVR_EINVAL;
-  // split-fp16, then its guarded split-bf16 re-run — not for the head launches (their positive counts are
-  // atomics) nor where the output overwrites the residual in place (the re-run needs the residual intact)
-  auto span = [&](const float* p, int64_t ps) {
-    const char* b = reinterpret_cast<const char*>(p);
-    return std::make_pair(b, b + ((int64_t)(g.batch - 1) * ps + (int64_t)g.M * g.ldc) * 4);
-  };
-  bool alias = false;
-  if (g.has_res && g.R) {
-    const auto c = span(g.C, g.sCb), r = span(g.R, g.sRb);
-    alias = c.first < r.second && r.first < c.second;
-  }
-  const bool h1 = g_pconv_h && !head && !alias;
+  // split-fp16, then its guarded split-bf16 re-run — only with a caller-provided (zeroed) flag word, not for the
+  // head launches (their positive counts are atomics) nor where the output overwrites the residual in place
+  // (the re-run needs the residual intact).  Which arithmetic a launch takes depends on its arguments and
+  // operand values only (no process state: no launch counters, no address-range tests).
+  const bool h1 = g_pconv_h && g.flag && !head && !(g.has_res && g.R == g.C);
   if (h1) {
-    static int* flags = nullptr;
-    static std::atomic<unsigned> launches{0};
-    if (!flags && hipGetSymbolAddress(reinterpret_cast<void**>(&flags), HIP_SYMBOL(g_pc_flags)) != hipSuccess)
-      return MVR_ELAUNCH;
-    const unsigned id = launches.fetch_add(1, std::memory_order_relaxed);
-    a.range = flags + id % 1024;
-    a.epoch = (int)(id & 0x3fffffffu) + 1;
+    a.range = g.flag;
+    a.epoch = 1;
   }
 #define MVR_PCL(THREADS, ...)                                                   \
   do {                                                                          \

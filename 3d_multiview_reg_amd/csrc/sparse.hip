@@ -570,7 +570,7 @@ static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel
     hipLaunchKernelGGL(insert_min_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h);
   hipLaunchKernelGGL(first_flag_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h, d.flags);
   const int nb = (int)((n + SCAN_B - 1) / SCAN_B);
-  (void)hipMemsetAsync(counts, 0, sizeof(int64_t) * (1 + B), s);
+  if (hipMemsetAsync(counts, 0, sizeof(int64_t) * (1 + B), s) != hipSuccess) return MVR_ELAUNCH;
   hipLaunchKernelGGL(scan_block_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.flags, n, d.pos, d.bsum);
   hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SCAN_B), 0, s, d.bsum, nb, counts);
   hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.pos, n, d.bsum);
@@ -709,10 +709,10 @@ extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, s
   BrickView v = brick_view(ws, M);
   int32_t* slot_of = v.rows + (M > 0 ? M : 1) * 64;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)v.h.cap * 12 + M * 300.0, s);
-  (void)hipMemsetAsync(v.count, 0, 16, s);
+  if (hipMemsetAsync(v.count, 0, 16, s) != hipSuccess) return MVR_ELAUNCH;
   hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)v.h.cap)), dim3(256), 0, s, v.h);
   if (M > 0) {
-    (void)hipMemsetAsync(v.rows, 0xff, (size_t)M * 64 * 4, s);
+    if (hipMemsetAsync(v.rows, 0xff, (size_t)M * 64 * 4, s) != hipSuccess) return MVR_ELAUNCH;
     const int4* c = reinterpret_cast<const int4*>(coords);
     hipLaunchKernelGGL(brick_insert_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h);
     hipLaunchKernelGGL(brick_ids_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, v.count, slot_of, v.bcoord);

@@ -12,7 +12,6 @@
 // gathers 16 input channels of the tile's neighbour rows (16-byte row loads) and the
 // matching W[k] slice into LDS, then runs v_mfma_f32_32x32x2_f32.  No atomics: every
 // output row is owned by exactly one workgroup (deterministic results).
-#include <atomic>
 
 #include "common.hpp"
 #include "mfma_bf16.hpp"
@@ -33,7 +32,7 @@ struct SpArgs {
   const float* res; int64_t ldres;
   int relu;
   float* out; int64_t ldout;
-  int* range; const int* guard; int epoch;   // split-fp16 flag slot / split-bf16 re-run guard (pconv.hip scheme)
+  int* range; const int* guard; int epoch;   // split-fp16 flag word (set to epoch 1) / split-bf16 re-run guard
 };
 
 constexpr int SP_BK = 16;
@@ -235,7 +234,7 @@ constexpr int SB_CP = 128;   // output-channel padding of the weight image (larg
 // H = 1: split-fp16 (mfma_bf16.hpp, 3 MFMAs per product): the image's fp16 section (each output channel's
 // weights scaled by a power of two to <= 2^14), the gathered features x XS = 2^6 as they are split, both undone
 // per column in the epilogue (isc); a lane that splits a value of 1023.5 or more, or whose values are all below
-// 2^-9 without being zero, marks the launch for its guarded split-bf16 re-run (pconv.hip's flag slots).
+// 2^-9 without being zero, marks the launch (the caller's flag word) for its guarded split-bf16 re-run.
 template <int TN, int NS, int H>
 __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP,
                                                            const float* __restrict__ isc) {
@@ -473,10 +472,9 @@ __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin
 }
 
 #ifndef SPCONV_MATH_DEFAULT
-#define SPCONV_MATH_DEFAULT 1
+#define SPCONV_MATH_DEFAULT 0
 #endif
 int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_spconv_math
-__device__ int g_sp_flags[1024];         // flag slots (pconv.hip scheme: slot i % 1024, epoch i + 1)
 
 }  // namespace mvr
 
@@ -523,7 +521,7 @@ extern "C" int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void*
 extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K,
                           int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
                           const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
-                          hipStream_t s) {
+                          int32_t* range_flag, hipStream_t s) {
   if (!in || !W || !out || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
   if (wimg && (reinterpret_cast<uintptr_t>(wimg) & 15)) return MVR_EINVAL;
   if (!nbr && K != 1) return MVR_EINVAL;
@@ -542,26 +540,17 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
     const float* isc = reinterpret_cast<const float*>(base + sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout)) +
                        CoutP;
     const unsigned gx = (unsigned)((Mout + 127) / 128);
-    // split-fp16 then its guarded split-bf16 re-run, unless the output overwrites the residual (the re-run reads it)
-    auto overlap = [&](const float* p, int64_t ld, int64_t rows, int cols) {
-      if (!p) return false;
-      const char *o0 = reinterpret_cast<const char*>(out), *o1 = o0 + ((Mout - 1) * ldout + Cout) * 4;
-      const char *p0 = reinterpret_cast<const char*>(p), *p1 = p0 + ((rows - 1) * ld + cols) * 4;
-      return o0 < p1 && p0 < o1;
-    };
-    // (in / out never alias: rows are gathered).  Output tiles of 32 / 64 channels stay split-bf16: there the
-    // split-fp16 kernel holds more VGPRs (155 vs 125 at TN = 32), one workgroup per CU fewer for a gather-latency
-    // bound loop — measured slower (tools/spconv_micro.py: s1:1:32:32 0.378 -> 0.384 ms, up:1:128:64 0.403 ->
-    // 0.453), where the 128-channel tiles gain (s1:4:128:128 0.304 -> 0.217, s1:8:256:256 0.437 -> 0.346)
-    const bool h1 = g_spconv_h && Cout > 64 && !overlap(res, ldres, Mout, Cout);
+    // split-fp16 then its guarded split-bf16 re-run: only with the caller's flag word (cleared here, stream-ordered)
+    // and not where the output is the residual (in place: the re-run reads it).  Output tiles of 32 / 64 channels
+    // stay split-bf16: there the split-fp16 kernel holds more VGPRs (155 vs 125 at TN = 32), one workgroup per CU
+    // fewer for a gather-latency bound loop — measured slower (tools/spconv_micro.py: s1:1:32:32 0.378 -> 0.384 ms,
+    // up:1:128:64 0.403 -> 0.453), where the 128-channel tiles gain (s1:4:128:128 0.304 -> 0.217, s1:8:256:256
+    // 0.437 -> 0.346).  (in / out never alias: rows are gathered.)
+    const bool h1 = g_spconv_h && range_flag && Cout > 64 && res != out;
     if (h1) {
-      static int* flags = nullptr;
-      static std::atomic<unsigned> launches{0};
-      if (!flags && hipGetSymbolAddress(reinterpret_cast<void**>(&flags), HIP_SYMBOL(g_sp_flags)) != hipSuccess)
-        return MVR_ELAUNCH;
-      const unsigned id = launches.fetch_add(1, std::memory_order_relaxed);
-      a.range = flags + id % 1024;
-      a.epoch = (int)(id & 0x3fffffffu) + 1;
+      if (hipMemsetAsync(range_flag, 0, sizeof(int32_t), s) != hipSuccess) return MVR_ELAUNCH;
+      a.range = range_flag;
+      a.epoch = 1;
     }
 #define MVR_SPL(TN_, NS_, GY)                                                                                   \
   do {                                                                                                          \

@@ -56,7 +56,7 @@ _SIGS = {
                            c_vp, c_vp, c_vp, c_vp, c_size, c_vp]),
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
                              c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int,
-                             c_int, c_int, c_vp]),
+                             c_int, c_int, c_vp, c_vp]),
     "mvr_set_gemm_math": (c_int, [c_int]),
     "mvr_set_pconv": (c_int, [c_int]),
     "mvr_set_feat_nn_fast": (c_int, [c_int]),
@@ -108,7 +108,7 @@ _SIGS = {
     "mvr_kernel_map_order_bytes": (c_size, [c_i64]),
     "mvr_kernel_map_order": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
-                           c_int, c_vp, c_i64, c_vp, c_vp]),
+                           c_int, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "mvr_spconv_wimage_bytes": (c_size, [c_int, c_int, c_int]),
     "mvr_spconv_wimage": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_size, c_vp]),
     "mvr_brick_map_bytes": (c_size, [c_i64]),
@@ -207,7 +207,54 @@ def prof_get(kind):
     return ms.value, n.value, fl.value, by.value
 
 
+_MATH_KNOBS = ("pconv_math", "attn_math", "spconv_math", "gemm_f16")
+
+
+def math_state():
+    """The library's arithmetic knobs as they are set now: {knob: value}.  feat_nn_fast: 1 = the fast Soft_NN
+    path on split-bf16 distances, 2 = on split-fp16 distances (0: online path only, split-bf16)."""
+    L = lib()
+    st = {}
+    for k in _MATH_KNOBS + ("feat_nn_fast",):
+        f = getattr(L, "mvr_set_" + k)
+        v = f(0)
+        f(v)
+        st[k] = v
+    return st
+
+
+def set_math(mode):
+    """Select the MFMA operand arithmetic of every kernel that has a choice.
+
+    f32eq   : every fp32 product on the 3-term bf16 split (h + m + l, 6 MFMA products: fp32-equivalent operands).
+    split16 : the 2-term fp16 split (h + l, 3 products, 22-bit operands) where a kernel has it, with the
+              split-bf16 re-run of any launch whose operands leave the fp16 window.
+    Returns {"mode", "dtype", "knobs"}: dtype derived from the knobs as read back, never from `mode`."""
+    L = lib()
+    h = {"f32eq": 0, "split16": 1}[mode]
+    for k in _MATH_KNOBS:
+        getattr(L, "mvr_set_" + k)(h)
+    L.mvr_set_feat_nn_fast(2 if h else 1)
+    st = math_state()
+    f16 = [k for k in _MATH_KNOBS if st[k]] + (["feat_nn"] if st["feat_nn_fast"] == 2 else [])
+    dtype = "f32 (bf16x3 MFMA operands)" if not f16 else "mixed: split-fp16 (22-bit) operands in " + ",".join(f16)
+    return {"mode": mode, "dtype": dtype, "knobs": st}
+
+
 _ws_cache = {}
+_flag_cache = {}
+
+
+def flag_word(device=None):
+    """A device int32 per (device, current stream): the range flag of the split-fp16 launches that take one
+    (mvr_spconv).  Stream-ordered use: the call clears it before its split-fp16 pass."""
+    idx = (device.index if device is not None and device.index is not None else torch.cuda.current_device())
+    key = (idx, torch.cuda.current_stream(idx).cuda_stream)
+    buf = _flag_cache.get(key)
+    if buf is None:
+        buf = torch.zeros(64, dtype=torch.int32, device=torch.device("cuda", idx))
+        _flag_cache[key] = buf
+    return buf
 
 
 def workspace(nbytes, device):

@@ -126,7 +126,8 @@ class FCGFNet(nn.Module):
         wimg = conv.wimage() if SPLIT_BF16 else None
         N.check(N.lib().mvr_spconv(N.ptr(x), ldx, cin, N.ptr(nbr), N.ptr(perm), K, M, N.ptr(conv.kernel), cout,
                                    N.ptr(bias), bnp, eps, N.ptr(res), ldres, int(relu), N.ptr(out), ldout,
-                                   N.ptr(wimg), N.stream()), "mvr_spconv")
+                                   N.ptr(wimg), N.ptr(N.flag_word(x.device)) if wimg is not None else None,
+                                   N.stream()), "mvr_spconv")
         return out
 
     def _block(self, blk, x, ldx, km, M, out, ldout):

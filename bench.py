@@ -262,6 +262,9 @@ def main():
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events in the timed region (A/B timing)")
     ap.add_argument("--no-pipeline", action="store_true", help="scene workload: run the stages of a step back to "
                     "back on one stream (default: two-stage pipeline over consecutive scenes, SceneWorkload.step_pipelined)")
+    ap.add_argument("--math", default=os.environ.get("MVR_MATH", "f32eq"), choices=["f32eq", "split16"],
+                    help="f32eq: every MFMA product on the 3-term bf16 split (fp32-equivalent operands, the reference's "
+                    "fp32); split16: the 2-term fp16 split (22-bit operands) where a kernel has it")
     ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
                     "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -283,6 +286,7 @@ def main():
 
     from lib import _native
     _native.lib()
+    math_info = _native.set_math(args.math)
     if args.workload == "scene":
         wl = SceneWorkload(dev, rank, npts=args.npts)
     else:
@@ -395,7 +399,7 @@ def main():
     line = {"metric": METRIC if args.workload == "scene" else METRIC + " [filter+SVD only: precomputed corr.]",
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32(bf16x3)", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
             "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
                            schedule=("3-stream pipeline over consecutive scenes: voxelisation + coordinate levels of "
                                      "scene k+1, FCGF + feature NN of scene k, OANet + Procrustes of scene k-1; every "

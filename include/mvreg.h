@@ -88,21 +88,24 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
                  int64_t sBb, int64_t ldb, int b_kcontig, float* C, int64_t sCb, int64_t ldc, const float* R,
                  int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
                  int64_t pld, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, int math,
-                 mvr_stream_t stream);
+                 int32_t* range_flag, mvr_stream_t stream);
 /* GEMM arithmetic used by mvr_oan_block_forward (process-wide; default 1 = bf16 split). */
 int mvr_set_gemm_math(int math);
-/* With the split math (1), run each generic GEMM launch as two-term split-fp16 first (A and B x 2^6, 3 MFMAs per
-   product) with a guarded split-bf16 re-run when an operand left the window (|x| >= 1023.5, or a lane's values
-   nonzero but all below 2^-9) or when the output overlaps an input: 1 (default) on, 0 off.  Returns the previous
-   setting. */
+/* With the split math (1), run each generic GEMM launch that has a range flag (mvr_gemm_f32's range_flag: a device
+   int32 the call clears; mvr_oan_block_forward: words of its workspace) as two-term split-fp16 first (A and B x 2^6,
+   3 MFMAs per product, 22-bit operands) with a guarded split-bf16 re-run when an operand left the window
+   (|x| >= 1023.5, or a lane's values nonzero but all below 2^-9); split-bf16 directly when the output is an input
+   (in place).  0 (default) off, 1 on.  Returns the previous setting.  The choice never depends on process state
+   (launch counts, buffer addresses). */
 int mvr_set_gemm_f16(int on);
 /* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */
 int mvr_set_pconv(int on);
-/* operand math of the point convs (not the output-head launches): 1 (default) split-fp16 (3 MFMAs per
-   product, weight rows range-scaled, activations x 2^6 after the prologue and range-checked, with a guarded
-   split-bf16 re-run of a launch that saw one past the fp16 range), 0 split-bf16.  Returns the previous setting. */
+/* operand math of the point convs (not the output-head launches): 0 (default) split-bf16 (fp32-equivalent);
+   1 split-fp16 for launches that have a range flag (see mvr_set_gemm_f16): 3 MFMAs per product, weight rows
+   range-scaled, activations x 2^6 after the prologue and range-checked, with a guarded split-bf16 re-run of a
+   launch that saw one past the fp16 range.  Returns the previous setting. */
 int mvr_set_pconv_math(int h);
 
 /* ------------------------------------------------------------------------
@@ -157,9 +160,10 @@ int mvr_set_pool_split(int on);
 /* diff_unpool kernel choice (process-wide): 1 (default) the 4-wave, two-per-CU kernel when clusters <= 512,
  * 0 the 8-wave kernel (A/B timing).  Returns the previous setting. */
 int mvr_set_unpool4(int on);
-/* operand math of diff_pool and the 4-wave diff_unpool: 1 (default) split-fp16 (3 MFMAs per product, weight
-   rows range-scaled, activations range-checked with a split-bf16 re-run when one exceeds the fp16 range),
-   0 split-bf16 (6 MFMAs).  Returns the previous setting. */
+/* operand math of diff_pool and the 4-wave diff_unpool: 0 (default) split-bf16 (6 MFMAs, fp32-equivalent);
+   1 split-fp16 (3 MFMAs per product, 22-bit operands, weight rows range-scaled, activations range-checked with a
+   split-bf16 re-run when one exceeds the fp16 range; the flag word lives in the caller's workspace: diff_pool
+   without a workspace runs split-bf16).  Returns the previous setting. */
 int mvr_set_attn_math(int h);
 /* Diagnostics: how many split-bf16 re-runs of split-fp16 attention launches ran on the current device since
    the last reset (synchronises the device); -1 on error. */
@@ -281,9 +285,10 @@ int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft
                 int32_t* idx_out, mvr_stream_t stream);
 /* Soft mode runs a bounded-shift softmax first (shift k2 |fs|^2 per query instead of a running maximum:
  * no max tracking or rescaling) and falls back to the online softmax per 128-query workgroup where a
- * softmax sum underflows (< 2^-60).  2 (default) on, its distance MFMAs on two-term split-fp16 of the features
- * scaled by 2^8 (3 MFMAs per k-step; a workgroup with a descriptor norm^2 >= 2^14 falls back too), 1 on with
- * three-term split-bf16 (6 MFMAs), 0 online only.  Returns the previous setting. */
+ * softmax sum underflows (< 2^-60).  1 (default) on with three-term split-bf16 distances (6 MFMAs,
+ * fp32-equivalent), 2 on with two-term split-fp16 of the features scaled by 2^8 (3 MFMAs per k-step, 22-bit
+ * operands; a workgroup with a descriptor norm^2 >= 2^14 falls back too), 0 online only.  Returns the previous
+ * setting. */
 int mvr_set_feat_nn_fast(int on);
 
 /* Two nearest neighbours in feature space (scripts/extract_data.py:178-184, sklearn NearestNeighbors
@@ -340,19 +345,25 @@ int mvr_kernel_map_order(const int32_t* nbr, int64_t Mout, int K, int32_t* perm,
  * perm (optional): order in which output rows are tiled (mvr_kernel_map_order); results are
  * written to their own rows either way.
  * wimg (optional, 16-byte aligned): the weights pre-split by mvr_spconv_wimage -> split-bf16 MFMA path
- * (fp32-level accuracy, ~2.7x the exact-fp32 MFMA rate); NULL -> exact fp32 MFMA on W. */
+ * (fp32-level accuracy, ~2.7x the exact-fp32 MFMA rate); NULL -> exact fp32 MFMA on W.
+ * range_flag (optional, device int32 owned by the stream's call sequence): enables the split-fp16 pass when
+ * mvr_set_spconv_math(1) (the flag is cleared by the call, set by a split-fp16 pass whose operands left the fp16
+ * window, and read by its guarded split-bf16 re-run); NULL -> split-bf16 only.  out is either disjoint from res
+ * or equal to it (in place). */
 int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K, int64_t Mout,
                const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
-               int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg, mvr_stream_t stream);
+               int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg, int32_t* range_flag,
+               mvr_stream_t stream);
 /* Weight image of mvr_spconv's split paths: W [K][Cin][Cout] fp32 -> three bf16 planes in
  * [K][ceil(Cin/32)][plane][round_up(Cout,128)][40] rows (80-byte rows, zero padded), then the same rows as two
  * fp16 planes of W[.][.][c] s_c (s_c: a power of two bringing output channel c's weights to <= 2^14), then
  * s_c and 1 / (s_c 2^6) per channel. */
 size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout);
 int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, mvr_stream_t stream);
-/* operand math of mvr_spconv with a weight image: 1 (default) split-fp16 (3 MFMAs per product; gathered
-   features x 2^6 and window-checked, a guarded split-bf16 re-run of a launch that saw one outside it; split-bf16
-   directly when the output overlaps the residual), 0 split-bf16.  Returns the previous setting. */
+/* operand math of mvr_spconv with a weight image: 0 (default) split-bf16 (fp32-equivalent); 1 split-fp16 where a
+   range_flag is passed (3 MFMAs per product, 22-bit operands; gathered features x 2^6 and window-checked, a guarded
+   split-bf16 re-run of a launch that saw one outside it; split-bf16 directly when the output is the residual).
+   Returns the previous setting. */
 int mvr_set_spconv_math(int h);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */

@@ -80,7 +80,7 @@ def _run(gpu, M, N, K, batch, pro, bkc, bias_mode, stats_mode, res, seed=0, shar
     rc = L.mvr_gemm_f32(M, N, K, batch, NV.ptr(tA), 0 if shared_a else M * K4, K4, NV.ptr(tB),
                         K * N4 if not bkc else N * K4, K4 if bkc else N4, bkc,
                         NV.ptr(C), M * N4, N4, NV.ptr(tR), M * N4, NV.ptr(tb), bias_mode, NV.ptr(pv[0]),
-                        NV.ptr(pv[1]), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats_mode, math, NV.stream())
+                        NV.ptr(pv[1]), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats_mode, math, NV.ptr(NV.flag_word()), NV.stream())
     assert rc == 0
     torch.cuda.synchronize()
     if raw:
@@ -270,7 +270,7 @@ def test_pconv_in_place_residual(gpu):
             tA, tB, tb = (torch.from_numpy(x).to(gpu) for x in (A, B, bias))
             C = torch.from_numpy(R.copy()).to(gpu)
             assert L.mvr_gemm_f32(M, N, K, P, NV.ptr(tA), 0, K, NV.ptr(tB), K * N4, N4, 0, NV.ptr(C), M * N4, N4,
-                                  NV.ptr(C), M * N4, NV.ptr(tb), 1, None, None, 0, 0, 0, None, 0, 0, 0, 1,
+                                  NV.ptr(C), M * N4, NV.ptr(tb), 1, None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.ptr(NV.flag_word()),
                                   NV.stream()) == 0
             torch.cuda.synchronize()
             outs.append(C.cpu().numpy())
@@ -327,7 +327,7 @@ def test_gemm_bf16x3_accuracy_vs_fp32(gpu):
         tA, tB = torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu)
         L = NV.lib()
         assert L.mvr_gemm_f32(M, N, K, b, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, N, 0, NV.ptr(C), M * N, N, None,
-                              0, None, 0, None, None, 0, 0, 0, None, 0, 0, 0, math, NV.stream()) == 0
+                              0, None, 0, None, None, 0, 0, 0, None, 0, 0, 0, math, NV.ptr(NV.flag_word()), NV.stream()) == 0
         errs.append(np.abs(C.cpu().numpy() - ref).max())
     assert errs[1] < 3 * errs[0] + 1e-6, errs
 
@@ -340,11 +340,11 @@ def test_gemm_rejects_bad_layout(gpu):
     B = torch.zeros(8, 16, device=gpu)
     C = torch.zeros(16, 16, device=gpu)
     ok = L.mvr_gemm_f32(16, 16, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C), 0, 16, None, 0, None, 0,
-                        None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.stream())
+                        None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.ptr(NV.flag_word()), NV.stream())
     assert ok == 0
     # lda not a multiple of 4 / row shorter than round_up(K, 4)
     assert L.mvr_gemm_f32(16, 16, 6, 1, NV.ptr(A), 0, 6, NV.ptr(B), 0, 16, 0, NV.ptr(C), 0, 16, None, 0, None, 0,
-                          None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.stream()) == -1
+                          None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.ptr(NV.flag_word()), NV.stream()) == -1
     # misaligned C
     assert L.mvr_gemm_f32(15, 12, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C[0, 1:]), 0, 16, None, 0,
-                          None, 0, None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.stream()) == -1
+                          None, 0, None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.ptr(NV.flag_word()), NV.stream()) == -1

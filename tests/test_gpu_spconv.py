@@ -66,7 +66,8 @@ def _run(gpu, Cin, Cout, K, Mout, Min, split, perm=False, epi=True, seed=0, edit
         res_t = out
     bn = NV.BnP(gb.data_ptr(), bb.data_ptr(), mb.data_ptr(), vb.data_ptr()) if epi else NV.BnP(None, None, None, None)
     rc = L.mvr_spconv(NV.ptr(F), Cin, Cin, NV.ptr(nbr_t), NV.ptr(perm_t), K, Mout, NV.ptr(Wt), Cout, NV.ptr(bias_t), bn,
-                      1e-5, NV.ptr(res_t), Cout, int(epi), NV.ptr(out), Cout, NV.ptr(wimg), NV.stream())
+                      1e-5, NV.ptr(res_t), Cout, int(epi), NV.ptr(out), Cout, NV.ptr(wimg),
+                      NV.ptr(NV.flag_word(gpu)) if split else None, NV.stream())
     assert rc == 0
     got = out.cpu().numpy()
     if raw:

@@ -58,7 +58,7 @@ def run(name, iters, math, pconv=1):
     def go():
         rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), sBb, Kk if bkc else Nl, bkc,
                             NV.ptr(Cout), M * Nl, Nl, NV.ptr(R), M * Nl, NV.ptr(bvec), bias, NV.ptr(sc),
-                            NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, math, NV.stream())
+                            NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, math, NV.ptr(NV.flag_word()), NV.stream())
         assert rc == 0
     for _ in range(2):
         go()

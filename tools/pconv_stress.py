@@ -52,7 +52,7 @@ def main():
                         torch.mm(mm, mm)
             rc = L.mvr_gemm_f32(C, N, K, P, NV.ptr(A), 0, K, NV.ptr(B), K * Nl, Nl, 0, NV.ptr(Y), C * Nl, Nl,
                                 NV.ptr(Y if res == 2 else R), C * Nl, NV.ptr(bv), bias, NV.ptr(sc), NV.ptr(sh), K, 0, pro, NV.ptr(st), C,
-                                0, stats, 1, NV.stream())
+                                0, stats, 1, NV.ptr(NV.flag_word()), NV.stream())
             assert rc == 0, rc
             torch.cuda.synchronize()
             outs.append((Y[..., :N].clone(), st.clone() if stats else None))

@@ -52,7 +52,8 @@ def main():
         for name, wi in (("f32", None), ("bx", wimg)):
             def go():
                 NV.check(L.mvr_spconv(NV.ptr(x), cin, cin, NV.ptr(nbr), NV.ptr(perm), 27, Mout, NV.ptr(W), cout, None,
-                                      bn, 1e-5, None, 0, 0, NV.ptr(out), cout, NV.ptr(wi), NV.stream()), "spconv")
+                                      bn, 1e-5, None, 0, 0, NV.ptr(out), cout, NV.ptr(wi),
+                                      NV.ptr(NV.flag_word()) if wi is not None else None, NV.stream()), "spconv")
             for _ in range(2):
                 go()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
