@@ -111,10 +111,12 @@ __global__ void hash_clear_kernel(HashView h) {
 // ------------------------------------------------------------------ key generation
 __device__ __forceinline__ int floor_div(int a, int s) { return (a >= 0) ? a / s : -((-a + s - 1) / s); }
 
-// voxel keys of raw points: coords = floor(xyz / voxel) in double (the reference floors the
-// float64 Open3D points, scripts/utils.py:108), batch index from the fragment offsets
+// voxel keys of raw points: coords = floor(xyz / voxel) with the reference's arithmetic: the float32 PLY values
+// widened to float64 (Open3D's points), divided (correctly rounded fp64 division, not a multiply by 1 / voxel)
+// by the float64 voxel size, floored (scripts/utils.py:108-109, scripts/pairwise_demo.py:75-79); batch index from
+// the fragment offsets
 __global__ void vox_keys_kernel(const float* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
-                                double inv_voxel, uint64_t* keys, int4* vcoords) {
+                                double voxel, uint64_t* keys, int4* vcoords) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int lo = 0, hi = B - 1;
@@ -122,9 +124,9 @@ __global__ void vox_keys_kernel(const float* __restrict__ xyz, const int64_t* __
     const int mid = (lo + hi + 1) >> 1;
     if (off[mid] <= i) lo = mid; else hi = mid - 1;
   }
-  const int x = (int)floor((double)xyz[3 * i] * inv_voxel);
-  const int y = (int)floor((double)xyz[3 * i + 1] * inv_voxel);
-  const int z = (int)floor((double)xyz[3 * i + 2] * inv_voxel);
+  const int x = (int)floor((double)xyz[3 * i] / voxel);
+  const int y = (int)floor((double)xyz[3 * i + 1] / voxel);
+  const int z = (int)floor((double)xyz[3 * i + 2] / voxel);
   keys[i] = pack_key(lo, x, y, z);
   vcoords[i] = make_int4(lo, x, y, z);
 }
@@ -599,16 +601,16 @@ extern "C" size_t mvr_hash_table_bytes(int64_t M) { return hash_table_bytes(M); 
 
 extern "C" size_t mvr_voxelize_workspace_bytes(int64_t n) { return dedup_ws_bytes(n); }
 
-extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel, void* ws,
+extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* ws,
                             size_t ws_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                             hipStream_t s) {
-  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.f) || !ws || !coords_out || !counts_out)
+  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !ws || !coords_out || !counts_out)
     return MVR_EINVAL;
   if (ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
   if (n == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   DedupWs d = dedup_ws(ws, n);
-  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, 1.0 / (double)voxel,
+  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
                      d.keys, d.cc);
   return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s);
 }
@@ -621,10 +623,10 @@ extern "C" size_t mvr_voxelize_hint_workspace_bytes(int64_t n, int64_t distinct_
   return dedup_ws_bytes(n, distinct_hint > 0 && distinct_hint < n ? distinct_hint : n);
 }
 
-extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel,
+extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel,
                                  int64_t distinct_hint, void* ws, size_t ws_bytes, int32_t* coords_out,
                                  int64_t* sel_out, int64_t* counts_out, hipStream_t s) {
-  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.f) || !ws || !coords_out || !counts_out ||
+  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !ws || !coords_out || !counts_out ||
       distinct_hint <= 0)
     return MVR_EINVAL;
   const int64_t keys = distinct_hint < n ? distinct_hint : n;
@@ -633,7 +635,7 @@ extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int 
   if (n == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   DedupWs d = dedup_ws(ws, n, keys);
-  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, 1.0 / (double)voxel,
+  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
                      d.keys, d.cc);
   return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s,
                    reinterpret_cast<int*>(counts_out + 1 + B));

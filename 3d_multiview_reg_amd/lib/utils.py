@@ -323,16 +323,11 @@ def run_ransac_batch(xyz_i, xyz_j, counts=None, seed=0, ransac_n=RANSAC_N, max_d
     return T.cpu().numpy()
 
 
-_ransac_calls = [0]
-
-
-def run_ransac(xyz_i, xyz_j, seed=None):
+def run_ransac(xyz_i, xyz_j, seed=0):
     """utils.py:671-709: RANSAC-based estimate of the transformation mapping xyz_i [n,3] onto xyz_j [n,3]
     (correspondences are row-aligned), returned as a 4x4 float64 array.  Open3D seeds its draws from the
-    clock; here each call draws from a counter-based stream (seed = call number unless given)."""
-    if seed is None:
-        seed = _ransac_calls[0]
-        _ransac_calls[0] += 1
+    clock; here the draws come from a counter-based stream keyed by `seed` (default 0: the same pair gives the
+    same estimate whatever ran before it in the process)."""
     x1 = np.asarray(xyz_i, dtype=np.float64).reshape(1, -1, 3)
     x2 = np.asarray(xyz_j, dtype=np.float64).reshape(1, -1, 3)
     return run_ransac_batch(x1, x2, seed=seed)[0]

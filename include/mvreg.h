@@ -312,17 +312,18 @@ int mvr_gather_rows(const float* src, int C, const int64_t* idx, int n, float* d
 size_t mvr_hash_table_bytes(int64_t M);
 size_t mvr_voxelize_workspace_bytes(int64_t n);
 /* ME.utils.sparse_quantize(floor(xyz/voxel), return_index=True) per fragment, batched:
- * fragment b owns points [frag_off[b], frag_off[b+1]).  Writes the unique voxels in
+ * fragment b owns points [frag_off[b], frag_off[b+1]).  floor((double)x / voxel) in float64 with a correctly
+ * rounded division — the reference's numpy arithmetic on Open3D's float64 points (scripts/utils.py:108-109).  Writes the unique voxels in
  * first-occurrence order: coords_out [n][4] (first count rows valid), sel_out [n]
  * (source point index), counts_out int64 [1+B] = {total, per-fragment}. */
-int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel, void* workspace,
+int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* workspace,
                  size_t workspace_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                  mvr_stream_t stream);
 /* mvr_voxelize with the dedup hash table sized for distinct_hint voxels instead of n raw points (the raw
  * cloud holds ~12 points per voxel); inserts probe at most 64 slots and a key that finds none sets
  * counts_out[B + 1] (counts_out has B + 2 entries): the caller then re-runs mvr_voxelize. */
 size_t mvr_voxelize_hint_workspace_bytes(int64_t n, int64_t distinct_hint);
-int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, float voxel,
+int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel,
                       int64_t distinct_hint, void* ws, size_t ws_bytes, int32_t* coords_out, int64_t* sel_out,
                       int64_t* counts_out, mvr_stream_t stream);
 size_t mvr_coords_downsample_workspace_bytes(int64_t M);

@@ -91,7 +91,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default=None, help="comma-separated fixture groups to (re)write: kabsch, oanet, "
+                    "oanet_full_train, softnn, sampler, pairs, pairwise (default: all)")
     args = ap.parse_args()
+    only = set(args.only.split(",")) if args.only else None
+
+    def want(tag):
+        return only is None or tag in only
     os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
     sys.dont_write_bytecode = True
     sys.path.insert(0, args.ref)
@@ -105,9 +111,37 @@ def main():
     out = args.out
     meta = {"generator": "tests/golden/make_golden.py", "reference": "zgojcic/3D_multiview_reg @ /root/reference",
             "torch": torch.__version__, "numpy": np.__version__, "fixtures": {}}
+    mpath = os.path.join(out, "GOLDEN_META.json")
+    if only is not None and os.path.exists(mpath):
+        with open(mpath) as f:
+            meta["fixtures"] = json.load(f)["fixtures"]
 
     # ---------------------------------------------------------------- Kabsch
     # lib/utils.py:164-237 (+ transformation_residuals :240-256)
+    if want("kabsch"):
+        kabsch_fixture(U, out, meta)
+
+    # ---------------------------------------------------------------- OANet
+    # lib/filtering/oanet.py:18-265
+    if want("oanet"):
+        oanet_fixtures(O, out, meta)
+    if want("oanet_full_train"):
+        oanet_full_train_fixture(O, out, meta)
+    if want("softnn"):
+        softnn_fixture(L, out, meta)
+    if want("sampler"):
+        sampler_fixture(L, out, meta)
+    if want("pairs"):
+        pairs_fixture(U, out, meta)
+    if want("pairwise"):
+        pairwise_fixture(L, O, out, meta)
+    with open(mpath, "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote golden fixtures to", out)
+
+
+def kabsch_fixture(U, out, meta):
+    import torch
     xs, Rg, tg = synth_correspondences(4, 5000, seed=11)
     r = np.random.RandomState(12)
     w = r.rand(4, 5000).astype(np.float32)
@@ -127,26 +161,44 @@ def main():
     np.savez_compressed(os.path.join(out, "kabsch.npz"), **fx)
     meta["fixtures"]["kabsch.npz"] = "lib/utils.py:164-256 kabsch_transformation_estimation, fp32+fp64, zero row"
 
-    # ---------------------------------------------------------------- OANet
-    # lib/filtering/oanet.py:18-265
-    def run_oanet(cfg, xs, seed, train=False, overrides=None):
-        torch.manual_seed(0)
-        net = O.OANet(cfg)
-        shapes = load_state(net, seed, overrides)
-        net.train(train)
-        with torch.no_grad():
-            o = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
-        return shapes, oanet_outputs(o)
 
+def run_oanet(O, cfg, xs, seed, train=False, overrides=None):
+    import torch
+    torch.manual_seed(0)
+    net = O.OANet(cfg)
+    shapes = load_state(net, seed, overrides)
+    net.train(train)
+    with torch.no_grad():
+        o = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
+    return shapes, oanet_outputs(o)
+
+
+def oanet_full_train_fixture(O, out, meta):
+    """The mode the reference benchmark runs (scripts/benchmark_pairwise_registration.py:159-197 never calls
+    model.eval(): BatchNorm normalises with the statistics of each 32-pair loader batch), RegBlock.yaml's network
+    at full size.  xs is regenerated from its seed by the test (synth_correspondences(32, 5000, seed=33)); its
+    sha1 is stored to prove it."""
+    import hashlib
+    xs, _, _ = synth_correspondences(32, 5000, seed=33)
+    _, o = run_oanet(O, small_cfg(net_channel=128, clusters=500), xs, seed=7, train=True)
+    o.pop("latent")
+    np.savez_compressed(os.path.join(out, "oanet_full_train.npz"), xs_sha1=np.asarray(hashlib.sha1(xs.tobytes()).hexdigest()),
+                        **o)
+    meta["fixtures"]["oanet_full_train.npz"] = ("lib/filtering/oanet.py:218-265 train-mode BatchNorm (the benchmark's "
+                                                "mode), RegBlock network C=128,K=500, B=32 x N=5000, weights "
+                                                "synth_state(seed 7), xs = synth_correspondences(32,5000,seed=33)")
+
+
+def oanet_fixtures(O, out, meta):
     keys = {}
     cfg = small_cfg()
     xs_s, _, _ = synth_correspondences(3, 300, seed=21)
-    shapes, o = run_oanet(cfg, xs_s, seed=5)
+    shapes, o = run_oanet(O, cfg, xs_s, seed=5)
     keys["small"] = {k: list(v) for k, v in shapes.items()}
     np.savez_compressed(os.path.join(out, "oanet_small_eval.npz"), xs=xs_s, **o)
-    _, o = run_oanet(cfg, xs_s, seed=5, train=True)
+    _, o = run_oanet(O, cfg, xs_s, seed=5, train=True)
     np.savez_compressed(os.path.join(out, "oanet_small_train.npz"), xs=xs_s, **o)
-    _, o = run_oanet(cfg, xs_s, seed=5, overrides={"reg_init.output.bias": [-50.0]})
+    _, o = run_oanet(O, cfg, xs_s, seed=5, overrides={"reg_init.output.bias": [-50.0]})
     assert o["scores0"].min() > 0, "guard should have fired"
     np.savez_compressed(os.path.join(out, "oanet_small_guard.npz"), xs=xs_s, **o)
     # NOTE: the side channel (use_mutuals == 2 -> 7 input channels, oanet.py:205) crashes in the
@@ -154,7 +206,7 @@ def main():
     # and kabsch's bmm then fails.  No fixture can be produced for it (reference defects).
     cfgF = small_cfg(net_channel=128, clusters=500)
     xs_f, _, _ = synth_correspondences(2, 5000, seed=31)
-    shapesF, o = run_oanet(cfgF, xs_f, seed=7)
+    shapesF, o = run_oanet(O, cfgF, xs_f, seed=7)
     keys["full"] = {k: list(v) for k, v in shapesF.items()}
     o.pop("latent")   # 5 MB; not needed at full size
     np.savez_compressed(os.path.join(out, "oanet_full_eval.npz"), xs=xs_f, **o)
@@ -164,8 +216,11 @@ def main():
     with open(os.path.join(out, "oanet_keys.json"), "w") as f:
         json.dump(keys, f, indent=0, sort_keys=True)
 
+
+def softnn_fixture(L, out, meta):
     # ---------------------------------------------------------------- Soft_NN
     # lib/layers.py:10-88 + lib/utils.py:968-992
+    import torch
     fs = unit_features(2, 1024, 32, seed=41)
     ft = unit_features(2, 1024, 32, seed=42)
     yc = np.random.RandomState(43).uniform(-2, 2, (2, 1024, 3)).astype(np.float32)
@@ -182,6 +237,9 @@ def main():
     np.savez_compressed(os.path.join(out, "softnn.npz"), **fx)
     meta["fixtures"]["softnn.npz"] = "lib/layers.py:44-88 soft / soft+st / hard, tau=0.3 and tau=0.005 (clamped)"
 
+
+def sampler_fixture(L, out, meta):
+    import torch
     # ---------------------------------------------------------------- Sampler
     # lib/layers.py:108-154 (host numpy RNG)
     fx = {}
@@ -198,6 +256,9 @@ def main():
     np.savez_compressed(os.path.join(out, "sampler.npz"), **fx)
     meta["fixtures"]["sampler.npz"] = "lib/layers.py:108-154 rand sampling indices after np.random.seed(41)"
 
+
+def pairs_fixture(U, out, meta):
+    import torch
     # ------------------------------------------- pairs + filtering input
     # lib/utils.py:850-932
     xyz = torch.from_numpy(np.random.RandomState(51).rand(5, 7, 3).astype(np.float32))
@@ -209,6 +270,10 @@ def main():
                         ys=fd["ys"].numpy(), Rs=fd["Rs"].numpy(), ts=fd["ts"].numpy())
     meta["fixtures"]["pairs.npz"] = "lib/utils.py:850-932 extract_overlaping_pairs + construct_filtering_input_data"
 
+
+def pairwise_fixture(L, O, out, meta):
+    import torch
+    cfg = small_cfg()
     # --------------------------- PairwiseReg composition with a fake descriptor
     # lib/pairwise/__init__.py:62-142 (compute_descriptors -> filter_correspondences)
     import functools
@@ -246,10 +311,6 @@ def main():
                         pts=np.asarray(pts), xs=fin["xs"].numpy(), **o)
     meta["fixtures"]["pairwise_fake_desc.npz"] = ("lib/pairwise/__init__.py:62-142 with a fixed feature table in place "
                                                   "of FCGF; np.random.seed(41); 3 fragments -> 3 pairs; small OANet seed 9")
-
-    with open(os.path.join(out, "GOLDEN_META.json"), "w") as f:
-        json.dump(meta, f, indent=1, sort_keys=True)
-    print("wrote golden fixtures to", out)
 
 
 if __name__ == "__main__":

@@ -103,3 +103,40 @@ def test_pairwise_demo(gpu, tmp_path, monkeypatch):
     assert keys.tolist() == [["0", "1", "True"]]
     np.testing.assert_allclose(traj[0], T, atol=1e-9)
     np.testing.assert_allclose(T[:3, :3] @ T[:3, :3].T, np.eye(3), atol=1e-5)
+
+
+DEMO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "demo")
+
+
+def test_pairwise_demo_reference_pair(gpu, tmp_path, monkeypatch):
+    """scripts/pairwise_demo.py mirror on the reference's own demo pair (data/demo/pairwise/raw_data/
+    cloud_bin_{0,1}.ply, committed as fixtures) with configs/pairwise_registration/demo/config.yaml's settings:
+    voxelisation at 0.025 m gives the 18,977 / 19,082 voxels of SURVEY §2.3, and the whole path (FCGF -> rand
+    5000 samples -> soft NN -> OANet -> Procrustes) writes est_T.log.  The pretrained weights are download-only
+    (offline here): random-init FCGF / OANet, so the estimate itself is not compared."""
+    import yaml
+    import torch
+    from lib.ply import read_ply_xyz
+    from lib.sparse import voxelize
+    from lib.utils import read_trajectory, load_config
+    from scripts.pairwise_demo import main, parser
+    src, tgt = os.path.join(DEMO, "cloud_bin_0.ply"), os.path.join(DEMO, "cloud_bin_1.ply")
+    pcs = [read_ply_xyz(src), read_ply_xyz(tgt)]
+    assert [len(p) for p in pcs] == [258342, 268977]
+    _, _, counts, _ = voxelize([torch.from_numpy(np.ascontiguousarray(p, dtype=np.float32)) for p in pcs], 0.025, gpu)
+    assert list(counts) == [18977, 19082]
+    cfg = {"method": {"task": "pairwise", "descriptor_module": "fcgf", "filter_module": "oanet"},
+           "misc": {"net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128, "use_gpu": True,
+                    "normalize_weights": True, "inlier_weight_threshold": 0.5, "voxel_size": 0.025,
+                    "matching_voxel_size": 0.0375},
+           "data": {"use_mutuals": True, "mutual_nn_thresh": 0.025, "max_num_points": 5000},
+           "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
+    with open(tmp_path / "config.yaml", "w") as f:
+        yaml.safe_dump(cfg, f)
+    monkeypatch.chdir(tmp_path)
+    a = parser().parse_args([str(tmp_path / "config.yaml"), "--source_pc", src, "--target_pc", tgt])
+    T = main(load_config(a.config), a)
+    keys, traj = read_trajectory(str(tmp_path / "data/demo/pairwise/results/est_T.log"))
+    assert keys.tolist() == [["0", "1", "True"]]
+    np.testing.assert_allclose(traj[0], T, atol=1e-9)
+    np.testing.assert_allclose(T[:3, :3] @ T[:3, :3].T, np.eye(3), atol=1e-5)

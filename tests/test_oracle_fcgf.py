@@ -76,3 +76,17 @@ def test_pack_roundtrip_unique():
     c = np.concatenate([r.randint(0, 40, (5000, 1)), r.randint(-60000, 60000, (5000, 3))], 1)
     k = pack(c)
     assert len(np.unique(k)) == len(np.unique(c, axis=0))
+
+
+def test_demo_pair_voxel_counts():
+    """The reference's demo pair (data/demo/pairwise/raw_data, committed under tests/golden/demo) voxelised at
+    0.025 m by the oracle's sparse_quantize restatement: SURVEY §2.3's 18,977 / 19,082 voxels."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "3d_multiview_reg_amd"))
+    from lib.ply import read_ply_xyz
+    from oracle.fcgf import voxelize
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "demo")
+    pcs = [read_ply_xyz(os.path.join(d, "cloud_bin_%d.ply" % k)) for k in range(2)]
+    _, _, counts = voxelize(pcs, 0.025)
+    assert list(counts) == [18977, 19082]

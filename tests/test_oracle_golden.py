@@ -113,3 +113,24 @@ def test_pairwise_composition_matches_reference():
     st = synth_state(_shapes("small"), seed=9)
     o = oanet_forward(st, g["xs"][:, 0])
     _check_oanet(o, g, 2e-4)
+
+
+def test_oracle_full_train_golden():
+    """oracle/oanet.py in train mode (the benchmark's BatchNorm mode) at full size against the reference:
+    block 0 R, t within 1e-4 on every pair; block 1 (chaotic random network) within max(1e-4, 2 x the
+    reference's own distance from exact arithmetic, oanet_full_train_f64.npz); masks identical away from 0.5."""
+    import hashlib
+    from synth import synth_correspondences
+    g = golden("oanet_full_train.npz")
+    g64 = golden("oanet_full_train_f64.npz")
+    xs, _, _ = synth_correspondences(32, 5000, seed=33)
+    assert hashlib.sha1(xs.tobytes()).hexdigest() == str(g["xs_sha1"])
+    o = oanet_forward(synth_state(_shapes("full"), seed=7), xs, train=True)
+    dist = lambda u, v: np.abs(u - v).reshape(u.shape[0], -1).max(1)   # noqa: E731
+    for i in range(2):
+        near = np.abs(g["scores%d" % i] - 0.5) < 1e-4
+        assert np.array_equal((o["scores"][i] > 0.5)[~near], (g["scores%d" % i] > 0.5)[~near])
+        for k, kg in (("rot_est", "R"), ("trans_est", "t")):
+            d = dist(o[k][i], g["%s%d" % (kg, i)])
+            bound = 1e-4 if i == 0 else np.maximum(1e-4, 2 * dist(g["%s%d" % (kg, i)], g64["%s%d" % (kg, i)]))
+            assert (d <= bound).all(), (i, k, d.max())
