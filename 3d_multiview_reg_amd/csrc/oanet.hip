@@ -749,6 +749,9 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     cx.chk_launch();
   }
   if (cx.err) return cx.err;
+  // guard_group < 0: the caller evaluates the zero-row guard itself (across ranks: lib/distributed.py scene
+  // mode) and runs mvr_procrustes; the block ends at the head (scores = relu(tanh(logits)), guard_pos counts)
+  if (guard_group < 0) return hipGetLastError() == hipSuccess ? MVR_OK : MVR_ELAUNCH;
   // weights = relu(tanh(logits)) already in `scores`; the guard (oanet.py:177-178) and
   // Kabsch (oanet.py:180-183, normalize_w=True, eps=1e-7)
   int e3 = mvr_procrustes(xs, xs + 3, xs_pstride, xs_nstride, scores, N, guard_pos, nullptr, 0, P, N, 1, 1e-7f, R,

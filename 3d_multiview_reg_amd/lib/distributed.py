@@ -12,6 +12,13 @@ all-gather of fixed-size per-pair records at the end:
     OANBlock (lib/filtering/oanet.py:177-178) sees exactly the reference's groups;
   * each rank runs Soft_NN -> OANet -> Procrustes on its block and packs one record per pair;
   * ``gather_records`` all-gathers the blocks (one collective, ~64 B per pair) into pair order.
+
+Guard scope.  The reference evaluates the zero-row guard of OANBlock over its forward batch: 32 pairs in the
+benchmark's loader batches ("group" mode, above: groups never straddle ranks, no exchange), but ALL pairs of a
+scene when PairwiseReg.forward registers a whole scene at once (config 3).  "scene" mode reproduces the latter
+across ranks: each block stops at its output head, one all-reduce (MAX) of the "some pair of mine has no positive
+weight" bit over the ranks tells every rank whether the guard fires, and each rank then runs the block's
+Procrustes on its own pairs (lib.filtering.oanet.OANet.guard_sync) — two 4-byte all-reduces per forward.
 """
 import math
 
@@ -85,25 +92,50 @@ def unpack_records(rec):
             a[:, 14] > 0)
 
 
-def register_pairs_sharded(model, filtering_input, world, rank, group=GROUP):
-    """Run model.filter_correspondences on this rank's block of the pair batch (one call, the
-    zero-row guard evaluated per `group` pairs as in the reference's batch-32 evaluation) and
-    all-gather the records.  `filtering_input` is the dict of
-    lib/utils.py:construct_filtering_input_data over ALL pairs (every rank holds it)."""
+def scene_guard_sync(world):
+    """guard_sync for OANet (lib.filtering.oanet.OANet.guard_sync): the zero-row guard over the pairs of every
+    rank.  guard_pos [p] int32 (positive weights per local pair) -> counts that fire the local guard exactly when
+    some pair on SOME rank has none: one all-reduce (MAX) of the local bit, no host synchronisation."""
+    def sync(guard_pos):
+        bit = (guard_pos == 0).any().to(torch.int32).reshape(1) if guard_pos.numel() else \
+            torch.zeros(1, dtype=torch.int32, device=guard_pos.device)
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(bit, op=dist.ReduceOp.MAX)
+        if guard_pos.numel() == 0:
+            return guard_pos
+        g = guard_pos.clone()
+        g[:1] = torch.where(bit > 0, torch.zeros_like(g[:1]), g[:1])   # a zero count fires the whole local batch
+        return g
+    return sync
+
+
+def register_pairs_sharded(model, filtering_input, world, rank, group=GROUP, guard="group"):
+    """Run model.filter_correspondences on this rank's block of the pair batch and all-gather the records.
+    guard="group": the zero-row guard evaluated per `group` pairs (the reference's batch-32 evaluation);
+    guard="scene": over the whole batch of all ranks (the reference's PairwiseReg.forward over a scene).
+    `filtering_input` is the dict of lib/utils.py:construct_filtering_input_data over ALL pairs (every rank
+    holds it)."""
+    if guard not in ("group", "scene"):
+        raise ValueError(guard)
     xs = filtering_input["xs"]
     P = xs.shape[0]
     s, e = shard_pairs(P, world, rank, group)
     filt = model.filtering_module if hasattr(model, "filtering_module") else model
+    sync = scene_guard_sync(world) if guard == "scene" else None
     if e > s:
-        prev = filt.guard_group
-        filt.guard_group = group
+        prev = (filt.guard_group, filt.guard_sync)
+        filt.guard_group, filt.guard_sync = (group, None) if guard == "group" else (0, sync)
         try:
             out = model.filter_correspondences({"xs": xs[s:e]}) if hasattr(model, "filter_correspondences") \
                 else model({"xs": xs[s:e]})
         finally:
-            filt.guard_group = prev
+            filt.guard_group, filt.guard_sync = prev
         rec = pack_records(s, out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1],
                            out.get("gradient_flag"))
     else:
+        if sync is not None:   # an empty block still takes part in every block's all-reduce
+            for _ in range(1 + getattr(filt, "iter_num", 0)):
+                sync(torch.zeros(0, dtype=torch.int32, device=xs.device))
         rec = torch.zeros(0, REC, device=xs.device)
     return gather_records(rec, P, world, group)

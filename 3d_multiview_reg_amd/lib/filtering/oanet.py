@@ -176,6 +176,11 @@ class OANet(nn.Module):
         # zero-row guard (oanet.py:177-178) scope: 0 = the whole forward batch (the reference);
         # lib.distributed sets 32 (the evaluation batch) when a batch is split across ranks
         self.guard_group = 0
+        # guard_sync(guard_pos) -> guard_pos: when set, each block stops at its output head, the callable widens
+        # the guard's scope beyond this forward's pairs (lib.distributed scene mode: one all-reduce of the
+        # "some pair has no positive weight" bit over the ranks that share the batch) and the block's Procrustes
+        # runs here with the returned counts
+        self.guard_sync = None
 
     def forward(self, data):
         xs_in = data["xs"]
@@ -214,12 +219,20 @@ class OANet(nn.Module):
                 for x in (logits, scores, R, t, res, latent):
                     x.fill_(3.0e38)
             last = bi == len(blocks) - 1
+            ext = self.guard_sync is not None
+            res_row = None if last else N.ptr(inp[:, Cxs])
+            score_row = None if last else N.ptr(inp[:, Cxs + 1])
             rc = L.mvr_oan_block_forward(
                 ctypes.byref(params), N.ptr(inp), rows * ld, ld, N.ptr(xs), Npts * Cxs, Cxs, P, Npts, int(self.training),
                 N.ptr(logits), N.ptr(scores), N.ptr(R), N.ptr(t), N.ptr(res), N.ptr(latent) if last else None,
-                None if last else N.ptr(inp[:, Cxs]), None if last else N.ptr(inp[:, Cxs + 1]), rows * ld,
-                N.ptr(guard), N.ptr(status[bi]), int(self.guard_group), N.ptr(ws), ws.numel(), st)
+                res_row, score_row, rows * ld, N.ptr(guard), N.ptr(status[bi]), -1 if ext else int(self.guard_group),
+                N.ptr(ws), ws.numel(), st)
             N.check(rc, "mvr_oan_block_forward")
+            if ext:   # the guard over the whole (sharded) batch, then oanet.py:180-183's Kabsch
+                gp = self.guard_sync(guard)
+                N.check(L.mvr_procrustes(N.ptr(xs), N.ptr(xs[..., 3:]), Npts * Cxs, Cxs, N.ptr(scores), Npts, N.ptr(gp),
+                                         score_row, rows * ld, P, Npts, 1, 1e-7, N.ptr(R), N.ptr(t), N.ptr(res), Npts,
+                                         res_row, rows * ld, N.ptr(status[bi]), 0, st), "mvr_procrustes")
             if bi == 0 and not last:
                 blk_in_ch = blocks[1].in_channels
                 if blk_in_ch != rows:

@@ -42,7 +42,6 @@ PEAK_BF16_TFLOPS = 16 * PEAK_FP32_TFLOPS   # dense bf16 MFMA (fp32 MFMA is 1/16 
 PEAK_SPLIT_TFLOPS = PEAK_BF16_TFLOPS / 6
 PEAK_HBM_GBS = 8000.0
 GEMM_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter")
-MFMA_PEAKS = {"feat_nn": PEAK_SPLIT_TFLOPS, "spconv": PEAK_SPLIT_TFLOPS}   # split-bf16 sparse convs (spconv_bx_kernel)
 
 
 def log(*a):
@@ -67,14 +66,19 @@ def synth_module(mod, seed):
 
 
 class PrecomputedWorkload:
+    """configs[3]/[4] shape: scripts/benchmark_pairwise_registration.py's hot loop (:193-200) on precomputed
+    correspondences — loader batches of 32 pairs, each one filter_correspondences call in TRAIN-mode BatchNorm
+    (the script never calls model.eval(), :159-174: batch statistics per 32-pair batch, the zero-row guard per
+    batch), then Procrustes."""
     name = "precomputed"
+    BATCH = 32
 
     def __init__(self, dev, rank, pairs, npts):
         from lib.filtering.oanet import OANet
         from synth import synth_correspondences
         self.net = OANet(oanet_cfg())
         self.state = synth_module(self.net, seed=7)
-        self.net = self.net.to(dev).eval()
+        self.net = self.net.to(dev).train()
         xs, _, _ = synth_correspondences(pairs, npts, seed=1000 + rank)
         self.xs_host = xs
         self.xs = torch.from_numpy(xs).to(dev).unsqueeze(1)
@@ -82,41 +86,47 @@ class PrecomputedWorkload:
         self.npts = npts
 
     def step(self):
-        out = self.net({"xs": self.xs})
-        R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
-        conf = (s > 0.5).float().mean(dim=1, keepdim=True)
-        return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)   # [P, 13] records
+        recs = []
+        for b0 in range(0, self.pairs, self.BATCH):
+            out = self.net({"xs": self.xs[b0:b0 + self.BATCH]})
+            R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
+            conf = (s > 0.5).float().mean(dim=1, keepdim=True)
+            recs.append(torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1))   # [b, 13] records
+        return torch.cat(recs)
 
     def config(self):
-        return {"workload": "precomputed correspondences (configs[3] shape): OANet(128ch,500 clusters,depth 12,"
-                            "2 blocks)+Procrustes", "pairs_per_gpu": self.pairs, "correspondences": self.npts}
+        return {"workload": "precomputed correspondences (configs[3] shape, scripts/benchmark_pairwise_registration.py "
+                            "hot loop): OANet(128ch,500 clusters,depth 12,2 blocks, train-mode BN per 32-pair batch)"
+                            "+Procrustes", "pairs_per_gpu": self.pairs, "correspondences": self.npts,
+                "batch": self.BATCH}
 
-    def cpu_baseline(self, budget_s=20.0):
-        """oracle OANet + diag_embed Kabsch (the reference op sequence) on a bounded sample."""
-        from oracle.oanet import oanet_forward
-        import oracle.kabsch as K
-        orig = K.kabsch
-        import oracle.oanet as O
-        O.kabsch = lambda x1, x2, w: orig(x1, x2, w, diag_embed=True)
+    def cpu_baseline(self, threads, budget_s=20.0):
+        """the reference's op sequence on torch CPU tensors (oracle/torch_port.py: N x N diag_embed Kabsch) over
+        whole 32-pair batches of the same workload, train-mode BN"""
+        from oracle import torch_port
+        torch.set_num_threads(threads)
         n, t0 = 0, time.time()
-        while time.time() - t0 < budget_s and n < self.pairs:
-            oanet_forward(self.state, self.xs_host[n:n + 1])
-            n += 1
-        O.kabsch = orig
+        with torch.no_grad():
+            while n < self.pairs and (n == 0 or time.time() - t0 < budget_s):
+                torch_port.oanet_forward(self.state, torch.from_numpy(self.xs_host[n:n + self.BATCH]), train=True)
+                n += min(self.BATCH, self.pairs - n)
         dt = time.time() - t0
-        return n / dt, "%d pair(s) of the same workload, batch 1, numpy oracle incl. N x N diag_embed Kabsch" % n
+        return n / dt, "%d pairs in batches of %d (oracle/torch_port.py, reference op sequence incl. N x N diag_embed " \
+                       "Kabsch, train-mode BN), measured" % (n, self.BATCH)
 
 
 class SceneWorkload:
     """configs[2]: one synthetic 3DMatch-scale scene per GPU (30 fragments, ~20k voxels each)."""
     name = "scene"
 
-    def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025):
+    def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025, samp="rand"):
         import lib.config
         from synth import synth_scene_fragments
         cfg = oanet_cfg()
         cfg["method"]["descriptor_module"] = "fcgf"
         cfg["data"]["max_num_points"] = npts
+        cfg["train"]["samp_type"] = samp
+        self.samp = samp
         self.model = lib.config.get_model(cfg)
         self.state = synth_module(self.model, seed=7)
         self.model = self.model.to(dev).eval()
@@ -200,43 +210,85 @@ class SceneWorkload:
 
     def config(self):
         return {"workload": "one synthetic 3DMatch-scale scene per GPU (configs[2]): %d fragments x ~%d voxels "
-                            "(0.025 m) -> FCGF -> rand %d samples -> soft feature-NN for all %d pairs -> OANet "
+                            "(0.025 m) -> FCGF -> %s %d samples -> soft feature-NN for all %d pairs -> OANet "
                             "(128ch, 500 clusters, 2 blocks) -> weighted Procrustes -> all-gather of (R,t,conf)"
-                            % (self.n_frag, int(np.mean(self.vox_counts or [0])), self.npts, self.pairs),
+                            % (self.n_frag, int(np.mean(self.vox_counts or [0])), self.samp, self.npts, self.pairs),
+                "sampler": self.samp,
                 "fragments_per_gpu": self.n_frag, "pairs_per_gpu": self.pairs, "samples": self.npts,
                 "voxels_mean": int(np.mean(self.vox_counts or [0]))}
 
-    def cpu_baseline(self, budget_s=20.0):
-        """numpy oracle, reference op sequence: FCGF on 2 fragments + for 1 pair both Soft_NN directions
-        + OANet + N x N diag_embed Kabsch; projected to the scene: 435 / (30 t_fcgf + 435 t_pair)."""
+    def cpu_baseline(self, threads, budget_s=20.0):
+        """The reference's CPU op sequence, timed on this host's cores: FCGF on one fragment (oracle/fcgf.py, numpy:
+        MinkowskiEngine is absent, so this is our sparse-conv restatement, "not ME"), then one 32-pair batch (the
+        benchmark's batch) through both Soft_NN directions (full [32, 5000, 5000] distance / softmax matrices),
+        OANet (eval BN) and the N x N diag_embed Kabsch (oracle/torch_port.py); the scene's rate is
+        pairs / (fragments x t_fcgf + ceil(pairs / 32) x t_batch)."""
         from oracle.fcgf import voxelize as ovox, fcgf_forward
-        from oracle.soft_nn import soft_nn, sample_rand
-        from oracle.oanet import oanet_forward
-        import oracle.kabsch as K
-        import oracle.oanet as O
+        from oracle.soft_nn import sample_rand
+        from oracle import torch_port
+        torch.set_num_threads(threads)
         st = {k: v.detach().cpu().numpy() for k, v in self.model.state_dict().items()}
         dst = {k[len("descriptor_module."):]: v for k, v in st.items() if k.startswith("descriptor_module.")}
         fst = {k[len("filtering_module."):]: v for k, v in st.items() if k.startswith("filtering_module.")}
         t0 = time.time()
-        c, sel, cnt = ovox(self.frags[:2], self.voxel)
+        c, sel, cnt = ovox(self.frags[:1], self.voxel)
         F, _ = fcgf_forward(dst, c, np.ones((len(c), 1), np.float32))
-        t_fcgf = (time.time() - t0) / 2
-        xyz = np.concatenate(self.frags[:2])[sel]
+        t_fcgf = time.time() - t0
+        # one 32-pair batch: the sampled descriptors of one fragment matched against 32 others' (the descriptors'
+        # values do not change the op count; the fragment's own are reused)
+        xyz = np.ascontiguousarray(self.frags[0][sel], dtype=np.float32)
         np.random.seed(0)
-        idx = sample_rand(cnt, self.npts)
-        fs, xs = F[idx], xyz[idx]
-        orig = K.kabsch
-        O.kabsch = lambda x1, x2, w: orig(x1, x2, w, diag_embed=True)
+        idx = sample_rand(cnt, self.npts)[0]
+        B = 32
+        fs = torch.from_numpy(np.repeat(F[idx][None], B, 0))
+        ft = torch.from_numpy(np.repeat(F[np.roll(idx, 17)][None], B, 0))
+        xs_, xt_ = torch.from_numpy(np.repeat(xyz[idx][None], B, 0)), torch.from_numpy(np.repeat(xyz[np.roll(idx, 17)][None], B, 0))
         t1 = time.time()
-        xc = soft_nn(fs[:1], fs[1:], xs[1:], "soft")
-        soft_nn(fs[1:], fs[:1], xs[:1], "soft")                       # reverse direction, as the reference
-        oanet_forward(fst, np.concatenate([xs[:1], xc], -1))
-        t_pair = time.time() - t1
-        O.kabsch = orig
-        v = self.pairs / (self.n_frag * t_fcgf + self.pairs * t_pair)
-        return v, ("measured FCGF %.2fs/fragment (2 fragments) + %.2fs/pair (1 pair: 2x Soft_NN + OANet + "
-                   "diag_embed Kabsch); projected to %d fragments / %d pairs" % (t_fcgf, t_pair, self.n_frag,
-                                                                              self.pairs))
+        with torch.no_grad():
+            xc = torch_port.soft_nn(fs, ft, xt_)
+            torch_port.soft_nn(ft, fs, xs_)                   # the reverse direction, as the reference
+            torch_port.oanet_forward(fst, torch.cat([xs_, xc], -1).contiguous())
+        t_batch = time.time() - t1
+        nb = -(-self.pairs // B)
+        v = self.pairs / (self.n_frag * t_fcgf + nb * t_batch)
+        return v, ("measured FCGF %.2fs/fragment (1 fragment, numpy sparse-conv restatement) + %.2fs per 32-pair batch "
+                   "(2x Soft_NN + OANet + diag_embed Kabsch, oracle/torch_port.py); scene rate = %d pairs / "
+                   "(%d x t_fcgf + %d x t_batch)" % (t_fcgf, t_batch, self.pairs, self.n_frag, nb))
+
+    def fcgf_work(self):
+        """Algorithmic work of one FCGF forward over the scene's fragments (lib/descriptor/fcgf.py:229-280), counted
+        from the scene's kernel maps: FLOPs = 2 Cin Cout per (input, output) pair of every conv; compulsory bytes =
+        input rows + output rows (+ residual rows) + weights + the neighbour table, fp32 / int32.  (Host syncs:
+        call outside the timed region.)"""
+        data = self.prepare()
+        cm = data["sinput0_coords_manager"]
+        M = {s: int(cm.coords_at(s).shape[0]) for s in (1, 2, 4, 8)}
+        fl, by = 0.0, 0.0
+
+        def conv(kind, s, ks, cin, cout, m_in, m_out, res=False):
+            nonlocal fl, by
+            if kind is None:
+                pairs, K = m_out, 1
+            else:
+                nbr = cm.kernel_map(kind, s, ks)
+                pairs, K = int((nbr >= 0).sum().item()), nbr.shape[1]
+            fl += 2.0 * cin * cout * pairs
+            by += 4.0 * (m_in * cin + m_out * cout * (2 if res else 1) + K * cin * cout) + (4.0 * m_out * K if kind else 0)
+
+        def block(s, c):
+            conv("s1", s, 3, c, c, M[s], M[s])
+            conv("s1", s, 3, c, c, M[s], M[s], res=True)
+        conv("s1", 1, 7, 1, 32, M[1], M[1])
+        block(1, 32)
+        conv("down", 1, 3, 32, 64, M[1], M[2]); block(2, 64)
+        conv("down", 2, 3, 64, 128, M[2], M[4]); block(4, 128)
+        conv("down", 4, 3, 128, 256, M[4], M[8]); block(8, 256)
+        conv("up", 4, 3, 256, 128, M[8], M[4]); block(4, 128)
+        conv("up", 2, 3, 256, 64, M[4], M[2]); block(2, 64)
+        conv("up", 1, 3, 128, 64, M[2], M[1]); block(1, 64)
+        conv(None, 1, 1, 96, 64, M[1], M[1])
+        conv(None, 1, 1, 64, 32, M[1], M[1])
+        return fl, by
 
 
 def records_allgather(rec, world):
@@ -248,51 +300,23 @@ def records_allgather(rec, world):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default=os.environ.get("MVR_BENCH_WORKLOAD", "scene"),
-                    choices=["scene", "precomputed"])
-    ap.add_argument("--pairs", type=int, default=435)
-    ap.add_argument("--npts", type=int, default=5000)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=20.0)
-    ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events in the timed region (A/B timing)")
-    ap.add_argument("--no-pipeline", action="store_true", help="scene workload: run the stages of a step back to "
-                    "back on one stream (default: two-stage pipeline over consecutive scenes, SceneWorkload.step_pipelined)")
-    ap.add_argument("--math", default=os.environ.get("MVR_MATH", "f32eq"), choices=["f32eq", "split16"],
-                    help="f32eq: every MFMA product on the 3-term bf16 split (fp32-equivalent operands, the reference's "
-                    "fp32); split16: the 2-term fp16 split (22-bit operands) where a kernel has it")
-    ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
-                    "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
-    args = ap.parse_args()
+MFMA_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter", "feat_nn", "spconv", "pointcn")
+# kernel classes with a split-fp16 form, and the knob that selects it (lib/_native.set_math)
+F16_KNOB = {"conv_pts": "pconv_math", "embed": "gemm_f16", "pool": "attn_math", "unpool": "attn_math",
+            "oafilter": "gemm_f16", "feat_nn": "feat_nn_fast", "spconv": "spconv_math"}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
 
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
+def class_peak_tflops(cls, knobs):
+    """fp32-equivalent MFMA peak of a kernel class at the arithmetic it runs: split-bf16 (6 products per fp32
+    product) = 16 x 157.3 / 6 TF; split-fp16 (3 products) = 16 x 157.3 / 3 TF"""
+    k = F16_KNOB.get(cls)
+    on = k is not None and (knobs.get(k) == 2 if k == "feat_nn_fast" else bool(knobs.get(k)))
+    return PEAK_BF16_TFLOPS / (3 if on else 6)
 
+
+def timed_run(wl, args, world, pipelined, barrier):
+    """warmup, one untimed profiled step (per-class breakdown, dominant class), the timed steps"""
     from lib import _native
-    _native.lib()
-    math_info = _native.set_math(args.math)
-    if args.workload == "scene":
-        wl = SceneWorkload(dev, rank, npts=args.npts)
-    else:
-        wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
-
-    pipelined = args.workload == "scene" and not args.no_pipeline
 
     def run_step():
         if pipelined:
@@ -331,26 +355,119 @@ def main():
         if prof_all is None:
             prof_all = {k: tuple(x / max(args.steps, 1) for x in v) for k, v in prof.items()}
             dom = max(prof, key=lambda k: prof[k][0])
-        if args.prof_seq and rank == 0:
+        if args.prof_seq and int(os.environ.get("RANK", "0")) == 0:
             with open(args.prof_seq, "w") as f:
                 json.dump(_native.prof_seq(), f)
         _native.prof_set(0)
         _native.prof_mask(None)
     if world > 1:
         import torch.distributed as dist
-        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        tt = torch.tensor([dt], device=rec.device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
+    return dt, rec, prof, prof_all, dom
+
+
+def golden_accuracy(dev):
+    """max |R - R_ref|, |t - t_ref| of the OANet (RegBlock network, train-mode BN) on the full-size golden
+    (tests/golden/oanet_full_train.npz: the reference's own outputs, 32 pairs x 5000 correspondences) and
+    against our float64 restatement of the same inputs (oanet_full_train_f64.npz), at the current maths"""
+    from lib.filtering.oanet import OANet
+    from synth import synth_correspondences
+    gd = os.path.join(ROOT, "tests", "golden")
+    g = dict(np.load(os.path.join(gd, "oanet_full_train.npz")))
+    g64 = dict(np.load(os.path.join(gd, "oanet_full_train_f64.npz")))
+    net = OANet(oanet_cfg())
+    synth_module(net, seed=7)
+    net = net.to(dev).train()
+    xs, _, _ = synth_correspondences(32, 5000, seed=33)
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(xs).to(dev).unsqueeze(1)})
+    r = {}
+    for ref, tag in ((g, "ref"), (g64, "f64")):
+        r["max_R_err_vs_" + tag] = max(float(np.abs(out["rot_est"][i].cpu().numpy() - ref["R%d" % i]).max())
+                                       for i in range(2))
+        r["max_t_err_vs_" + tag] = max(float(np.abs(out["trans_est"][i].cpu().numpy() - ref["t%d" % i]).max())
+                                       for i in range(2))
+    masks = sum(int(((out["scores"][i].cpu().numpy() > 0.5) != (g["scores%d" % i] > 0.5))
+                    [np.abs(g["scores%d" % i] - 0.5) >= 1e-4].sum()) for i in range(2))
+    r["mask_mismatches_vs_ref"] = masks
+    return {k: (round(v, 8) if isinstance(v, float) else v) for k, v in r.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default=os.environ.get("MVR_BENCH_WORKLOAD", "scene"),
+                    choices=["scene", "precomputed"])
+    ap.add_argument("--pairs", type=int, default=435)
+    ap.add_argument("--npts", type=int, default=5000)
+    ap.add_argument("--samp", default="rand", choices=["rand", "fps"],
+                    help="scene workload: interest sampling (lib/layers.py Sampler: rand = the reference's numpy draws, "
+                    "fps = furthest-point sampling, csrc/fps.hip)")
+    ap.add_argument("--math", default=os.environ.get("MVR_MATH", "f32eq"), choices=["f32eq", "split16"],
+                    help="f32eq: every MFMA product on the 3-term bf16 split (fp32-equivalent operands, the reference's "
+                    "fp32); split16: the 2-term fp16 split (22-bit operands) where a kernel has it")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the secondary timed leg at the other maths")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events in the timed region (A/B timing)")
+    ap.add_argument("--no-pipeline", action="store_true", help="scene workload: run the stages of a step back to "
+                    "back on one stream (default: two-stage pipeline over consecutive scenes, SceneWorkload.step_pipelined)")
+    ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
+                    "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    from lib import _native
+    _native.lib()
+    math_info = _native.set_math(args.math)
+    if args.workload == "scene":
+        wl = SceneWorkload(dev, rank, npts=args.npts, samp=args.samp)
+    else:
+        wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
+    pipelined = args.workload == "scene" and not args.no_pipeline
+
+    dt, rec, prof, prof_all, dom = timed_run(wl, args, world, pipelined, barrier)
     pairs_per_step = int(rec.shape[-2]) * world
     value = pairs_per_step * args.steps / dt
+    ms_step = dt / args.steps * 1e3
+
+    # FCGF sparse convs: the launch-level ProfScope cannot see how many kernel-map pairs a launch has (no host
+    # sync); the class's algorithmic FLOPs / bytes are counted here from the scene's kernel maps instead
+    fcgf = None
+    if args.workload == "scene":
+        fl, by = wl.fcgf_work()
+        fcgf = {"flops_per_step": fl, "bytes_per_step": by}
+        for d in (prof_all, prof):
+            if d.get("spconv") and d["spconv"][1]:
+                scale = 1.0 if d is prof_all else float(args.steps)
+                d["spconv"] = (d["spconv"][0], d["spconv"][1], fl * scale, by * scale)
 
     # dominant kernel class (by device time in the profiled untimed step), timed with HIP events around
     # each of its launches inside the timed region and priced against the roofline that binds it:
     # arithmetic intensity vs the ridge of the MFMA path it runs on
+    knobs = math_info["knobs"]
     ms, nl, fl, by = prof[dom]
     if ms <= 0:   # --no-prof: no per-launch timings
         ms, nl = 1e-9, 1
-    mpeak = PEAK_SPLIT_TFLOPS if dom in GEMM_CLASSES else MFMA_PEAKS.get(dom, PEAK_FP32_TFLOPS)
+    mpeak = class_peak_tflops(dom, knobs) if dom in MFMA_CLASSES else PEAK_FP32_TFLOPS
     ridge = mpeak * 1e12 / (PEAK_HBM_GBS * 1e9)                     # FLOP per byte
     bound = "mfma" if (by > 0 and fl / by >= ridge) else "hbm"
     avg_s = ms * 1e-3 / max(nl, 1)
@@ -363,7 +480,7 @@ def main():
     if os.path.exists(tfile):
         with open(tfile) as f:
             tr = json.load(f)
-        if dom in tr.get("classes", {}):
+        if dom in tr.get("classes", {}) and tr.get("math", "split16") == args.math:
             traffic = tr["classes"][dom]["pmc_bytes_per_launch"]
             tsrc = tr.get("source")
     # the same kernel class alone on the GPU (the untimed profiled step runs the stages back to back):
@@ -373,6 +490,15 @@ def main():
     if iso[0] > 0 and iso[1]:
         iso_s = iso[0] * 1e-3 / iso[1]
         iso_ach = (iso[2] / iso[1] / iso_s / 1e12) if bound == "mfma" else (iso[3] / iso[1] / iso_s / 1e9)
+    # SURVEY §8d whole-step roofline: T_floor = sum over kernel classes of max(FLOP / MFMA peak at the class's
+    # arithmetic, algorithmic bytes / 8 TB/s), per step, against the measured step time
+    floor_ms = {}
+    for k, v in prof_all.items():
+        if not v[1]:
+            continue
+        pk = class_peak_tflops(k, knobs) if k in MFMA_CLASSES else PEAK_FP32_TFLOPS
+        floor_ms[k] = 1e3 * max(v[2] / (pk * 1e12), v[3] / (PEAK_HBM_GBS * 1e9))
+    t_floor = sum(floor_ms.values())
     roof = {"bound": bound, "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "achieved_isolated": round(iso_ach, 3) if iso_ach else None,
@@ -381,31 +507,56 @@ def main():
             "avg_launch_ms": round(ms / max(nl, 1), 4), "share_of_step": round(ms / (dt * 1e3), 3),
             "arith_intensity": round(fl / by, 2) if by else None, "ridge": round(ridge, 1),
             "algorithmic_bytes_per_launch": by / max(nl, 1),
-            "peak_note": ("split-bf16 MFMA fp32-equivalent peak = 16*157.3/6 TF" if dom in GEMM_CLASSES else
-                          "MI355X_MICROARCH.md"),
+            "peak_note": ("fp32-equivalent MFMA peak of the class's operand split (split-bf16 16*157.3/6 TF, "
+                          "split-fp16 16*157.3/3 TF); HBM 8 TB/s (MI355X_MICROARCH.md)"),
             "traffic_source": tsrc,
             # per kernel class, from the profiled untimed step (events on every launch):
             # [ms per step, algorithmic TFLOP/s, algorithmic GB/s]
             "classes": {k: [round(v[0], 3), round(v[2] / (v[0] * 1e9), 1), round(v[3] / (v[0] * 1e6))]
-                        for k, v in prof_all.items() if v[1] and v[0] > 0}}
+                        for k, v in prof_all.items() if v[1] and v[0] > 0},
+            "whole_step": {"t_floor_ms": round(t_floor, 3), "ms_per_step": round(ms_step, 3),
+                           "achieved": round(t_floor / ms_step, 4),
+                           "floor_ms_by_class": {k: round(v, 3) for k, v in floor_ms.items()},
+                           "note": "SURVEY §8d: T_floor = sum over classes of max(FLOP / MFMA peak at the class's "
+                                   "operand split, algorithmic bytes / 8 TB/s); achieved = T_floor / measured step"},
+            "fcgf_work": fcgf}
+
+    # the other operand maths as a secondary line (same workload, same step count), and the accuracy of both on
+    # the full-size golden
+    secondary, accuracy = None, None
+    if not args.no_secondary and args.workload == "scene":
+        other = "split16" if args.math == "f32eq" else "f32eq"
+        oinfo = _native.set_math(other)
+        odt, orec, _, _, _ = timed_run(wl, args, world, pipelined, barrier)
+        if rank == 0:
+            acc_o = golden_accuracy(dev)
+        _native.set_math(args.math)
+        secondary = {"math": other, "dtype": oinfo["dtype"], "value": round(pairs_per_step * args.steps / odt, 3),
+                     "ms_per_step": round(odt / args.steps * 1e3, 3)}
+        if rank == 0:
+            secondary["accuracy"] = acc_o
+    if rank == 0:
+        accuracy = golden_accuracy(dev)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the box's CPU share per GPU (OMP_NUM_THREADS is set to it there; affinity shows the whole host)
         cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-        torch.set_num_threads(cores)
-        v, sample = wl.cpu_baseline(args.cpu_budget)
-        cpu = {"value": round(v, 4), "unit": "pairs/s", "cores": cores, "kind": "port", "sample": sample}
+        v, sample = wl.cpu_baseline(cores, args.cpu_budget)
+        v8, _ = wl.cpu_baseline(8, args.cpu_budget)
+        cpu = {"value": round(v, 4), "unit": "pairs/s", "cores": cores, "kind": "port", "sample": sample,
+               "value_8_threads": round(v8, 4)}
     line = {"metric": METRIC if args.workload == "scene" else METRIC + " [filter+SVD only: precomputed corr.]",
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
-            "config": dict(wl.config(), parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
+            "config": dict(wl.config(), math=args.math,
+                           parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
                            schedule=("3-stream pipeline over consecutive scenes: voxelisation + coordinate levels of "
                                      "scene k+1, FCGF + feature NN of scene k, OANet + Procrustes of scene k-1; every "
                                      "timed step runs every stage in full"
                                      if pipelined else "stages back to back on one stream")),
-            "roofline": roof, "cpu_baseline": cpu}
+            "roofline": roof, "cpu_baseline": cpu, "accuracy": accuracy, "secondary": secondary}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

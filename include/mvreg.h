@@ -155,7 +155,11 @@ int mvr_set_pool_split(int on);
  * Outputs: logits/scores [P,N] (contiguous), R [P,3,3], t [P,3], res [P,N];
  * latent(p,c,n) = latent[p*C*ld + c*ld + n] (may be NULL); res_row/score_row: optional copies written at
  * row pointers with pair stride row_pstride (the next block's input rows 6,7).
- * guard_pos: int32 [P] scratch (zeroed here).  status: int32 [P] (may be NULL).
+ * guard_pos: int32 [P]: per-pair counts of positive weights (zeroed here).  status: int32 [P] (may be NULL).
+ * guard_group: scope of the zero-row guard (see mvr_procrustes): 0 the whole batch, > 0 groups of that many
+ * pairs; < 0 the block stops after its output head — scores hold relu(tanh(logits)) unguarded, guard_pos the
+ * counts, and R, t, res, res_row, score_row are left to the caller's mvr_procrustes (a guard evaluated over
+ * pairs on other devices: lib/distributed.py scene mode).
  * bn_train: BatchNorm layers normalise with batch statistics (module.train()). */
 /* diff_unpool kernel choice (process-wide): 1 (default) the 4-wave, two-per-CU kernel when clusters <= 512,
  * 0 the 8-wave kernel (A/B timing).  Returns the previous setting. */

@@ -35,65 +35,100 @@ def test_shard_pairs_partition(P, world):
 
 
 class _StubFilter(torch.nn.Module):
-    """Deterministic per-pair stand-in for PairwiseReg.filter_correspondences (CPU): R, t and
-    scores are functions of each pair's own xs, so sharding must not change them."""
+    """Deterministic per-pair stand-in for PairwiseReg.filter_correspondences (CPU) with the reference's
+    batch-coupled zero-row guard (oanet.py:177-178): weights relu(x0) per point; if some pair of the guard's scope
+    has no positive weight, every pair of that scope gets + 1/N; R, t from the weighted means.  The guard's scope
+    follows the OANet contract: guard_sync (scene mode: the whole sharded batch), else guard_group (> 0: groups of
+    that many pairs), else the whole forward batch."""
+
+    iter_num = 0
 
     def __init__(self):
         super().__init__()
         self.guard_group = 0
-        self.seen_groups = []
+        self.guard_sync = None
+        self.seen = []
 
     def filter_correspondences(self, d):
         xs = d["xs"][:, 0]                                          # [p, N, 6]
-        self.seen_groups.append(self.guard_group)
-        m = xs.mean(dim=1)                                          # [p, 6]
-        R = torch.eye(3).repeat(xs.shape[0], 1, 1) + m[:, :3, None] * 1e-3
+        self.seen.append((self.guard_group, self.guard_sync is not None))
+        p, n = xs.shape[:2]
+        w = torch.relu(xs[..., 0])
+        pos = (w > 0).sum(dim=1).to(torch.int32)
+        if self.guard_sync is not None:
+            fire = torch.full((p,), bool((self.guard_sync(pos) == 0).any()))
+        else:
+            g = self.guard_group if self.guard_group > 0 else max(p, 1)
+            grp = torch.arange(p) // g
+            zero = (pos == 0)
+            fire = torch.stack([zero[grp == k].any() for k in grp.tolist()]) if p else torch.zeros(0, dtype=torch.bool)
+        w = w + fire[:, None].float() / n
+        wn = w / (w.sum(dim=1, keepdim=True) + 1e-7)
+        m = (wn[..., None] * xs).sum(dim=1)                          # [p, 6]
+        R = torch.eye(3).repeat(p, 1, 1) + m[:, :3, None] * 1e-3
         t = m[:, 3:6, None]
-        scores = torch.sigmoid(xs[..., 0])
-        return {"rot_est": [R], "trans_est": [t], "scores": [scores], "gradient_flag": False}
+        return {"rot_est": [R], "trans_est": [t], "scores": [w], "gradient_flag": False}
 
 
-def _xs(P, N=16):
+def _xs(P, N=16, zero_pair=None):
     g = torch.Generator().manual_seed(5)
-    return torch.randn(P, 1, N, 6, generator=g)
+    xs = torch.randn(P, 1, N, 6, generator=g)
+    if zero_pair is not None and zero_pair < P:
+        xs[zero_pair, 0, :, 0] = -xs[zero_pair, 0, :, 0].abs() - 0.1   # no positive weight: the guard fires
+    return xs
 
 
-def _worker(rank, world, port, P, q):
+def _worker(rank, world, port, P, guard, zero_pair, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         stub = _StubFilter()
-        rec = D.register_pairs_sharded(stub, {"xs": _xs(P)}, world, rank)
+        rec = D.register_pairs_sharded(stub, {"xs": _xs(P, zero_pair=zero_pair)}, world, rank, guard=guard)
         # the raw gather of hand-made records, too
         s, e = D.shard_pairs(P, world, rank)
         mine = torch.arange(s, e, dtype=torch.float32)[:, None].repeat(1, D.REC)
         g = D.gather_records(mine, P, world)
-        q.put((rank, rec.numpy(), g.numpy(), stub.guard_group, stub.seen_groups))
+        q.put((rank, rec.numpy(), g.numpy(), (stub.guard_group, stub.guard_sync), stub.seen))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("P", [70, 435])
-def test_register_sharded_gloo_world2(P):
+@pytest.mark.parametrize("P,guard,zero_pair", [(70, "group", None), (435, "group", None), (70, "group", 66),
+                                               (70, "scene", 66), (70, "scene", None), (40, "scene", 35)])
+def test_register_sharded_gloo_world2(P, guard, zero_pair):
+    """world 2 reproduces the single-rank records exactly, in pair order.  With a zero-weight pair on rank 1
+    (pair 66 of 70: rank 0 holds pairs 0-63): "group" mode fires the guard in that pair's 32-pair group only,
+    "scene" mode on every pair of both ranks (one all-reduce per block), as the single-rank run over the batch."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, P, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, guard, zero_pair, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = D.register_pairs_sharded(_StubFilter(), {"xs": _xs(P)}, 1, 0)
-    for rank, rec, g, gg, seen in res:
+    ref = D.register_pairs_sharded(_StubFilter(), {"xs": _xs(P, zero_pair=zero_pair)}, 1, 0, guard=guard).numpy()
+    for rank, rec, g, restored, seen in res:
         assert rec.shape == (P, D.REC)
         np.testing.assert_array_equal(rec[:, 0], np.arange(P))        # pair order
-        np.testing.assert_allclose(rec, ref.numpy(), rtol=0, atol=0)   # identical to one rank
+        np.testing.assert_allclose(rec, ref, rtol=0, atol=0)           # identical to one rank
         np.testing.assert_array_equal(g[:, 0], np.arange(P))
-        assert gg == 0 and all(x == D.GROUP for x in seen)             # guard scope set, then restored
+        assert restored == (0, None)                                   # guard scope set, then restored
+        if seen:
+            assert all(x == ((D.GROUP, False) if guard == "group" else (0, True)) for x in seen)
+    if zero_pair is not None:
+        # the guard's reach: every pair (scene) or the zero pair's 32-pair group only (group)
+        plain = D.register_pairs_sharded(_StubFilter(), {"xs": _xs(P)}, 1, 0, guard=guard).numpy()
+        hit = np.any(ref != plain, axis=1)
+        if guard == "scene":
+            assert hit.all()
+        else:
+            grp = np.arange(P) // D.GROUP
+            np.testing.assert_array_equal(hit, grp == zero_pair // D.GROUP)
 
 
 def test_pack_unpack_roundtrip():

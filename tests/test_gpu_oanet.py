@@ -217,3 +217,25 @@ def test_oanet_fused_head_guard_and_pconv_off(gpu):
         np.testing.assert_allclose(res[0]["logits"][i].cpu().numpy(), res[1]["logits"][i].cpu().numpy(), atol=2e-3,
                                    rtol=1e-4)
         np.testing.assert_allclose(res[0]["rot_est"][i].cpu().numpy(), res[1]["rot_est"][i].cpu().numpy(), atol=1e-4)
+
+
+@pytest.mark.parametrize("ovr", [None, {"reg_init.output.bias": [-1.0e4]}])
+def test_oanet_external_guard_equals_internal(gpu, ovr):
+    """guard_sync (lib/distributed.py scene mode: the block stops at its head, the caller evaluates the zero-row
+    guard and runs mvr_procrustes) on one rank gives the in-block guard + Procrustes bit for bit — with the guard
+    idle and with it firing on every pair (output bias -1e4)"""
+    import torch
+    from lib.distributed import scene_guard_sync
+    xs, _, _ = synth_correspondences(4, 900, seed=81)
+    net = _oanet(128, 500, 9, gpu, which="full", overrides=ovr)
+    outs = []
+    for sync in (None, scene_guard_sync(1)):
+        net.guard_sync = sync
+        with torch.no_grad():
+            outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    net.guard_sync = None
+    for k in ("logits", "scores", "rot_est", "trans_est"):
+        for i in range(2):
+            assert torch.equal(outs[0][k][i], outs[1][k][i]), (k, i)
+    if ovr:
+        assert np.all(outs[0]["logits"][0].cpu().numpy() < 0)

@@ -134,3 +134,21 @@ def test_oracle_full_train_golden():
             d = dist(o[k][i], g["%s%d" % (kg, i)])
             bound = 1e-4 if i == 0 else np.maximum(1e-4, 2 * dist(g["%s%d" % (kg, i)], g64["%s%d" % (kg, i)]))
             assert (d <= bound).all(), (i, k, d.max())
+
+
+@pytest.mark.parametrize("fx,train", [("oanet_small_eval.npz", False), ("oanet_small_train.npz", True)])
+def test_torch_port_matches_golden(fx, train):
+    """oracle/torch_port.py (the CPU baseline bench.py times: the reference's op sequence on torch CPU tensors,
+    N x N diag_embed Kabsch included) reproduces the reference's outputs"""
+    import torch
+    from oracle import torch_port
+    g = golden(fx)
+    st = synth_state(_shapes("small"), seed=5)
+    with torch.no_grad():
+        logits, R, t = torch_port.oanet_forward(st, torch.from_numpy(g["xs"]), train=train)
+    np.testing.assert_allclose(logits.numpy(), g["logits1"], atol=5e-4, rtol=1e-4)
+    np.testing.assert_allclose(R.numpy(), g["R1"], atol=1e-4)
+    np.testing.assert_allclose(t.numpy(), g["t1"], atol=1e-4)
+    s = golden("softnn.npz")
+    x = torch_port.soft_nn(torch.from_numpy(s["fs"]), torch.from_numpy(s["ft"]), torch.from_numpy(s["yc"]))
+    np.testing.assert_allclose(x.numpy(), s["x_soft"], atol=2e-5)

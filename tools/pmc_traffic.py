@@ -63,6 +63,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("outdir")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--math", default="f32eq", help="the bench's --math of the profiled run")
     a = ap.parse_args()
     res = {}
     seq_f = json.load(open(os.path.join(a.outdir, "seq_FETCH_SIZE.json")))
@@ -85,7 +86,7 @@ def main():
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py --steps 1 --warmup 1` with "
                      "MVR_PROF_MARK=1 (tools/pmc_bench.sh): dispatches joined to the timed step's launch sequence "
                      "by region markers; FETCH x2 (gfx950 16 B/lane correction), KB -> B",
-           "classes": res}
+           "math": a.math, "classes": res}
     txt = json.dumps(doc, indent=1)
     print(txt)
     if a.out:
