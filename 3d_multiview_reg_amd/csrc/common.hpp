@@ -53,4 +53,12 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
+// XCD-aware workgroup -> tile map.  Workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one, each
+// XCD with its own L2): this bijection on [0, nb) gives XCD b % 8 a contiguous range of tiles instead, so the
+// workgroups one XCD runs together work on neighbouring tiles and share what they read in its L2.
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
+  return x * q + (x < r ? x : r) + b / 8;
+}
+
 }  // namespace mvr

@@ -88,6 +88,98 @@ __global__ __launch_bounds__(FPS_T) void fps_kernel(const float* __restrict__ xy
   }
 }
 
+// One-barrier form for fragments of up to 1024 * PER points, all held in registers (4 VGPRs per point).
+// Step: every thread updates its points' running minimum and keeps its own best (first maximum in its index
+// order: strict '>' over ascending j, so the lowest index among equal distances); each wave finds its best by a
+// float max (DPP within rows, lane reads across them) and, only when several lanes tie on it, a min over their
+// indices; the winning lane writes (d, index, coordinates) of its point to its wave's slot; ONE barrier; every
+// thread then reads the 16 slots and picks the block's best (ties -> lowest index) with its coordinates, so the
+// next step starts without a global load on the critical path.  Slots alternate by step parity (a wave can only
+// reach step i + 2's writes after every wave passed step i + 1's barrier, i.e. finished reading step i's slots).
+// Same arithmetic and tie rule as fps_kernel (explicitly rounded fp32 distances): identical indices.
+__device__ __forceinline__ float row_max16(float v) {   // max over the 16 lanes of a DPP row, in every lane
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true)));    // quad 1,0,3,2
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, true)));    // quad 2,3,0,1
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, true)));   // half mirror
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, true)));   // row mirror
+  return v;
+}
+__device__ __forceinline__ float wave_max_uniform(float v) {
+  v = row_max16(v);
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
+
+struct FpsSlot {
+  float d, x, y, z;
+  int k, pad0, pad1, pad2;
+};
+
+template <int T, int PER>
+__global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xyz, const int64_t* __restrict__ off,
+                                                    int m, int64_t* __restrict__ idx_out) {
+  constexpr int NW = T / 64;
+  __shared__ FpsSlot slot[2][NW];
+  const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t s0 = off[f];
+  const int n = (int)(off[f + 1] - s0);
+  const float* p = xyz + s0 * 3;
+  float px[PER], py[PER], pz[PER], d[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int k = tid + j * T;
+    const bool ok = k < n;
+    px[j] = ok ? p[3 * k] : 0.f;
+    py[j] = ok ? p[3 * k + 1] : 0.f;
+    pz[j] = ok ? p[3 * k + 2] : 0.f;
+    d[j] = ok ? __builtin_inff() : -1.f;   // absent points never win
+  }
+  int64_t* out = idx_out + (int64_t)f * m;
+  if (tid == 0) out[0] = s0;
+  float lx = p[0], ly = p[1], lz = p[2];
+  for (int it = 1; it < m; ++it) {
+    float bd = -2.f;
+    int bj = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      d[j] = fminf(d[j], d[j] >= 0.f ? fps_d2(px[j], py[j], pz[j], lx, ly, lz) : -1.f);
+      if (d[j] > bd) { bd = d[j]; bj = j; }
+    }
+    const float wm = wave_max_uniform(bd);
+    uint64_t cand = __ballot(bd == wm);
+    const int mk = tid + bj * T;
+    if (__popcll(cand) > 1) {   // several lanes hold the wave's best distance: the lowest index wins
+      int km = (bd == wm) ? mk : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) km = min(km, __shfl_xor(km, o, 64));
+      cand = __ballot(bd == wm && mk == km);
+    }
+    const int wl = __ffsll((unsigned long long)cand) - 1;
+    if (lane == wl) {   // the winner's coordinates: a select over its registers
+      float x = px[0], y = py[0], z = pz[0];
+#pragma unroll
+      for (int j = 1; j < PER; ++j)
+        if (bj == j) { x = px[j]; y = py[j]; z = pz[j]; }
+      FpsSlot& sl = slot[it & 1][wid];
+      sl.d = wm; sl.k = mk; sl.x = x; sl.y = y; sl.z = z;
+    }
+    __syncthreads();
+    float gd = -3.f;
+    int gk = 0x7fffffff, gw = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const float dw = slot[it & 1][w].d;
+      const int kw = slot[it & 1][w].k;
+      if (dw > gd || (dw == gd && kw < gk)) { gd = dw; gk = kw; gw = w; }
+    }
+    lx = slot[it & 1][gw].x; ly = slot[it & 1][gw].y; lz = slot[it & 1][gw].z;
+    if (tid == 0) out[it] = s0 + gk;
+  }
+}
+
 }  // namespace mvr
 
 // xyz [sum n, 3] fp32 (fragments back to back, offsets off[B+1]); idx_out [B][m] int64 global rows
@@ -109,9 +201,19 @@ extern "C" int mvr_fps(const float* xyz, const int64_t* offsets, const int64_t* 
     MVR_CHECK_LAUNCH();                                                                                 \
     return MVR_OK;                                                                                      \
   }
-  MVR_FPS(1024, 8, true)
-  MVR_FPS(1024, 16, true)
-  MVR_FPS(512, 40, true)
+#define MVR_FPSR(T, PER)                                                                                  \
+  if (nmax <= (int64_t)(T) * (PER)) {                                                                  \
+    hipLaunchKernelGGL((mvr::fps_reg_kernel<T, PER>), g, dim3(T), 0, stream, xyz, offsets, m, idx_out); \
+    MVR_CHECK_LAUNCH();                                                                                \
+    return MVR_OK;                                                                                     \
+  }
+  // 1024 threads: 4 VGPRs per point within the 128 a 1024-thread workgroup allows; 512 threads: 256
+  MVR_FPSR(1024, 4)
+  MVR_FPSR(1024, 8)
+  MVR_FPSR(1024, 16)
+  MVR_FPSR(1024, 20)
+  MVR_FPSR(512, 48)
+#undef MVR_FPSR
   MVR_FPS(1024, 64, false)
   MVR_FPS(512, 160, false)
 #undef MVR_FPS

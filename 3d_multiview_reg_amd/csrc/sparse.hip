@@ -584,12 +584,32 @@ static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel
 }
 
 // ------------------------------------------------------------------ kernel-map row order
-__global__ void offset_mask_kernel(const int32_t* __restrict__ nbr, int64_t Mo, int K, uint32_t* keys, int32_t* rows) {
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {   // 9 bits -> every third bit of 27
+  v &= 511u;
+  v = (v | (v << 16)) & 0x030000FFu;
+  v = (v | (v << 8)) & 0x0300F00Fu;
+  v = (v | (v << 4)) & 0x030C30C3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+// sort key of an output row: its active-offset mask (the tile's offset union stays small), then — when the
+// row's coordinates are given — its fragment and the Morton code of its coordinates / step (9 bits per axis,
+// wrapped): rows of one mask class are tiled in spatial order, so the tiles an XCD runs together gather
+// neighbour rows from one compact region (L2 reuse).  Only the tiling order changes: every output row is
+// computed the same way wherever it sits.
+__global__ void offset_mask_kernel(const int32_t* __restrict__ nbr, const int4* __restrict__ coords, int step,
+                                   int64_t Mo, int K, uint64_t* keys, int32_t* rows) {
   const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= Mo) return;
   uint32_t m = 0;
   for (int k = 0; k < K; ++k) m |= (nbr[o * K + k] >= 0 ? 1u : 0u) << k;
-  keys[o] = m;
+  uint32_t lo = 0;
+  if (coords) {
+    const int4 c = coords[o];
+    lo = ((uint32_t)c.x & 31u) << 27 | spread3((uint32_t)(c.y / step)) << 2 | spread3((uint32_t)(c.z / step)) << 1 |
+         spread3((uint32_t)(c.w / step));
+  }
+  keys[o] = (uint64_t)m << 32 | lo;
   rows[o] = (int32_t)o;
 }
 
@@ -765,34 +785,40 @@ extern "C" int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, hipStream
   return MVR_OK;
 }
 
-// Order the output rows of a kernel map by their active-offset mask (LSD radix sort, stable):
-// perm[i] = i-th row.  Workspace: mvr_kernel_map_order_bytes(Mo).
+// Order the output rows of a kernel map by their active-offset mask, then (out_coords given) fragment and
+// Morton code (LSD radix sort of 64-bit keys, stable): perm[i] = i-th row.  Workspace:
+// mvr_kernel_map_order_bytes(Mo).
 static size_t order_sort_bytes(int64_t Mo) {
   size_t tmp = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)(Mo > 0 ? Mo : 1), 0, 32);
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                         (const int32_t*)nullptr, (int32_t*)nullptr, (int)(Mo > 0 ? Mo : 1), 0,
+                                         64) != hipSuccess)
+    return 0;
   return tmp;
 }
 extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) {
   const size_t n = (size_t)(Mo > 0 ? Mo : 1);
-  return order_sort_bytes(Mo) + n * 12 + 3 * 256;
+  return order_sort_bytes(Mo) + n * 20 + 3 * 256;
 }
-extern "C" int mvr_kernel_map_order(const int32_t* nbr, int64_t Mo, int K, int32_t* perm, void* ws, size_t ws_bytes,
-                                    hipStream_t s) {
+extern "C" int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mo, int K,
+                                    int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s) {
   if (!nbr || !perm || Mo < 0 || K <= 0 || K > 32 || !ws || ws_bytes < mvr_kernel_map_order_bytes(Mo) ||
-      Mo > 0x7fffffff)
+      Mo > 0x7fffffff || (out_coords && step <= 0))
     return MVR_EINVAL;
   if (Mo == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mo * (4.0 * K + 32), s);
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
-  uint32_t* kin = reinterpret_cast<uint32_t*>(take((size_t)Mo * 4));
-  uint32_t* kout = reinterpret_cast<uint32_t*>(take((size_t)Mo * 4));
+  uint64_t* kin = reinterpret_cast<uint64_t*>(take((size_t)Mo * 8));
+  uint64_t* kout = reinterpret_cast<uint64_t*>(take((size_t)Mo * 8));
   int32_t* vin = reinterpret_cast<int32_t*>(take((size_t)Mo * 4));
   size_t tmp = order_sort_bytes(Mo);
+  if (!tmp) return MVR_ELAUNCH;
   void* tbuf = take(tmp);
-  hipLaunchKernelGGL(offset_mask_kernel, dim3(nblk(Mo)), dim3(256), 0, s, nbr, Mo, K, kin, vin);
-  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, kin, kout, vin, perm, (int)Mo, 0, K, s) != hipSuccess)
+  hipLaunchKernelGGL(offset_mask_kernel, dim3(nblk(Mo)), dim3(256), 0, s, nbr, reinterpret_cast<const int4*>(out_coords),
+                     step, Mo, K, kin, vin);
+  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, kin, kout, vin, perm, (int)Mo, out_coords ? 0 : 32, 32 + K, s) !=
+      hipSuccess)
     return MVR_ELAUNCH;
   MVR_CHECK_LAUNCH();
   return MVR_OK;

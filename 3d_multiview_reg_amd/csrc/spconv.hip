@@ -33,6 +33,7 @@ struct SpArgs {
   int relu;
   float* out; int64_t ldout;
   int* range; const int* guard; int epoch;   // split-fp16 flag word (set to epoch 1) / split-bf16 re-run guard
+  int xcd;                                   // spconv_bx: XCD-contiguous tile order (mvr_set_spconv_xcd)
 };
 
 constexpr int SP_BK = 16;
@@ -256,8 +257,12 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t o0 = (int64_t)blockIdx.x * TM;
-  const int c0 = blockIdx.y * TN;
+  // 1-D grid of (row tile, column tile) in XCD-contiguous order: the column tiles of a row tile (same gathered
+  // rows) and neighbouring row tiles (spatially close in the kernel map's row order) share an XCD's L2
+  const int gy = (a.Cout + TN - 1) / TN;
+  const int64_t t = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t o0 = (t / gy) * TM;
+  const int c0 = (int)(t % gy) * TN;
   const int K = a.K;
 
   if (tid < SP_KMAX) kact[tid] = 0;
@@ -475,6 +480,7 @@ __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin
 #define SPCONV_MATH_DEFAULT 0
 #endif
 int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_spconv_math
+int g_spconv_xcd = 1;                   // mvr_set_spconv_xcd
 
 }  // namespace mvr
 
@@ -491,6 +497,12 @@ static size_t sp_f16_bytes(int K, int Cin, int Cout) { return sp_bf16_bytes(K, C
 extern "C" size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout) {
   if (K <= 0 || Cin <= 0 || Cout <= 0) return 0;
   return sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout) + 2 * sp_coutp(Cout) * sizeof(float);
+}
+
+extern "C" int mvr_set_spconv_xcd(int on) {
+  const int prev = g_spconv_xcd;
+  g_spconv_xcd = on ? 1 : 0;
+  return prev;
 }
 
 extern "C" int mvr_set_spconv_math(int h) {
@@ -530,7 +542,7 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
     return MVR_EINVAL;
   if (Mout == 0) return MVR_OK;
   SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout,
-           nullptr, nullptr, 0};
+           nullptr, nullptr, 0, g_spconv_xcd};
   ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
   if (wimg) {   // split paths (weights pre-split by mvr_spconv_wimage)
     const char* base = reinterpret_cast<const char*>(wimg);
@@ -555,12 +567,12 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
 #define MVR_SPL(TN_, NS_, GY)                                                                                   \
   do {                                                                                                          \
     if (h1) {                                                                                                   \
-      hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 1>), dim3(gx, GY), dim3(256), 0, s, a, wi16, CoutP, isc);  \
+      hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 1>), dim3(gx * (GY)), dim3(256), 0, s, a, wi16, CoutP, isc); \
       MVR_CHECK_LAUNCH();                                                                                       \
       a.guard = a.range;                                                                                        \
       a.range = nullptr;                                                                                        \
     }                                                                                                           \
-    hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx, GY), dim3(256), 0, s, a, wi, CoutP, isc);      \
+    hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc);    \
   } while (0)
     if (Cout <= 32)
       MVR_SPL(32, SPBX_NS32, 1);

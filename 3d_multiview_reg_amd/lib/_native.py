@@ -67,6 +67,7 @@ _SIGS = {
     "mvr_set_attn_math": (c_int, [c_int]),
     "mvr_set_pconv_math": (c_int, [c_int]),
     "mvr_set_spconv_math": (c_int, [c_int]),
+    "mvr_set_spconv_xcd": (c_int, [c_int]),
     "mvr_set_gemm_f16": (c_int, [c_int]),
     "mvr_attn_reruns": (c_int, [c_int]),
     "mvr_debug_stage_hash": (c_int, [c_vp, c_int]),
@@ -107,7 +108,7 @@ _SIGS = {
     "mvr_hash_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),
     "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
     "mvr_kernel_map_order_bytes": (c_size, [c_i64]),
-    "mvr_kernel_map_order": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
+    "mvr_kernel_map_order": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
                            c_int, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "mvr_spconv_wimage_bytes": (c_size, [c_int, c_int, c_int]),

@@ -5,7 +5,7 @@ The parameter tree reproduces the reference's state-dict keys exactly
 (e.g. 'reg_init.l1_1.0.conv.3.weight', 'reg_iter.0.l2.2.conv2.0.running_var'),
 so reference checkpoints load unchanged (lib/checkpoints.py).  The forward
 pass is ONE native call per block (mvr_oan_block_forward in
-libmvreg_hip.so: fused fp32-MFMA GEMMs + InstanceNorm/softmax statistics +
+libmvreg_hip.so: fused GEMMs on split-bf16 MFMA (fp32-equivalent operands) + InstanceNorm/softmax statistics +
 output head + zero-weight guard + weighted Procrustes).  There is no torch
 fallback: a CPU module raises.
 """
@@ -231,8 +231,10 @@ class OANet(nn.Module):
             if ext:   # the guard over the whole (sharded) batch, then oanet.py:180-183's Kabsch
                 gp = self.guard_sync(guard)
                 N.check(L.mvr_procrustes(N.ptr(xs), N.ptr(xs[..., 3:]), Npts * Cxs, Cxs, N.ptr(scores), Npts, N.ptr(gp),
-                                         score_row, rows * ld, P, Npts, 1, 1e-7, N.ptr(R), N.ptr(t), N.ptr(res), Npts,
+                                         None, 0, P, Npts, 1, 1e-7, N.ptr(R), N.ptr(t), N.ptr(res), Npts,
                                          res_row, rows * ld, N.ptr(status[bi]), 0, st), "mvr_procrustes")
+                if not last:   # the next block's input row 7: the (guarded) scores (oanet.py:247-248)
+                    inp[:, Cxs + 1, :Npts].copy_(scores)
             if bi == 0 and not last:
                 blk_in_ch = blocks[1].in_channels
                 if blk_in_ch != rows:

@@ -82,15 +82,18 @@ class CoordinateManager:
 
 
     def kernel_map_order(self, kind, s, ks=3):
-        """Rows of kernel_map(kind, s) sorted by their active-offset mask (tiling order of mvr_spconv)."""
+        """Rows of kernel_map(kind, s) sorted by their active-offset mask, then fragment and Morton code of their
+        coordinates (tiling order of mvr_spconv)."""
         key = (kind, s, ks)
         if key not in self.orders:
             nbr = self.kernel_map(kind, s, ks)
+            out_c = self.coords_at(2 * s if kind == "down" else s)
             L = N.lib()
             ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr.shape[0]), self.device)
             perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.device)
-            N.check(L.mvr_kernel_map_order(N.ptr(nbr), nbr.shape[0], nbr.shape[1], N.ptr(perm), N.ptr(ws), ws.numel(),
-                                           N.stream()), "mvr_kernel_map_order")
+            N.check(L.mvr_kernel_map_order(N.ptr(nbr), N.ptr(out_c), 2 * s if kind == "down" else s, nbr.shape[0],
+                                           nbr.shape[1], N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
+                    "mvr_kernel_map_order")
             self.orders[key] = perm
         return self.orders[key]
 

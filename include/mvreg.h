@@ -340,10 +340,13 @@ int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_b
 int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
                    int step, int transposed, int32_t* nbr, mvr_stream_t stream);
 /* Row order of a kernel map: output rows sorted by their active-offset mask (K <= 32), so that a
- * tile of consecutive rows shares its active offsets.  Workspace: mvr_kernel_map_order_bytes(Mout). */
+ * tile of consecutive rows shares its active offsets; with out_coords (int32 [Mout][4], the map's output
+ * coordinates, multiples of step) rows of one mask are further ordered by fragment and Morton code of
+ * coordinates / step (spatially compact tiles: L2 reuse of the gathered rows).  Workspace:
+ * mvr_kernel_map_order_bytes(Mout). */
 size_t mvr_kernel_map_order_bytes(int64_t Mout);
-int mvr_kernel_map_order(const int32_t* nbr, int64_t Mout, int K, int32_t* perm, void* workspace,
-                         size_t workspace_bytes, mvr_stream_t stream);
+int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mout, int K, int32_t* perm,
+                         void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 /* MinkowskiConvolution forward, gather-GEMM over the neighbour table (nbr NULL & K==1:
  * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
  * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
@@ -370,6 +373,9 @@ int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_
    split-bf16 re-run of a launch that saw one outside it; split-bf16 directly when the output is the residual).
    Returns the previous setting. */
 int mvr_set_spconv_math(int h);
+/* tile order of mvr_spconv's split kernels: 1 (default) XCD-contiguous (the workgroups one XCD runs together take
+   neighbouring tiles of the row order), 0 round-robin dispatch order (A/B timing).  Returns the previous setting. */
+int mvr_set_spconv_xcd(int on);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
 size_t mvr_brick_map_bytes(int64_t M);

@@ -74,7 +74,8 @@ def test_kernel_map_k7_property(gpu, frags):
 
 @pytest.mark.parametrize("split_bf16", [False, True])
 def test_fcgf_forward_matches_oracle(gpu, frags, split_bf16, monkeypatch):
-    """both sparse-conv paths: exact fp32 MFMA (default) and split-bf16 (mvr_spconv_wimage images)"""
+    """both sparse-conv paths: split-bf16 on mvr_spconv_wimage images (the default) and exact fp32 MFMA
+    (MVR_SPCONV_BF16=0); the oracle is our restatement of ME's sparse conv (parity unpinned: ME is absent)"""
     import torch
     from lib.descriptor import fcgf as fcgf_mod
     from lib.descriptor.fcgf import FCGFNet
@@ -95,3 +96,30 @@ def test_fcgf_forward_matches_oracle(gpu, frags, split_bf16, monkeypatch):
     np.testing.assert_allclose(np.linalg.norm(out, axis=1), 1.0, atol=1e-5)
     err = np.abs(out - ref).max()
     assert err < 2e-4, err
+
+
+def test_kernel_map_order_mask_then_morton(gpu, frags):
+    """mvr_kernel_map_order: perm is a permutation of the output rows, sorted by active-offset mask, then (with the
+    output coordinates) by fragment and Morton code of coordinates / step, stably — the tiling order of the sparse
+    convs (only the order changes: test_gpu_spconv checks results with and without it)"""
+    from lib.sparse import voxelize, CoordinateManager
+    c, _, counts, _ = voxelize(frags, 0.025, gpu)
+    cm = CoordinateManager(c, len(counts))
+    for kind, s in (("s1", 1), ("down", 1), ("up", 2), ("s1", 4)):
+        nbr = cm.kernel_map(kind, s).cpu().numpy()
+        perm = cm.kernel_map_order(kind, s).cpu().numpy()
+        out_c = cm.coords_at(2 * s if kind == "down" else s).cpu().numpy().astype(np.int64)
+        step = 2 * s if kind == "down" else s
+        assert np.array_equal(np.sort(perm), np.arange(len(nbr)))
+        mask = ((nbr >= 0).astype(np.int64) << np.arange(nbr.shape[1])).sum(1)
+
+        def spread(v):
+            v = v & 511
+            out = np.zeros_like(v)
+            for b in range(9):
+                out |= ((v >> b) & 1) << (3 * b)
+            return out
+        q = out_c[:, 1:] // step
+        lo = ((out_c[:, 0] & 31) << 27) | (spread(q[:, 0] & 511) << 2) | (spread(q[:, 1] & 511) << 1) | spread(q[:, 2] & 511)
+        key = (mask << 32) | lo
+        assert np.array_equal(perm, np.argsort(key, kind="stable"))

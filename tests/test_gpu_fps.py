@@ -8,7 +8,8 @@ from synth import synth_scene_fragments
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("sizes,m", [([100, 257], 50), ([3000, 5000, 1024], 700), ([20000], 600)])
+@pytest.mark.parametrize("sizes,m", [([100, 257], 50), ([3000, 5000, 1024], 700), ([20000], 600), ([24000, 17000], 900),
+                                    ([30000], 300), ([4096, 8192, 16384], 1000)])
 def test_fps_matches_oracle(gpu, sizes, m):
     import torch
     from lib.fps import furthest_point_sample
@@ -39,3 +40,16 @@ def test_fps_rejects_too_few_points(gpu):
     from lib.fps import furthest_point_sample
     with pytest.raises(RuntimeError):
         furthest_point_sample(torch.zeros(10, 3, device=gpu), [10], 11)
+
+
+def test_fps_ties_take_the_lowest_index(gpu):
+    """exact distance ties (duplicated points, a lattice): the first maximum in fragment order wins, as numpy's
+    argmax in the oracle"""
+    import torch
+    from lib.fps import furthest_point_sample
+    from oracle.fps import sample_fps
+    g = np.stack(np.meshgrid(*[np.arange(12, dtype=np.float32)] * 3, indexing="ij"), -1).reshape(-1, 3)
+    xyz = np.concatenate([g, g[::-1], g[:500]])            # every point at least twice
+    sizes = [len(xyz)]
+    got = furthest_point_sample(torch.from_numpy(xyz).to(gpu), sizes, 700).cpu().numpy()
+    np.testing.assert_array_equal(got, sample_fps(xyz, sizes, 700))

@@ -3,9 +3,9 @@ lib/filtering/oanet.py:96-129 on the same inputs, including ragged sizes (N and 
 multiples, pair counts not a multiple of the 8-pair XCD group), the per-tile InstanceNorm
 partials, and the whole OANet block with the fused path on vs off.
 
-Tolerance: the kernels compute in fp32 with split MFMA products — split-bf16 (three bf16 terms, 6 MFMAs) or the
-default split-fp16 (two fp16 terms, 22 significant bits, 3 MFMAs; mvr_set_attn_math) — so outputs are compared to
-fp64 at 2e-5 relative to the output scale.  Operands outside the fp16 range send a split-fp16 launch to its
+Tolerance: the kernels compute in fp32 with split MFMA products — the default split-bf16 (three bf16 terms,
+6 MFMAs: fp32-equivalent operands) or the opt-in split-fp16 (two fp16 terms, 22 significant bits, 3 MFMAs;
+mvr_set_attn_math(1)) — so outputs are compared to fp64 at 2e-5 relative to the output scale.  Operands outside the fp16 range send a split-fp16 launch to its
 split-bf16 re-run: the outputs are then bit-identical to a split-bf16 launch."""
 import os
 
@@ -347,9 +347,9 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
     (fp32 itself lands up to 2e-4 from exact arithmetic, and either GPU path up to ~1.6e-4 from the fp32
     oracle on pairs where fp32 and fp64 happen to agree: tools/diag_fold2.py; the two GPU paths differ
     only by fp32 rounding of x and its statistics), so the folded path must be as close to the fp64 oracle
-    as the materialised path or the fp32 oracle is (within 3x), or within 2e-4 of it (the split-fp16 attention
-    carries 22-bit operands: on the most sensitive pair (1200 points, train mode) the folded path lands 1.7e-4
-    from fp64 where the fp32 oracle is 1.7e-5 away and the materialised path 5e-5).  (The materialised path's own parity: the golden and oracle tests of test_gpu_oanet.py.)  Below ~100 points the Procrustes is
+    as the materialised path or the fp32 oracle is (within 3x), or within the north star's 1e-4 of it (round 2's
+    2e-4 allowance was for the then-default split-fp16 attention, 22-bit operands; the default maths are now
+    fp32-equivalent).  (The materialised path's own parity: the golden and oracle tests of test_gpu_oanet.py.)  Below ~100 points the Procrustes is
     ill-conditioned for every path (1e-2..1 from fp64 at 33 points: tools/diag_fold.py): block-0 logits
     only.  Eval and train-mode BatchNorm, ragged point counts."""
     import torch
@@ -402,5 +402,5 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
         for k in ("rot_est", "trans_est"):
             f, m = a[k][i].cpu().numpy(), b[k][i].cpu().numpy()
             r32, r64 = o32[k][i], o64[k][i]
-            bound = np.maximum(2e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
+            bound = np.maximum(1e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
             assert (dist(f, r64) <= bound).all(), (i, k, dist(f, r64), dist(m, r64), dist(r32, r64))

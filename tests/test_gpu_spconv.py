@@ -54,7 +54,8 @@ def _run(gpu, Cin, Cout, K, Mout, Min, split, perm=False, epi=True, seed=0, edit
     if perm and nbr is not None:
         ws = torch.empty(L.mvr_kernel_map_order_bytes(Mout), dtype=torch.uint8, device=gpu)
         perm_t = torch.empty(Mout, dtype=torch.int32, device=gpu)
-        NV.check(L.mvr_kernel_map_order(NV.ptr(nbr_t), Mout, K, NV.ptr(perm_t), NV.ptr(ws), ws.numel(), NV.stream()),
+        NV.check(L.mvr_kernel_map_order(NV.ptr(nbr_t), None, 1, Mout, K, NV.ptr(perm_t), NV.ptr(ws), ws.numel(),
+                                         NV.stream()),
                  "order")
     wimg = None
     if split:

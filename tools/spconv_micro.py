@@ -48,27 +48,44 @@ def main():
         NV.check(L.mvr_spconv_wimage(NV.ptr(W), 27, cin, cout, NV.ptr(wimg), nb, NV.stream()), "wimage")
         bn = NV.BnP(None, None, None, None)
         act = (nbr >= 0).sum().item()
+        out_c = cm.coords_at(2 * s if kind == "down" else s)
+        step = 2 * s if kind == "down" else s
+        mask = ((nbr >= 0).to(torch.int64) << torch.arange(27, device=dev)).sum(1)
+        q = (out_c[:, 1:].to(torch.int64) // step) & 511
+        mort = torch.zeros_like(mask)
+        for b in range(9):
+            for ax in range(3):
+                mort |= ((q[:, ax] >> b) & 1) << (3 * b + 2 - ax)
+        mort |= (out_c[:, 0].to(torch.int64) & 31) << 27
+        orders = {"none": None,
+                  "mask": torch.argsort(mask, stable=True).to(torch.int32),
+                  "mask+morton": perm,
+                  "morton": torch.argsort(mort, stable=True).to(torch.int32),
+                  "frag+mask": torch.argsort(((out_c[:, 0].to(torch.int64) & 31) << 32) | mask, stable=True).to(torch.int32)}
         res = {}
-        for name, wi in (("f32", None), ("bx", wimg)):
-            def go():
-                NV.check(L.mvr_spconv(NV.ptr(x), cin, cin, NV.ptr(nbr), NV.ptr(perm), 27, Mout, NV.ptr(W), cout, None,
-                                      bn, 1e-5, None, 0, 0, NV.ptr(out), cout, NV.ptr(wi),
-                                      NV.ptr(NV.flag_word()) if wi is not None else None, NV.stream()), "spconv")
-            for _ in range(2):
-                go()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            e0.record()
-            for _ in range(a.iters):
-                go()
-            e1.record()
-            torch.cuda.synchronize()
-            res[name] = e0.elapsed_time(e1) / a.iters
+        for oname, pm in orders.items():
+            for xcd in (0, 1):
+                L.mvr_set_spconv_xcd(xcd)
+
+                def go():
+                    NV.check(L.mvr_spconv(NV.ptr(x), cin, cin, NV.ptr(nbr), NV.ptr(pm), 27, Mout, NV.ptr(W), cout, None,
+                                          bn, 1e-5, None, 0, 0, NV.ptr(out), cout, NV.ptr(wimg), None, NV.stream()),
+                             "spconv")
+                for _ in range(2):
+                    go()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(a.iters):
+                    go()
+                e1.record()
+                torch.cuda.synchronize()
+                res["%s/x%d" % (oname, xcd)] = e0.elapsed_time(e1) / a.iters
+        L.mvr_set_spconv_xcd(1)
         fl = 2.0 * act * cin * cout
-        gb = act * cin * 4.0
-        print("%-16s Mout %7d  active/row %.1f  f32 %.3f ms  bx %.3f ms  (useful %.1f / %.1f TF/s, gather %.2f / %.2f TB/s)"
-              % (tag, Mout, act / Mout, res["f32"], res["bx"], fl / res["f32"] / 1e9, fl / res["bx"] / 1e9,
-                 gb / res["f32"] / 1e9, gb / res["bx"] / 1e9), flush=True)
+        print("%-16s Mout %7d active/row %.1f  %s   (useful TF/s at best %.1f)" % (
+            tag, Mout, act / Mout, "  ".join("%s %.3f" % kv for kv in res.items()), fl / min(res.values()) / 1e9),
+            flush=True)
 
 
 if __name__ == "__main__":
