@@ -118,35 +118,53 @@ struct FpsSlot {
   int k, pad0, pad1, pad2;
 };
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// squared distances of two points at once on packed fp32 (v_pk_add_f32 / v_pk_mul_f32: two lanes of IEEE
+// round-to-nearest arithmetic per instruction; contraction off, so each op rounds exactly like fps_d2's)
+__device__ __forceinline__ f32x2 fps_d2x2(f32x2 px, f32x2 py, f32x2 pz, f32x2 lx, f32x2 ly, f32x2 lz) {
+#pragma clang fp contract(off)
+  const f32x2 dx = px - lx, dy = py - ly, dz = pz - lz;
+  return (dx * dx + dy * dy) + dz * dz;
+}
+
 template <int T, int PER>
 __global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xyz, const int64_t* __restrict__ off,
                                                     int m, int64_t* __restrict__ idx_out) {
-  constexpr int NW = T / 64;
+  static_assert(PER % 2 == 0, "points are processed in pairs");
+  constexpr int NW = T / 64, P2 = PER / 2;
   __shared__ FpsSlot slot[2][NW];
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t s0 = off[f];
   const int n = (int)(off[f + 1] - s0);
   const float* p = xyz + s0 * 3;
-  float px[PER], py[PER], pz[PER], d[PER];
+  // point j of this thread: index tid + j T, held in pair j / 2, component j % 2
+  f32x2 px[P2], py[P2], pz[P2], d[P2];
 #pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int k = tid + j * T;
-    const bool ok = k < n;
-    px[j] = ok ? p[3 * k] : 0.f;
-    py[j] = ok ? p[3 * k + 1] : 0.f;
-    pz[j] = ok ? p[3 * k + 2] : 0.f;
-    d[j] = ok ? __builtin_inff() : -1.f;   // absent points never win
+  for (int j2 = 0; j2 < P2; ++j2) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int k = tid + (2 * j2 + e) * T;
+      const bool ok = k < n;
+      px[j2][e] = ok ? p[3 * k] : 0.f;
+      py[j2][e] = ok ? p[3 * k + 1] : 0.f;
+      pz[j2][e] = ok ? p[3 * k + 2] : 0.f;
+      d[j2][e] = ok ? __builtin_inff() : -1.f;   // absent points: min(-1, distance) stays -1, never the best
+    }
   }
   int64_t* out = idx_out + (int64_t)f * m;
   if (tid == 0) out[0] = s0;
-  float lx = p[0], ly = p[1], lz = p[2];
+  f32x2 lx = {p[0], p[0]}, ly = {p[1], p[1]}, lz = {p[2], p[2]};
   for (int it = 1; it < m; ++it) {
     float bd = -2.f;
     int bj = 0;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      d[j] = fminf(d[j], d[j] >= 0.f ? fps_d2(px[j], py[j], pz[j], lx, ly, lz) : -1.f);
-      if (d[j] > bd) { bd = d[j]; bj = j; }
+    for (int j2 = 0; j2 < P2; ++j2) {
+      const f32x2 dd = fps_d2x2(px[j2], py[j2], pz[j2], lx, ly, lz);
+      d[j2][0] = fminf(d[j2][0], dd[0]);
+      d[j2][1] = fminf(d[j2][1], dd[1]);
+      if (d[j2][0] > bd) { bd = d[j2][0]; bj = 2 * j2; }
+      if (d[j2][1] > bd) { bd = d[j2][1]; bj = 2 * j2 + 1; }
     }
     const float wm = wave_max_uniform(bd);
     uint64_t cand = __ballot(bd == wm);
@@ -158,13 +176,14 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xy
       cand = __ballot(bd == wm && mk == km);
     }
     const int wl = __ffsll((unsigned long long)cand) - 1;
-    if (lane == wl) {   // the winner's coordinates: a select over its registers
-      float x = px[0], y = py[0], z = pz[0];
+    if (lane == wl) {   // the winner's point: a select over its registers (one lane: the rest are masked)
+      f32x2 x2 = px[0], y2 = py[0], z2 = pz[0];
 #pragma unroll
-      for (int j = 1; j < PER; ++j)
-        if (bj == j) { x = px[j]; y = py[j]; z = pz[j]; }
+      for (int j2 = 1; j2 < P2; ++j2)
+        if ((bj >> 1) == j2) { x2 = px[j2]; y2 = py[j2]; z2 = pz[j2]; }
+      const int e = bj & 1;
       FpsSlot& sl = slot[it & 1][wid];
-      sl.d = wm; sl.k = mk; sl.x = x; sl.y = y; sl.z = z;
+      sl.d = wm; sl.k = mk; sl.x = e ? x2[1] : x2[0]; sl.y = e ? y2[1] : y2[0]; sl.z = e ? z2[1] : z2[0];
     }
     __syncthreads();
     float gd = -3.f;
@@ -175,7 +194,8 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xy
       const int kw = slot[it & 1][w].k;
       if (dw > gd || (dw == gd && kw < gk)) { gd = dw; gk = kw; gw = w; }
     }
-    lx = slot[it & 1][gw].x; ly = slot[it & 1][gw].y; lz = slot[it & 1][gw].z;
+    const float nx = slot[it & 1][gw].x, ny = slot[it & 1][gw].y, nz = slot[it & 1][gw].z;
+    lx = f32x2{nx, nx}; ly = f32x2{ny, ny}; lz = f32x2{nz, nz};
     if (tid == 0) out[it] = s0 + gk;
   }
 }
@@ -212,6 +232,8 @@ extern "C" int mvr_fps(const float* xyz, const int64_t* offsets, const int64_t* 
   MVR_FPSR(1024, 8)
   MVR_FPSR(1024, 16)
   MVR_FPSR(1024, 20)
+  MVR_FPSR(1024, 24)
+  MVR_FPSR(768, 32)
   MVR_FPSR(512, 48)
 #undef MVR_FPSR
   MVR_FPS(1024, 64, false)

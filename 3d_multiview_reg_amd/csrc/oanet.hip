@@ -475,7 +475,7 @@ struct Ctx {
     finalize_in(x, 1e-5f, pc.bn1);
     Act t{pl.T1, (int64_t)y.C * pl.Np, pl.Np, y.C, pl.N, pl.stT, y.C, 0};
     const bool sc = pc.shortcut.weight != nullptr;
-    if (pl.fused_pcn && !sc && x.C == pl.C && y.C == pl.C && y.st_off + pl.C <= y.st_ld) {
+    if (pl.fused_pcn && !sc && !head && x.C == pl.C && y.C == pl.C && y.st_off + pl.C <= y.st_ld) {
       // statistics-only conv3 -> fold of t -> fused conv3 . IN/BN/ReLU . conv7 + x
       Act ts = t;
       ts.p = nullptr;
@@ -618,7 +618,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   f3.stats_mode = ST_ROW; f3.stats = pl.stT; f3.st_ld = C; f3.st_off = 0;
   f3.xin = 1; f3.xci = Cin; f3.xw = pl.W8; f3.xb = blk->conv1.bias; f3.xld = ld;
   f3.prof_kind = PK_CONV_PTS;
-  const bool fold1 = (g_oan_fused & 4) && !pl.fused_pcn && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
+  const bool fold1 = (g_oan_fused & 4) && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
                      pconv_covers(f3);
   if (fold1) {
     const int n8 = C * 8;
@@ -731,7 +731,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   probe.math = g_default_math; probe.M = C; probe.N = N; probe.K = C; probe.batch = P; probe.pro = PRO_B_K;
   probe.has_res = 1; probe.bias_mode = BIAS_M; probe.head_w = blk->output.weight;
   probe.no_store = latent ? 0 : 1;   // a block whose activation is not returned keeps only the head's output
-  const bool fuse_head = !pl.fused_pcn && pconv_covers(probe);   // (the fused-PointCN experiment keeps the head kernel)
+  const bool fuse_head = pconv_covers(probe);   // (that PointCN then stays on the conv3 + conv7 pair)
   for (int i = 0; i < H; ++i) {
     if (fuse_head && i == H - 1) {
       cx.head = &blk->output;

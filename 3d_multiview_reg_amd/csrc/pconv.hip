@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
     float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + n0 + ec0;
     const bool full = n0 + CH <= N;   // uniform: every column of the chunk is valid
-    if (HEAD != 2) {
+    if (HEAD != 2 && a.Y) {   // (a.Y null: a statistics-only pass)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (full || n0 + ec0 < N4) {
@@ -650,7 +650,8 @@ bool pconv_covers(const GemmArgs& g) {
     return ok && ((g.xin == 1 && !g.has_res) || (g.xin == 2 && g.has_res));
   }
   if (g.head_w && g.stats_mode != ST_NONE) return false;
-  if (g.no_store && !g.head_w) return false;   // statistics-only passes stay on gemm_kernel
+  // statistics-only passes (the fused PointCN's conv3 pass): 128 -> 128 with the prologue, no residual
+  if (g.no_store && !g.head_w && !(g.stats_mode == ST_ROW && !g.has_res && g.K == PC && g.pro == PRO_B_K)) return false;
   if (g.K == 2 * PC && (g.has_res || g.head_w)) return false;   // KS = 16 runs the 256 -> 128 convs only
   return g_pconv && g.math == MATH_BF16X3 && g.M == PC && (g.K == PC || g.K == 2 * PC) && !g.bkc && g.sAb == 0 &&
          (g.pro == PRO_NONE || g.pro == PRO_B_K) && (g.stats_mode == ST_NONE || g.stats_mode == ST_ROW) &&

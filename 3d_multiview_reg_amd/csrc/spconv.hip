@@ -480,7 +480,7 @@ __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin
 #define SPCONV_MATH_DEFAULT 0
 #endif
 int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_spconv_math
-int g_spconv_xcd = 1;                   // mvr_set_spconv_xcd
+int g_spconv_xcd = 0;                   // mvr_set_spconv_xcd (0: load-balanced round robin measured faster)
 
 }  // namespace mvr
 

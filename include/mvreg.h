@@ -373,8 +373,10 @@ int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_
    split-bf16 re-run of a launch that saw one outside it; split-bf16 directly when the output is the residual).
    Returns the previous setting. */
 int mvr_set_spconv_math(int h);
-/* tile order of mvr_spconv's split kernels: 1 (default) XCD-contiguous (the workgroups one XCD runs together take
-   neighbouring tiles of the row order), 0 round-robin dispatch order (A/B timing).  Returns the previous setting. */
+/* tile order of mvr_spconv's split kernels: 0 (default) round-robin dispatch order, 1 XCD-contiguous (the
+   workgroups one XCD runs together take neighbouring tiles of the row order: measured slower, up to 1.5x on the
+   transposed convs, whose mask-sorted tiles differ in cost — one XCD gets all the expensive ones; A/B timing).
+   Returns the previous setting. */
 int mvr_set_spconv_xcd(int on);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
