@@ -133,6 +133,7 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xy
                                                     int m, int64_t* __restrict__ idx_out) {
   static_assert(PER % 2 == 0, "points are processed in pairs");
   constexpr int NW = T / 64, P2 = PER / 2;
+  static_assert(NW <= 16, "the slot reduction runs in one DPP row");
   __shared__ FpsSlot slot[2][NW];
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t s0 = off[f];
@@ -186,14 +187,18 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xy
       sl.d = wm; sl.k = mk; sl.x = e ? x2[1] : x2[0]; sl.y = e ? y2[1] : y2[0]; sl.z = e ? z2[1] : z2[0];
     }
     __syncthreads();
-    float gd = -3.f;
-    int gk = 0x7fffffff, gw = 0;
+    // every wave reduces the NW slots itself, lane-parallel: lane i (< NW) reads slot i; max distance over the
+    // lanes, then the lowest index among the lanes holding it; the winner's coordinates: three uniform reads
+    const bool sv = lane < NW;
+    const float dw = sv ? slot[it & 1][lane].d : -3.f;
+    const int kw = sv ? slot[it & 1][lane].k : 0x7fffffff;
+    const float gm = row_max16(dw);   // NW <= 16: the slots sit in lanes 0..15 (one DPP row)
+    const float gd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gm), 0));
+    int kk = (sv && dw == gd) ? kw : 0x7fffffff;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const float dw = slot[it & 1][w].d;
-      const int kw = slot[it & 1][w].k;
-      if (dw > gd || (dw == gd && kw < gk)) { gd = dw; gk = kw; gw = w; }
-    }
+    for (int o = 8; o >= 1; o >>= 1) kk = min(kk, __shfl_xor(kk, o, 64));
+    const int gk = __builtin_amdgcn_readlane(kk, 0);
+    const int gw = __ffsll((unsigned long long)__ballot(sv && dw == gd && kw == gk)) - 1;
     const float nx = slot[it & 1][gw].x, ny = slot[it & 1][gw].y, nz = slot[it & 1][gw].z;
     lx = f32x2{nx, nx}; ly = f32x2{ny, ny}; lz = f32x2{nz, nz};
     if (tid == 0) out[it] = s0 + gk;

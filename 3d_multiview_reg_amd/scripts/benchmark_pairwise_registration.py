@@ -7,7 +7,8 @@ report), with the per-pair host loop replaced by batched GPU calls:
     inliers (scores > 0.5, benchmark:209-212);
   * method RANSAC: batched GPU RANSAC over all correspondences of a batch (benchmark:56-133);
   * T_est = inv(estimate), overlap flag = compute_overlap_ratio(xyz1, xyz2, T_est) >= 0.3 (3DMatch) / 0.23
-    (Redwood) on the GPU (lib/overlap.py), trajectories written per scene (benchmark:222-245, with the
+    (Redwood) on the GPU (lib/overlap.py; every pair of a loader batch in one FragmentOverlap.ratios call),
+    trajectories written per scene (benchmark:222-245, with the
     bool-flag fix of lib/utils.py write_trajectory), then precision / recall / rotation and translation
     errors per scene against gt.log / gt.info (benchmark:250-345).
 Optional reference dependencies that are absent here (open3d, coloredlogs, matplotlib) are not needed.
@@ -32,10 +33,11 @@ if _PKG not in sys.path:
 
 from lib.utils import (ensure_dir, read_trajectory, write_trajectory, read_trajectory_info,  # noqa: E402
                        get_folder_list, Timer, rotation_error, translation_error, load_config,
-                       evaluate_registration, compute_overlap_ratio, extract_corresponding_trajectors,
+                       evaluate_registration, extract_corresponding_trajectors,
                        run_ransac_batch)
 from scripts.utils import make_pairwise_eval_data_loader  # noqa: E402
 from lib.checkpoints import CheckpointIO  # noqa: E402
+from lib.overlap import FragmentOverlap  # noqa: E402
 import lib.config as config  # noqa: E402
 
 SHORT_NAMES = {
@@ -113,13 +115,17 @@ def estimate_trans_params(eval_data, source_path, dataset, scene_info, method, m
                 T = np.tile(np.eye(4), (len(R), 1, 1))
                 T[:, :3, :3], T[:, :3, 3] = R, t
         timer.toc()
+        # the overlap gate of every pair of the batch in one call (benchmark:217-220 scores one pair at a time on
+        # the CPU): the batch's 2B clouds indexed once on the GPU, pair k = clouds (2k, 2k + 1)
+        T_est = np.linalg.inv(T)
+        clouds = [c for k in range(T.shape[0]) for c in (batch["xyz1"][k][0], batch["xyz2"][k][0])]
+        ratios = FragmentOverlap(clouds, method=overlap_method).ratios(
+            [[2 * k, 2 * k + 1] for k in range(T.shape[0])], list(T_est)) if T.shape[0] else []
         for k in range(T.shape[0]):
-            T_est = np.linalg.inv(T[k])
             pair_idx = int(batch["idx"][k].numpy().item())
             meta = batch["metadata"][k]
-            ratio = compute_overlap_ratio(batch["xyz1"][k][0], batch["xyz2"][k][0], T_est, method=overlap_method)
-            est[4 * pair_idx:4 * pair_idx + 4, :] = T_est
-            reg_metadata.append([str(int(meta[1])), str(int(meta[2])), bool(ratio >= overlap_threshold)])
+            est[4 * pair_idx:4 * pair_idx + 4, :] = T_est[k]
+            reg_metadata.append([str(int(meta[1])), str(int(meta[2])), bool(ratios[k] >= overlap_threshold)])
     if num_pairs:
         logging.info("%d pairwise registration parameters estimated in %.3fs (%.4fs per batch of pure run time)",
                      num_pairs, full.toc(average=False), timer.avg)
