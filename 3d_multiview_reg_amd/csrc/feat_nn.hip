@@ -36,9 +36,6 @@ constexpr int NN_STAGE = 128;      // targets per LDS stage
 constexpr int NN_ROW = 32;         // bf16 per LDS plane row; 16-byte chunk c of row r sits at slot
                                    // c ^ ((r >> 2) & 3): conflict-free ds_read_b128 down 16 rows
 constexpr float NN_NEG = -3.0e38f;
-#ifndef NN_ABL
-#define NN_ABL 0   // timing ablations of the fast path (wrong results): 1 no MFMA, 2 no softmax, 4 no staging
-#endif
 
 struct NNArgs {
   const float* Fq; int64_t fq_fs;    // query features [*][Nq][32], fragment stride (elements)
@@ -459,11 +456,6 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       if (H) {
         const f16x8 th = *reinterpret_cast<const f16x8*>(&Fp[cur][0][row][c]);
         const f16x8 tl = *reinterpret_cast<const f16x8*>(&Fp[cur][1][row][c]);
-        if (NN_ABL & 1) {
-          asm volatile("" ::"v"(th), "v"(tl));
-          acc[s] += 1.f;
-          continue;
-        }
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(q16l[s], th, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(q16h[s], tl, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(q16h[s], th, acc, 0, 0, 0);
@@ -472,11 +464,6 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       const bf16x8 th = *reinterpret_cast<const bf16x8*>(&Fp[cur][0][row][c]);
       const bf16x8 tm = *reinterpret_cast<const bf16x8*>(&Fp[cur][1][row][c]);
       const bf16x8 tl = *reinterpret_cast<const bf16x8*>(&Fp[cur][2][row][c]);
-      if (NN_ABL & 1) {
-        asm volatile("" ::"v"(th), "v"(tm), "v"(tl));
-        acc[s] += 1.f;
-        continue;
-      }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ql[s], th, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qh[s], tl, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qm[s], tm, acc, 0, 0, 0);

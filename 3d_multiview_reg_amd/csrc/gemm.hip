@@ -59,7 +59,6 @@ __device__ unsigned long long g_gemm_trace[8];
 #define TSTAMP(slot) do {} while (0)
 #endif
 
-int g_default_math = MATH_BF16X3;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -68,12 +67,9 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // Which 16-byte chunk q (4 consecutive k of the 32-k stage) lane half h reads as its s4-th
-// register.  f32 MFMA 32x32x2: step (s4, e) takes k = 4(2 s4 + h) + e.  bf16 32x32x16: step st
-// takes k = 16 st + 8h + j, i.e. chunks 4st + 2h and 4st + 2h + 1 as registers 2st, 2st + 1.
-template <int MATH>
-__device__ __forceinline__ int chunk_of(int s4, int h) {
-  return MATH == MATH_F32 ? 2 * s4 + h : 4 * (s4 >> 1) + 2 * h + (s4 & 1);
-}
+// register: the 32x32x16 MFMA step st takes k = 16 st + 8h + j, i.e. chunks 4st + 2h and 4st + 2h + 1 as
+// registers 2st, 2st + 1.
+__device__ __forceinline__ int chunk_of(int s4, int h) { return 4 * (s4 >> 1) + 2 * h + (s4 & 1); }
 
 constexpr int BM = GEMM_BM, BN = GEMM_BN, BK = GEMM_BK;
 constexpr int KV_MAX = 512;        // max K with a per-k prologue vector held in LDS
@@ -185,16 +181,8 @@ __device__ __forceinline__ f32x2 unpack_bf16(unsigned p) {
   r.y = __uint_as_float(p & 0xffff0000u);
   return r;
 }
-#ifndef GEMM_ABL
-#define GEMM_ABL 0   // ablation bits (timing only, wrong results): 1 = single-term split, 2 = one MFMA per product
-#endif
 __device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& H, u32x4& Mm, u32x4& L) {
   const f32x2 x[4] = {{a.x, a.y}, {a.z, a.w}, {b.x, b.y}, {b.z, b.w}};
-  if (GEMM_ABL & 1) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) H[i] = Mm[i] = L[i] = cvt_pk_bf16(x[i]);
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const unsigned hp = cvt_pk_bf16(x[i]);
@@ -800,7 +788,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     f32x2 bkr[2][4][2];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      const int q = chunk_of<MATH>(s4, kh);   // 16-byte chunk (4 consecutive k) of this lane half
+      const int q = chunk_of(s4, kh);   // 16-byte chunk (4 consecutive k) of this lane half
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         const int x = wm * 64 + ii * 32 + l32;
@@ -840,7 +828,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
     TSTAMP(3);
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
-      const int kb = k0 + 4 * chunk_of<MATH>(s4, kh);
+      const int kb = k0 + 4 * chunk_of(s4, kh);
       if (PRO == PRO_A_K || PRO == PRO_B_K) {
         const float4 sc4 = *reinterpret_cast<const float4*>(vsc + kb);
         const float4 sh4 = *reinterpret_cast<const float4*>(vsh + kb);
@@ -863,18 +851,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
           for (int e = 0; e < 4; ++e) f4(b4[j][s4], e) *= fm[j];
       }
     }
-    if (MATH == MATH_F32) {
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4(a4[ii][s4], e), f4(b4[j][s4], e), acc[ii][j], 0,
-                                                                0, 0);
-    } else if (MATH == MATH_F16X2) {
+    if (MATH == MATH_F16X2) {
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         bx::FragT<1> fa[2], fb[2];
@@ -919,10 +896,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             // small terms first
-            if (GEMM_ABL & 2) {
-              acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bh[j], acc[ii][j], 0, 0, 0);
-              continue;
-            }
             acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[ii], bh[j], acc[ii][j], 0, 0, 0);
             acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[ii], bl[j], acc[ii][j], 0, 0, 0);
             acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[ii], bm[j], acc[ii][j], 0, 0, 0);
@@ -977,10 +950,6 @@ template <int PRO, int BKC, int BIAS, int STATS, int RES>
 static void launch_t(const KArgs& ka0, long long tiles, hipStream_t s) {
   KArgs ka = ka0;
   const unsigned wgs = (unsigned)(tiles < ka.persist ? tiles : ka.persist);
-  if (ka.g.math == MATH_F32) {
-    hipLaunchKernelGGL((gemm_kernel<MATH_F32, PRO, BKC, BIAS, STATS, RES>), dim3(wgs), dim3(256), 0, s, ka);
-    return;
-  }
   // split-fp16 first when the caller provides a zeroed flag word, unless the output is an operand or the residual
   // (in place: the re-run reads them).  Outputs never partially overlap inputs (launch_gemm contract), so the test is
   // pointer equality — a property of the call, not of where the allocator placed the buffers.
@@ -1008,7 +977,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   if (g.stats_mode != ST_NONE && !g.stats) return MVR_EINVAL;
   if (g.bias_mode != BIAS_NONE && !g.bias) return MVR_EINVAL;
   if (g.has_res && !g.R) return MVR_EINVAL;
-  if (g.math != MATH_F32 && g.math != MATH_BF16X3) return MVR_EINVAL;
+  if (g.math != MATH_BF16X3) return MVR_EINVAL;
   // layout contract (gemm.hpp)
   const int64_t K4 = round4(g.K), N4 = round4(g.N);
   bool ok = al16(g.A) && al16(g.B) && al16(g.C) && g.lda % 4 == 0 && g.ldb % 4 == 0 && g.ldc % 4 == 0 &&
@@ -1101,8 +1070,3 @@ extern "C" int mvr_set_gemm_f16(int on) {
   return prev;
 }
 
-extern "C" int mvr_set_gemm_math(int math) {
-  if (math != mvr::MATH_F32 && math != mvr::MATH_BF16X3) return MVR_EINVAL;
-  mvr::g_default_math = math;
-  return MVR_OK;
-}

@@ -28,15 +28,13 @@ enum Stats : int {
                   //                                                           -> train-mode BN over m
 };
 
-// Arithmetic of the MFMA main loop.  MATH_F32: v_mfma_f32_32x32x2_f32 (an exact fp32 fma chain).
-// MATH_BF16X3: each fp32 operand split into three bf16 terms (x = h + m + l to 2^-25 |x|) and the
+// Arithmetic of the MFMA main loop.  MATH_BF16X3 (the only value a caller passes): each fp32 operand split into three bf16 terms (x = h + m + l to 2^-25 |x|) and the
 // six products hh, hm, mh, mm, hl, lh accumulated in fp32 by v_mfma_f32_32x32x16_bf16 — fp32-level
 // accuracy (the dropped ml, lm, ll terms are <= 2^-23 relative) at 6/16 of the fp32 MFMA cycles.
 // MATH_F16X2 (internal): two-term split-fp16 (mfma_bf16.hpp) of A x 2^6 and B x 2^6, 3 MFMAs per product; what a
 // MATH_BF16X3 launch runs first when mvr_set_gemm_f16 is on, with a guarded MATH_BF16X3 re-run when an operand
 // left the split-fp16 window (gemm.hip launch_t).
-enum Math : int { MATH_F32 = 0, MATH_BF16X3 = 1, MATH_F16X2 = 2 };
-extern int g_default_math;   // used by the OANet orchestrator (mvr_set_gemm_math)
+enum Math : int { MATH_BF16X3 = 1, MATH_F16X2 = 2 };
 extern int g_gemm_h;         // mvr_set_gemm_f16
 extern int g_pconv_h;        // mvr_set_pconv_math
 
@@ -54,7 +52,7 @@ struct GemmArgs {
   float2* stats; int64_t st_ld; int st_off;            // partial statistics (see Stats)
   int pro, bias_mode, stats_mode, has_res;
   int prof_kind;                                       // ProfKind tag (prof.hpp); 0 by default
-  int math;                                            // Math (MATH_F32 = 0 by default)
+  int math;                                            // Math: MATH_BF16X3 (anything else is MVR_EINVAL)
   int no_store;                                        // 1: statistics only, C is not written (may be null)
   // output head fused into the epilogue (pconv only, M = 128): logits[b*N + n] = head_w . C(:, n) + head_bp[0] (nullable),
   // scores = relu(tanh(logits)), pos[b] += #positive scores (oanet.py:163,174-178)

@@ -98,10 +98,6 @@ __device__ __forceinline__ bool v_row_bad(float rmax) { return !(rmax < F16_RANG
       __builtin_amdgcn_sched_group_barrier(0x200, 1, 0); \
     }                                               \
   } while (0)
-#ifndef ATTN_ABL
-#define ATTN_ABL 0   // pool timing ablations (wrong results; tools/build_variant.sh): 1 no softmax, 2 no
-                     // tile split, 4 no P.V MFMAs, 8 no S MFMAs
-#endif
 
 // Byte offset of the 4 keys 4q .. 4q+3 (q = 0..7) of row `row` in a [row][32 keys] bf16 image
 // whose 16-byte chunk (s, h) holds the 8 keys of k-step s, lane half h in the C-register k order
@@ -349,7 +345,6 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     return x;
   };
   auto store_v = [&](int st, int i, float4 x) {
-    if (ATTN_ABL & 2) return;
     asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));   // keep the split at its placement
     char* V = smem + st * STAGET + IMGT;
     const int c = (tid >> 3) + 64 * i;
@@ -361,7 +356,6 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     if (H) vmax[i] = fmaxf(fmaxf(vmax[i], fmaxf(fabsf(x.x), fabsf(x.y))), fmaxf(fabsf(x.z), fabsf(x.w)));
   };
   auto store_k = [&](int st, int i, float4 x, const float2& f) {
-    if (ATTN_ABL & 2) return;
     asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w));
     char* K = smem + st * STAGET;
     const int c = (tid >> 3) + 64 * i;
@@ -434,10 +428,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       if (ks == 2) store_v(st ^ 1, 0, x0);
       if (ks == 5) store_k(st ^ 1, 0, x0, ssh[tid >> 3]);
       if (ks == 6) x1 = load_x(kb + 1, 1);
-      if (ATTN_ABL & 8)
-        asm volatile("" ::"v"(cur.p[0]), "v"(cur.p[1]));
-      else
-        S = mma<H>(cur, q[ks], S);
+      S = mma<H>(cur, q[ks], S);
       if (ks == 2 || ks == 5) {
         if (H) ATTN_INTERLEAVE3(); else ATTN_INTERLEAVE6();
       }
@@ -453,7 +444,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       for (int r = 0; r < 16; ++r)
         if (kb * AKB + (r & 3) + 8 * (r >> 2) + 4 * h >= N) v[r] = -__builtin_inff();
     }
-    if (!(ATTN_ABL & 1)) online_softmax<H ? 7 : 0>(v, m, l, O);
+    online_softmax<H ? 7 : 0>(v, m, l, O);
     FragT<H> pf[2] = {split8t<H>(v), split8t<H>(v + 8)};
     // O[c][j] += sum_n x[c][n] P[n][j]
 #pragma unroll
@@ -464,10 +455,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       SCHED_FENCE();
       if (i == 2) store_v(st ^ 1, 1, x1);
       if (i == 5) store_k(st ^ 1, 1, x1, ssh[(tid >> 3) + 64]);
-      if (ATTN_ABL & 4)
-        asm volatile("" ::"v"(vf.p[0]), "v"(vf.p[1]), "v"(pf[s].p[0]), "v"(pf[s].p[1]));
-      else
-        O[cb] = mma<H>(vf, pf[s], O[cb]);
+      O[cb] = mma<H>(vf, pf[s], O[cb]);
       if (i == 2 || i == 5) {
         if (H) ATTN_INTERLEAVE3(); else ATTN_INTERLEAVE6();
       }
@@ -756,7 +744,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kb = 0; kb < ((ATTN_ABL & 16) ? 0 : nkb); ++kb) {
+  for (int kb = 0; kb < nkb; ++kb) {
     const int st = kb & 1;
     if (kb + 1 < nkb) issue(kb + 1, st ^ 1);
     const char* Wi = smem + st * USTAGE;
@@ -778,10 +766,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
       Frag nxt;
       if (ks < 7) nxt = read_w(Wi, ks + 1);
       SCHED_FENCE();
-      if (ATTN_ABL & 8)
-        asm volatile("" ::"v"(cur.h), "v"(cur.m), "v"(cur.l));
-      else
-        S = mfma6(cur, q[ks], S);
+      S = mfma6(cur, q[ks], S);
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
@@ -789,7 +774,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = S[r];
-    if (!(ATTN_ABL & 1)) online_softmax(v, m, l, O);
+    online_softmax(v, m, l, O);
     Frag pf[2];
     split8(v, pf[0].h, pf[0].m, pf[0].l);
     split8(v + 8, pf[1].h, pf[1].m, pf[1].l);

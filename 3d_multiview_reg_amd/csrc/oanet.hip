@@ -258,8 +258,8 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
-int g_oan_fused = 5;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 1 PointCN (off: not faster yet),
-                       // bit 2 conv1 folded into the first PointCN (point-conv XI variants)
+int g_oan_fused = 5;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 2 conv1 folded into the first PointCN
+                       // (point-conv XI variants); bit 1 is unused
 int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B timing)
 
 namespace {
@@ -323,8 +323,6 @@ struct Act {
   int tw1 = 128;              // ... and of channels [csplit, C)
 };
 
-constexpr int PCN_TILE = 32;   // statistics tile of the fused PointCN (pointcn.hip)
-
 struct Ws {
   char* base;
   size_t off, cap;
@@ -341,11 +339,10 @@ struct Plan {
   int P, N, C, Kc, Cin;
   int64_t Np, Kp, Cinp;  // padded row lengths (points, clusters, conv1 input channels)
   bool fused;            // diff_pool / diff_unpool as fused attention kernels (oan_attn.hip)
-  bool fused_pcn;        // PointCN(C -> C) as statistics-only conv3 + fused kernel (pointcn.hip)
   char* uimg;            // their split-bf16 operand images
   size_t uimg_bytes;
   size_t bytes;
-  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *sc2, *sh2, *scK, *shK, *fac, *W1, *W8;
+  float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *fac, *W1, *W8;
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
   int* flags;            // FLAG_SLOTS range flags of the split-fp16 launches (zeroed at the block's start)
 };
@@ -364,8 +361,7 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc; pl.Cin = Cin;
   pl.Np = round32(N); pl.Kp = round32(Kc); pl.Cinp = round4(Cin);
   pl.fused = (g_oan_fused & 1) && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
-  pl.fused_pcn = (g_oan_fused & 2) && C == 128;
-  const int TS = pl.fused_pcn ? (N + PCN_TILE - 1) / PCN_TILE : gemm_ntiles(N);   // statistics tiles over points
+  const int TS = gemm_ntiles(N);   // statistics tiles over points
   Ws w{reinterpret_cast<char*>(base), 0, 0};
   const size_t PN = (size_t)P * pl.Np, PK = (size_t)P * pl.Kp;
   const int TN = gemm_ntiles(N), TK = gemm_ntiles(Kc), MK = gemm_mtiles(Kc), MC = gemm_mtiles(C);
@@ -378,8 +374,6 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.O2 = w.take<float>(PK * C);
   pl.sc = w.take<float>((size_t)P * 2 * C);
   pl.sh = w.take<float>((size_t)P * 2 * C);
-  pl.sc2 = w.take<float>((size_t)P * C);
-  pl.sh2 = w.take<float>((size_t)P * C);
   pl.scK = w.take<float>(pl.Kp);
   pl.shK = w.take<float>(pl.Kp);
   size_t nf = (size_t)P * TN * pl.Kp;
@@ -455,7 +449,7 @@ struct Ctx {
       g.logits = h_logits; g.scores = h_scores; g.pos = h_pos;
     }
     g.no_store = no_store ? 1 : 0;
-    g.math = g_default_math;
+    g.math = MATH_BF16X3;
     g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
     g.A = w_padded ? w_padded : cv.weight; g.sAb = 0; g.lda = w_padded ? round4(in.C) : in.C;
     g.B = in.p; g.sBb = in.ps; g.ldb = in.ld; g.bkc = 0;
@@ -475,19 +469,6 @@ struct Ctx {
     finalize_in(x, 1e-5f, pc.bn1);
     Act t{pl.T1, (int64_t)y.C * pl.Np, pl.Np, y.C, pl.N, pl.stT, y.C, 0};
     const bool sc = pc.shortcut.weight != nullptr;
-    if (pl.fused_pcn && !sc && !head && x.C == pl.C && y.C == pl.C && y.st_off + pl.C <= y.st_ld) {
-      // statistics-only conv3 -> fold of t -> fused conv3 . IN/BN/ReLU . conv7 + x
-      Act ts = t;
-      ts.p = nullptr;
-      conv(pc.conv3, x, true, ts, nullptr, ST_ROW, nullptr, true);
-      finalize_in(t, 1e-5f, pc.bn5, pl.sc2, pl.sh2);
-      chk(mvr_pointcn_fused(x.p, x.ps, x.ld, y.p, y.ps, y.ld, pl.sc, pl.sh, pl.sc2, pl.sh2, pc.conv3.weight,
-                            pc.conv3.bias, pc.conv7.weight, pc.conv7.bias, pl.P, pl.C, pl.N,
-                            reinterpret_cast<float*>(y.st), y.st_ld, y.st_off, s));
-      y.tw0 = PCN_TILE;
-      y.csplit = 1 << 30;
-      return;
-    }
     y.tw0 = 128;
     y.csplit = 1 << 30;
     const mvr_conv_p* hd = head;   // the head goes with conv7 only
@@ -528,7 +509,7 @@ struct Ctx {
     // out2(c,k') = sum_k relu(bn2_k(o1(c,k))) W2[k'][k] + b2[k'] + o1(c,k')   (conv on the transpose)
     Act o2{pl.O2, (int64_t)C * Kp, Kp, C, Kc, pl.stO, C, 0};
     GemmArgs g{};
-    g.math = g_default_math;
+    g.math = MATH_BF16X3;
     g.M = C; g.N = Kc; g.K = Kc; g.batch = pl.P;
     g.A = pl.O1; g.sAb = (int64_t)C * Kp; g.lda = Kp;
     g.B = f.conv2.weight; g.sBb = 0; g.ldb = Kc; g.bkc = 1;
@@ -565,7 +546,7 @@ extern "C" int mvr_set_pool_split(int on) {
 
 extern "C" int mvr_set_oan_fused(int on) {
   const int prev = g_oan_fused;
-  g_oan_fused = on & 7;
+  g_oan_fused = on & 5;
   return prev;
 }
 
@@ -609,7 +590,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   // recomputed by that PointCN's conv3 (B operand) and conv7 (residual) from the input's <= 8 rows, and
   // for its InstanceNorm statistics (xin_stats_kernel)
   GemmArgs f3{};
-  f3.math = g_default_math; f3.M = C; f3.N = N; f3.K = C; f3.batch = P;
+  f3.math = MATH_BF16X3; f3.M = C; f3.N = N; f3.K = C; f3.batch = P;
   f3.A = blk->l1_1[0].conv3.weight; f3.lda = C;
   f3.B = input; f3.sBb = in_pstride; f3.ldb = ld;
   f3.C = pl.T1; f3.sCb = CN; f3.ldc = Np;
@@ -639,7 +620,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     dbg_hash(pl.sh, P, 1, C, C, 0, s);
     Act& y = (H == 1) ? x11top : xa;
     GemmArgs f7{};
-    f7.math = g_default_math; f7.M = C; f7.N = N; f7.K = C; f7.batch = P;
+    f7.math = MATH_BF16X3; f7.M = C; f7.N = N; f7.K = C; f7.batch = P;
     f7.A = blk->l1_1[0].conv7.weight; f7.lda = C;
     f7.B = pl.T1; f7.sBb = CN; f7.ldb = Np;
     f7.C = y.p; f7.sCb = y.ps; f7.ldc = y.ld;
@@ -676,7 +657,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);
     cx.smx_factors(TN, Kc, Kp);
     GemmArgs g{};
-    g.math = g_default_math;
+    g.math = MATH_BF16X3;
     g.M = C; g.N = Kc; g.K = N; g.batch = P;
     g.A = pl.X11; g.sAb = 2 * CN; g.lda = Np;
     g.B = pl.E; g.sBb = (int64_t)Kc * Np; g.ldb = Np; g.bkc = 1;
@@ -706,7 +687,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     const int MK = gemm_mtiles(Kc);
     cx.smx_factors(MK, N, Np);
     GemmArgs g{};
-    g.math = g_default_math;
+    g.math = MATH_BF16X3;
     g.M = C; g.N = N; g.K = Kc; g.batch = P;
     g.A = pl.XD; g.sAb = (int64_t)C * Kp; g.lda = Kp;
     g.B = pl.E; g.sBb = (int64_t)Kc * Np; g.ldb = Np; g.bkc = 0;
@@ -728,7 +709,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   // point-conv kernel takes it; the guard counts start at zero either way
   if (hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s) != hipSuccess) return MVR_ELAUNCH;
   GemmArgs probe{};
-  probe.math = g_default_math; probe.M = C; probe.N = N; probe.K = C; probe.batch = P; probe.pro = PRO_B_K;
+  probe.math = MATH_BF16X3; probe.M = C; probe.N = N; probe.K = C; probe.batch = P; probe.pro = PRO_B_K;
   probe.has_res = 1; probe.bias_mode = BIAS_M; probe.head_w = blk->output.weight;
   probe.no_store = latent ? 0 : 1;   // a block whose activation is not returned keeps only the head's output
   const bool fuse_head = pconv_covers(probe);   // (that PointCN then stays on the conv3 + conv7 pair)

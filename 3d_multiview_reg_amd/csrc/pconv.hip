@@ -45,10 +45,6 @@ namespace mvr {
 #ifndef PCONV_NTL
 #define PCONV_NTL 2   // cache-policy bits of the activation buffer loads: nt (streamed once; -3 % per step's point convs)
 #endif
-#ifndef PCONV_ABL
-#define PCONV_ABL 0   // timing ablations (wrong results; tools/build_variant.sh): 1 no MFMA, 2 no split,
-                      // 4 no epilogue, 8 no activation loads
-#endif
 
 int g_pconv = 1;   // mvr_set_pconv: 0 routes these convs to gemm_kernel (A/B timing)
 #ifndef PCONV_MATH_DEFAULT
@@ -64,7 +60,6 @@ using namespace bx;
 constexpr int PC = 128;              // output channels (input channels: 16 KS, KS = 8 or 16 k-steps)
 constexpr int CH = 32;               // points per chunk (one MFMA column block)
 constexpr int GRP = 4;               // chunks per statistics group (128 points, gemm.hpp GEMM_BN)
-constexpr int FRB = 3 * 64 * 16;     // one k-step's fragment set: h, m, l planes x 64 lanes x 16 B
 constexpr int YLD = 32;              // row stride (floats) of the per-wave transpose scratch
 
 struct PcArgs {
@@ -254,9 +249,8 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        r[8 * t + i] = (PCONV_ABL & 8) ? (float)(i + t)
-                                       : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                                       rs, vo, (16 * t + i) * xld4, PCONV_NTL));
+        r[8 * t + i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (16 * t + i) * xld4,
+                                                                                      PCONV_NTL));
   };
   // normalise + split half t of a chunk's registers -> its k-step fragment in image slot
   auto split_half = [&](const Cur& c, const float (&r)[NX], int slot, int t) {
@@ -304,13 +298,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       return;
     }
     Frag f;
-    if (PCONV_ABL & 2) {
-      f.h = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
-      f.m = __builtin_bit_cast(bf16x8, u32x4{__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
-      f.l = f.h;
-    } else {
-      split8(v, f.h, f.m, f.l);
-    }
+    split8(v, f.h, f.m, f.l);
     *reinterpret_cast<bf16x8*>(dst) = f.h;
     *reinterpret_cast<bf16x8*>(dst + 1024) = f.m;
     *reinterpret_cast<bf16x8*>(dst + 2048) = f.l;
@@ -363,8 +351,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       FragT<H> nxt;
       if (ks < KSW - 1) nxt = ld_frag<H>(img + (ks + 1) * FRBT, 1024);
       PC_FENCE();
-      if (PCONV_ABL & 1) asm volatile("" ::"v"(cur.p[0]), "v"(cur.p[1]), "v"(wf[ks].p[0]));
-      else acc = mma<H>(wf[ks], cur, acc);
+      acc = mma<H>(wf[ks], cur, acc);
       hook(ks);
       PC_FENCE();
       if (ks < KSW - 1) cur = nxt;
@@ -374,10 +361,6 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   // epilogue of chunk c (accumulator acc): bias (+ residual), stores, head, statistics
   auto epilogue = [&](const Cur& c, const floatx16& acc) {
     const int n0 = c.kc * CH;
-    if (PCONV_ABL & 4) {
-      asm volatile("" ::"v"(acc));
-      return;
-    }
     // value (q, e) of this lane: row erow + 8q of the wave's 32, column n0 + ec0 + e
     float4 ev[4];
     if (RES && !(XI & 2)) {

@@ -6,12 +6,12 @@
 //
 // nbr is the kernel map as a neighbour table (csrc/sparse.hip); -1 entries contribute
 // nothing.  Output rows are visited in the order `perm` (mvr_kernel_map_order: rows sorted by
-// their active-offset mask), so a tile's rows share their active offsets and the union the tile
-// iterates stays small (a transposed stride-2 conv has <= 8 of 27 per row, by coordinate parity).  Per 64/128-row output tile the workgroup first lists the stencil offsets
-// that have at least one neighbour in the tile and skips the empty ones; each step
-// gathers 16 input channels of the tile's neighbour rows (16-byte row loads) and the
-// matching W[k] slice into LDS, then runs v_mfma_f32_32x32x2_f32.  No atomics: every
-// output row is owned by exactly one workgroup (deterministic results).
+// their active-offset mask, then spatially), so a tile's rows share their active offsets and the union the tile
+// iterates stays small (a transposed stride-2 conv has <= 8 of 27 per row, by coordinate parity).  Per 128-row
+// output tile the workgroup first lists the stencil offsets that have at least one neighbour in the tile and
+// skips the empty ones; each step gathers 32 input channels of the tile's neighbour rows straight into registers
+// and multiplies them with the pre-split weights on the bf16 MFMAs (below).  No atomics: every output row is
+// owned by exactly one workgroup (deterministic results).
 
 #include "common.hpp"
 #include "mfma_bf16.hpp"
@@ -36,179 +36,11 @@ struct SpArgs {
   int xcd;                                   // spconv_bx: XCD-contiguous tile order (mvr_set_spconv_xcd)
 };
 
-constexpr int SP_BK = 16;
 constexpr int SP_KMAX = 32;
 
-template <int TM, int TN, int WM, int WN>
-__global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
-  constexpr int WTN = TN / WN;  // wave tile columns (32 or 64)
-  constexpr int NJ = WTN / 32;
-  static_assert(TM / WM == 32, "wave tile rows must be 32");
-  __shared__ float As[2][SP_BK][TM + 4];
-  __shared__ float Bs[2][SP_BK][TN + 4];
-  __shared__ int32_t nb[TM][SP_KMAX + 1];
-  __shared__ int kact[SP_KMAX];
-  __shared__ int klist[SP_KMAX];
-  __shared__ int nk;
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int l32 = lane & 31, kh = lane >> 5;
-  const int64_t o0 = (int64_t)blockIdx.x * TM;
-  const int c0 = blockIdx.y * TN;
-  const int K = a.K;
-
-  if (tid < SP_KMAX) kact[tid] = 0;
-  __syncthreads();
-  for (int e = tid; e < TM * K; e += 256) {
-    const int row = e / K, k = e - row * K;
-    const int64_t o = o0 + row;
-    int v = -1;
-    if (o < a.Mout) {
-      const int64_t orow = a.perm ? a.perm[o] : o;
-      v = a.nbr ? a.nbr[orow * K + k] : (int)orow;
-    }
-    nb[row][k] = v;
-    if (v >= 0) kact[k] = 1;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int n = 0;
-    for (int k = 0; k < K; ++k)
-      if (kact[k]) klist[n++] = k;
-    nk = n;
-  }
-  __syncthreads();
-
-  const int nch = (a.Cin + SP_BK - 1) / SP_BK;
-  const int steps = nk * nch;
-
-  constexpr int AV = TM * SP_BK / 4 / 256;                       // float4 per thread for A (1 or 2)
-  constexpr int BV = (SP_BK * TN / 4 + 255) / 256;               // float4 per thread for B (1 or 2)
-  // Three steps of gathered rows in flight in registers (the gather is latency-bound: a step's
-  // MFMAs are far shorter than a dependent HBM/L2 round trip), two LDS buffers.
-  // Loads are issued unconditionally (clamped addresses, validity kept as bit masks applied when the
-  // registers are stored) so that the compiler's vmcnt bookkeeping keeps the steps in flight.
-  // Register set i: a_i (gathered rows), b_i (weights), m_i (validity bits: A in 0..AV-1, B above).
-  float4 a_0[AV], a_1[AV], a_2[AV], b_0[BV], b_1[BV], b_2[BV];
-  uint32_t m_0 = 0, m_1 = 0, m_2 = 0;
-
-  auto load = [&](int s, float4 (&ra)[AV], float4 (&rb)[BV], uint32_t& msk) {
-    if (s >= steps) s = steps - 1;   // clamped re-read past the end
-    const int k = klist[s / nch];
-    const int ci0 = (s % nch) * SP_BK;
-    uint32_t mm = 0;
-#pragma unroll
-    for (int r = 0; r < AV; ++r) {
-      const int idx = tid + 256 * r;
-      const int row = idx >> 2, ciq = (idx & 3) * 4;
-      const int src = nb[row][k];
-      mm |= (src >= 0 && ci0 + ciq < a.Cin) ? (1u << r) : 0u;
-      ra[r] = *reinterpret_cast<const float4*>(a.in + (int64_t)(src >= 0 ? src : 0) * a.ldin + min(ci0 + ciq, a.Cin - 4));
-    }
-#pragma unroll
-    for (int r = 0; r < BV; ++r) {
-      const int idx = tid + 256 * r;
-      const int kk = min(idx / (TN / 4), SP_BK - 1), nq = (idx % (TN / 4)) * 4;
-      const int ci = ci0 + kk, c = c0 + nq;
-      mm |= (idx < SP_BK * TN / 4 && ci < a.Cin && c < a.Cout) ? (1u << (AV + r)) : 0u;
-      rb[r] = *reinterpret_cast<const float4*>(a.W + ((int64_t)k * a.Cin + min(ci, a.Cin - 1)) * a.Cout + min(c, a.Cout - 4));
-    }
-    msk = mm;
-  };
-  auto store = [&](int buf, const float4 (&ra)[AV], const float4 (&rb)[BV], uint32_t msk) {
-#pragma unroll
-    for (int r = 0; r < AV; ++r) {
-      const int idx = tid + 256 * r;
-      const int row = idx >> 2, ciq = (idx & 3) * 4;
-      const bool ok = (msk >> r) & 1;   // value selects (a select of references would go through scratch)
-      const float4 v = make_float4(ok ? ra[r].x : 0.f, ok ? ra[r].y : 0.f, ok ? ra[r].z : 0.f, ok ? ra[r].w : 0.f);
-      As[buf][ciq + 0][row] = v.x;
-      As[buf][ciq + 1][row] = v.y;
-      As[buf][ciq + 2][row] = v.z;
-      As[buf][ciq + 3][row] = v.w;
-    }
-#pragma unroll
-    for (int r = 0; r < BV; ++r) {
-      const int idx = tid + 256 * r;
-      if (idx < SP_BK * TN / 4) {
-        const int kk = idx / (TN / 4), nq = (idx % (TN / 4)) * 4;
-        const bool ok = (msk >> (AV + r)) & 1;
-        *reinterpret_cast<float4*>(&Bs[buf][kk][nq]) =
-            make_float4(ok ? rb[r].x : 0.f, ok ? rb[r].y : 0.f, ok ? rb[r].z : 0.f, ok ? rb[r].w : 0.f);
-      }
-    }
-  };
-
-  floatx16 acc[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-
-  if (steps > 0) {
-    load(0, a_0, b_0, m_0);
-    load(1, a_1, b_1, m_1);
-    load(2, a_2, b_2, m_2);
-    store(0, a_0, b_0, m_0);
-  }
-  __syncthreads();
-  // step s: MFMAs on buffer s & 1, store step s + 1 (set (s+1) % 3) into the other buffer, refill
-  // set s % 3 (stored one step ago) with step s + 3
-  auto mfmas = [&](int cur) {
-#pragma unroll
-    for (int kk = 0; kk < SP_BK; kk += 2) {
-      const float av = As[cur][kk + kh][wm * 32 + l32];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const float bv = Bs[cur][kk + kh][wn * WTN + j * 32 + l32];
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[j], 0, 0, 0);
-      }
-    }
-  };
-#define SP_STEP(S_, AS, BS, MS, AN, BN, MN) \
-  mfmas((S_) & 1);                          \
-  store(((S_) & 1) ^ 1, AN, BN, MN);        \
-  load((S_) + 3, AS, BS, MS);               \
-  __syncthreads();
-  int s = 0;
-  for (; s + 2 < steps; s += 3) {
-    SP_STEP(s, a_0, b_0, m_0, a_1, b_1, m_1)
-    SP_STEP(s + 1, a_1, b_1, m_1, a_2, b_2, m_2)
-    SP_STEP(s + 2, a_2, b_2, m_2, a_0, b_0, m_0)
-  }
-  if (s < steps) { SP_STEP(s, a_0, b_0, m_0, a_1, b_1, m_1) }
-  if (s + 1 < steps) { SP_STEP(s + 1, a_1, b_1, m_1, a_2, b_2, m_2) }
-#undef SP_STEP
-
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int c = c0 + wn * WTN + j * 32 + l32;
-    if (c >= a.Cout) continue;
-    float bsc = 1.f, bsh = 0.f;
-    if (a.bn.gamma) {
-      bsc = a.bn.gamma[c] / sqrtf(a.bn.var[c] + a.bn_eps);
-      bsh = a.bn.beta[c] - a.bn.mean[c] * bsc;
-    }
-    const float bias = a.bias ? a.bias[c] : 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t ot = o0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (ot >= a.Mout) continue;
-      const int64_t o = a.perm ? a.perm[ot] : ot;
-      float v = acc[j][r] + bias;
-      v = fmaf(v, bsc, bsh);
-      if (a.res) v += a.res[o * a.ldres + c];
-      if (a.relu) v = fmaxf(v, 0.f);
-      a.out[o * a.ldout + c] = v;
-    }
-  }
-}
-
-
 // ---------------------------------------------------------------------------------------------
-// Split-bf16 variant: the same output-stationary gather-GEMM on v_mfma_f32_32x32x16_bf16 with both
-// operands as three bf16 terms (fp32-level accuracy, see mfma_bf16.hpp) — 2.7x the fp32 MFMA rate.
+// The gather-GEMM on v_mfma_f32_32x32x16_bf16 with both operands as three bf16 terms (fp32-level accuracy, see
+// mfma_bf16.hpp) — 2.7x the fp32 MFMA rate.
 // 128 output rows per workgroup, one 32-row slab per wave over all TN output channels (NJ = TN / 32
 // accumulator tiles), so a wave's gathered rows are its own A operand: each lane gathers its row's 8
 // channels of each k-step straight into registers (three steps in flight), splits them itself — no LDS
@@ -219,9 +51,6 @@ __global__ __launch_bounds__(256) void spconv_kernel(SpArgs a) {
 constexpr int SB_K = 32;     // input channels per step
 constexpr int SB_BST = 40;   // bf16 row stride of the weight image (80 B)
 constexpr int SB_CP = 128;   // output-channel padding of the weight image (largest TN)
-#ifndef SPBX_ABL
-#define SPBX_ABL 0   // timing ablation (wrong results; tools/build_variant.sh): 1 no MFMAs
-#endif
 #ifndef SPBX_NS32   // gathered steps in flight per output-channel tile width (register budget)
 #define SPBX_NS32 3
 #endif
@@ -378,11 +207,7 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
         for (int j = 0; j < NJ; ++j) {
           const uint16_t* bp = Bq + (32 * j + l32) * SB_BST + 16 * st + 8 * h;
           const FragT<H> fb = ld_frag<H>(reinterpret_cast<const char*>(bp), 2 * BPL);
-#if SPBX_ABL & 1
-          asm volatile("" ::"v"(fa.p[0]), "v"(fa.p[1]), "v"(fb.p[0]), "v"(fb.p[1]));
-#else
           acc[j] = mma<H>(fa, fb, acc[j]);
-#endif
         }
       }
       __syncthreads();
@@ -534,8 +359,8 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
                           int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
                           const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
                           int32_t* range_flag, hipStream_t s) {
-  if (!in || !W || !out || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
-  if (wimg && (reinterpret_cast<uintptr_t>(wimg) & 15)) return MVR_EINVAL;
+  if (!in || !W || !out || !wimg || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
+  if (reinterpret_cast<uintptr_t>(wimg) & 15) return MVR_EINVAL;
   if (!nbr && K != 1) return MVR_EINVAL;
   if ((Cin & 3) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
       (reinterpret_cast<uintptr_t>(W) & 15))
@@ -544,56 +369,42 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
   SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout,
            nullptr, nullptr, 0, g_spconv_xcd};
   ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
-  if (wimg) {   // split paths (weights pre-split by mvr_spconv_wimage)
-    const char* base = reinterpret_cast<const char*>(wimg);
-    const uint16_t* wi = reinterpret_cast<const uint16_t*>(wimg);
-    const uint16_t* wi16 = reinterpret_cast<const uint16_t*>(base + sp_bf16_bytes(K, Cin, Cout));
-    const int64_t CoutP = sp_coutp(Cout);
-    const float* isc = reinterpret_cast<const float*>(base + sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout)) +
-                       CoutP;
-    const unsigned gx = (unsigned)((Mout + 127) / 128);
-    // split-fp16 then its guarded split-bf16 re-run: only with the caller's flag word (cleared here, stream-ordered)
-    // and not where the output is the residual (in place: the re-run reads it).  Output tiles of 32 / 64 channels
-    // stay split-bf16: there the split-fp16 kernel holds more VGPRs (155 vs 125 at TN = 32), one workgroup per CU
-    // fewer for a gather-latency bound loop — measured slower (tools/spconv_micro.py: s1:1:32:32 0.378 -> 0.384 ms,
-    // up:1:128:64 0.403 -> 0.453), where the 128-channel tiles gain (s1:4:128:128 0.304 -> 0.217, s1:8:256:256
-    // 0.437 -> 0.346).  (in / out never alias: rows are gathered.)
-    const bool h1 = g_spconv_h && range_flag && Cout > 64 && res != out;
-    if (h1) {
-      if (hipMemsetAsync(range_flag, 0, sizeof(int32_t), s) != hipSuccess) return MVR_ELAUNCH;
-      a.range = range_flag;
-      a.epoch = 1;
-    }
+  const char* base = reinterpret_cast<const char*>(wimg);
+  const uint16_t* wi = reinterpret_cast<const uint16_t*>(wimg);
+  const uint16_t* wi16 = reinterpret_cast<const uint16_t*>(base + sp_bf16_bytes(K, Cin, Cout));
+  const int64_t CoutP = sp_coutp(Cout);
+  const float* isc = reinterpret_cast<const float*>(base + sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout)) +
+                     CoutP;
+  const unsigned gx = (unsigned)((Mout + 127) / 128);
+  // split-fp16 then its guarded split-bf16 re-run: only with the caller's flag word (cleared here, stream-ordered)
+  // and not where the output is the residual (in place: the re-run reads it).  Output tiles of 32 / 64 channels
+  // stay split-bf16: there the split-fp16 kernel holds more VGPRs (155 vs 125 at TN = 32), one workgroup per CU
+  // fewer for a gather-latency bound loop — measured slower (tools/spconv_micro.py: s1:1:32:32 0.378 -> 0.384 ms,
+  // up:1:128:64 0.403 -> 0.453), where the 128-channel tiles gain (s1:4:128:128 0.304 -> 0.217, s1:8:256:256
+  // 0.437 -> 0.346).  (in / out never alias: rows are gathered.)
+  const bool h1 = g_spconv_h && range_flag && Cout > 64 && res != out;
+  if (h1) {
+    if (hipMemsetAsync(range_flag, 0, sizeof(int32_t), s) != hipSuccess) return MVR_ELAUNCH;
+    a.range = range_flag;
+    a.epoch = 1;
+  }
 #define MVR_SPL(TN_, NS_, GY)                                                                                   \
-  do {                                                                                                          \
-    if (h1) {                                                                                                   \
+  do {                                                                                                         \
+    if (h1) {                                                                                                  \
       hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 1>), dim3(gx * (GY)), dim3(256), 0, s, a, wi16, CoutP, isc); \
-      MVR_CHECK_LAUNCH();                                                                                       \
-      a.guard = a.range;                                                                                        \
-      a.range = nullptr;                                                                                        \
-    }                                                                                                           \
-    hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc);    \
+      MVR_CHECK_LAUNCH();                                                                                      \
+      a.guard = a.range;                                                                                       \
+      a.range = nullptr;                                                                                       \
+    }                                                                                                          \
+    hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc);   \
   } while (0)
-    if (Cout <= 32)
-      MVR_SPL(32, SPBX_NS32, 1);
-    else if (Cout <= 64)
-      MVR_SPL(64, SPBX_NS64, 1);
-    else
-      MVR_SPL(128, SPBX_NS128, (Cout + 127) / 128);
+  if (Cout <= 32)
+    MVR_SPL(32, SPBX_NS32, 1);
+  else if (Cout <= 64)
+    MVR_SPL(64, SPBX_NS64, 1);
+  else
+    MVR_SPL(128, SPBX_NS128, (Cout + 127) / 128);
 #undef MVR_SPL
-    MVR_CHECK_LAUNCH();
-    return MVR_OK;
-  }
-  if (Cout <= 32) {
-    hipLaunchKernelGGL((spconv_kernel<128, 32, 4, 1>), dim3((unsigned)((Mout + 127) / 128), (Cout + 31) / 32),
-                       dim3(256), 0, s, a);
-  } else if (Cout <= 64) {
-    hipLaunchKernelGGL((spconv_kernel<64, 64, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 63) / 64), dim3(256),
-                       0, s, a);
-  } else {
-    hipLaunchKernelGGL((spconv_kernel<64, 128, 2, 2>), dim3((unsigned)((Mout + 63) / 64), (Cout + 127) / 128),
-                       dim3(256), 0, s, a);
-  }
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }

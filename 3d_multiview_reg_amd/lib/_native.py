@@ -57,7 +57,6 @@ _SIGS = {
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
                              c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int,
                              c_int, c_int, c_vp, c_vp]),
-    "mvr_set_gemm_math": (c_int, [c_int]),
     "mvr_set_pconv": (c_int, [c_int]),
     "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
@@ -72,8 +71,6 @@ _SIGS = {
     "mvr_attn_reruns": (c_int, [c_int]),
     "mvr_debug_stage_hash": (c_int, [c_vp, c_int]),
     "mvr_debug_stage_dump": (c_int, [c_int, c_vp, c_size]),
-    "mvr_pointcn_fused": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                  c_vp, c_int, c_int, c_int, c_vp, c_i64, c_int, c_vp]),
     "mvr_oan_diff_pool": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                   c_vp, c_i64, c_i64, c_vp, c_i64, c_int, c_vp]),
     "mvr_oan_diff_pool_ws": (c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_int, c_int, c_int, c_int,
@@ -91,6 +88,9 @@ _SIGS = {
     "mvr_sample_rand_mt19937": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "mvr_feat_knn2": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "mvr_fps": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
+    "mvr_knn1": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "mvr_mutuals": (c_int, [c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int,
+                            c_int, c_float, c_vp, c_vp, c_vp]),
     "mvr_voxel_centroids_workspace_bytes": (c_size, [c_i64]),
     "mvr_voxel_centroids": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_vp, c_size, c_vp, c_vp, c_vp]),
     "mvr_radius_index_bytes": (c_size, [c_i64]),

@@ -19,10 +19,6 @@ from lib import _native as N
 from lib.sparse import SparseTensor
 
 
-# split-bf16 sparse convs (csrc/spconv.hip spconv_bx_kernel, weights pre-split once per weight version):
-# the default (scene step: 9.0 -> 8.3 ms of sparse convs); MVR_SPCONV_BF16=0 selects the exact-fp32 MFMA
-# kernel (A/B timing)
-SPLIT_BF16 = os.environ.get("MVR_SPCONV_BF16", "1") == "1"
 # conv1 (7^3) as brick-tiled dense windows on split-bf16 MFMA (csrc/sparse.hip spconv_c1_brick_kernel);
 # MVR_CONV1_BRICKS=0 selects the per-row gather kernel (A/B timing)
 CONV1_BRICKS = os.environ.get("MVR_CONV1_BRICKS", "1") == "1"
@@ -123,11 +119,11 @@ class FCGFNet(nn.Module):
         bnp, eps = _bn(norm)
         K, cin, cout = conv.kernel.shape
         nbr, perm = km if km is not None else (None, None)
-        wimg = conv.wimage() if SPLIT_BF16 else None
+        # split-bf16 sparse convs (csrc/spconv.hip) on weights pre-split once per weight version
+        wimg = conv.wimage()
         N.check(N.lib().mvr_spconv(N.ptr(x), ldx, cin, N.ptr(nbr), N.ptr(perm), K, M, N.ptr(conv.kernel), cout,
                                    N.ptr(bias), bnp, eps, N.ptr(res), ldres, int(relu), N.ptr(out), ldout,
-                                   N.ptr(wimg), N.ptr(N.flag_word(x.device)) if wimg is not None else None,
-                                   N.stream()), "mvr_spconv")
+                                   N.ptr(wimg), N.ptr(N.flag_word(x.device)), N.stream()), "mvr_spconv")
         return out
 
     def _block(self, blk, x, ldx, km, M, out, ldout):

@@ -120,20 +120,62 @@ def transform_point_cloud(x1, R, t):
     return (torch.matmul(R, x1.transpose(1, 2)) + t).transpose(1, 2)
 
 
+def _rows3(x):
+    """(tensor, batch stride, row stride) of a [b, n, 3] float32 view whose 3 coordinates are contiguous."""
+    if x.dim() != 3 or x.shape[2] != 3 or x.dtype != torch.float32:
+        raise TypeError("expected a float32 [b, n, 3] tensor, got %s %s" % (x.dtype, tuple(x.shape)))
+    if x.stride(2) != 1 or x.stride(1) < 3:
+        x = x.contiguous()
+    return x, x.stride(0), x.stride(1)
+
+
 def knn_point(k, pos1, pos2):
-    """utils.py:274-299: squared distances and indices of the k nearest pos1 points for each pos2 point."""
-    d = torch.cdist(pos2, pos1) ** 2
-    val, idx = torch.topk(d, k=k, dim=-1, largest=False)
-    return val, idx
+    """utils.py:274-299: (squared distances, indices) [b, m, k] of the k nearest pos1 [b, n, 3] points for each pos2
+    [b, m, 3] point, nearest first.  k = 1 (the reference's only use, extract_mutuals) is csrc/knn.hip mvr_knn1 in
+    the reference's fp32 arithmetic without materialising the [b, m, n, 3] repeats; k > 1 evaluates the same
+    expression in query chunks with torch.topk on the device."""
+    N.require_hip(pos1)
+    B, n, _ = pos1.shape
+    m = pos2.shape[1]
+    if k == 1:
+        p1, s1b, s1r = _rows3(pos1)
+        p2, s2b, s2r = _rows3(pos2.to(pos1.device))
+        d = torch.empty(B, m, 1, dtype=torch.float32, device=pos1.device)
+        idx = torch.empty(B, m, 1, dtype=torch.int64, device=pos1.device)
+        if B and m:
+            N.check(N.lib().mvr_knn1(N.ptr(p1), s1b, s1r, N.ptr(p2), s2b, s2r, B, n, m, N.ptr(d), N.ptr(idx),
+                                     N.stream()), "mvr_knn1")
+        return d, idx
+    vals, idxs = [], []
+    step = max(1, (1 << 26) // max(1, B * n * 3))
+    for q0 in range(0, m, step):
+        q = pos2[:, q0:q0 + step]
+        d = pos1[:, None, :, :] - q[:, :, None, :]
+        dist = -((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])   # the reference's order
+        v, i = dist.topk(k=k, dim=-1)
+        vals.append(-v)
+        idxs.append(i)
+    return torch.cat(vals, 1), torch.cat(idxs, 1)
 
 
 def extract_mutuals(x1, x2, x1_soft_matches, x2_soft_matches, threshold=0.05):
-    """utils.py:822-848: 1 where x1 -> (its match in x2) -> back lands within `threshold` of x1."""
-    B, Np, C = x1.shape
-    _, idx = knn_point(1, x2, x1_soft_matches)
-    back = torch.gather(x2_soft_matches, 1, idx.expand(-1, -1, C))
-    d = ((x1 - back) ** 2).sum(dim=2)
-    return (d < threshold ** 2).float().cpu()
+    """utils.py:822-848: mutuals [b, n] float32, 1 where x1[i]'s soft match, snapped to its nearest x2 point j, maps
+    back (x2_soft_matches[j]) to within `threshold` of x1[i].  One csrc/knn.hip mvr_mutuals launch (NN search,
+    gather and threshold fused).  The reference fills a host tensor from a device mask (which fails for CUDA
+    inputs); the flags stay on the inputs' device here."""
+    N.require_hip(x1)
+    B, Np, _ = x1.shape
+    dev = x1.device
+    a, ab, ar = _rows3(x1)
+    b, bb, br = _rows3(x2.to(dev))
+    c, cb, cr = _rows3(x1_soft_matches.to(dev))
+    d, db, dr = _rows3(x2_soft_matches.to(dev))
+    out = torch.empty(B, Np, dtype=torch.float32, device=dev)
+    if B and Np:
+        thr2 = float(np.float32(threshold ** 2))
+        N.check(N.lib().mvr_mutuals(N.ptr(a), ab, ar, N.ptr(b), bb, br, N.ptr(c), cb, cr, N.ptr(d), db, dr, B, Np,
+                                    thr2, N.ptr(out), None, N.stream()), "mvr_mutuals")
+    return out
 
 
 def pair_index(B, device=None):

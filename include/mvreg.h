@@ -71,7 +71,7 @@ int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride, const int3
                int32_t* best_iter, double* hyp_out, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
- * One fused fp32-MFMA batched GEMM of the OANet schedule (exposed for tests):
+ * One fused MFMA batched GEMM of the OANet schedule (exposed for tests):
  *   C[b](m,n) = sum_k pro_A(A(m,k)) pro_B(B(k,n)) + bias + R[b](m,n)
  * pro: 0 none, 1 relu(A*sc[k]+sh[k]), 2 relu(B*sc[k]+sh[k]) (sc/sh at [b*sPb + k]),
  *      3 B(k,n) * f[b*sPb + (k/128)*pld + n] (per-tile softmax factor).
@@ -80,8 +80,9 @@ int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride, const int3
  * 4 column sum/sumsq (float2 partials, see csrc/gemm.hpp).
  * Layout: 16-byte aligned pointers, all strides multiples of 4 floats, rows padded to
  * round_up(K|N, 4) floats holding finite values (MVR_EINVAL otherwise).
- * math: 0 exact fp32 MFMA (v_mfma_f32_32x32x2_f32); 1 three-term bf16 split (x = h+m+l,
- * products hh+hm+mh+mm+hl+lh on v_mfma_f32_32x32x16_bf16, fp32 accumulation: fp32-level accuracy).
+ * math: must be 1, the three-term bf16 split (x = h+m+l, products hh+hm+mh+mm+hl+lh on
+ * v_mfma_f32_32x32x16_bf16, fp32 accumulation: fp32-level accuracy); other values return MVR_EINVAL (the exact
+ * fp32-MFMA variant of round 2 was removed: 2.7x slower at the same accuracy class).
  * Replaces the nn.Conv2d(k=1) / torch.matmul calls of lib/filtering/oanet.py.
  * ---------------------------------------------------------------------- */
 int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* B,
@@ -89,8 +90,6 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
                  int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
                  int64_t pld, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, int math,
                  int32_t* range_flag, mvr_stream_t stream);
-/* GEMM arithmetic used by mvr_oan_block_forward (process-wide; default 1 = bf16 split). */
-int mvr_set_gemm_math(int math);
 /* With the split math (1), run each generic GEMM launch that has a range flag (mvr_gemm_f32's range_flag: a device
    int32 the call clears; mvr_oan_block_forward: words of its workspace) as two-term split-fp16 first (A and B x 2^6,
    3 MFMAs per product, 22-bit operands) with a guarded split-bf16 re-run when an operand left the window
@@ -138,11 +137,11 @@ typedef struct {
 } mvr_oan_block_p;
 
 size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N);
-/* Fused paths inside mvr_oan_block_forward (process-wide; default 1; query workspace bytes after setting):
+/* Fused paths inside mvr_oan_block_forward (process-wide; query workspace bytes after setting):
  *   bit 0: diff_pool / diff_unpool as the fused attention kernels (mvr_oan_diff_pool / _unpool) when
  *          channels == 128 and clusters <= 1024 (else embedding GEMM + softmax factors + pooling GEMM);
- *   bit 1: PointCN(128 -> 128) as a statistics-only conv3 pass + mvr_pointcn_fused (else conv3, conv7);
- *          correct (tested) but not yet faster than the two GEMMs, so off by default.
+ *   bit 2: the block's conv1 (in_channels <= 8 -> 128) folded into the first PointCN's point convs;
+ *   bit 1 is unused (ignored).  Default 5.
  * Returns the previous value. */
 int mvr_set_oan_fused(int on);
 /* Key-split diff_pool launches inside mvr_oan_block_forward (mvr_oan_diff_pool_ws): 1 (default) on, 0 off
@@ -222,18 +221,6 @@ int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t x_ld, cons
                         int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld, int st_off,
                         void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 
-/* Fused PointCN (lib/filtering/oanet.py:18-43) with channels == out_channels == 128 (identity shortcut):
- *   y = W7 . relu(t * sc2 + sh2) + b7 + x,   t = W3 . relu(x * sc1 + sh1) + b3
- * sc1/sh1, sc2/sh2 [P][128]: the two InstanceNorm+BatchNorm layers folded per (pair, channel) — sc2/sh2 come
- * from the statistics of t (a statistics-only conv3 pass), so t is never stored.  x, y [P][128][ld] (y may
- * be x), ld >= round_up(N,4), multiples of 4, 16-byte aligned; columns [N, round_up(N,4)) of y written 0.
- * stats (may be NULL): float pairs (sum, squared deviations from the chunk mean) of y per 32-point chunk,
- * at stats[2*((p*ceil(N/32) + chunk)*st_ld + st_off + c)]. */
-int mvr_pointcn_fused(const float* x, int64_t x_pstride, int64_t x_ld, float* y, int64_t y_pstride, int64_t y_ld,
-                      const float* sc1, const float* sh1, const float* sc2, const float* sh2, const float* w3,
-                      const float* b3, const float* w7, const float* b7, int P, int channels, int N, float* stats,
-                      int64_t st_ld, int st_off, mvr_stream_t stream);
-
 /* Correspondences [P][N][C] (strided) -> channel-major network input out[p*out_pstride + c*out_ld + n]
  * (the transpose of lib/filtering/oanet.py:234). */
 int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N, float* out,
@@ -270,6 +257,21 @@ int mvr_radius_overlap_count(const void* index, size_t bytes, const double* xyz,
  * every fragment, n <= 81920. */
 int mvr_fps(const float* xyz, const int64_t* offsets, const int64_t* offsets_host, int B, int m, int64_t* idx_out,
             mvr_stream_t stream);
+
+/* Coordinate-space nearest neighbour, knn_point(k=1, pos1, pos2) (lib/utils.py:274-299): for batch row b and
+ * query i of pos2 ([B][M] rows of 3 floats at pos2 + b*p2_bstride + i*p2_rstride), the nearest of the N rows of
+ * pos1 under the reference's fp32 squared distance ((dx^2 + dy^2) + dz^2, no contraction); first index on equal
+ * distances.  dist_out [B][M] (may be NULL), idx_out [B][M] int64 (may be NULL, not both).  Row strides >= 3. */
+int mvr_knn1(const float* pos1, int64_t p1_bstride, int64_t p1_rstride, const float* pos2, int64_t p2_bstride,
+             int64_t p2_rstride, int B, int N, int M, float* dist_out, int64_t* idx_out, mvr_stream_t stream);
+
+/* Mutual nearest-neighbour flag of the soft matches, extract_mutuals (lib/utils.py:822-848): j = knn1 of x1m[b,i]
+ * among x2[b, 0..N), flag_out[b*N + i] = |x1[b,i] - x2m[b,j]|^2 < thr2 ? 1 : 0 (thr2 = threshold^2 rounded to
+ * fp32, as the reference's float32 comparison does).  idx_out [B][N] (may be NULL) receives j. */
+int mvr_mutuals(const float* x1, int64_t x1_bstride, int64_t x1_rstride, const float* x2, int64_t x2_bstride,
+                int64_t x2_rstride, const float* x1m, int64_t x1m_bstride, int64_t x1m_rstride, const float* x2m,
+                int64_t x2m_bstride, int64_t x2m_rstride, int B, int N, float thr2, float* flag_out, int64_t* idx_out,
+                mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Feature-space (soft) nearest neighbour for a batch of fragment pairs.

@@ -92,7 +92,7 @@ def main():
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--only", default=None, help="comma-separated fixture groups to (re)write: kabsch, oanet, "
-                    "oanet_full_train, softnn, sampler, pairs, pairwise (default: all)")
+                    "oanet_full_train, softnn, sampler, pairs, pairwise, mutuals, evalharness (default: all)")
     args = ap.parse_args()
     only = set(args.only.split(",")) if args.only else None
 
@@ -135,6 +135,10 @@ def main():
         pairs_fixture(U, out, meta)
     if want("pairwise"):
         pairwise_fixture(L, O, out, meta)
+    if want("mutuals"):
+        mutuals_fixture(U, out, meta)
+    if want("evalharness"):
+        evalharness_fixture(U, out, meta)
     with open(mpath, "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("wrote golden fixtures to", out)
@@ -311,6 +315,121 @@ def pairwise_fixture(L, O, out, meta):
                         pts=np.asarray(pts), xs=fin["xs"].numpy(), **o)
     meta["fixtures"]["pairwise_fake_desc.npz"] = ("lib/pairwise/__init__.py:62-142 with a fixed feature table in place "
                                                   "of FCGF; np.random.seed(41); 3 fragments -> 3 pairs; small OANet seed 9")
+
+
+def mutuals_fixture(U, out, meta):
+    """lib/utils.py:274-299 knn_point and :822-848 extract_mutuals.  Soft matches are target points plus noise
+    (so the NN snap is well defined) and the back-matches land at distances straddling the 5 cm threshold."""
+    import torch
+    r = np.random.RandomState(71)
+    B, n = 3, 700
+    x1 = r.uniform(-1, 1, (B, n, 3)).astype(np.float32)
+    x2 = r.uniform(-1, 1, (B, n, 3)).astype(np.float32)
+    perm = np.stack([r.permutation(n) for _ in range(B)])
+    x1m = (np.take_along_axis(x2, perm[..., None], 1) + r.normal(0, 0.004, (B, n, 3))).astype(np.float32)
+    x2m = r.uniform(-1, 1, (B, n, 3)).astype(np.float32)
+    back = x1 + r.normal(0, 1, (B, n, 3)) * r.choice([0.005, 0.02, 0.2], (B, n, 1))
+    for b in range(B):
+        x2m[b, perm[b]] = back[b]
+    t = {k: torch.from_numpy(v) for k, v in (("x1", x1), ("x2", x2), ("x1m", x1m), ("x2m", x2m))}
+    mut = U.extract_mutuals(t["x1"], t["x2"], t["x1m"], t["x2m"])
+    d1, i1 = U.knn_point(1, t["x2"], t["x1m"])
+    d3, i3 = U.knn_point(3, t["x2"], t["x1m"][:, :50])
+    np.savez_compressed(os.path.join(out, "mutuals.npz"), x1=x1, x2=x2, x1m=x1m, x2m=x2m, mutuals=mut.numpy(),
+                        knn1_d=d1.numpy(), knn1_i=i1.numpy(), knn3_d=d3.numpy(), knn3_i=i3.numpy())
+    meta["fixtures"]["mutuals.npz"] = ("lib/utils.py:274-299 knn_point (k=1 over 700 points, k=3 for 50 queries) and "
+                                       ":822-848 extract_mutuals (threshold 0.05), B=3, RandomState(71)")
+
+
+def _mat2quat(M):
+    """nibabel.quaternions.mat2quat (absent here; the stub gets this restatement — Bar-Itzhack's eigenvector of
+    the symmetric K matrix, w >= 0).  Everything around it in the fixture is the reference's own code; the
+    quaternion itself stays parity-unpinned."""
+    Qxx, Qyx, Qzx, Qxy, Qyy, Qzy, Qxz, Qyz, Qzz = np.asarray(M, dtype=np.float64).flat
+    K = np.array([[Qxx - Qyy - Qzz, 0, 0, 0], [Qyx + Qxy, Qyy - Qxx - Qzz, 0, 0],
+                  [Qzx + Qxz, Qzy + Qyz, Qzz - Qxx - Qyy, 0],
+                  [Qyz - Qzy, Qzx - Qxz, Qxy - Qyx, Qxx + Qyy + Qzz]]) / 3.0
+    vals, vecs = np.linalg.eigh(K)
+    q = vecs[[3, 0, 1, 2], np.argmax(vals)]
+    return -q if q[0] < 0 else q
+
+
+def evalharness_fixture(U, out, meta):
+    """The 3DMatch / Redwood evaluation harness (lib/utils.py:438-637): trajectory write / read, info read,
+    extract_corresponding_trajectors, computeTransformationErr and evaluate_registration (with its quirk that GT
+    row 0 is never counted: gt_mask stores the row index and tests > 0).  Text files the reference writes are kept
+    as fixture data; the .info text is synthetic input."""
+    import tempfile
+    sys.modules["nibabel.quaternions"].mat2quat = _mat2quat
+    U.nq = sys.modules["nibabel.quaternions"]
+    r = np.random.RandomState(81)
+    nfrag = 9
+
+    def rigid(scale):
+        a = r.normal(size=3)
+        a = a / np.linalg.norm(a) * r.uniform(0, scale)
+        K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+        th = np.linalg.norm(a)
+        R = np.eye(3) + (np.sin(th) / max(th, 1e-12)) * K + ((1 - np.cos(th)) / max(th, 1e-12) ** 2) * K @ K
+        T = np.eye(4)
+        T[:3, :3] = R
+        T[:3, 3] = r.uniform(-2, 2, 3)
+        return T
+    # GT pairs: row 0 is a non-consecutive pair (the quirk), consecutive pairs mixed in
+    gt_pairs = [(0, 2), (0, 1), (1, 4), (2, 3), (2, 7), (3, 8), (4, 6), (5, 8), (6, 7), (1, 8)]
+    gt_T = np.stack([rigid(3.0) for _ in gt_pairs])
+    A = r.normal(size=(len(gt_pairs), 6, 6))
+    gt_info = np.einsum("pij,pkj->pik", A, A) + 6 * np.eye(6)
+    info_txt = "".join("%d\t%d\t%d\n" % (i, j, nfrag) + "".join("\t".join("%.10f" % v for v in row) + "\n"
+                                                                  for row in gt_info[k])
+                       for k, (i, j) in enumerate(gt_pairs))
+    # estimates: every GT pair (some accurate, some off) plus extra non-GT pairs, in a shuffled order
+    est_pairs, est_T = [], []
+    for k, (i, j) in enumerate(gt_pairs):
+        d = rigid([0.001, 0.05, 0.5][k % 3])
+        d[:3, 3] = r.normal(0, [0.001, 0.05, 0.4][k % 3], 3)
+        est_pairs.append((i, j))
+        est_T.append(gt_T[k] @ d)
+    for (i, j) in [(0, 5), (3, 4), (2, 6), (1, 3)]:
+        est_pairs.append((i, j))
+        est_T.append(rigid(3.0))
+    order = r.permutation(len(est_pairs))
+    est_pairs = np.asarray(est_pairs)[order]
+    est_T = np.stack(est_T)[order]
+    flags = np.where(r.rand(len(est_pairs)) < 0.8, "True", "False")
+    meta_arr = np.asarray([[str(i), str(j), f] for (i, j), f in zip(est_pairs, flags)])
+    with tempfile.TemporaryDirectory() as td:
+        tp = os.path.join(td, "traj.txt")
+        U.write_trajectory(est_T, meta_arr, tp)
+        with open(tp) as f:
+            traj_txt = f.read()
+        keys, traj_read = U.read_trajectory(tp)
+        gp = os.path.join(td, "gt.log")
+        U.write_trajectory(gt_T, np.asarray([[str(i), str(j), "True"] for i, j in gt_pairs]), gp)
+        with open(gp) as f:
+            gt_txt = f.read()
+        ip = os.path.join(td, "gt.info")
+        with open(ip, "w") as f:
+            f.write(info_txt)
+        n_frame, info_read = U.read_trajectory_info(ip)
+        gt_keys, gt_read = U.read_trajectory(gp)
+    # as the reference benchmark does (benchmark_pairwise_registration.py:289-313): the string keys of both files
+    ext_est, ext_gt = U.extract_corresponding_trajectors(keys, gt_keys, traj_read, gt_read)
+    errs = np.asarray([U.computeTransformationErr(np.linalg.inv(gt_T[k]) @ est_T[order.tolist().index(k)],
+                                                  gt_info[k]) for k in range(len(gt_pairs))])
+    res = {}
+    for err2 in (0.2, 0.05):
+        p, rc = U.evaluate_registration(n_frame, traj_read, keys, gt_keys, gt_read, info_read, err2=err2)
+        res["precision_%g" % err2], res["recall_%g" % err2] = p, rc
+    np.savez_compressed(os.path.join(out, "evalharness.npz"), nfrag=nfrag, gt_pairs=np.asarray(gt_pairs), gt_T=gt_T,
+                        gt_info=gt_info, info_txt=np.asarray(info_txt), est_pairs=est_pairs, est_T=est_T,
+                        flags=flags, traj_txt=np.asarray(traj_txt), gt_txt=np.asarray(gt_txt), keys=keys,
+                        gt_keys=gt_keys, gt_read=gt_read,
+                        traj_read=traj_read, n_frame=n_frame, info_read=info_read, ext_est=ext_est, ext_gt=ext_gt,
+                        errs=errs, **{k: np.asarray(v) for k, v in res.items()})
+    meta["fixtures"]["evalharness.npz"] = ("lib/utils.py:438-637 write/read_trajectory, read_trajectory_info, "
+                                           "extract_corresponding_trajectors, computeTransformationErr (mat2quat "
+                                           "restated: unpinned), evaluate_registration at err2 0.2 / 0.05")
 
 
 if __name__ == "__main__":

@@ -72,14 +72,11 @@ def test_kernel_map_k7_property(gpu, frags):
     assert np.array_equal(nbr[nbr[o, k], K - 1 - k], o)
 
 
-@pytest.mark.parametrize("split_bf16", [False, True])
-def test_fcgf_forward_matches_oracle(gpu, frags, split_bf16, monkeypatch):
-    """both sparse-conv paths: split-bf16 on mvr_spconv_wimage images (the default) and exact fp32 MFMA
-    (MVR_SPCONV_BF16=0); the oracle is our restatement of ME's sparse conv (parity unpinned: ME is absent)"""
+def test_fcgf_forward_matches_oracle(gpu, frags):
+    """split-bf16 sparse convs on mvr_spconv_wimage images; the oracle is our restatement of ME's sparse conv
+    (parity unpinned: ME is absent)"""
     import torch
-    from lib.descriptor import fcgf as fcgf_mod
     from lib.descriptor.fcgf import FCGFNet
-    monkeypatch.setattr(fcgf_mod, "SPLIT_BF16", split_bf16)
     from lib.sparse import voxelize, SparseTensor
     from oracle.fcgf import fcgf_forward
     net = FCGFNet()

@@ -138,21 +138,18 @@ def gf16(request):
     NV.lib().mvr_set_gemm_f16(prev)
 
 
-@pytest.mark.parametrize("math", [0, 1])       # exact fp32 MFMA / split (fp16 x2 first, or bf16 x3: gf16)
 @pytest.mark.parametrize("combo", COMBOS)
 @pytest.mark.parametrize("shape", [(128, 256, 128, 2), (130, 517, 36, 3), (500, 300, 64, 1), (1, 40, 8, 2),
                                    (130, 518, 36, 3), (256, 1000, 500, 2), (128, 5000, 4, 1), (64, 999, 260, 2),
                                    (128, 5000, 128, 3), (128, 517, 128, 2), (128, 500, 128, 5), (128, 31, 128, 2),
                                    (128, 517, 256, 3), (128, 5000, 256, 2)])
-def test_gemm_modes(gpu, combo, shape, math, gf16):
+def test_gemm_modes(gpu, combo, shape, gf16):
+    """split arithmetic: split-fp16 first with its guarded split-bf16 re-run, or split-bf16 only (gf16)"""
     M, N, K, b = shape
     pro, bkc, bias, stats, res = combo
-    if math == 0 and gf16 == 0:
-        pytest.skip("gf16 applies to the split math")
     if pro in (1, 2) and K % 4:
         pytest.skip("per-k prologue needs K % 4 == 0")
-    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1),
-         math=math)
+    _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=hash((combo, shape)) % 1000, shared_a=(pro != 1))
 
 
 @pytest.mark.parametrize("shape", [(128, 32, 128, 1200), (128, 20, 128, 1100), (128, 33, 128, 1100)])
@@ -165,13 +162,23 @@ def test_gemm_short_rows_many_pairs(gpu, combo, shape):
     _run(gpu, M, N, K, b, pro, bkc, bias, stats, res, seed=5, shared_a=True, math=1)
 
 
-@pytest.mark.parametrize("math", [0, 1])
-def test_gemm_ragged_k(gpu, math):
+def test_gemm_ragged_k(gpu, gf16):
     # K = 6 (conv1 of reg_init, weight rows zero-padded to 8) and odd K for plain GEMMs
-    _run(gpu, 128, 5000, 6, 2, 0, 0, 1, 1, 0, shared_a=True, math=math)
-    _run(gpu, 128, 999, 7, 2, 0, 0, 1, 1, 0, shared_a=True, math=math)
-    _run(gpu, 70, 333, 45, 2, 0, 1, 0, 0, 0, math=math)
-    _run(gpu, 70, 333, 45, 2, 3, 1, 0, 1, 0, math=math)
+    _run(gpu, 128, 5000, 6, 2, 0, 0, 1, 1, 0, shared_a=True)
+    _run(gpu, 128, 999, 7, 2, 0, 0, 1, 1, 0, shared_a=True)
+    _run(gpu, 70, 333, 45, 2, 0, 1, 0, 0, 0)
+    _run(gpu, 70, 333, 45, 2, 3, 1, 0, 1, 0)
+
+
+def test_gemm_rejects_removed_math(gpu):
+    """math must be 1 (split-bf16); the round-2 exact-fp32 value 0 is refused, not silently rerouted"""
+    import torch
+    from lib import _native as NV
+    a = torch.zeros(128, 128, device=gpu)
+    c = torch.empty(128, 128, device=gpu)
+    rc = NV.lib().mvr_gemm_f32(128, 128, 128, 1, NV.ptr(a), 0, 128, NV.ptr(a), 0, 128, 0, NV.ptr(c), 0, 128, None, 0,
+                               None, 0, None, None, 0, 0, 0, None, 0, 0, 0, 0, None, NV.stream())
+    assert rc == -1
 
 
 PCONV_COMBOS = [(2, 0, 1, 1, 0), (2, 0, 1, 1, 1), (2, 0, 1, 0, 0), (0, 0, 1, 0, 0), (0, 0, 1, 1, 0), (2, 0, 1, 0, 1)]
@@ -313,7 +320,8 @@ def test_gemm_f16_window(gpu, edit, combo):
 
 
 def test_gemm_bf16x3_accuracy_vs_fp32(gpu):
-    """The split path's error against float64 stays at the exact-fp32 path's level."""
+    """The split path's error against float64 stays at plain fp32's level (a float32 BLAS product of the same
+    operands)."""
     import torch
     from lib import _native as NV
     r = np.random.RandomState(3)
@@ -321,15 +329,14 @@ def test_gemm_bf16x3_accuracy_vs_fp32(gpu):
     A = r.standard_normal((b, M, K)).astype(np.float32)
     B = r.standard_normal((b, K, N)).astype(np.float32)
     ref = A.astype(np.float64) @ B.astype(np.float64)
-    errs = []
-    for math in (0, 1):
-        C = torch.empty(b, M, N, device=gpu)
-        tA, tB = torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu)
-        L = NV.lib()
-        assert L.mvr_gemm_f32(M, N, K, b, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, N, 0, NV.ptr(C), M * N, N, None,
-                              0, None, 0, None, None, 0, 0, 0, None, 0, 0, 0, math, NV.ptr(NV.flag_word()), NV.stream()) == 0
-        errs.append(np.abs(C.cpu().numpy() - ref).max())
-    assert errs[1] < 3 * errs[0] + 1e-6, errs
+    e32 = np.abs((A @ B).astype(np.float64) - ref).max()
+    C = torch.empty(b, M, N, device=gpu)
+    tA, tB = torch.from_numpy(A).to(gpu), torch.from_numpy(B).to(gpu)
+    L = NV.lib()
+    assert L.mvr_gemm_f32(M, N, K, b, NV.ptr(tA), M * K, K, NV.ptr(tB), K * N, N, 0, NV.ptr(C), M * N, N, None,
+                          0, None, 0, None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.ptr(NV.flag_word()), NV.stream()) == 0
+    err = np.abs(C.cpu().numpy() - ref).max()
+    assert err < 3 * e32 + 1e-6, (err, e32)
 
 
 def test_gemm_rejects_bad_layout(gpu):

@@ -308,10 +308,10 @@ def test_diff_pool_rejects_bad_layout(gpu):
     assert L.mvr_oan_diff_unpool_workspace_bytes(1, 64, 16) == 0
 
 
-@pytest.mark.parametrize("fused", [1, 2, 3, 4, 5, 7])
+@pytest.mark.parametrize("fused", [1, 4, 5])
 def test_oanet_fused_vs_gemm_path(gpu, fused):
-    """Whole filter with the fused kernels (bit 0: diff_pool/diff_unpool, bit 1: PointCN, bit 2: conv1
-    folded into the first PointCN) vs the plain GEMM path: same R, t (1e-4) and inlier masks."""
+    """Whole filter with the fused kernels (bit 0: diff_pool/diff_unpool, bit 2: conv1 folded into the first
+    PointCN) vs the plain GEMM path: same R, t (1e-4) and inlier masks."""
     import torch
     from lib import _native as NV
     from test_gpu_oanet import _oanet

@@ -1,7 +1,6 @@
 """Sparse convolution kernels (csrc/spconv.hip, the MinkowskiConvolution forward of
-lib/descriptor/fcgf.py:118-227) against an fp64 gather-GEMM restatement: both arithmetic paths (exact
-fp32 MFMA, and with pre-split weight images split-fp16 (default) / split-bf16), every channel shape FCGF
-uses, partial stencils (-1 neighbours), the row order of mvr_kernel_map_order, the identity map (1x1x1 conv)
+lib/descriptor/fcgf.py:118-227) against an fp64 gather-GEMM restatement: both split arithmetics on the
+pre-split weight images (split-bf16, the default, and the opt-in split-fp16), every channel shape FCGF uses, partial stencils (-1 neighbours), the row order of mvr_kernel_map_order, the identity map (1x1x1 conv)
 and the fused bias / BatchNorm / residual / ReLU epilogue; features outside the split-fp16 window re-run the
 launch in split-bf16 (bit-identical results)."""
 import numpy as np
@@ -18,7 +17,7 @@ def smath(request):
     NV.lib().mvr_set_spconv_math(prev)
 
 
-def _run(gpu, Cin, Cout, K, Mout, Min, split, perm=False, epi=True, seed=0, edit=None, raw=False, inplace=False):
+def _run(gpu, Cin, Cout, K, Mout, Min, perm=False, epi=True, seed=0, edit=None, raw=False, inplace=False):
     import torch
     from lib import _native as NV
     rng = np.random.default_rng(seed)
@@ -57,45 +56,51 @@ def _run(gpu, Cin, Cout, K, Mout, Min, split, perm=False, epi=True, seed=0, edit
         NV.check(L.mvr_kernel_map_order(NV.ptr(nbr_t), None, 1, Mout, K, NV.ptr(perm_t), NV.ptr(ws), ws.numel(),
                                          NV.stream()),
                  "order")
-    wimg = None
-    if split:
-        nbytes = L.mvr_spconv_wimage_bytes(K, Cin, Cout)
-        wimg = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
-        NV.check(L.mvr_spconv_wimage(NV.ptr(Wt), K, Cin, Cout, NV.ptr(wimg), nbytes, NV.stream()), "wimage")
+    nbytes = L.mvr_spconv_wimage_bytes(K, Cin, Cout)
+    wimg = torch.empty(nbytes, dtype=torch.uint8, device=gpu)
+    NV.check(L.mvr_spconv_wimage(NV.ptr(Wt), K, Cin, Cout, NV.ptr(wimg), nbytes, NV.stream()), "wimage")
     out = res_t.clone() if inplace else torch.full((Mout, Cout), float("nan"), device=gpu)
     if inplace:
         res_t = out
     bn = NV.BnP(gb.data_ptr(), bb.data_ptr(), mb.data_ptr(), vb.data_ptr()) if epi else NV.BnP(None, None, None, None)
     rc = L.mvr_spconv(NV.ptr(F), Cin, Cin, NV.ptr(nbr_t), NV.ptr(perm_t), K, Mout, NV.ptr(Wt), Cout, NV.ptr(bias_t), bn,
                       1e-5, NV.ptr(res_t), Cout, int(epi), NV.ptr(out), Cout, NV.ptr(wimg),
-                      NV.ptr(NV.flag_word(gpu)) if split else None, NV.stream())
+                      NV.ptr(NV.flag_word(gpu)), NV.stream())
     assert rc == 0
     got = out.cpu().numpy()
     if raw:
         return got
     scale = np.abs(ref).max() + 1e-30
     err = np.abs(got - ref).max() / scale
-    assert np.isfinite(got).all() and err < 2e-6, (Cin, Cout, K, split, err)
+    assert np.isfinite(got).all() and err < 2e-6, (Cin, Cout, K, err)
 
 
-@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("cin,cout", [(32, 32), (32, 64), (64, 64), (64, 128), (128, 128), (128, 256), (256, 256),
                                       (256, 128), (256, 64), (128, 64), (96, 64)])
-def test_spconv_3x3x3(gpu, cin, cout, split, smath):
-    _run(gpu, cin, cout, 27, 1000, 900, split, perm=True, seed=cin + cout)
+def test_spconv_3x3x3(gpu, cin, cout, smath):
+    _run(gpu, cin, cout, 27, 1000, 900, perm=True, seed=cin + cout)
 
 
-@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("cin,cout,mout", [(96, 64, 777), (64, 32, 300), (32, 32, 129)])
-def test_spconv_identity_map(gpu, cin, cout, mout, split, smath):
+def test_spconv_identity_map(gpu, cin, cout, mout, smath):
     """1x1x1 convs (conv1_tr, final: fcgf.py:209-227) run with the identity map (nbr NULL)"""
-    _run(gpu, cin, cout, 1, mout, mout, split, epi=cout != 32, seed=cin)
+    _run(gpu, cin, cout, 1, mout, mout, epi=cout != 32, seed=cin)
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_spconv_ragged_rows_no_perm(gpu, split, smath):
+def test_spconv_ragged_rows_no_perm(gpu, smath):
     """a row count far from the tile size, natural row order, no epilogue, 8 offsets (transposed-conv size)"""
-    _run(gpu, 64, 64, 8, 130, 2000, split, perm=False, epi=False, seed=9)
+    _run(gpu, 64, 64, 8, 130, 2000, perm=False, epi=False, seed=9)
+
+
+def test_spconv_requires_weight_image(gpu):
+    """the exact-fp32 kernel of round 2 is gone: a call without the pre-split image is refused"""
+    import torch
+    from lib import _native as NV
+    x = torch.zeros(8, 32, device=gpu)
+    W = torch.zeros(1, 32, 32, device=gpu)
+    rc = NV.lib().mvr_spconv(NV.ptr(x), 32, 32, None, None, 1, 8, NV.ptr(W), 32, None, NV.BnP(None, None, None, None),
+                             1e-5, None, 0, 0, NV.ptr(x), 32, None, None, NV.stream())
+    assert rc == -1
 
 
 def _big_feat(f):
@@ -117,9 +122,8 @@ def test_spconv_fp16_window(gpu, edit, inplace):
     try:
         for m in (0, 1):
             L.mvr_set_spconv_math(m)
-            outs.append(_run(gpu, 64, 128, 27, 1000, 900, True, perm=True, seed=4, edit=edit, raw=True,
-                             inplace=inplace))
-        _run(gpu, 64, 128, 27, 1000, 900, True, perm=True, seed=4, edit=edit, inplace=inplace)
+            outs.append(_run(gpu, 64, 128, 27, 1000, 900, perm=True, seed=4, edit=edit, raw=True, inplace=inplace))
+        _run(gpu, 64, 128, 27, 1000, 900, perm=True, seed=4, edit=edit, inplace=inplace)
     finally:
         L.mvr_set_spconv_math(prev)
     assert np.array_equal(outs[0], outs[1])
