@@ -122,10 +122,11 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
 
   // gathered A of one step: k-step st, channels ci0 + 16 st + 8h + (0..7) of the lane's row, as two
   // float4 each (clamped addresses; validity bits applied at the split)
+  typedef float f32x4 __attribute__((ext_vector_type(4)));   // (a HIP float4 copy becomes a memcpy through scratch)
   struct ASet {
     float4 v[4];
     uint32_t m;
-    float4 bq[GPT];   // the step's weight stage granules (this thread's share)
+    f32x4 bq[GPT];   // the step's weight stage granules (this thread's share)
   };
   auto load_a = [&](int s, ASet& A) {
     if (s >= steps) s = steps - 1;   // clamped re-read past the end
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     for (int i = 0; i < GPT; ++i) {
       const int g = min(tid + 256 * i, BG - 1);
       const int pl = g / (TN * 5), wi = g - pl * (TN * 5);
-      A.bq[i] = *reinterpret_cast<const float4*>(wb + (int64_t)pl * CoutP * SB_BST * 2 + wi * 16);
+      A.bq[i] = *reinterpret_cast<const f32x4*>(wb + (int64_t)pl * CoutP * SB_BST * 2 + wi * 16);
     }
   };
   bool xbad = false;   // H = 1: a gathered value past the fp16 window
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
 #pragma unroll
     for (int i = 0; i < GPT; ++i) {
       const int g = tid + 256 * i;
-      if (g < BG) *reinterpret_cast<float4*>(dst + g * 16) = A.bq[i];
+      if (g < BG) *reinterpret_cast<f32x4*>(dst + g * 16) = A.bq[i];
     }
   };
 

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--frags", type=int, default=30)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--order", default=None, help="run only this row order (e.g. mask+morton)")
+    ap.add_argument("--xcd", type=int, default=None, help="run only this xcd setting (0/1)")
     a = ap.parse_args()
     from synth import synth_scene_fragments
     from lib.sparse import voxelize, CoordinateManager
@@ -61,10 +63,17 @@ def main():
                   "mask": torch.argsort(mask, stable=True).to(torch.int32),
                   "mask+morton": perm,
                   "morton": torch.argsort(mort, stable=True).to(torch.int32),
-                  "frag+mask": torch.argsort(((out_c[:, 0].to(torch.int64) & 31) << 32) | mask, stable=True).to(torch.int32)}
+                  "frag+mask": torch.argsort(((out_c[:, 0].to(torch.int64) & 31) << 32) | mask, stable=True).to(torch.int32),
+                  # spatial cells (16^3 / 32^3 voxels of the level: the Morton code's top bits) first, mask inside
+                  "cell12+mask": torch.argsort(((mort >> 12) << 27) | mask, stable=True).to(torch.int32),
+                  "cell15+mask": torch.argsort(((mort >> 15) << 27) | mask, stable=True).to(torch.int32)}
         res = {}
         for oname, pm in orders.items():
+            if a.order and oname != a.order:
+                continue
             for xcd in (0, 1):
+                if a.xcd is not None and xcd != a.xcd:
+                    continue
                 L.mvr_set_spconv_xcd(xcd)
 
                 def go():
