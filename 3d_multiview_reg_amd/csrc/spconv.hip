@@ -369,7 +369,11 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
   if (Mout == 0) return MVR_OK;
   SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout,
            nullptr, nullptr, 0, g_spconv_xcd};
-  ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout, (double)Mout * (Cin * 4.0 * K + Cout * 4.0), s);
+  // the launch cannot see how many kernel-map entries are present (no host sync): FLOPs as if every offset were,
+  // bytes compulsory (input rows ~ output rows, the neighbour table, the weights); bench.py replaces both class
+  // totals with counts from the kernel maps
+  ProfScope prof(PK_SPCONV, 2.0 * Mout * (double)K * Cin * Cout,
+                 (double)Mout * (Cin + Cout) * 4.0 + (nbr ? (double)Mout * K * 4.0 : 0.0) + 4.0 * K * Cin * Cout, s);
   const char* base = reinterpret_cast<const char*>(wimg);
   const uint16_t* wi = reinterpret_cast<const uint16_t*>(wimg);
   const uint16_t* wi16 = reinterpret_cast<const uint16_t*>(base + sp_bf16_bytes(K, Cin, Cout));

@@ -17,8 +17,9 @@ of the hot path over one batch of synthetic input resident in HBM:
 Weak scaling: every rank processes its own scene / pair batch (different seed).
 Rank 0 prints ONE JSON line (the driver contract); the roofline object prices
 the dominant kernel class from per-launch hipEvent timings taken inside the
-timed region; cpu_baseline times the numpy oracle (oracle/) on a bounded
-sample of the same workload on this host's cores.
+timed region (plus the SURVEY §8d whole-step floor); cpu_baseline times the
+reference's CPU op sequence (oracle/torch_port.py, numpy FCGF restatement) on a
+bounded sample of the same workload on this host's cores, and on 8 threads.
 """
 import argparse
 import json
