@@ -84,19 +84,22 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
   sh[(int64_t)p * out_ld + c] = (float)((double)b - (mean * (double)rin + (double)rm) * (double)gs);
 }
 
-__global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int C, float eps_in, mvr_bn_p bn, float* sc,
-                                   float* sh, int64_t out_ld) {
+// BatchNorm statistics per group of G consecutive pairs (the reference's forward batch: G = P, or one loader batch
+// of the benchmark each, mvr_oan_block_forward bn_train > 1): blockIdx.y = group
+__global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int G, int C, float eps_in, mvr_bn_p bn,
+                                   float* sc, float* sh, int64_t out_ld) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  const int p0 = blockIdx.y * G, p1 = min(P, p0 + G);
   double bv = 0.0;
-  for (int p = 0; p < P; ++p) {
+  for (int p = p0; p < p1; ++p) {
     const double var = mv[(int64_t)p * C + c].y;
     bv += var / (var + eps_in);
   }
-  bv /= P;
+  bv /= (p1 - p0);
   const float g = bn.gamma ? bn.gamma[c] : 1.f, b = bn.gamma ? bn.beta[c] : 0.f;
   const float gs = g / sqrtf((float)bv + 1e-5f);
-  for (int p = 0; p < P; ++p) {
+  for (int p = p0; p < p1; ++p) {
     const float2 m = mv[(int64_t)p * C + c];
     const float rin = (float)(1.0 / sqrt((double)m.y + (double)eps_in));
     sc[(int64_t)p * out_ld + c] = rin * gs;
@@ -180,12 +183,15 @@ __global__ void bn_fold_eval_kernel(mvr_bn_p bn, int C, float* sc, float* sh) {
 }
 
 // train-mode BN(points): batch stats over (pairs, channels) from ST_COL partials [P][MT][Kc].
-__global__ void bn_col_train_kernel(const float2* __restrict__ st, int P, int MT, int Kc, int rows, mvr_bn_p bn,
-                                    float* sc, float* sh) {
+// per group of G pairs (blockIdx.y); the fold is written for every pair of the group (row stride ld), the
+// consumer GEMM reads it per pair
+__global__ void bn_col_train_kernel(const float2* __restrict__ st, int P, int G, int MT, int Kc, int rows, mvr_bn_p bn,
+                                    float* sc, float* sh, int64_t ld) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= Kc) return;
+  const int p0 = blockIdx.y * G, p1 = min(P, p0 + G);
   double n = 0.0, mean = 0.0, m2 = 0.0;   // Chan's merge of (sum, squared deviations) per row tile
-  for (int i = 0; i < P * MT; ++i) {
+  for (int i = p0 * MT; i < p1 * MT; ++i) {
     const float2 v = st[(int64_t)i * Kc + k];
     const double nb = (double)min(128, rows - 128 * (i % MT));
     const double d = (double)v.x / nb - mean, tot = n + nb;
@@ -195,8 +201,11 @@ __global__ void bn_col_train_kernel(const float2* __restrict__ st, int P, int MT
   }
   const double var = fmax(m2 / n, 0.0);
   const float g = bn.gamma[k] / sqrtf((float)var + 1e-5f);
-  sc[k] = g;
-  sh[k] = bn.beta[k] - (float)mean * g;
+  const float b = bn.beta[k] - (float)mean * g;
+  for (int p = p0; p < p1; ++p) {
+    sc[(int64_t)p * ld + k] = g;
+    sh[(int64_t)p * ld + k] = b;
+  }
 }
 
 // softmax partials (tile max m_t, sum_t exp(v - m_t)) [P][T][L] -> per-tile factors
@@ -374,8 +383,8 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.O2 = w.take<float>(PK * C);
   pl.sc = w.take<float>((size_t)P * 2 * C);
   pl.sh = w.take<float>((size_t)P * 2 * C);
-  pl.scK = w.take<float>(pl.Kp);
-  pl.shK = w.take<float>(pl.Kp);
+  pl.scK = w.take<float>((size_t)P * pl.Kp);   // train-mode BN over clusters: per pair (its group's statistics)
+  pl.shK = w.take<float>((size_t)P * pl.Kp);
   size_t nf = (size_t)P * TN * pl.Kp;
   if ((size_t)P * MK * pl.Np > nf) nf = (size_t)P * MK * pl.Np;
   pl.fac = pl.fused ? nullptr : w.take<float>(nf);
@@ -405,6 +414,8 @@ struct Ctx {
   const Plan& pl;
   hipStream_t s;
   int train;
+  int bn_group;   // train: BatchNorm statistics over groups of bn_group consecutive pairs
+  int ngroups() const { return (pl.P + bn_group - 1) / bn_group; }
   bool f16;   // split-fp16 launches enabled (flags zeroed)
   int err = 0;
   int nflag = 0;
@@ -427,8 +438,8 @@ struct Ctx {
                        a.tw0, a.csplit, a.tw1, a.C, a.L, eps, bn, train, sc, sh, (int64_t)a.C, pl.mv);
     chk_launch();
     if (train) {
-      hipLaunchKernelGGL(in_bn_train_kernel, dim3((a.C + 255) / 256), dim3(256), 0, s, pl.mv, pl.P, a.C, eps, bn,
-                         sc, sh, (int64_t)a.C);
+      hipLaunchKernelGGL(in_bn_train_kernel, dim3((a.C + 255) / 256, ngroups()), dim3(256), 0, s, pl.mv, pl.P,
+                         bn_group, a.C, eps, bn, sc, sh, (int64_t)a.C);
       chk_launch();
     }
   }
@@ -500,8 +511,8 @@ struct Ctx {
     Act o1{pl.O1, (int64_t)C * Kp, Kp, C, Kc, pl.stcol, Kc, 0};
     conv(f.conv1, xd, true, o1, nullptr, train ? ST_COL : ST_NONE);
     if (train) {
-      hipLaunchKernelGGL(bn_col_train_kernel, dim3((Kc + 255) / 256), dim3(256), 0, s, pl.stcol, pl.P,
-                         gemm_mtiles(C), Kc, C, f.bn2, pl.scK, pl.shK);
+      hipLaunchKernelGGL(bn_col_train_kernel, dim3((Kc + 255) / 256, ngroups()), dim3(256), 0, s, pl.stcol, pl.P,
+                         bn_group, gemm_mtiles(C), Kc, C, f.bn2, pl.scK, pl.shK, Kp);
     } else {
       hipLaunchKernelGGL(bn_fold_eval_kernel, dim3((Kc + 255) / 256), dim3(256), 0, s, f.bn2, Kc, pl.scK, pl.shK);
     }
@@ -516,7 +527,7 @@ struct Ctx {
     g.C = o2.p; g.sCb = o2.ps; g.ldc = Kp;
     g.R = pl.O1; g.sRb = (int64_t)C * Kp; g.has_res = 1;
     g.bias = f.conv2.bias; g.bias_mode = BIAS_N;
-    g.pro = PRO_A_K; g.psc = pl.scK; g.psh = pl.shK; g.sPb = 0;
+    g.pro = PRO_A_K; g.psc = pl.scK; g.psh = pl.shK; g.sPb = train ? Kp : 0;   // train: the pair's group fold
     g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
     g.prof_kind = PK_OAFILTER;
     g.flag = flag();
@@ -568,7 +579,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (!blk->l1_2[0].shortcut.weight) return MVR_EINVAL;
   const Plan pl = plan(C, Kc, Cin, P, N, workspace);
   if (workspace_bytes < pl.bytes) return MVR_EINVAL;
-  Ctx cx{pl, s, bn_train, g_gemm_h || g_pconv_h};
+  Ctx cx{pl, s, bn_train ? 1 : 0, bn_train > 1 ? std::min(bn_train, P) : P, g_gemm_h || g_pconv_h};
   if (cx.f16 && hipMemsetAsync(pl.flags, 0, sizeof(int) * FLAG_SLOTS, s) != hipSuccess) return MVR_ELAUNCH;
   const int64_t Np = pl.Np, Kp = pl.Kp;
   const int64_t CN = (int64_t)C * Np;

@@ -181,6 +181,10 @@ class OANet(nn.Module):
         # "some pair has no positive weight" bit over the ranks that share the batch) and the block's Procrustes
         # runs here with the returned counts
         self.guard_sync = None
+        # train mode: BatchNorm batch statistics per group of bn_group consecutive pairs (0: the whole forward
+        # batch, the reference).  With guard_group = bn_group = 32 one forward runs the reference benchmark's
+        # 32-pair loader batches side by side (scripts/benchmark_pairwise_registration.py:159-197)
+        self.bn_group = 0
 
     def forward(self, data):
         xs_in = data["xs"]
@@ -223,7 +227,8 @@ class OANet(nn.Module):
             res_row = None if last else N.ptr(inp[:, Cxs])
             score_row = None if last else N.ptr(inp[:, Cxs + 1])
             rc = L.mvr_oan_block_forward(
-                ctypes.byref(params), N.ptr(inp), rows * ld, ld, N.ptr(xs), Npts * Cxs, Cxs, P, Npts, int(self.training),
+                ctypes.byref(params), N.ptr(inp), rows * ld, ld, N.ptr(xs), Npts * Cxs, Cxs, P, Npts,
+                (int(self.bn_group) if self.bn_group > 1 else 1) if self.training else 0,
                 N.ptr(logits), N.ptr(scores), N.ptr(R), N.ptr(t), N.ptr(res), N.ptr(latent) if last else None,
                 res_row, score_row, rows * ld, N.ptr(guard), N.ptr(status[bi]), -1 if ext else int(self.guard_group),
                 N.ptr(ws), ws.numel(), st)

@@ -80,6 +80,13 @@ class PrecomputedWorkload:
         self.net = OANet(oanet_cfg())
         self.state = synth_module(self.net, seed=7)
         self.net = self.net.to(dev).train()
+        # the loader batches side by side in one forward: BatchNorm statistics and the zero-row guard per 32-pair
+        # group, exactly the per-batch semantics (tests/test_gpu_oanet.py::test_oanet_bn_groups_equal_batches);
+        # MVR_PRECOMP_SEQUENTIAL=1 runs one forward per batch instead
+        self.grouped = os.environ.get("MVR_PRECOMP_SEQUENTIAL", "0") != "1"
+        if self.grouped:
+            self.net.bn_group = self.BATCH
+            self.net.guard_group = self.BATCH
         xs, _, _ = synth_correspondences(pairs, npts, seed=1000 + rank)
         self.xs_host = xs
         self.xs = torch.from_numpy(xs).to(dev).unsqueeze(1)
@@ -87,6 +94,11 @@ class PrecomputedWorkload:
         self.npts = npts
 
     def step(self):
+        if self.grouped:
+            out = self.net({"xs": self.xs})
+            R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
+            conf = (s > 0.5).float().mean(dim=1, keepdim=True)
+            return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)
         recs = []
         for b0 in range(0, self.pairs, self.BATCH):
             out = self.net({"xs": self.xs[b0:b0 + self.BATCH]})
@@ -99,7 +111,8 @@ class PrecomputedWorkload:
         return {"workload": "precomputed correspondences (configs[3] shape, scripts/benchmark_pairwise_registration.py "
                             "hot loop): OANet(128ch,500 clusters,depth 12,2 blocks, train-mode BN per 32-pair batch)"
                             "+Procrustes", "pairs_per_gpu": self.pairs, "correspondences": self.npts,
-                "batch": self.BATCH}
+                "batch": self.BATCH, "batches": "one forward, per-batch BN / guard groups" if self.grouped else
+                "one forward per batch"}
 
     def cpu_baseline(self, threads, budget_s=20.0):
         """the reference's op sequence on torch CPU tensors (oracle/torch_port.py: N x N diag_embed Kabsch) over

@@ -159,7 +159,10 @@ int mvr_set_pool_split(int on);
  * pairs; < 0 the block stops after its output head — scores hold relu(tanh(logits)) unguarded, guard_pos the
  * counts, and R, t, res, res_row, score_row are left to the caller's mvr_procrustes (a guard evaluated over
  * pairs on other devices: lib/distributed.py scene mode).
- * bn_train: BatchNorm layers normalise with batch statistics (module.train()). */
+ * bn_train: 0 BatchNorm with running statistics (module.eval()); 1 batch statistics over all P pairs
+ * (module.train(): the reference's forward batch); G > 1 batch statistics per group of G consecutive pairs (the
+ * last group may be smaller) — G forwards of the reference's loader batches in one call (pair it with
+ * guard_group = G). */
 /* diff_unpool kernel choice (process-wide): 1 (default) the 4-wave, two-per-CU kernel when clusters <= 512,
  * 0 the 8-wave kernel (A/B timing).  Returns the previous setting. */
 int mvr_set_unpool4(int on);

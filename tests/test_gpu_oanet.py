@@ -239,3 +239,25 @@ def test_oanet_external_guard_equals_internal(gpu, ovr):
             assert torch.equal(outs[0][k][i], outs[1][k][i]), (k, i)
     if ovr:
         assert np.all(outs[0]["logits"][0].cpu().numpy() < 0)
+
+
+def test_oanet_bn_groups_equal_batches(gpu):
+    """bn_group = guard_group = 32 (train mode): one forward over 70 pairs equals the reference benchmark's three
+    loader batches (32, 32, 6) run one by one — BatchNorm statistics and the zero-row guard per batch (the second
+    batch's correspondences are all gross outliers and the output bias is lowered, so the batches differ in what
+    their guard sees)."""
+    import torch
+    xs, _, _ = synth_correspondences(70, 1500, seed=29)
+    xs[32:64, :, 3:] = xs[32:64, :, :3] + 5.0          # gross outliers: no positive weight in the second batch
+    net = _oanet(128, 500, 7, gpu, train=True, which="full",
+                 overrides={"reg_init.output.bias": [-3.0]})
+    X = torch.from_numpy(xs).unsqueeze(1)
+    with torch.no_grad():
+        net.bn_group, net.guard_group = 32, 32
+        a = net({"xs": X})
+        net.bn_group, net.guard_group = 0, 0
+        parts = [net({"xs": X[b0:b0 + 32]}) for b0 in range(0, 70, 32)]
+    for i in range(2):
+        for k, tol in (("logits", 2e-3), ("rot_est", 1e-4), ("trans_est", 1e-4)):
+            ref = torch.cat([p[k][i] for p in parts]).cpu().numpy()
+            np.testing.assert_allclose(a[k][i].cpu().numpy(), ref, atol=tol, rtol=1e-4 if k == "logits" else 0)
