@@ -96,6 +96,15 @@ struct NNSmem {
   int flag;
 };
 
+// Workgroup -> (pair, 128-query block): XCD-contiguous (common.hpp xcd_tile), so the query blocks of a pair, which
+// all stream the same target fragment, run on one XCD and share its L2 instead of each XCD fetching the targets
+__device__ __forceinline__ void nn_block(int& p, int& qb) {
+  const int64_t nb = (int64_t)gridDim.x * gridDim.y;
+  const int64_t t = xcd_tile((int64_t)blockIdx.y * gridDim.x + blockIdx.x, nb);
+  p = (int)(t / gridDim.x);
+  qb = (int)(t % gridDim.x);
+}
+
 // Online-softmax path (any temperature / feature scale; argmax modes).
 template <int MODE>
 __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
@@ -103,12 +112,13 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
   auto& Xs = sm.Xs;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l32 = lane & 31, kh = lane >> 5;
-  const int p = blockIdx.y;
+  int p, qb;
+  nn_block(p, qb);
   const int64_t src = a.pairs[2 * p], tgt = a.pairs[2 * p + 1];
   const float* Fq = a.Fq + src * a.fq_fs;
   const float* Ft = a.Ft + tgt * a.ft_fs;
   const float* Xt = a.Xt + tgt * a.xt_fs;
-  const int j = blockIdx.x * 128 + wid * 32 + l32;  // this lane's query
+  const int j = qb * 128 + wid * 32 + l32;  // this lane's query
   const bool jok = j < a.Nq;
   const int Mt = a.Mt;
 
@@ -350,12 +360,13 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   auto& Xf = sm.Xf;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l32 = lane & 31, kh = lane >> 5;
-  const int p = blockIdx.y;
+  int p, qb;
+  nn_block(p, qb);
   const int64_t src = a.pairs[2 * p], tgt = a.pairs[2 * p + 1];
   const float* Fq = a.Fq + src * a.fq_fs;
   const float* Ft = a.Ft + tgt * a.ft_fs;
   const float* Xt = a.Xt + tgt * a.xt_fs;
-  const int q0 = blockIdx.x * 128 + wid * 32;   // this wave's 32 queries
+  const int q0 = qb * 128 + wid * 32;   // this wave's 32 queries
   const int Mt = a.Mt;
 
   // queries = A operand rows: lane row l32, dims 16s + 8kh + (0..7)
