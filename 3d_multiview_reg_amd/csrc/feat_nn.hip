@@ -32,7 +32,13 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
-constexpr int NN_STAGE = 128;      // targets per LDS stage
+#ifndef NN_STAGE_ROWS
+#define NN_STAGE_ROWS 128
+#endif
+constexpr int NN_STAGE = NN_STAGE_ROWS;   // targets per LDS stage
+constexpr int NN_TPR = 256 / NN_STAGE;    // staging threads per target row
+constexpr int NN_FPT = 32 / NN_TPR;       // ... and the feature dims each of them loads (multiple of 8)
+static_assert(NN_STAGE % 32 == 0 && NN_FPT % 8 == 0, "stage: whole 32-target chunks, 8-dim split groups");
 constexpr int NN_ROW = 32;         // bf16 per LDS plane row; 16-byte chunk c of row r sits at slot
                                    // c ^ ((r >> 2) & 3): conflict-free ds_read_b128 down 16 rows
 constexpr float NN_NEG = -3.0e38f;
@@ -137,14 +143,14 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
   }
 
   // stage staging: thread -> target row (tid >> 1), dims 16 (tid & 1) .. +15; coords by tid < 128
-  const int srow = tid >> 1, shalf = tid & 1;
-  float4 fr[4];
+  const int srow = tid / NN_TPR, spart = tid % NN_TPR;
+  float4 fr[NN_FPT / 4];
   float xr0 = 0.f, xr1 = 0.f, xr2 = 0.f;
   auto load_regs = [&](int t0) {
     const int gi = t0 + srow;
-    const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + 16 * shalf);
+    const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + NN_FPT * spart);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int v = 0; v < NN_FPT / 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (MODE != 2 && tid < NN_STAGE) {
       const int gc = t0 + tid;
       if (gc < Mt) {
@@ -155,20 +161,21 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
   };
   auto store_lds = [&](int buf, int t0) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {   // dims 16 shalf + 8g .. +7
+    for (int g = 0; g < NN_FPT / 8; ++g) {   // dims NN_FPT spart + 8g .. +7
       u32x4 H, Mm, L;
       nn_split8(fr[2 * g], fr[2 * g + 1], H, Mm, L);
-      const int c = 8 * ((2 * shalf + g) ^ ((srow >> 2) & 3));
+      const int c = 8 * (((NN_FPT / 8) * spart + g) ^ ((srow >> 2) & 3));
       *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = H;
       *reinterpret_cast<u32x4*>(&Fp[buf][1][srow][c]) = Mm;
       *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
     }
     float n2 = 0.f;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
-    n2 += __shfl_xor(n2, 1, 64);
+    for (int v = 0; v < NN_FPT / 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
+#pragma unroll
+    for (int o = 1; o < NN_TPR; o <<= 1) n2 += __shfl_xor(n2, o, 64);
     // invalid targets: +inf -> logit -inf -> weight 0, never the argmax
-    if (shalf == 0) Xs[buf][3][srow] = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
+    if (spart == 0) Xs[buf][3][srow] = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
     if (MODE != 2 && tid < NN_STAGE) {
       Xs[buf][0][tid] = xr0;
       Xs[buf][1][tid] = xr1;
@@ -403,14 +410,14 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) init[r] = -0.5f * ACC_UNIT * __shfl(q2, 8 * (r >> 2) + 4 * kh + (r & 3), 64);
 
-  const int srow = tid >> 1, shalf = tid & 1;
-  float4 fr[4];
+  const int srow = tid / NN_TPR, spart = tid % NN_TPR;
+  float4 fr[NN_FPT / 4];
   float xr0 = 0.f, xr1 = 0.f, xr2 = 0.f;
   auto load_regs = [&](int t0) {
     const int gi = t0 + srow;
-    const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + 16 * shalf);
+    const float4* fp = reinterpret_cast<const float4*>(Ft + (int64_t)(gi < Mt ? gi : 0) * 32 + NN_FPT * spart);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int v = 0; v < NN_FPT / 4; ++v) fr[v] = gi < Mt ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (tid < NN_STAGE) {
       const int gc = t0 + tid;
       if (gc < Mt) {
@@ -421,9 +428,9 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   };
   auto store_lds = [&](int buf, int t0) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < NN_FPT / 8; ++g) {
       u32x4 Hh, Mm, L;
-      const int c = 8 * ((2 * shalf + g) ^ ((srow >> 2) & 3));
+      const int c = 8 * (((NN_FPT / 8) * spart + g) ^ ((srow >> 2) & 3));
       if (H) {
         nn_split8h(fr[2 * g], fr[2 * g + 1], Hh, L);
         *reinterpret_cast<u32x4*>(&Fp[buf][0][srow][c]) = Hh;
@@ -437,8 +444,9 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
     }
     float n2 = 0.f;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
-    n2 += __shfl_xor(n2, 1, 64);
+    for (int v = 0; v < NN_FPT / 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
+#pragma unroll
+    for (int o = 1; o < NN_TPR; o <<= 1) n2 += __shfl_xor(n2, o, 64);
     if (H) bad |= !(n2 < 16384.f);   // rows past Mt are zeros
     if (tid < NN_STAGE) {
       Xf[buf][tid].x = xr0;
@@ -446,7 +454,7 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       Xf[buf][tid].z = xr2;
     }
     // invalid targets: +inf -> logit -inf -> weight 0 (their coordinates stay finite)
-    if (shalf == 0) Xf[buf][srow].w = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
+    if (spart == 0) Xf[buf][srow].w = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
   };
 
   float S[16], AX[16], AY[16], AZ[16];
@@ -554,7 +562,10 @@ int g_nn_fast = 1;   // mvr_set_feat_nn_fast: 0 online path only, 1 fast path sp
 // MODE 0 (soft) with a.fast: the bounded-shift path, falling back to the online path for a workgroup
 // whose softmax sums underflowed; otherwise the online path (MODE 1 argmax, 2 two nearest).
 template <int MODE>
-__global__ __launch_bounds__(256, MODE == 0 ? 2 : 3) void feat_nn_kernel(NNArgs a) {
+#ifndef NN_OCC
+#define NN_OCC 2
+#endif
+__global__ __launch_bounds__(256, MODE == 0 ? NN_OCC : 3) void feat_nn_kernel(NNArgs a) {
   __shared__ __attribute__((aligned(16))) NNSmem sm;
   if (MODE == 0 && a.fast) {
     if (a.fast == 2 ? feat_nn_fast<1>(a, sm) : feat_nn_fast<0>(a, sm)) return;
