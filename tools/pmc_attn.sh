@@ -13,5 +13,5 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VA
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp -d "$OUT/p$i" -o p$i --output-format csv -- \
-    python3 "$R/tools/attn_micro.py" --only "$CASE" --iters 3 > "$OUT/p$i.log" 2>&1 || exit $?
+    python3 "$R/tools/attn_micro.py" --only "$CASE" --iters 3 --math 0 > "$OUT/p$i.log" 2>&1 || exit $?
 done
