@@ -243,6 +243,20 @@ __device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
                : "memory");
 }
 
+// the same from a wave-uniform base (SGPR pair) + 32-bit lane byte offset into the LDS byte address `lds` (wave
+// uniform): no 64-bit per-lane pointers and no generic-to-LDS pointer casts to keep live across a loop
+__device__ __forceinline__ void glds16s(const void* base, uint32_t off, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {   // byte address of a __shared__ object
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 constexpr int XT = AC * AKB * 4;   // raw fp32 key tile [128 c][32 n] (16 KB)
 template <int H> constexpr int pool_smem() {
   return 4 * planes<H>() * PLANE > 64 * ATL * 4 ? 4 * planes<H>() * PLANE : 64 * ATL * 4;
@@ -282,13 +296,18 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   // raw tile kb -> xraw[kb & 1] as [c][32] fp32 rows: wave w moves rows 16 w .. 16 w + 15 in two
   // 1 KB DMAs (lane: row + lane / 8, keys 4 (lane & 7)); keys past the end read a clamped column
   // and are zeroed when the tile is split
+  // (uniform pair base + 32-bit lane offsets: 64-bit per-lane pointers held across the key loop spilled to scratch,
+  // and each reload's vmcnt(0) also waited for the tile DMA just issued)
+  const uint32_t xraw_lds = lds_addr(xraw);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t xld4 = (uint32_t)a.xld * 4u;
   auto dma_tile = [&](int kb) {
     const int n = min(kb * AKB + 4 * (lane & 7), nlast);
-    char* dst = xraw + (kb & 1) * XT;
+    const uint32_t dst = xraw_lds + (uint32_t)((kb & 1) * XT);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int r0 = 16 * w + 8 * i;
-      glds16b(reinterpret_cast<const char*>(X + (int64_t)(r0 + (lane >> 3)) * a.xld + n), dst + r0 * 128);
+      const int r0 = 16 * wu + 8 * i;
+      glds16s(X, (uint32_t)(r0 + (lane >> 3)) * xld4 + 4u * (uint32_t)n, dst + (uint32_t)(r0 * 128));
     }
   };
   dma_tile(kb0);
@@ -417,8 +436,10 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     const char* V = K + IMGT;
     // S^T[n][j] = b[j] + sum_c xn[c][n] W[j][c] (log2 units; H = 1: times wsc), fragments one k-step ahead
     floatx16 S;
+    float bjl = bj;
+    asm volatile("" : "+v"(bjl));   // a per-stage splat: hoisted, the 16-register splat of bj stayed live (spills)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) S[r] = bj;
+    for (int r = 0; r < 16; ++r) S[r] = bjl;
     FragT<H> cur = read_k(K, 0);
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
@@ -1105,6 +1126,7 @@ extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x
   if (x_ld < round_up4(N) || (x_ld & 3) || (x_pstride & 3) || !al16(x) || !al16(weight) || !al16(out) ||
       out_ld < round_up4(clusters) || (out_ld & 3) || (out_pstride & 3) || (stats && (st_ld < channels + st_off)))
     return MVR_EINVAL;
+  if ((int64_t)AC * x_ld * 4 >= ((int64_t)1 << 31)) return MVR_EINVAL;   // 32-bit lane offsets of the tile DMAs
   if (P == 0) return MVR_OK;
   PoolArgs a{};
   a.X = x; a.xps = x_pstride; a.xld = x_ld;
