@@ -861,15 +861,25 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
 
   // W image block kb -> smem + (kb & 1) WI4 (1 KB DMAs dealt over the 4 waves; the last may be partial);
   // x_down image block kb -> smem + XDO
+  // (uniform bases + 32-bit lane offsets, fixed trip counts: the per-stage DMA issue stays a few scalar ops)
+  const uint32_t smem_lds = lds_addr(smem);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
   auto issue_w = [&](int kb) {
-    char* dst = smem + (kb & 1) * WI4;
+    const uint32_t dst = smem_lds + (uint32_t)((kb & 1) * WI4);
     const char* src = a.wimg + (int64_t)kb * WSTR;
-    for (int off = w * 1024; off < WI4; off += 4 * 1024)
-      if (off + 16 * lane < WI4) glds16b(src + off + 16 * lane, dst + off);
+#pragma unroll
+    for (int i = 0; i < (WI4 + 4095) / 4096; ++i) {
+      const int off = wu * 1024 + 4096 * i;
+      if (off < WI4 && off + 16 * lane < WI4) glds16s(src, (uint32_t)(off + 16 * lane), dst + (uint32_t)off);
+    }
   };
   auto issue_xd = [&](int kb) {
     const char* src = dimg + (int64_t)kb * XIMG;
-    for (int off = w * 1024; off < XIMG; off += 4 * 1024) glds16b(src + off + 16 * lane, smem + XDO + off);
+#pragma unroll
+    for (int i = 0; i < (XIMG + 4095) / 4096; ++i) {
+      const int off = wu * 1024 + 4096 * i;
+      if (off < XIMG) glds16s(src, (uint32_t)(off + 16 * lane), smem_lds + (uint32_t)(XDO + off));
+    }
   };
   issue_w(0);
 

@@ -90,7 +90,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res["%s/x%d" % (oname, xcd)] = e0.elapsed_time(e1) / a.iters
-        L.mvr_set_spconv_xcd(1)
+        L.mvr_set_spconv_xcd(0)
         fl = 2.0 * act * cin * cout
         print("%-16s Mout %7d active/row %.1f  %s   (useful TF/s at best %.1f)" % (
             tag, Mout, act / Mout, "  ".join("%s %.3f" % kv for kv in res.items()), fl / min(res.values()) / 1e9),
