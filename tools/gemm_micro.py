@@ -21,6 +21,7 @@ CASES = {
     "pool": (C, K, N, 3, 1, 0, 1, 0),
     "unpool": (C, N, K, 3, 0, 0, 1, 0),
     "oaf_conv2": (C, K, K, 1, 1, 2, 1, 1),    # OAFilter conv2 (oanet.hip oafilter): W2 shared, bias per n, residual
+    "conv_oaf1": (C, K, C, 2, 0, 1, 4, 0),    # OAFilter conv1 over the clusters: IN/BN/ReLU prologue, column stats
 }
 
 
