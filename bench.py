@@ -317,9 +317,9 @@ class SceneWorkload:
 
 
 def records_allgather(rec, world):
-    if world == 1:
-        return rec
     import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return rec
     out = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(out, rec.contiguous())
     return out
@@ -385,8 +385,8 @@ def timed_run(wl, args, world, pipelined, barrier):
                 json.dump(_native.prof_seq(), f)
         _native.prof_set(0)
         _native.prof_mask(None)
-    if world > 1:
-        import torch.distributed as dist
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():   # max over ranks
         tt = torch.tensor([dt], device=rec.device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
@@ -450,13 +450,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # MVR_BENCH_PG=1: the RCCL process group (barriers, record all-gather) also at one rank, to exercise the N > 1
+    # data path on a one-GPU box
+    use_pg = world > 1 or os.environ.get("MVR_BENCH_PG") == "1"
+    if use_pg:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
 
     def barrier():
-        if world > 1:
+        if use_pg:
             import torch.distributed as dist
             dist.barrier()
 
@@ -584,7 +588,7 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "accuracy": accuracy, "secondary": secondary}
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         import torch.distributed as dist
         dist.destroy_process_group()
 
