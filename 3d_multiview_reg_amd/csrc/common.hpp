@@ -53,6 +53,22 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* red) {
   __syncthreads();
 }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4): lane l's bytes from base + off land at LDS byte address
+// lds + 16 l.  base and lds wave-uniform (SGPRs), off a 32-bit lane offset: no 64-bit per-lane pointers or
+// generic-to-LDS casts stay live in a loop.  Inline asm: the compiler does not count it, so the caller waits
+// (s_waitcnt vmcnt) before the data is read.
+__device__ __forceinline__ void glds16s(const void* base, uint32_t off, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory");
+}
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(T* p) {   // byte address of a __shared__ object
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 // XCD-aware workgroup -> tile map.  Workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one, each
 // XCD with its own L2): this bijection on [0, nb) gives XCD b % 8 a contiguous range of tiles instead, so the
 // workgroups one XCD runs together work on neighbouring tiles and share what they read in its L2.

@@ -55,7 +55,15 @@ struct NNArgs {
   float* out; int64_t o_ps, o_ns;    // out(p,n,:) = [x_q(0..2) |] x_corr(0..2)
   int32_t* idx;                      // optional argmax index [P][Nq]
   int fast;                          // soft mode: try the bounded-shift path first (feat_nn_fast)
+  const char* timg; int64_t timg_fs; // optional: targets pre-split per stage (nn_presplit_kernel), bytes per fragment
 };
+
+// Pre-split target image (mvr_feat_nn_ws): per target fragment and 128-target stage, the bytes the fast path's LDS
+// stage holds — the three bf16 planes of the features in the swizzled [row][32] layout, then (x, y, z, k2 |ft|^2)
+// per target — so that a stage is two LDS-DMA copies instead of loads, splits and LDS stores in every workgroup
+// (each target fragment is staged by 40 query blocks x 29 pairs).
+constexpr int NN_IMG_PLANES = 3 * NN_STAGE * NN_ROW * 2;   // 24 KB
+constexpr int NN_IMG_STAGE = NN_IMG_PLANES + NN_STAGE * 16; // + 2 KB of (x, y, z, w)
 
 __device__ __forceinline__ unsigned nn_cvt_pk(f32x2 x) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
@@ -92,6 +100,19 @@ __device__ __forceinline__ void nn_split8h(const float4& a, const float4& b, u32
   }
 }
 __device__ __forceinline__ float nn_max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
+// |f|^2 over a stage thread's 16 dims in one fixed fma order (the stage split and the pre-split image share it:
+// identical stages)
+__device__ __forceinline__ float nn_norm16(const float4 (&fr)[4]) {
+  float n2 = 0.f;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    n2 = fmaf(fr[v].x, fr[v].x, n2);
+    n2 = fmaf(fr[v].y, fr[v].y, n2);
+    n2 = fmaf(fr[v].z, fr[v].z, n2);
+    n2 = fmaf(fr[v].w, fr[v].w, n2);
+  }
+  return n2;
+}
 
 struct NNSmem {
   unsigned short Fp[2][3][NN_STAGE][NN_ROW];   // bf16 planes h, m, l of the target features
@@ -442,9 +463,8 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
         *reinterpret_cast<u32x4*>(&Fp[buf][2][srow][c]) = L;
       }
     }
-    float n2 = 0.f;
-#pragma unroll
-    for (int v = 0; v < NN_FPT / 4; ++v) n2 += fr[v].x * fr[v].x + fr[v].y * fr[v].y + fr[v].z * fr[v].z + fr[v].w * fr[v].w;
+    static_assert(NN_FPT == 16, "nn_norm16");
+    float n2 = nn_norm16(fr);
 #pragma unroll
     for (int o = 1; o < NN_TPR; o <<= 1) n2 += __shfl_xor(n2, o, 64);
     if (H) bad |= !(n2 < 16384.f);   // rows past Mt are zeros
@@ -457,13 +477,33 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
     if (spart == 0) Xf[buf][srow].w = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
   };
 
+  // pre-split image: stage st -> buffer buf by LDS-DMA (each wave copies its 1 KB slices; completion awaited before
+  // the barrier that publishes the buffer)
+  const bool dma = !H && a.timg;
+  const char* timg = dma ? a.timg + tgt * a.timg_fs : nullptr;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  auto dma_stage = [&](int buf, int st) {
+    const char* src = timg + (int64_t)st * NN_IMG_STAGE;
+    const uint32_t fp = lds_addr(&Fp[buf][0][0][0]), xf = lds_addr(&Xf[buf][0]);
+#pragma unroll
+    for (int i = 0; i < NN_IMG_PLANES / 4096; ++i)
+      glds16s(src, (uint32_t)(i * 4096 + wu * 1024 + lane * 16), fp + (uint32_t)(i * 4096 + wu * 1024));
+    if (wu < NN_STAGE * 16 / 1024)
+      glds16s(src, (uint32_t)(NN_IMG_PLANES + wu * 1024 + lane * 16), xf + (uint32_t)(wu * 1024));
+  };
+
   float S[16], AX[16], AY[16], AZ[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) S[r] = AX[r] = AY[r] = AZ[r] = 0.f;
   const float kk2 = 2.f * a.k2 / ACC_UNIT;
   const int nst = (Mt + NN_STAGE - 1) / NN_STAGE;
-  load_regs(0);
-  store_lds(0, 0);
+  if (dma) {
+    dma_stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    load_regs(0);
+    store_lds(0, 0);
+  }
   __syncthreads();
   int cur = 0;
   auto mfma_chunk = [&](int i0) {
@@ -506,7 +546,10 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   };
   for (int st = 0; st < nst; ++st) {
     const int t0 = st * NN_STAGE;
-    if (st + 1 < nst) load_regs(t0 + NN_STAGE);
+    if (st + 1 < nst) {
+      if (dma) dma_stage(cur ^ 1, st + 1);   // buffer last read in stage st - 1
+      else load_regs(t0 + NN_STAGE);
+    }
     floatx16 acc = mfma_chunk(0);
 #pragma unroll 1
     for (int i0 = 0; i0 < NN_STAGE - 32; i0 += 32) {
@@ -515,7 +558,10 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       acc = nxt;
     }
     consume(acc, NN_STAGE - 32);
-    if (st + 1 < nst) store_lds(cur ^ 1, t0 + NN_STAGE);
+    if (st + 1 < nst) {
+      if (dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else store_lds(cur ^ 1, t0 + NN_STAGE);
+    }
     __syncthreads();
     cur ^= 1;
   }
@@ -555,6 +601,49 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
     }
   }
   return true;
+}
+
+// two threads per (fragment, padded target row), 16 dims each — the split and the norm in exactly store_lds's
+// order (bit-identical stages): the row's three bf16 planes (swizzled as the LDS stage) and, from the first thread,
+// (x, y, z, k2 |ft|^2) (+inf past Mt: weight 0)
+__global__ void nn_presplit_kernel(const float* __restrict__ Ft, int64_t ft_fs, const float* __restrict__ Xt,
+                                   int64_t xt_fs, int nfrag, int Mt, int nst, float k2, char* img, int64_t img_fs) {
+  static_assert(NN_TPR == 2 && NN_FPT == 16, "presplit mirrors the 2-threads-per-row stage");
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int spart = (int)(e & 1);
+  const int64_t rr = e >> 1;
+  const int rows = nst * NN_STAGE;
+  const bool in = rr < (int64_t)nfrag * rows;   // (whole shuffle pairs stay active)
+  const int f = in ? (int)(rr / rows) : 0, r = in ? (int)(rr - (int64_t)f * rows) : 0;
+  const int st = r / NN_STAGE, srow = r - st * NN_STAGE;
+  const bool ok = in && r < Mt;
+  float4 fr[4];
+  const float4* fp = reinterpret_cast<const float4*>(Ft + f * ft_fs + (int64_t)(ok ? r : 0) * 32 + NN_FPT * spart);
+#pragma unroll
+  for (int v = 0; v < 4; ++v) fr[v] = ok ? fp[v] : make_float4(0.f, 0.f, 0.f, 0.f);
+  char* base = img + f * img_fs + (int64_t)st * NN_IMG_STAGE;
+  constexpr int plane = NN_STAGE * NN_ROW * 2;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    u32x4 H, Mm, L;
+    nn_split8(fr[2 * g], fr[2 * g + 1], H, Mm, L);
+    const int c = 8 * ((2 * spart + g) ^ ((srow >> 2) & 3));
+    if (in) {
+      *reinterpret_cast<u32x4*>(base + (srow * NN_ROW + c) * 2) = H;
+      *reinterpret_cast<u32x4*>(base + plane + (srow * NN_ROW + c) * 2) = Mm;
+      *reinterpret_cast<u32x4*>(base + 2 * plane + (srow * NN_ROW + c) * 2) = L;
+    }
+  }
+  float n2 = nn_norm16(fr);
+  n2 += __shfl_xor(n2, 1, 64);
+  if (in && spart == 0) {
+    float4 x = make_float4(0.f, 0.f, 0.f, __builtin_inff());
+    if (ok) {
+      const float* xp = Xt + f * xt_fs + (int64_t)r * 3;
+      x = make_float4(xp[0], xp[1], xp[2], n2 * k2);
+    }
+    *reinterpret_cast<float4*>(base + NN_IMG_PLANES + srow * 16) = x;
+  }
 }
 
 int g_nn_fast = 1;   // mvr_set_feat_nn_fast: 0 online path only, 1 fast path split-bf16 (default), 2 fast path split-fp16
@@ -605,11 +694,36 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int C, const i
 
 }  // namespace mvr
 
+static int64_t nn_img_fs(int Mt) { return (int64_t)((Mt + mvr::NN_STAGE - 1) / mvr::NN_STAGE) * mvr::NN_IMG_STAGE; }
+
+extern "C" size_t mvr_feat_nn_workspace_bytes(int n_frag, int Mt) {
+  if (n_frag <= 0 || Mt <= 0) return 0;
+  return (size_t)n_frag * nn_img_fs(Mt);
+}
+
+extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride,
+                              const float* Xq, int64_t xq_fstride, const float* Xt, int64_t xt_fstride,
+                              const int64_t* pairs, int P, int Nq, int Mt, int C, float inv_tau2, int mode, float* out,
+                              int64_t out_pstride, int64_t out_nstride, int32_t* idx_out, int n_frag, void* workspace,
+                              size_t workspace_bytes, hipStream_t stream);
+
 extern "C" int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride, const float* Xq,
                            int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P,
                            int Nq, int Mt, int C, float inv_tau2, int mode, float* out, int64_t out_pstride,
                            int64_t out_nstride, int32_t* idx_out, hipStream_t stream) {
+  return mvr_feat_nn_ws(Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt, C, inv_tau2,
+                        mode, out, out_pstride, out_nstride, idx_out, 0, nullptr, 0, stream);
+}
+
+extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride,
+                              const float* Xq, int64_t xq_fstride, const float* Xt, int64_t xt_fstride,
+                              const int64_t* pairs, int P, int Nq, int Mt, int C, float inv_tau2, int mode, float* out,
+                              int64_t out_pstride, int64_t out_nstride, int32_t* idx_out, int n_frag, void* workspace,
+                              size_t workspace_bytes, hipStream_t stream) {
   if (!Fq || !Ft || !Xt || !pairs || !out || P < 0 || Nq < 0 || Mt <= 0) return MVR_EINVAL;
+  if (workspace && (n_frag <= 0 || workspace_bytes < mvr_feat_nn_workspace_bytes(n_frag, Mt) ||
+                    (reinterpret_cast<uintptr_t>(workspace) & 15)))
+    return MVR_EINVAL;
   if (C != 32) return MVR_EINVAL;  // FCGF descriptor width (fcgf.py:108 out_channels=32)
   if ((reinterpret_cast<uintptr_t>(Fq) & 15) || (reinterpret_cast<uintptr_t>(Ft) & 15) || (fq_fstride & 3) ||
       (ft_fstride & 3))
@@ -617,7 +731,19 @@ extern "C" int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft,
   if (mode != 0 && mode != 1) return MVR_EINVAL;
   if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt,
-                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out, mvr::g_nn_fast};
+                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out, mvr::g_nn_fast,
+                nullptr, 0};
+  // the split-bf16 fast path stages its targets from a pre-split image when the caller gives the workspace (the
+  // pair list's target fragments must be < n_frag)
+  if (workspace && mode == 0 && mvr::g_nn_fast == 1) {
+    const int nst = (Mt + mvr::NN_STAGE - 1) / mvr::NN_STAGE;
+    const int64_t n = (int64_t)n_frag * nst * mvr::NN_STAGE * 2;
+    hipLaunchKernelGGL(mvr::nn_presplit_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, Ft, ft_fstride,
+                       Xt, xt_fstride, n_frag, Mt, nst, a.k2, reinterpret_cast<char*>(workspace), nn_img_fs(Mt));
+    MVR_CHECK_LAUNCH();
+    a.timg = reinterpret_cast<const char*>(workspace);
+    a.timg_fs = nn_img_fs(Mt);
+  }
   mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * (C + 3) * 4 + P * Nq * 24.0,
                       stream);
   const dim3 grid((Nq + 127) / 128, P);
@@ -638,7 +764,7 @@ extern "C" int mvr_feat_knn2(const float* Fq, int64_t fq_fstride, const float* F
     return MVR_EINVAL;
   if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, nullptr, 0, Ft, 0, pairs, P, Nq, Mt, 1.4426950408889634f, 2,
-                nullptr, 0, 0, idx2_out, 0};
+                nullptr, 0, 0, idx2_out, 0, nullptr, 0};
   mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * C * 4 + P * Nq * 8.0,
                       stream);
   hipLaunchKernelGGL(mvr::feat_nn_kernel<2>, dim3((Nq + 127) / 128, P), dim3(256), 0, stream, a);

@@ -243,19 +243,7 @@ __device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
                : "memory");
 }
 
-// the same from a wave-uniform base (SGPR pair) + 32-bit lane byte offset into the LDS byte address `lds` (wave
-// uniform): no 64-bit per-lane pointers and no generic-to-LDS pointer casts to keep live across a loop
-__device__ __forceinline__ void glds16s(const void* base, uint32_t off, uint32_t lds) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(off), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds))
-               : "memory");
-}
-template <typename T>
-__device__ __forceinline__ uint32_t lds_addr(T* p) {   // byte address of a __shared__ object
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
+// (glds16s: the same from a wave-uniform base + 32-bit lane offset, common.hpp)
 
 constexpr int XT = AC * AKB * 4;   // raw fp32 key tile [128 c][32 n] (16 KB)
 template <int H> constexpr int pool_smem() {

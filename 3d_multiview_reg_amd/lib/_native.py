@@ -84,6 +84,9 @@ _SIGS = {
                                       c_size, c_vp]),
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "mvr_feat_nn_workspace_bytes": (c_size, [c_int, c_int]),
+    "mvr_feat_nn_ws": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
+                               c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_int, c_vp, c_size, c_vp]),
     "mvr_gather_rows": (c_int, [c_vp, c_int, c_vp, c_int, c_vp, c_vp]),
     "mvr_sample_rand_mt19937": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
     "mvr_feat_knn2": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),

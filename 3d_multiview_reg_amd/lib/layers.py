@@ -54,10 +54,12 @@ class Soft_NN(torch.nn.Module):
         pairs int64 [P,2] (query frag, target frag) -> out(p, i, :) = [xyz_q | x_corr]."""
         P = pairs.shape[0]
         B, n, C = f_frag.shape
-        N.check(N.lib().mvr_feat_nn(N.ptr(f_frag), n * C, N.ptr(f_frag), n * C,
-                                    N.ptr(xyz_frag) if with_query_xyz else None, n * 3, N.ptr(xyz_frag), n * 3,
-                                    N.ptr(pairs), P, n, n, C, self._inv_tau2(), self.mode(), N.ptr(out),
-                                    out_pstride, out_nstride, None, N.stream()), "mvr_feat_nn")
+        L = N.lib()
+        ws = N.workspace(L.mvr_feat_nn_workspace_bytes(B, n), f_frag.device)   # pre-split target stages
+        N.check(L.mvr_feat_nn_ws(N.ptr(f_frag), n * C, N.ptr(f_frag), n * C,
+                                 N.ptr(xyz_frag) if with_query_xyz else None, n * 3, N.ptr(xyz_frag), n * 3,
+                                 N.ptr(pairs), P, n, n, C, self._inv_tau2(), self.mode(), N.ptr(out),
+                                 out_pstride, out_nstride, None, B, N.ptr(ws), ws.numel(), N.stream()), "mvr_feat_nn_ws")
         return out
 
     def forward(self, x_f, y_f, y_c):

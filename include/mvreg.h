@@ -292,6 +292,14 @@ int mvr_feat_nn(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft
                 int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P, int Nq, int Mt,
                 int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
                 int32_t* idx_out, mvr_stream_t stream);
+/* mvr_feat_nn with a workspace (mvr_feat_nn_workspace_bytes(n_frag, Mt), 16-byte aligned): the soft fast path then
+ * splits the target fragments' features once per call into an image of its LDS stages (Ft holds n_frag fragments of
+ * Mt targets; every pair's target index < n_frag) and stages them by LDS-DMA.  Results identical to mvr_feat_nn. */
+size_t mvr_feat_nn_workspace_bytes(int n_frag, int Mt);
+int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride, const float* Xq,
+                   int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P, int Nq,
+                   int Mt, int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
+                   int32_t* idx_out, int n_frag, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 /* Soft mode runs a bounded-shift softmax first (shift k2 |fs|^2 per query instead of a running maximum:
  * no max tracking or rescaling) and falls back to the online softmax per 128-query workgroup where a
  * softmax sum underflows (< 2^-60).  1 (default) on with three-term split-bf16 distances (6 MFMAs,

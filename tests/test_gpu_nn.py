@@ -106,3 +106,34 @@ def test_sampler_indices_and_gather(gpu):
         idx = sc[..., 0].long()
         assert np.array_equal(idx.cpu().numpy(), g["idx_" + tag])
         assert torch.equal(sf, F[idx])
+
+
+@pytest.mark.parametrize("n,m,scale", [(5000, 5000, 1.0), (1000, 777, 1.0), (33, 4097, 1.0), (2000, 2000, 2.5)])
+def test_feat_nn_presplit_image_identical(gpu, n, m, scale):
+    """mvr_feat_nn_ws (targets split once per call into an image of the LDS stages, staged by LDS-DMA) against
+    mvr_feat_nn (each workgroup loads and splits its stages): bit-identical outputs, soft and argmax modes, ragged
+    target counts (partial last stage), fragments whose softmax sums underflow (workgroup fallback, scale 2.5)"""
+    import torch
+    from lib import _native as NV
+    B = 4
+    L_ = max(n, m)
+    f = unit_features(B, L_, 32, seed=n + m + 1)
+    f[1] *= np.float32(scale)
+    x = np.random.RandomState(9).uniform(-2, 2, (B, L_, 3)).astype(np.float32)
+    pairs = np.array([[0, 1], [2, 3], [3, 0], [1, 1], [1, 2]], dtype=np.int64)
+    tf, tx, tp = (torch.from_numpy(a).to(gpu) for a in (f, x, pairs))
+    L = NV.lib()
+    nb = L.mvr_feat_nn_workspace_bytes(B, m)
+    ws = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    for mode in (0, 1):
+        outs = []
+        for use_ws in (False, True):
+            out = torch.full((len(pairs), n, 6), float("nan"), device=gpu)
+            args = (NV.ptr(tf), L_ * 32, NV.ptr(tf), L_ * 32, NV.ptr(tx), L_ * 3, NV.ptr(tx), L_ * 3, NV.ptr(tp),
+                    len(pairs), n, m, 32, 1.0 / 0.09, mode, NV.ptr(out), n * 6, 6, None)
+            rc = (L.mvr_feat_nn_ws(*args, B, NV.ptr(ws), nb, NV.stream()) if use_ws
+                  else L.mvr_feat_nn(*args, NV.stream()))
+            assert rc == 0
+            outs.append(out.cpu().numpy())
+        assert np.array_equal(outs[0], outs[1]), np.nanmax(np.abs(outs[0] - outs[1]))
+    assert L.mvr_feat_nn_ws(*args, B, NV.ptr(ws), nb - 16, NV.stream()) == -1   # workspace too small

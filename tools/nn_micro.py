@@ -17,6 +17,7 @@ if __name__ == "__main__":
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--frags", type=int, default=30)
     ap.add_argument("--fast", type=int, default=1)
+    ap.add_argument("--no-ws", action="store_true")
     a = ap.parse_args()
     d = torch.device("cuda")
     B, N, C = a.frags, 5000, 32
@@ -30,9 +31,13 @@ if __name__ == "__main__":
     L = NV.lib()
     L.mvr_set_feat_nn_fast(a.fast)
 
-    def go():
-        rc = L.mvr_feat_nn(NV.ptr(F), N * C, NV.ptr(F), N * C, NV.ptr(X), N * 3, NV.ptr(X), N * 3, NV.ptr(pairs), P, N, N,
-                           C, 1.0 / 0.09, a.mode, NV.ptr(out), N * 6, 6, None, NV.stream())
+    nb = L.mvr_feat_nn_workspace_bytes(B, N)
+    ws = torch.empty(nb, dtype=torch.uint8, device=d)
+
+    def go():   # the pipeline's form: targets pre-split into the workspace (mvr_feat_nn_ws); --no-ws: mvr_feat_nn
+        args = (NV.ptr(F), N * C, NV.ptr(F), N * C, NV.ptr(X), N * 3, NV.ptr(X), N * 3, NV.ptr(pairs), P, N, N,
+                C, 1.0 / 0.09, a.mode, NV.ptr(out), N * 6, 6, None)
+        rc = L.mvr_feat_nn(*args, NV.stream()) if a.no_ws else L.mvr_feat_nn_ws(*args, B, NV.ptr(ws), nb, NV.stream())
         assert rc == 0
     for _ in range(2):
         go()
