@@ -41,8 +41,56 @@ __device__ __forceinline__ uint64_t pack_key(int b, int x, int y, int z) {
          ((uint64_t)((uint32_t)(y + KEY_BIAS) & KEY_MASK) << 17) | (uint64_t)((uint32_t)(z + KEY_BIAS) & KEY_MASK);
 }
 
-__device__ __forceinline__ int64_t hash_find(const HashView& h, uint64_t key) {
-  uint64_t s = mix64(key) & (h.cap - 1);
+// Home slot of a key.  t < 0: a hashed slot.  t >= 0 (coordinate tables of a level whose coordinates are
+// multiples of 2^t): every voxel of a 2x2x2 cell of that lattice has the first slot of the cell's hashed 8-slot
+// bucket (64 bytes of keys) as its home, so the cell's voxels sit side by side and a 3^3 stencil's 27 probes scan
+// the buckets of <= 8 cells (shared by the neighbouring outputs) instead of 27 scattered lines.  (A slot per cell
+// bit triple inside the bucket was slower: buckets hold ~2.3 keys at the tables' load, cells ~3 of their 8 voxels,
+// so per-voxel slots made the buckets overflow into long probe chains.)  Linear probing from the home either way.
+__device__ __forceinline__ uint64_t hash_home(const HashView& h, uint64_t key, int t) {
+  if (t < 0) return mix64(key) & (h.cap - 1);
+  const uint64_t cell = key & ~((1ULL << t) | (1ULL << (17 + t)) | (1ULL << (34 + t)));
+  return (mix64(cell) << 3) & (h.cap - 1);
+}
+// where an insert into a lattice table starts probing: the voxel's cell bit triple inside its bucket (the voxels of
+// one cell, inserted side by side by neighbouring threads, then do not all race for the bucket's first slot)
+__device__ __forceinline__ int lattice_sub(uint64_t key, int t) {
+  return (int)(((key >> t) & 1) | (((key >> (17 + t)) & 1) << 1) | (((key >> (34 + t)) & 1) << 2));
+}
+
+// lookup in a lattice table (t >= 0): the home bucket's 8 keys in one round trip (4 x 16-byte loads).  The insert
+// probed from slot lattice_sub of the home bucket onwards, so an empty slot at or after it in the home bucket, or
+// anywhere in a later bucket, that the key is not before proves it absent (slots never empty again)
+__device__ __forceinline__ int64_t hash_find_bucket(const HashView& h, uint64_t key, int t) {
+  uint64_t b = hash_home(h, key, t);
+  int from = lattice_sub(key, t);
+  for (uint64_t n = 0; n < h.cap; n += 8) {
+    const uint4* kp = reinterpret_cast<const uint4*>(h.keys + b);
+    uint64_t k[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 u = kp[q];
+      k[2 * q] = ((uint64_t)u.y << 32) | u.x;
+      k[2 * q + 1] = ((uint64_t)u.w << 32) | u.z;
+    }
+    int hit = -1;
+    bool empty = false;
+#pragma unroll
+    for (int j = 7; j >= 0; --j) {
+      if (k[j] == key) hit = j;
+      empty |= j >= from && k[j] == EMPTY_KEY;
+    }
+    if (hit >= 0) return h.vals[b + hit];
+    if (empty) return -1;
+    b = (b + 8) & (h.cap - 1);
+    from = 0;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int64_t hash_find(const HashView& h, uint64_t key, int t = -1) {
+  if (t >= 0) return hash_find_bucket(h, key, t);
+  uint64_t s = hash_home(h, key, t);
   for (uint64_t probe = 0; probe < h.cap; ++probe) {
     const uint64_t k = h.keys[s];
     if (k == key) return h.vals[s];
@@ -56,8 +104,8 @@ __device__ __forceinline__ int64_t hash_find(const HashView& h, uint64_t key) {
 // never changes once set and its value only decreases, so a (possibly stale) read that already shows
 // the key with a value <= v proves the atomic unnecessary — duplicate keys (raw points of one voxel)
 // then skip the contended CAS / atomicMin on their slot.
-__device__ __forceinline__ void hash_insert_min(HashView h, uint64_t key, int32_t v) {
-  uint64_t s = mix64(key) & (h.cap - 1);
+__device__ __forceinline__ void hash_insert_min(HashView h, uint64_t key, int32_t v, int t = -1) {
+  uint64_t s = hash_home(h, key, t) + (t >= 0 ? lattice_sub(key, t) : 0);
   for (uint64_t probe = 0; probe < h.cap; ++probe) {
     unsigned long long cur = h.keys[s];
     if (cur == EMPTY_KEY)
@@ -100,8 +148,9 @@ __device__ __forceinline__ int64_t hash_slot(const HashView& h, uint64_t key) {
   return -1;
 }
 
-__global__ void hash_clear_kernel(HashView h) {
+__global__ void hash_clear_kernel(HashView h, int t = -1) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && h.hdr) h.hdr[0] = t;   // the home mode of the table (read by its lookups)
   if (i < h.cap) {
     h.keys[i] = EMPTY_KEY;
     h.vals[i] = 0x7fffffff;
@@ -228,11 +277,11 @@ __global__ void batch_count_kernel(const int4* __restrict__ coords, int B, int64
     if (hist[b]) atomicAdd(reinterpret_cast<unsigned long long*>(&counts[1 + b]), (unsigned long long)hist[b]);
 }
 
-__global__ void build_table_kernel(const int4* __restrict__ c, int64_t M, HashView h) {
+__global__ void build_table_kernel(const int4* __restrict__ c, int64_t M, HashView h, int t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < M) {
     const int4 v = c[i];
-    hash_insert_min(h, pack_key(v.x, v.y, v.z, v.w), (int32_t)i);
+    hash_insert_min(h, pack_key(v.x, v.y, v.z, v.w), (int32_t)i, t);
   }
 }
 
@@ -248,7 +297,9 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
   const int r = ks / 2;
   const int dx = k % ks - r, dy = (k / ks) % ks - r, dz = k / (ks * ks) - r;
   const int4 c = oc[o];
-  const int64_t v = hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step, c.w + sign * dz * step));
+  const int t = h.hdr[0];   // uniform: the table's home mode
+  const int64_t v =
+      hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step, c.w + sign * dz * step), t);
   nbr[e] = (int32_t)v;
 }
 
@@ -531,6 +582,7 @@ HashView hash_view(void* table, size_t bytes) {
   h.cap = cap;
   h.keys = reinterpret_cast<uint64_t*>(base + 16);
   h.vals = reinterpret_cast<int32_t*>(base + 16 + cap * 8);
+  h.hdr = reinterpret_cast<int32_t*>(base);
   return h;
 }
 
@@ -676,17 +728,27 @@ extern "C" int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, in
   return dedup_run(d, M, reinterpret_cast<int4*>(coords_out), nullptr, counts_out, B, s);
 }
 
-extern "C" int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_bytes, hipStream_t s) {
+static int hash_build(const int32_t* coords, int64_t M, int t, void* table, size_t table_bytes, hipStream_t s) {
   if (!coords || M < 0 || !table) return MVR_EINVAL;
   if (table_bytes < hash_table_bytes(M)) return MVR_EINVAL;
   HashView h = hash_view(table, table_bytes);
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)h.cap * 12 + M * 28.0, s);
-  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)h.cap)), dim3(256), 0, s, h);
+  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)h.cap)), dim3(256), 0, s, h, t);
   if (M > 0)
     hipLaunchKernelGGL(build_table_kernel, dim3(nblk(M)), dim3(256), 0, s, reinterpret_cast<const int4*>(coords), M,
-                       h);
+                       h, t);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_bytes, hipStream_t s) {
+  return hash_build(coords, M, -1, table, table_bytes, s);
+}
+
+extern "C" int mvr_hash_build_lattice(const int32_t* coords, int64_t M, int stride, void* table, size_t table_bytes,
+                                      hipStream_t s) {
+  if (stride <= 0 || (stride & (stride - 1)) || stride > (1 << 15)) return MVR_EINVAL;
+  return hash_build(coords, M, __builtin_ctz((unsigned)stride), table, table_bytes, s);
 }
 
 extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,

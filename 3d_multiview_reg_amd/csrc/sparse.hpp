@@ -15,6 +15,7 @@ struct HashView {
   uint64_t* keys;
   int32_t* vals;
   uint64_t cap;  // power of two
+  int32_t* hdr;  // table header (plain tables: word 0 = the home mode, see hash_home); null for brick maps
 };
 
 size_t hash_table_bytes(int64_t M);

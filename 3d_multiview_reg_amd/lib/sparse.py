@@ -46,7 +46,8 @@ class CoordinateManager:
             L = N.lib()
             nb = L.mvr_hash_table_bytes(c.shape[0])
             t = torch.empty(nb, dtype=torch.uint8, device=self.device)
-            N.check(L.mvr_hash_build(N.ptr(c), c.shape[0], N.ptr(t), nb, N.stream()), "mvr_hash_build")
+            N.check(L.mvr_hash_build_lattice(N.ptr(c), c.shape[0], s, N.ptr(t), nb, N.stream()),
+                    "mvr_hash_build_lattice")
             self.tables[s] = t
         return self.tables[s]
 

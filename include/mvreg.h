@@ -348,6 +348,12 @@ size_t mvr_coords_downsample_workspace_bytes(int64_t M);
 int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, int stride_out, void* workspace,
                           size_t workspace_bytes, int32_t* coords_out, int64_t* counts_out, mvr_stream_t stream);
 int mvr_hash_build(const int32_t* coords, int64_t M, void* table, size_t table_bytes, mvr_stream_t stream);
+/* the same for a coordinate set on the lattice of `stride` (a power of two: every coordinate a multiple of it, the
+ * tensor stride of an FCGF level): the 2x2x2 cells of that lattice share one 8-slot bucket of the table, so a kernel
+ * map's stencil probes read a few runs instead of scattered slots (MinkowskiEngine's CoordinateManager keeps one map
+ * per tensor stride likewise, fcgf.py:118-227).  Same lookups and results as mvr_hash_build. */
+int mvr_hash_build_lattice(const int32_t* coords, int64_t M, int stride, void* table, size_t table_bytes,
+                           mvr_stream_t stream);
 /* kernel map as a neighbour table nbr[o][k] (k = (dx+r) + ks(dy+r) + ks^2(dz+r)):
  * row of out_coords[o] + sign*off_k*step in the input table (sign -1 if transposed), or -1 */
 int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,

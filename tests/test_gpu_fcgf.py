@@ -72,6 +72,50 @@ def test_kernel_map_k7_property(gpu, frags):
     assert np.array_equal(nbr[nbr[o, k], K - 1 - k], o)
 
 
+@pytest.mark.parametrize("stride", [1, 2, 4])
+def test_lattice_table_kernel_maps_dense_and_sparse(gpu, stride):
+    """mvr_hash_build_lattice (cells of 8 voxels share a bucket): dense blocks fill whole buckets so inserts overflow
+    into the next ones, beside scattered voxels and two batches; the kernel maps (s1, transposed) equal the hashed
+    table's (mvr_hash_build) and a brute-force dictionary lookup"""
+    import torch
+    from lib import _native as N
+    L = N.lib()
+    rng = np.random.default_rng(3 + stride)
+    pts = set()
+    for b in range(2):
+        g = np.arange(-6, 6) * stride
+        for x in g:
+            for y in g:
+                for z in g[:4]:
+                    pts.add((b, int(x), int(y), int(z)))
+        for _ in range(3000):
+            pts.add((b,) + tuple(int(v) * stride for v in rng.integers(-200, 200, 3)))
+    coords = np.array(sorted(pts, key=lambda p: rng.random()), dtype=np.int32)
+    M = len(coords)
+    cd = torch.from_numpy(coords).to(gpu)
+    nb = L.mvr_hash_table_bytes(M)
+    tl = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    th = torch.empty(nb, dtype=torch.uint8, device=gpu)
+    N.check(L.mvr_hash_build_lattice(N.ptr(cd), M, stride, N.ptr(tl), nb, N.stream()), "lattice")
+    N.check(L.mvr_hash_build(N.ptr(cd), M, N.ptr(th), nb, N.stream()), "hashed")
+    assert L.mvr_hash_build_lattice(N.ptr(cd), M, 3, N.ptr(tl), nb, N.stream()) != 0   # not a power of two
+    index = {tuple(r): i for i, r in enumerate(coords.tolist())}
+    for tr in (0, 1):
+        maps = []
+        for t in (tl, th):
+            nbr = torch.empty(M, 27, dtype=torch.int32, device=gpu)
+            N.check(L.mvr_kernel_map(N.ptr(cd), M, N.ptr(t), nb, 3, stride, tr, N.ptr(nbr), N.stream()), "map")
+            maps.append(nbr.cpu().numpy())
+        np.testing.assert_array_equal(maps[0], maps[1])
+        sg = -1 if tr else 1
+        ref = np.full((M, 27), -1, np.int32)
+        for o, (b, x, y, z) in enumerate(coords.tolist()):
+            for k in range(27):
+                dx, dy, dz = k % 3 - 1, (k // 3) % 3 - 1, k // 9 - 1
+                ref[o, k] = index.get((b, x + sg * dx * stride, y + sg * dy * stride, z + sg * dz * stride), -1)
+        np.testing.assert_array_equal(maps[0], ref)
+
+
 def test_fcgf_forward_matches_oracle(gpu, frags):
     """split-bf16 sparse convs on mvr_spconv_wimage images; the oracle is our restatement of ME's sparse conv
     (parity unpinned: ME is absent)"""
