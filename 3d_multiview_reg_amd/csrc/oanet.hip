@@ -1,7 +1,7 @@
 // OANet inlier-weight block (lib/filtering/oanet.py:132-185) on MI355X.
 //
 // The host orchestrator below issues, per block, ~70 stream-ordered launches of
-// the fused fp32-MFMA GEMM (gemm.hip) plus small finalize kernels.  Every
+// the fused split-bf16 MFMA GEMMs (gemm.hip, pconv.hip) plus small finalize kernels.  Every
 // InstanceNorm / BatchNorm / ReLU / softmax / residual of the reference is fused
 // into a GEMM prologue or epilogue; only per-(pair,channel) statistics travel
 // between launches (a few KB).  Activations are [P][C][L] (pair, channel,

@@ -1,4 +1,4 @@
-"""Fused fp32-MFMA GEMM (csrc/gemm.hip) vs a float64 numpy reference, every
+"""Fused split-bf16 (fp32-equivalent) MFMA GEMM (csrc/gemm.hip) vs a float64 numpy reference, every
 prologue/epilogue combination the OANet schedule uses, ragged shapes, padded rows."""
 import numpy as np
 import pytest

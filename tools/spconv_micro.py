@@ -1,6 +1,6 @@
 """Micro-benchmark of the sparse 3^3 convolution (csrc/spconv.hip) on a real kernel map: the synthetic
 3DMatch-scale scene (tests/golden/synth.py, 30 fragments, 0.025 m voxels), every FCGF level, both
-arithmetic paths (exact fp32 MFMA; split-bf16 with pre-split weights), timed with HIP events.
+split-bf16 arithmetic with pre-split weights, timed with HIP events.
 usage: python tools/spconv_micro.py [--frags 30] [--iters 10] [--only s1:1:64:64]"""
 import argparse
 import os
