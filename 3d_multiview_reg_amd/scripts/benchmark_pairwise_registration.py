@@ -49,12 +49,6 @@ SHORT_NAMES = {
     "redwood": {"iclnuim-livingroom1": "livingroom1", "iclnuim-livingroom2": "livingroom2",
                 "iclnuim-office1": "office1", "iclnuim-office2": "office2"}}
 
-REGBLOCK = {"misc": {"net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128, "use_gpu": True,
-                     "normalize_weights": True},
-            "data": {"use_mutuals": 0, "max_num_points": 5000},
-            "method": {"task": "pairwise", "descriptor_module": None, "filter_module": "oanet"},
-            "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
-
 
 def _save_path(source_path, method, mutuals):
     return os.path.join(source_path, "results", method) + ("/mutuals/" if mutuals else "/all/")
@@ -71,12 +65,10 @@ def _ransac(xs, keep=None, seed=0):
 
 
 def load_model(method, model_path, cfg_path=None):
+    """benchmark:155-169: the method's YAML, read with load_config exactly as the reference does (a missing file
+    is an error there and here), then lib.config.get_model and the optional checkpoint"""
     cfg_path = cfg_path or os.path.join("./configs/pairwise_registration/eval", method + ".yaml")
-    if os.path.exists(cfg_path):
-        cfg = load_config(cfg_path)
-    else:
-        logging.warning("config %s not found: using the RegBlock configuration", cfg_path)
-        cfg = REGBLOCK
+    cfg = load_config(cfg_path)
     model = config.get_model(cfg)
     if model_path:
         ckpt = CheckpointIO("/".join(model_path.split("/")[0:-1]), initialize_from=None,
@@ -190,7 +182,7 @@ def parser():
     ap.add_argument("--only_gt_overlaping", action="store_true", help="Only the GT overlapping pairs")
     ap.add_argument("--refine", action="store_true", help="RANSAC over the network's inliers")
     ap.add_argument("--config", default=None, type=str, help="filtering config YAML (default ./configs/pairwise_"
-                    "registration/eval/<method>.yaml, else the RegBlock configuration)")
+                    "registration/eval/<method>.yaml, as the reference reads it)")
     ap.add_argument("--seed", type=int, default=0, help="RANSAC draw stream seed")
     ap.add_argument("--num_workers", type=int, default=4)
     return ap

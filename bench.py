@@ -126,8 +126,9 @@ class PrecomputedWorkload:
                 torch_port.oanet_forward(self.state, torch.from_numpy(self.xs_host[n:n + self.BATCH]), train=True)
                 n += min(self.BATCH, self.pairs - n)
         dt = time.time() - t0
-        return n / dt, "%d pairs in batches of %d (oracle/torch_port.py, reference op sequence incl. N x N diag_embed " \
-                       "Kabsch, train-mode BN), measured" % (n, self.BATCH)
+        return n / dt, ("%d pairs in batches of %d (oracle/torch_port.py, reference op sequence incl. N x N diag_embed "
+                        "Kabsch, train-mode BN), measured" % (n, self.BATCH)), \
+            {"extrapolated": n < self.pairs, "pairs_timed": n, "batches_timed": -(-n // self.BATCH)}
 
 
 class SceneWorkload:
@@ -276,9 +277,12 @@ class SceneWorkload:
         t_batch = time.time() - t1
         nb = -(-self.pairs // B)
         v = self.pairs / (self.n_frag * t_fcgf + nb * t_batch)
-        return v, ("measured FCGF %.2fs/fragment (1 fragment, numpy sparse-conv restatement) + %.2fs per 32-pair batch "
-                   "(2x Soft_NN + OANet + diag_embed Kabsch, oracle/torch_port.py); scene rate = %d pairs / "
-                   "(%d x t_fcgf + %d x t_batch)" % (t_fcgf, t_batch, self.pairs, self.n_frag, nb))
+        return v, ("EXTRAPOLATED from 1 timed fragment and 1 timed batch: FCGF %.2fs/fragment (numpy sparse-conv "
+                   "restatement) + %.2fs per 32-pair batch (2x Soft_NN + OANet + diag_embed Kabsch, oracle/torch_port.py);"
+                   " scene rate = %d pairs / (%d x t_fcgf + %d x t_batch)"
+                   % (t_fcgf, t_batch, self.pairs, self.n_frag, nb)), \
+            {"extrapolated": True, "fragments_timed": 1, "batches_timed": 1, "t_fcgf_s": round(t_fcgf, 3),
+             "t_batch_s": round(t_batch, 3)}
 
     def fcgf_work(self):
         """Algorithmic work of one FCGF forward over the scene's fragments (lib/descriptor/fcgf.py:229-280), counted
@@ -369,13 +373,27 @@ def timed_run(wl, args, world, pipelined, barrier):
         _native.prof_set(0 if args.no_prof else 1)
         barrier()
         torch.cuda.synchronize()
+        # per-step boundaries for the median: an event on every stream a step enqueues on, recorded after the
+        # step; step i ends when the last of them completes (events only, no host synchronisation per step)
+        marks = wl.streams[:2] if pipelined else (torch.cuda.current_stream(),)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(torch.cuda.current_stream())
+        step_ev = []
         t0 = time.perf_counter()
         for _ in range(args.steps):
             rec = run_step()
+            evs = []
+            for st_ in marks:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(st_)
+                evs.append(e)
+            step_ev.append(evs)
         torch.cuda.synchronize()
         barrier()
         t1 = time.perf_counter()
         dt = t1 - t0
+        ends = [max(ev0.elapsed_time(e) for e in evs) for evs in step_ev]
+        step_ms = np.diff([0.0] + ends)
         prof = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
         if prof_all is None:
             prof_all = {k: tuple(x / max(args.steps, 1) for x in v) for k, v in prof.items()}
@@ -390,34 +408,65 @@ def timed_run(wl, args, world, pipelined, barrier):
         tt = torch.tensor([dt], device=rec.device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    return dt, rec, prof, prof_all, dom
+    return dt, rec, prof, prof_all, dom, step_ms
+
+
+def _oanet_golden(dev, fx, seed, xs):
+    from lib.filtering.oanet import OANet
+    net = OANet(oanet_cfg())
+    synth_module(net, seed=seed)
+    net = net.to(dev).train()
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(xs).to(dev).unsqueeze(1)})
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", fx)))
+    return out, g
+
+
+def _errs(out, ref, i, suffix=""):
+    P = out["rot_est"][i].shape[0]
+    dR = np.abs(out["rot_est"][i].cpu().numpy() - ref["R%d%s" % (i, suffix)]).reshape(P, -1).max(1)
+    dt = np.abs(out["trans_est"][i].cpu().numpy() - ref["t%d%s" % (i, suffix)]).reshape(P, -1).max(1)
+    return dR, dt
 
 
 def golden_accuracy(dev):
-    """max |R - R_ref|, |t - t_ref| of the OANet (RegBlock network, train-mode BN) on the full-size golden
-    (tests/golden/oanet_full_train.npz: the reference's own outputs, 32 pairs x 5000 correspondences) and
-    against our float64 restatement of the same inputs (oanet_full_train_f64.npz), at the current maths"""
-    from lib.filtering.oanet import OANet
+    """R / t error of the OANet (RegBlock network, train-mode BN: the benchmark's mode) at the current maths, on
+    full-size reference fixtures of 32 pairs x 5000 correspondences:
+      * strict (headline): tests/golden/oanet_full_train_strict.npz, well conditioned (the reference's fp32 output
+        within 1e-5 of the reference's own float64 output): per-block maxima vs the reference's fp32 and fp64
+        outputs, the number of pairs over north_star's 1e-4 bound, mask mismatches away from 0.5;
+      * stress: tests/golden/oanet_full_train.npz, chaotic in block 1 (the reference's own fp32 output sits up to
+        2.6e-4 from exact arithmetic there; oanet_full_train_f64.npz = our float64 restatement)."""
     from synth import synth_correspondences
-    gd = os.path.join(ROOT, "tests", "golden")
-    g = dict(np.load(os.path.join(gd, "oanet_full_train.npz")))
-    g64 = dict(np.load(os.path.join(gd, "oanet_full_train_f64.npz")))
-    net = OANet(oanet_cfg())
-    synth_module(net, seed=7)
-    net = net.to(dev).train()
-    xs, _, _ = synth_correspondences(32, 5000, seed=33)
-    with torch.no_grad():
-        out = net({"xs": torch.from_numpy(xs).to(dev).unsqueeze(1)})
-    r = {}
-    for ref, tag in ((g, "ref"), (g64, "f64")):
-        r["max_R_err_vs_" + tag] = max(float(np.abs(out["rot_est"][i].cpu().numpy() - ref["R%d" % i]).max())
-                                       for i in range(2))
-        r["max_t_err_vs_" + tag] = max(float(np.abs(out["trans_est"][i].cpu().numpy() - ref["t%d" % i]).max())
-                                       for i in range(2))
-    masks = sum(int(((out["scores"][i].cpu().numpy() > 0.5) != (g["scores%d" % i] > 0.5))
-                    [np.abs(g["scores%d" % i] - 0.5) >= 1e-4].sum()) for i in range(2))
-    r["mask_mismatches_vs_ref"] = masks
-    return {k: (round(v, 8) if isinstance(v, float) else v) for k, v in r.items()}
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "oanet_full_train_strict.npz")))
+    p = json.loads(str(g["params"]))
+    xs, _, _ = synth_correspondences(32, 5000, seed=p["xs_seed"], inlier_lo=p["inlier_lo"], inlier_hi=p["inlier_hi"])
+    out, g = _oanet_golden(dev, "oanet_full_train_strict.npz", p["weights_seed"], xs)
+    r = {"fixture": "oanet_full_train_strict.npz (32 pairs x 5000, train-mode BN, well conditioned)"}
+    over = 0
+    for i in range(2):
+        for suffix, tag in (("", "ref"), ("_f64", "ref_f64")):
+            dR, dt = _errs(out, g, i, suffix)
+            r["block%d_max_R_err_vs_%s" % (i, tag)] = round(float(dR.max()), 8)
+            r["block%d_max_t_err_vs_%s" % (i, tag)] = round(float(dt.max()), 8)
+            if tag == "ref":
+                over += int(((dR > 1e-4) | (dt > 1e-4)).sum())
+    r["max_R_err_vs_ref"] = max(r["block%d_max_R_err_vs_ref" % i] for i in range(2))
+    r["max_t_err_vs_ref"] = max(r["block%d_max_t_err_vs_ref" % i] for i in range(2))
+    r["pair_blocks_over_1e-4"] = over
+    r["mask_mismatches_vs_ref"] = sum(int(((out["scores"][i].cpu().numpy() > 0.5) != (g["scores%d" % i] > 0.5))
+                                          [np.abs(g["scores%d" % i] - 0.5) >= 1e-4].sum()) for i in range(2))
+    xs2, _, _ = synth_correspondences(32, 5000, seed=33)
+    out2, g2 = _oanet_golden(dev, "oanet_full_train.npz", 7, xs2)
+    g64 = dict(np.load(os.path.join(ROOT, "tests", "golden", "oanet_full_train_f64.npz")))
+    st = {}
+    for ref, tag in ((g2, "ref"), (g64, "f64_restatement")):
+        st["max_R_err_vs_" + tag] = round(max(float(_errs(out2, ref, i)[0].max()) for i in range(2)), 8)
+        st["max_t_err_vs_" + tag] = round(max(float(_errs(out2, ref, i)[1].max()) for i in range(2)), 8)
+    st["ref_fp32_vs_f64_max"] = round(max(float(np.abs(g2[k % i] - g64[k % i]).max()) for i in range(2)
+                                          for k in ("R%d", "t%d")), 8)
+    r["stress"] = st
+    return r
 
 
 def main():
@@ -473,7 +522,7 @@ def main():
         wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
     pipelined = args.workload == "scene" and not args.no_pipeline
 
-    dt, rec, prof, prof_all, dom = timed_run(wl, args, world, pipelined, barrier)
+    dt, rec, prof, prof_all, dom, step_ms = timed_run(wl, args, world, pipelined, barrier)
     pairs_per_step = int(rec.shape[-2]) * world
     value = pairs_per_step * args.steps / dt
     ms_step = dt / args.steps * 1e3
@@ -556,12 +605,13 @@ def main():
     if not args.no_secondary and args.workload == "scene":
         other = "split16" if args.math == "f32eq" else "f32eq"
         oinfo = _native.set_math(other)
-        odt, orec, _, _, _ = timed_run(wl, args, world, pipelined, barrier)
+        odt, orec, _, _, _, ostep = timed_run(wl, args, world, pipelined, barrier)
         if rank == 0:
             acc_o = golden_accuracy(dev)
         _native.set_math(args.math)
         secondary = {"math": other, "dtype": oinfo["dtype"], "value": round(pairs_per_step * args.steps / odt, 3),
-                     "ms_per_step": round(odt / args.steps * 1e3, 3)}
+                     "ms_per_step": round(odt / args.steps * 1e3, 3),
+                     "ms_per_step_median": round(float(np.median(ostep)), 3)}
         if rank == 0:
             secondary["accuracy"] = acc_o
     if rank == 0:
@@ -571,13 +621,16 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the box's CPU share per GPU (OMP_NUM_THREADS is set to it there; affinity shows the whole host)
         cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-        v, sample = wl.cpu_baseline(cores, args.cpu_budget)
-        v8, _ = wl.cpu_baseline(8, args.cpu_budget)
-        cpu = {"value": round(v, 4), "unit": "pairs/s", "cores": cores, "kind": "port", "sample": sample,
-               "value_8_threads": round(v8, 4)}
+        v, sample, extra = wl.cpu_baseline(cores, args.cpu_budget)
+        v8, _, _ = wl.cpu_baseline(8, args.cpu_budget)
+        cpu = dict({"value": round(v, 4), "unit": "pairs/s", "cores": cores, "kind": "port", "sample": sample,
+                    "value_8_threads": round(v8, 4)}, **extra)
     line = {"metric": METRIC if args.workload == "scene" else METRIC + " [filter+SVD only: precomputed corr.]",
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "ms_per_step_median": round(float(np.median(step_ms)), 3),
+            "ms_per_step_min_max": [round(float(step_ms.min()), 3), round(float(step_ms.max()), 3)],
+            "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
             "config": dict(wl.config(), math=args.math,
                            parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,

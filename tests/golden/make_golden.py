@@ -92,7 +92,8 @@ def main():
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=HERE)
     ap.add_argument("--only", default=None, help="comma-separated fixture groups to (re)write: kabsch, oanet, "
-                    "oanet_full_train, softnn, sampler, pairs, pairwise, mutuals, evalharness (default: all)")
+                    "oanet_full_train, oanet_full_train_strict, softnn, sampler, pairs, pairwise, mutuals, evalharness, "
+                    "configs (default: all)")
     args = ap.parse_args()
     only = set(args.only.split(",")) if args.only else None
 
@@ -127,6 +128,8 @@ def main():
         oanet_fixtures(O, out, meta)
     if want("oanet_full_train"):
         oanet_full_train_fixture(O, out, meta)
+    if want("oanet_full_train_strict"):
+        oanet_full_train_strict_fixture(O, out, meta)
     if want("softnn"):
         softnn_fixture(L, out, meta)
     if want("sampler"):
@@ -139,6 +142,8 @@ def main():
         mutuals_fixture(U, out, meta)
     if want("evalharness"):
         evalharness_fixture(U, out, meta)
+    if want("configs"):
+        configs_fixture(U, args.ref, out, meta)
     with open(mpath, "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("wrote golden fixtures to", out)
@@ -191,6 +196,43 @@ def oanet_full_train_fixture(O, out, meta):
     meta["fixtures"]["oanet_full_train.npz"] = ("lib/filtering/oanet.py:218-265 train-mode BatchNorm (the benchmark's "
                                                 "mode), RegBlock network C=128,K=500, B=32 x N=5000, weights "
                                                 "synth_state(seed 7), xs = synth_correspondences(32,5000,seed=33)")
+
+
+STRICT_TRAIN = {"weights_seed": 19, "xs_seed": 40, "inlier_lo": 0.2, "inlier_hi": 0.5}
+
+
+def oanet_full_train_strict_fixture(O, out, meta):
+    """The benchmark's mode (train-mode BatchNorm over one 32-pair batch, RegBlock network at full size) on a
+    WELL-CONDITIONED input, so north_star's R/t <= 1e-4 can be enforced on every pair of both blocks.  The
+    chaotic fixture above (oanet_full_train.npz) has pairs where the reference's own fp32 result sits 2.6e-4 from
+    exact arithmetic; here the weights seed and the (structured, 20-50 % inlier) correspondences were chosen
+    from a seed scan so that the reference's fp32 output is within 1e-5 of the reference's own float64 forward
+    (the same module, net.double()) on every pair — that fp64 output is stored beside it (R%d_f64, t%d_f64)."""
+    import hashlib
+    import torch
+    p = STRICT_TRAIN
+    xs, _, _ = synth_correspondences(32, 5000, seed=p["xs_seed"], inlier_lo=p["inlier_lo"], inlier_hi=p["inlier_hi"])
+    cfg = small_cfg(net_channel=128, clusters=500)
+    _, o = run_oanet(O, cfg, xs, seed=p["weights_seed"], train=True)
+    o.pop("latent")
+    torch.manual_seed(0)
+    net = O.OANet(cfg)
+    load_state(net, p["weights_seed"])
+    net = net.double().train(True)
+    with torch.no_grad():
+        o64 = net({"xs": torch.from_numpy(xs).double().unsqueeze(1)})
+    for i in range(2):
+        o["R%d_f64" % i] = o64["rot_est"][i].numpy()
+        o["t%d_f64" % i] = o64["trans_est"][i].numpy()
+        gap = max(np.abs(o["R%d" % i] - o["R%d_f64" % i]).max(), np.abs(o["t%d" % i] - o["t%d_f64" % i]).max())
+        assert gap < 1e-5, ("not well conditioned", i, gap)
+    np.savez_compressed(os.path.join(out, "oanet_full_train_strict.npz"),
+                        xs_sha1=np.asarray(hashlib.sha1(xs.tobytes()).hexdigest()),
+                        params=np.asarray(json.dumps(p, sort_keys=True)), **o)
+    meta["fixtures"]["oanet_full_train_strict.npz"] = (
+        "lib/filtering/oanet.py:218-265 train-mode BatchNorm, RegBlock network C=128,K=500, B=32 x N=5000, weights "
+        "synth_state(seed 19), xs = synth_correspondences(32,5000,seed=40,inliers 20-50%%); reference fp32 output and "
+        "the reference module's own float64 output (R%d_f64/t%d_f64): well conditioned, fp32-fp64 gap < 1e-5")
 
 
 def oanet_fixtures(O, out, meta):
@@ -430,6 +472,56 @@ def evalharness_fixture(U, out, meta):
     meta["fixtures"]["evalharness.npz"] = ("lib/utils.py:438-637 write/read_trajectory, read_trajectory_info, "
                                            "extract_corresponding_trajectors, computeTransformationErr (mat2quat "
                                            "restated: unpinned), evaluate_registration at err2 0.2 / 0.05")
+
+
+CONFIGS = ("configs/pairwise_registration/demo/config.yaml", "configs/pairwise_registration/eval/RegBlock.yaml")
+
+
+def configs_fixture(U, ref, out, meta):
+    """The reference's own YAMLs (data files, copied byte for byte to tests/golden/configs/) and what the
+    reference's factory builds from each: lib/utils.py:19-33 load_config -> lib/config.py:9-25 get_model ->
+    lib/pairwise/config.py:7-37.  Recorded per file: the parsed dict, the PairwiseReg attributes, the filter's
+    attributes and its state-dict key -> shape map.  The demo config names the FCGF descriptor, which needs
+    MinkowskiEngine (absent): the reference's get_descriptor is given a parameter-free placeholder, so the
+    descriptor's keys stay parity-unpinned and only the rest of the model is recorded."""
+    import functools
+    import shutil
+    import torch
+    import lib.layers as L
+    L.Soft_NN.__init__ = functools.partialmethod(L.Soft_NN.__init__, device="cpu")
+    import lib.config as RC
+    import lib.pairwise.config as RPC
+    real_get_descriptor = RPC.get_descriptor
+    RPC.get_descriptor = lambda cfg, device: (torch.nn.Identity() if cfg["method"]["descriptor_module"]
+                                              else real_get_descriptor(cfg, device))
+    rec = {}
+    for rel in CONFIGS:
+        src = os.path.join(ref, rel)
+        dst = os.path.join(out, rel)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copyfile(src, dst)
+        cfg = U.load_config(src)
+        model = RC.get_model(cfg)
+        f = model.filtering_module
+        r = {"cfg": cfg,
+             "pairwise": {"samp_type": model.samp_type, "corr_type": model.corr_type,
+                          "precomputed_desc": bool(model.precomputed_desc), "mutuals": bool(model.mutuals),
+                          "train_descriptor": bool(model.train_descriptor)},
+             "filter": {"class": type(f).__name__, "iter_num": int(f.iter_num), "side_channel": bool(f.side_channel),
+                        "keys": {k: list(v.shape) for k, v in f.state_dict().items()}}}
+        if not model.precomputed_desc:
+            r["pairwise"].update({"targeted_num_points": int(model.sampler.targeted_num_points),
+                                  "sampler_samp_type": model.sampler.samp_type,
+                                  "matching_corr_type": model.feature_matching.corr_type,
+                                  "matching_st": bool(model.feature_matching.st),
+                                  "descriptor": "placeholder (FCGF needs MinkowskiEngine: keys unpinned)"})
+        rec[rel] = r
+    RPC.get_descriptor = real_get_descriptor
+    with open(os.path.join(out, "config_models.json"), "w") as fh:
+        json.dump(rec, fh, indent=0, sort_keys=True)
+    meta["fixtures"]["config_models.json"] = ("lib/utils.py:19-33 load_config + lib/config.py:9-25 get_model on the "
+                                              "reference's demo/config.yaml and eval/RegBlock.yaml (copied under "
+                                              "configs/): PairwiseReg / filter attributes and filter state-dict keys")
 
 
 if __name__ == "__main__":

@@ -9,7 +9,12 @@ import os
 import numpy as np
 import pytest
 
+from conftest import GOLDEN
 from synth import random_rotation
+
+DEMO = os.path.join(GOLDEN, "demo")
+# the reference's configs/pairwise_registration/demo/config.yaml, unchanged (tests/golden/configs/)
+DEMO_CFG = os.path.join(GOLDEN, "configs", "pairwise_registration", "demo", "config.yaml")
 
 pytestmark = pytest.mark.gpu
 
@@ -67,12 +72,13 @@ def test_ransac_method_registers_every_pair(gpu, tmp_path):
 
 
 @pytest.mark.parametrize("refine", [False, True])
-def test_filter_method_plumbing(gpu, tmp_path, refine):
+def test_filter_method_plumbing(gpu, tmp_path, monkeypatch, refine):
     from scripts.benchmark_pairwise_registration import main
     root = str(tmp_path)
     _scene(os.path.join(root, "redwood"), scene="iclnuim-office1", n_frag=4, n_corr=600)
     argv = ["--source_path", root, "--dataset", "redwood", "--method", "RegBlock", "--batch_size", "32",
             "--num_workers", "0"] + (["--refine"] if refine else [])
+    monkeypatch.chdir(GOLDEN)     # the reference's eval/RegBlock.yaml, read from ./configs/... as benchmark:159 does
     s = main(argv)
     assert 0.0 <= s["recall"] <= 1.0 and "iclnuim-office1" in s["scenes"]
     assert os.path.exists(os.path.join(root, "redwood", "results", "RegBlock", "all", "iclnuim-office1", "traj.txt"))
@@ -80,7 +86,6 @@ def test_filter_method_plumbing(gpu, tmp_path, refine):
 
 def test_pairwise_demo(gpu, tmp_path, monkeypatch):
     """scripts/pairwise_demo.py mirror: two synthetic fragments (PLY) -> est_T.log in the reference's place"""
-    import yaml
     from lib.ply import write_ply_xyz
     from lib.utils import read_trajectory, load_config
     from synth import synth_scene_fragments
@@ -88,15 +93,8 @@ def test_pairwise_demo(gpu, tmp_path, monkeypatch):
     frags, _ = synth_scene_fragments(n_frag=2, seed=5, n_pts=60000)
     for k in range(2):
         write_ply_xyz(str(tmp_path / ("cloud_bin_%d.ply" % k)), frags[k])
-    cfg = {"misc": {"voxel_size": 0.025, "net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128,
-                    "use_gpu": True, "normalize_weights": True},
-           "data": {"use_mutuals": 0, "max_num_points": 5000},
-           "method": {"task": "pairwise", "descriptor_module": "fcgf", "filter_module": "oanet"},
-           "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
-    with open(tmp_path / "config.yaml", "w") as f:
-        yaml.safe_dump(cfg, f)
     monkeypatch.chdir(tmp_path)
-    a = parser().parse_args([str(tmp_path / "config.yaml"), "--source_pc", str(tmp_path / "cloud_bin_0.ply"),
+    a = parser().parse_args([DEMO_CFG, "--source_pc", str(tmp_path / "cloud_bin_0.ply"),
                              "--target_pc", str(tmp_path / "cloud_bin_1.ply"), "--verbose"])
     T = main(load_config(a.config), a)
     keys, traj = read_trajectory(str(tmp_path / "data/demo/pairwise/results/est_T.log"))
@@ -105,16 +103,14 @@ def test_pairwise_demo(gpu, tmp_path, monkeypatch):
     np.testing.assert_allclose(T[:3, :3] @ T[:3, :3].T, np.eye(3), atol=1e-5)
 
 
-DEMO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "demo")
 
 
 def test_pairwise_demo_reference_pair(gpu, tmp_path, monkeypatch):
     """scripts/pairwise_demo.py mirror on the reference's own demo pair (data/demo/pairwise/raw_data/
-    cloud_bin_{0,1}.ply, committed as fixtures) with configs/pairwise_registration/demo/config.yaml's settings:
+    cloud_bin_{0,1}.ply, committed as fixtures) read through the reference's own configs/pairwise_registration/demo/config.yaml (unchanged):
     voxelisation at 0.025 m gives the 18,977 / 19,082 voxels of SURVEY §2.3, and the whole path (FCGF -> rand
     5000 samples -> soft NN -> OANet -> Procrustes) writes est_T.log.  The pretrained weights are download-only
     (offline here): random-init FCGF / OANet, so the estimate itself is not compared."""
-    import yaml
     import torch
     from lib.ply import read_ply_xyz
     from lib.sparse import voxelize
@@ -125,16 +121,8 @@ def test_pairwise_demo_reference_pair(gpu, tmp_path, monkeypatch):
     assert [len(p) for p in pcs] == [258342, 268977]
     _, _, counts, _ = voxelize([torch.from_numpy(np.ascontiguousarray(p, dtype=np.float32)) for p in pcs], 0.025, gpu)
     assert list(counts) == [18977, 19082]
-    cfg = {"method": {"task": "pairwise", "descriptor_module": "fcgf", "filter_module": "oanet"},
-           "misc": {"net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128, "use_gpu": True,
-                    "normalize_weights": True, "inlier_weight_threshold": 0.5, "voxel_size": 0.025,
-                    "matching_voxel_size": 0.0375},
-           "data": {"use_mutuals": True, "mutual_nn_thresh": 0.025, "max_num_points": 5000},
-           "train": {"samp_type": "rand", "corr_type": "soft", "st_grad_flag": False}}
-    with open(tmp_path / "config.yaml", "w") as f:
-        yaml.safe_dump(cfg, f)
     monkeypatch.chdir(tmp_path)
-    a = parser().parse_args([str(tmp_path / "config.yaml"), "--source_pc", src, "--target_pc", tgt])
+    a = parser().parse_args([DEMO_CFG, "--source_pc", src, "--target_pc", tgt])
     T = main(load_config(a.config), a)
     keys, traj = read_trajectory(str(tmp_path / "data/demo/pairwise/results/est_T.log"))
     assert keys.tolist() == [["0", "1", "True"]]

@@ -106,7 +106,8 @@ def test_oanet_full_golden(gpu):
 
 
 def test_oanet_full_train_golden(gpu):
-    """The benchmark's mode (scripts/benchmark_pairwise_registration.py:159-197 never calls model.eval():
+    """STRESS fixture (the strict bound is enforced on the well-conditioned oanet_full_train_strict.npz below).
+    The benchmark's mode (scripts/benchmark_pairwise_registration.py:159-197 never calls model.eval():
     BatchNorm on the statistics of each 32-pair batch) at full size against the reference (RegBlock network,
     32 pairs x 5000 correspondences).  Masks identical away from 0.5 in both blocks; block 0 R, t within 1e-4.
     This random network is chaotic in block 1 (it consumes block 0's residuals): there the reference's own fp32
@@ -135,6 +136,34 @@ def test_oanet_full_train_golden(gpu):
             else:
                 assert (d <= np.maximum(1e-4, 2 * dist(r32, r64))).all(), (i, k, d, dist(r32, r64))
                 assert (d <= 1e-4).sum() >= 30, (i, k, d)
+    assert out["gradient_flag"] == bool(g["gradient_flag"])
+
+
+def test_oanet_full_train_strict_golden(gpu):
+    """north_star's bound on the benchmark's mode: train-mode BatchNorm over one 32-pair batch, RegBlock network,
+    32 pairs x 5000 correspondences, on the well-conditioned reference fixture (the reference's fp32 output sits
+    within 1e-5 of its own fp64 output on every pair).  R and t within 1e-4 of the reference on EVERY pair of
+    BOTH blocks, inlier masks identical away from 0.5 (|score - 0.5| < 1e-4, counted), logits within 2e-3."""
+    import json
+    import torch
+    from test_oracle_golden import strict_train_inputs
+    g, xs, _ = strict_train_inputs()
+    seed = json.loads(str(g["params"]))["weights_seed"]
+    net = _oanet(128, 500, seed, gpu, train=True, which="full")
+    with torch.no_grad():
+        out = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
+    for i in range(2):
+        sc, ref = out["scores"][i].cpu().numpy(), g["scores%d" % i]
+        near = np.abs(ref - 0.5) < 1e-4
+        assert near.sum() <= 16, near.sum()
+        assert np.array_equal((sc > 0.5)[~near], (ref > 0.5)[~near]), i
+        np.testing.assert_allclose(out["logits"][i].cpu().numpy(), g["logits%d" % i], atol=2e-3, rtol=1e-4)
+        for k, kg in (("rot_est", "R"), ("trans_est", "t")):
+            got = out[k][i].cpu().numpy()
+            d = np.abs(got - g["%s%d" % (kg, i)]).reshape(32, -1).max(1)
+            assert (d <= 1e-4).all(), (i, k, d.max())
+            d64 = np.abs(got - g["%s%d_f64" % (kg, i)]).reshape(32, -1).max(1)
+            assert (d64 <= 1e-4).all(), (i, k, d64.max())
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
 

@@ -116,7 +116,8 @@ def test_pairwise_composition_matches_reference():
 
 
 def test_oracle_full_train_golden():
-    """oracle/oanet.py in train mode (the benchmark's BatchNorm mode) at full size against the reference:
+    """STRESS fixture (chaotic block 1; the strict bound is enforced on oanet_full_train_strict.npz).
+    oracle/oanet.py in train mode (the benchmark's BatchNorm mode) at full size against the reference:
     block 0 R, t within 1e-4 on every pair; block 1 (chaotic random network) within max(1e-4, 2 x the
     reference's own distance from exact arithmetic, oanet_full_train_f64.npz); masks identical away from 0.5."""
     import hashlib
@@ -134,6 +135,35 @@ def test_oracle_full_train_golden():
             d = dist(o[k][i], g["%s%d" % (kg, i)])
             bound = 1e-4 if i == 0 else np.maximum(1e-4, 2 * dist(g["%s%d" % (kg, i)], g64["%s%d" % (kg, i)]))
             assert (d <= bound).all(), (i, k, d.max())
+
+
+def strict_train_inputs():
+    """inputs of oanet_full_train_strict.npz, regenerated from the parameters stored in it"""
+    import hashlib
+    import json
+    from synth import synth_correspondences
+    g = golden("oanet_full_train_strict.npz")
+    p = json.loads(str(g["params"]))
+    xs, _, _ = synth_correspondences(32, 5000, seed=p["xs_seed"], inlier_lo=p["inlier_lo"], inlier_hi=p["inlier_hi"])
+    assert hashlib.sha1(xs.tobytes()).hexdigest() == str(g["xs_sha1"])
+    return g, xs, synth_state(_shapes("full"), seed=p["weights_seed"])
+
+
+def test_oracle_full_train_strict_f64_equals_reference_f64():
+    """The well-conditioned benchmark-mode fixture: oracle/oanet.py in float64 against the reference module's own
+    float64 forward (net.double(), train-mode BN, B = 32 x 5000) — equal to rounding (1e-10) in both blocks, and
+    the masks equal the reference's fp32 masks away from 0.5.  This pins the oracle at full size in the
+    benchmark's mode."""
+    g, xs, st = strict_train_inputs()
+    o = oanet_forward(st, xs, train=True, dtype=np.float64)
+    for i in range(2):
+        np.testing.assert_allclose(o["rot_est"][i], g["R%d_f64" % i], atol=1e-10)
+        np.testing.assert_allclose(o["trans_est"][i], g["t%d_f64" % i], atol=1e-10)
+        near = np.abs(g["scores%d" % i] - 0.5) < 1e-4
+        assert np.array_equal((o["scores"][i] > 0.5)[~near], (g["scores%d" % i] > 0.5)[~near])
+        # the fixture is well conditioned: the reference's fp32 result is within 1e-5 of its fp64 result
+        assert np.abs(g["R%d" % i] - g["R%d_f64" % i]).max() < 1e-5
+        assert np.abs(g["t%d" % i] - g["t%d_f64" % i]).max() < 1e-5
 
 
 @pytest.mark.parametrize("fx,train", [("oanet_small_eval.npz", False), ("oanet_small_train.npz", True)])
