@@ -62,22 +62,47 @@ def pack_records(first_pair, R, t, scores, flag=None):
     return rec
 
 
-def gather_records(rec, P, world, group=GROUP):
+def _host_staged(pg=None):
+    """gloo moves host tensors only: device tensors are staged through host memory (the CPU tests and the
+    several-ranks-on-one-GPU rehearsal run gloo; RCCL takes device tensors directly)."""
+    import torch.distributed as dist
+    return dist.get_backend(pg) == "gloo"
+
+
+def all_reduce_max(t, pg=None):
+    """in-place MAX all-reduce of a small tensor (host-staged under gloo)"""
+    import torch.distributed as dist
+    if _host_staged(pg) and t.device.type != "cpu":
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=pg)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=pg)
+    return t
+
+
+def all_gather_rows(buf, world, pg=None):
+    """[world * rows, ...] = every rank's equal-shape `buf` in rank order (host-staged under gloo)"""
+    import torch.distributed as dist
+    if _host_staged(pg):
+        h = buf.cpu()
+        parts = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(parts, h, group=pg)
+        return torch.cat(parts).to(buf.device)
+    out = torch.empty((world * buf.shape[0],) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
+    dist.all_gather_into_tensor(out, buf.contiguous(), group=pg)
+    return out
+
+
+def gather_records(rec, P, world, group=GROUP, pg=None):
     """All-gather every rank's block of records (padded to block_capacity rows) and return the
     [P, 16] records of all pairs in pair order, on every rank."""
     if world == 1:
         return rec
-    import torch.distributed as dist
     cap = block_capacity(P, world, group)
     buf = torch.zeros(cap, REC, dtype=rec.dtype, device=rec.device)
     buf[:rec.shape[0]] = rec
-    if dist.get_backend() == "gloo":
-        parts = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(parts, buf)
-        out = torch.cat(parts)
-    else:
-        out = torch.empty(world * cap, REC, dtype=rec.dtype, device=rec.device)
-        dist.all_gather_into_tensor(out, buf)
+    out = all_gather_rows(buf, world, pg)
     rows = []
     for r in range(world):
         s, e = shard_pairs(P, world, r, group)
@@ -92,16 +117,17 @@ def unpack_records(rec):
             a[:, 14] > 0)
 
 
-def scene_guard_sync(world):
+def scene_guard_sync(world, pg=None):
     """guard_sync for OANet (lib.filtering.oanet.OANet.guard_sync): the zero-row guard over the pairs of every
     rank.  guard_pos [p] int32 (positive weights per local pair) -> counts that fire the local guard exactly when
-    some pair on SOME rank has none: one all-reduce (MAX) of the local bit, no host synchronisation."""
+    some pair on SOME rank has none: one all-reduce (MAX) of the local bit, no host synchronisation (RCCL).
+    The returned counts only steer the guard (mvr_procrustes tests them for a zero and uses them for nothing
+    else), so forcing the first one to 0 fires it for every local pair."""
     def sync(guard_pos):
         bit = (guard_pos == 0).any().to(torch.int32).reshape(1) if guard_pos.numel() else \
             torch.zeros(1, dtype=torch.int32, device=guard_pos.device)
         if world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(bit, op=dist.ReduceOp.MAX)
+            all_reduce_max(bit, pg)
         if guard_pos.numel() == 0:
             return guard_pos
         g = guard_pos.clone()
@@ -110,27 +136,45 @@ def scene_guard_sync(world):
     return sync
 
 
-def register_pairs_sharded(model, filtering_input, world, rank, group=GROUP, guard="group"):
+def register_pairs_sharded(model, filtering_input, world, rank, group=GROUP, guard="group", pg=None,
+                           first_pair=None):
     """Run model.filter_correspondences on this rank's block of the pair batch and all-gather the records.
-    guard="group": the zero-row guard evaluated per `group` pairs (the reference's batch-32 evaluation);
-    guard="scene": over the whole batch of all ranks (the reference's PairwiseReg.forward over a scene).
+    guard="group": the zero-row guard evaluated per `group` pairs (the reference's batch-32 evaluation), and in
+    train mode the BatchNorm batch statistics per `group` pairs too (the benchmark's 32-pair loader batches,
+    scripts/benchmark_pairwise_registration.py:159-197, which never calls model.eval());
+    guard="scene": over the whole batch of all ranks (the reference's PairwiseReg.forward over a scene, eval mode:
+    train-mode statistics over a batch split across ranks would need an exchange of BatchNorm moments, which
+    this path does not do, so it raises).
     `filtering_input` is the dict of lib/utils.py:construct_filtering_input_data over ALL pairs (every rank
-    holds it)."""
+    holds it), or — with first_pair given — only this rank's block [first_pair, first_pair + n) of a batch of
+    filtering_input["num_pairs"] pairs (the bench's pair-sharded scene: each rank matches its own block)."""
     if guard not in ("group", "scene"):
         raise ValueError(guard)
     xs = filtering_input["xs"]
-    P = xs.shape[0]
-    s, e = shard_pairs(P, world, rank, group)
+    if first_pair is None:
+        P = xs.shape[0]
+        s, e = shard_pairs(P, world, rank, group)
+        xs_mine = xs[s:e]
+    else:
+        P = int(filtering_input["num_pairs"])
+        s, e = shard_pairs(P, world, rank, group)
+        if (s, e) != (first_pair, first_pair + xs.shape[0]):
+            raise ValueError("block [%d, %d) is not rank %d's shard [%d, %d)" % (first_pair, first_pair + xs.shape[0],
+                                                                                rank, s, e))
+        xs_mine = xs
     filt = model.filtering_module if hasattr(model, "filtering_module") else model
-    sync = scene_guard_sync(world) if guard == "scene" else None
+    if guard == "scene" and filt.training:
+        raise ValueError("guard='scene' shards an eval-mode forward (train-mode BatchNorm statistics would span ranks)")
+    sync = scene_guard_sync(world, pg) if guard == "scene" else None
     if e > s:
-        prev = (filt.guard_group, filt.guard_sync)
+        prev = (filt.guard_group, filt.guard_sync, getattr(filt, "bn_group", 0))
         filt.guard_group, filt.guard_sync = (group, None) if guard == "group" else (0, sync)
+        filt.bn_group = group if guard == "group" else 0
         try:
-            out = model.filter_correspondences({"xs": xs[s:e]}) if hasattr(model, "filter_correspondences") \
-                else model({"xs": xs[s:e]})
+            out = model.filter_correspondences({"xs": xs_mine}) if hasattr(model, "filter_correspondences") \
+                else model({"xs": xs_mine})
         finally:
-            filt.guard_group, filt.guard_sync = prev
+            filt.guard_group, filt.guard_sync, filt.bn_group = prev
         rec = pack_records(s, out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1],
                            out.get("gradient_flag"))
     else:
@@ -138,4 +182,4 @@ def register_pairs_sharded(model, filtering_input, world, rank, group=GROUP, gua
             for _ in range(1 + getattr(filt, "iter_num", 0)):
                 sync(torch.zeros(0, dtype=torch.int32, device=xs.device))
         rec = torch.zeros(0, REC, device=xs.device)
-    return gather_records(rec, P, world, group)
+    return gather_records(rec, P, world, group, pg)

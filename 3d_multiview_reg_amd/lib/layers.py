@@ -127,13 +127,18 @@ class Sampler(torch.nn.Module):
 
     def forward(self, input_C, input_F, pts_list):
         N.require_hip(input_F)
-        idx = self.indices(pts_list, input_C)
+        return self.gather(input_C, input_F, self.indices(pts_list, input_C))
+
+    def gather(self, input_C, input_F, idx):
+        """sampled (coordinates [B, k, 3], features [B, k, C]) at global row indices idx [B, k] (lib/layers.py:
+        146-152's index_select per fragment, one launch each for all fragments)"""
+        N.require_hip(input_F)
+        B = idx.shape[0]
         if idx.device.type == "cpu":
             # the host draws reach the device through pinned memory without blocking the host (a pageable
             # copy would wait for everything already queued on the stream, i.e. the whole FCGF pass)
             idx = idx.pin_memory().to(input_F.device, non_blocking=True)
         idx = idx.reshape(-1).contiguous()
-        B = len(pts_list)
         C = input_F.float().contiguous()
         X = input_C.float().contiguous()
         k = idx.numel() // B

@@ -108,6 +108,9 @@ class PrecomputedWorkload:
             recs.append(torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1))   # [b, 13] records
         return torch.cat(recs)
 
+    def gather(self, rec, world):
+        return records_allgather(rec, world)
+
     def config(self):
         return {"workload": "precomputed correspondences (configs[3] shape, scripts/benchmark_pairwise_registration.py "
                             "hot loop): OANet(128ch,500 clusters,depth 12,2 blocks, train-mode BN per 32-pair batch)"
@@ -135,7 +138,8 @@ class SceneWorkload:
     """configs[2]: one synthetic 3DMatch-scale scene per GPU (30 fragments, ~20k voxels each)."""
     name = "scene"
 
-    def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025, samp="rand"):
+    def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025, samp="rand", shard="scenes", world=1,
+                 groups=None):
         import lib.config
         from synth import synth_scene_fragments
         cfg = oanet_cfg()
@@ -146,39 +150,104 @@ class SceneWorkload:
         self.model = lib.config.get_model(cfg)
         self.state = synth_module(self.model, seed=7)
         self.model = self.model.to(dev).eval()
-        self.frags, self.poses = synth_scene_fragments(n_frag, seed=41 + 1000 * rank)
-        self.raw = [torch.from_numpy(f).to(dev) for f in self.frags]     # resident in HBM
+        self.shard, self.world, self.rank = shard, world, rank
+        # scenes: every rank its own scene (weak scaling); pairs: ONE scene, its fragments and pairs split over the
+        # ranks (strong scaling, north_star's pair-sharded batch)
+        self.frags, self.poses = synth_scene_fragments(n_frag, seed=41 + (1000 * rank if shard == "scenes" else 0))
         self.dev, self.voxel, self.npts, self.n_frag = dev, voxel, npts, n_frag
-        self.rng_seed = 41 + rank
+        self.rng_seed = 41 + (rank if shard == "scenes" else 0)
         self.pairs = n_frag * (n_frag - 1) // 2
         self.vox_counts = None
+        if shard == "pairs":
+            from lib import distributed as D
+            from lib.utils import pair_index
+            # fragments: contiguous blocks of ceil(n_frag / world) (FCGF + sampling of its block per rank);
+            # pairs: contiguous blocks of the lexicographic pair list (feature NN + OANet + Procrustes per rank)
+            self.fper = -(-n_frag // world)
+            self.f0, self.f1 = min(rank * self.fper, n_frag), min((rank + 1) * self.fper, n_frag)
+            self.p0, self.p1 = D.shard_pairs(self.pairs, world, rank, group=1)
+            self.pair_block = pair_index(n_frag, dev)[self.p0:self.p1].contiguous()
+            self.pg_counts, self.pg_samples, self.pg_filter = groups
+            self.raw = [torch.from_numpy(f).to(dev) for f in self.frags[self.f0:self.f1]]
+        else:
+            self.raw = [torch.from_numpy(f).to(dev) for f in self.frags]     # resident in HBM
 
     def prepare(self):
         """voxelise (prepare_data on the GPU) and build the strided coordinate sets of the sparse input: every
-        host synchronisation of the scene (voxel counts, the size of each coordinate level) happens here"""
+        host synchronisation of the scene (voxel counts, the size of each coordinate level) happens here.
+        shard=pairs: this rank's fragments only; the voxel counts of all fragments (the sampler's draws depend on
+        them) arrive by one host all-gather (gloo group)."""
         from lib.sparse import voxelize, CoordinateManager
         coords, sel, counts, xyz_down = voxelize(self.raw, self.voxel, self.dev)
         cm = CoordinateManager(coords, len(counts))
         for s in (2, 4, 8):   # FCGF's tensor strides (fcgf.py:118-227)
             cm.coords_at(s)
+        d = {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
+             "pts_list": torch.tensor(counts), "sinput0_coords_manager": cm}
+        if self.shard == "pairs":
+            import torch.distributed as dist
+            mine = torch.full((self.fper,), -1, dtype=torch.int64)
+            mine[:len(counts)] = torch.tensor(counts, dtype=torch.int64)
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine, group=self.pg_counts)
+            allc = torch.cat(parts)
+            counts = [int(c) for c in allc[allc >= 0]]
+            d["pts_all"] = counts
         self.vox_counts = counts
-        return {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
-                "pts_list": torch.tensor(counts), "sinput0_coords_manager": cm}
+        return d
 
     def describe(self, data=None):
-        """(voxelise ->) FCGF -> Sampler -> feature NN over all pairs (compute_descriptors)"""
+        """(voxelise ->) FCGF -> Sampler -> feature NN over all pairs (compute_descriptors).
+        shard=pairs: FCGF + sampling of this rank's fragments (the sampler's numpy draws replayed for the whole
+        scene, lib/layers.py:128-148, so every fragment gets the draws it gets on one GPU), one all-gather of the
+        sampled (xyz, descriptor) of every fragment (RCCL, ~21 MB per scene), then the feature NN of this rank's
+        block of pairs only."""
         if data is None:
             data = self.prepare()
         np.random.seed(self.rng_seed)
-        fin, _, _ = self.model.compute_descriptors(data)
-        return fin
+        if self.shard != "pairs":
+            fin, _, _ = self.model.compute_descriptors(data)
+            return fin
+        from lib import distributed as D
+        from lib.sparse import SparseTensor
+        m = self.model
+        allc = data["pts_all"]
+        if self.samp == "rand":
+            idx = m.sampler.indices(allc)                                 # [n_frag, k] rows of the whole scene
+            idx = idx[self.f0:self.f1] - int(np.sum(allc[:self.f0]))      # -> rows of this rank's fragments
+        else:                                                             # fps: per fragment, no shared state
+            idx = m.sampler.indices(data["pts_list"], data["pcd0"])
+        n = min(m.sampler.targeted_num_points, min(allc))
+        buf = torch.zeros(self.fper, n, 35, device=self.dev)
+        if self.f1 > self.f0:
+            F0 = m.descriptor_module(SparseTensor(data["sinput0_F"], coords_manager=data["sinput0_coords_manager"])).F
+            sc, sf = m.sampler.gather(data["pcd0"], F0, idx)
+            buf[:self.f1 - self.f0, :, :3] = sc
+            buf[:self.f1 - self.f0, :, 3:] = sf
+        allb = D.all_gather_rows(buf, self.world, self.pg_samples)[:self.n_frag]   # every fragment, pair order
+        xyz_b, f_b = allb[..., :3].contiguous(), allb[..., 3:].contiguous()
+        xs = torch.empty(self.p1 - self.p0, n, 6, device=self.dev)
+        if self.p1 > self.p0:
+            m.feature_matching.match_pairs(f_b, xyz_b, self.pair_block, xs, n * 6, 6)
+        return {"xs": xs.unsqueeze(1), "num_pairs": self.pairs}
 
     def finish(self, fin):
-        """OANet -> Procrustes -> per-pair records (R, t, inlier fraction)"""
+        """OANet -> Procrustes -> per-pair records (R, t, inlier fraction).  shard=pairs: this rank's block
+        through lib.distributed.register_pairs_sharded (guard over the whole scene's batch, as on one GPU), whose
+        RCCL all-gather returns the records of ALL pairs on every rank"""
+        if self.shard == "pairs":
+            from lib import distributed as D
+            rec = D.register_pairs_sharded(self.model, fin, self.world, self.rank, group=1, guard="scene",
+                                           pg=self.pg_filter, first_pair=self.p0)
+            return rec[:, 1:14]
         out = self.model.filter_correspondences(fin)
         R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
         conf = (s > 0.5).float().mean(dim=1, keepdim=True)
         return torch.cat([R.reshape(-1, 9), t.reshape(-1, 3), conf], dim=1)
+
+    def gather(self, rec, world):
+        """records of every rank: pairs mode's finish() already returns all pairs"""
+        return rec if self.shard == "pairs" else records_allgather(rec, world)
 
     def step(self):
         return self.finish(self.describe())
@@ -208,7 +277,7 @@ class SceneWorkload:
             with torch.cuda.stream(sB):
                 sB.wait_event(ev)
                 fin["xs"].record_stream(sB)
-                rec = records_allgather(self.finish(fin), world)
+                rec = self.gather(self.finish(fin), world)
         if self.prepared is None:
             self.prepared = self.prepare_on(sC)
         data, evc = self.prepared.result() if hasattr(self.prepared, "result") else self.prepared
@@ -235,6 +304,17 @@ class SceneWorkload:
         return data, ev
 
     def config(self):
+        if self.shard == "pairs":
+            return {"workload": "ONE synthetic 3DMatch-scale scene per step over all ranks (configs[2]/[3] pair "
+                                "sharding): %d fragments x ~%d voxels (0.025 m), FCGF + %s %d samples of %d fragments "
+                                "per rank -> all-gather of the samples -> soft feature-NN + OANet (128ch, 500 clusters, "
+                                "2 blocks) + weighted Procrustes of %d-%d of the %d pairs per rank (scene-wide zero-row "
+                                "guard) -> all-gather of (R,t,conf)"
+                                % (self.n_frag, int(np.mean(self.vox_counts or [0])), self.samp, self.npts, self.fper,
+                                   self.pairs // self.world, -(-self.pairs // self.world), self.pairs),
+                    "sampler": self.samp, "fragments": self.n_frag, "pairs": self.pairs,
+                    "fragments_per_gpu": self.fper, "pairs_per_gpu": -(-self.pairs // self.world),
+                    "samples": self.npts, "voxels_mean": int(np.mean(self.vox_counts or [0]))}
         return {"workload": "one synthetic 3DMatch-scale scene per GPU (configs[2]): %d fragments x ~%d voxels "
                             "(0.025 m) -> FCGF -> %s %d samples -> soft feature-NN for all %d pairs -> OANet "
                             "(128ch, 500 clusters, 2 blocks) -> weighted Procrustes -> all-gather of (R,t,conf)"
@@ -322,11 +402,10 @@ class SceneWorkload:
 
 def records_allgather(rec, world):
     import torch.distributed as dist
+    from lib import distributed as D
     if not (dist.is_available() and dist.is_initialized()):
         return rec
-    out = torch.empty((world,) + tuple(rec.shape), dtype=rec.dtype, device=rec.device)
-    dist.all_gather_into_tensor(out, rec.contiguous())
-    return out
+    return D.all_gather_rows(rec.unsqueeze(0), world)
 
 
 MFMA_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter", "feat_nn", "spconv", "pointcn")
@@ -350,7 +429,7 @@ def timed_run(wl, args, world, pipelined, barrier):
     def run_step():
         if pipelined:
             return wl.step_pipelined(world)
-        return records_allgather(wl.step(), world)
+        return wl.gather(wl.step(), world)
 
     with torch.no_grad():
         for _ in range(max(args.warmup, 1 if pipelined else 0)):   # the pipeline is filled before timing
@@ -364,7 +443,7 @@ def timed_run(wl, args, world, pipelined, barrier):
         _native.prof_mask(None)
         if not args.prof_seq:
             _native.prof_set(1)
-            records_allgather(wl.step(), world)   # stages back to back: per-class times without overlap
+            wl.gather(wl.step(), world)   # stages back to back: per-class times without overlap
             torch.cuda.synchronize()
             prof_all = {k: _native.prof_get(k) for k in _native.PROF_KINDS}
             _native.prof_set(0)
@@ -405,8 +484,9 @@ def timed_run(wl, args, world, pipelined, barrier):
         _native.prof_mask(None)
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():   # max over ranks
+        from lib import distributed as D
         tt = torch.tensor([dt], device=rec.device, dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        D.all_reduce_max(tt)
         dt = float(tt.item())
     return dt, rec, prof, prof_all, dom, step_ms
 
@@ -490,6 +570,10 @@ def main():
     ap.add_argument("--no-prof", action="store_true", help="no per-launch HIP events in the timed region (A/B timing)")
     ap.add_argument("--no-pipeline", action="store_true", help="scene workload: run the stages of a step back to "
                     "back on one stream (default: two-stage pipeline over consecutive scenes, SceneWorkload.step_pipelined)")
+    ap.add_argument("--shard", default=os.environ.get("MVR_BENCH_SHARD", "scenes"), choices=["scenes", "pairs"],
+                    help="scene workload at N > 1: scenes = one scene per rank (weak scaling); pairs = ONE scene per "
+                    "step, its fragments (FCGF + sampling) and its pair batch (feature NN + OANet + Procrustes) split "
+                    "over the ranks, with an RCCL all-gather of the samples and of the per-pair records (strong scaling)")
     ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
                     "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -497,16 +581,30 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MVR_BENCH_BACKEND", "nccl") != "nccl":   # rehearsal: ranks may share the box's GPUs
+        local %= max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     # MVR_BENCH_PG=1: the RCCL process group (barriers, record all-gather) also at one rank, to exercise the N > 1
     # data path on a one-GPU box
     use_pg = world > 1 or os.environ.get("MVR_BENCH_PG") == "1"
+    # MVR_BENCH_BACKEND=gloo: several ranks on one GPU (a rehearsal of the N > 1 paths on a one-GPU box; RCCL
+    # refuses two ranks on one device): the collectives are staged through host memory (lib/distributed.py)
+    backend = os.environ.get("MVR_BENCH_BACKEND", "nccl")
+    groups = None
     if use_pg:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        if args.shard == "pairs" and args.workload == "scene":
+            # voxel counts (host, gloo) | sampled descriptors (stream A) | filter guard + records (stream B): one
+            # communicator per stream, so the two streams' collectives never queue behind each other
+            groups = (dist.new_group(backend="gloo"), dist.new_group(backend=backend),
+                      dist.group.WORLD)
 
     def barrier():
         if use_pg:
@@ -517,13 +615,18 @@ def main():
     _native.lib()
     math_info = _native.set_math(args.math)
     if args.workload == "scene":
-        wl = SceneWorkload(dev, rank, npts=args.npts, samp=args.samp)
+        if args.shard == "pairs" and not use_pg:
+            raise SystemExit("--shard pairs needs a process group (torchrun, or MVR_BENCH_PG=1 at one rank)")
+        if args.shard == "pairs" and world > 30:
+            raise SystemExit("--shard pairs: at most one rank per fragment (30)")
+        wl = SceneWorkload(dev, rank, npts=args.npts, samp=args.samp, shard=args.shard, world=world, groups=groups)
     else:
         wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
     pipelined = args.workload == "scene" and not args.no_pipeline
 
     dt, rec, prof, prof_all, dom, step_ms = timed_run(wl, args, world, pipelined, barrier)
-    pairs_per_step = int(rec.shape[-2]) * world
+    pair_sharded = args.workload == "scene" and args.shard == "pairs"
+    pairs_per_step = int(rec.shape[0]) if pair_sharded else int(rec.shape[-2]) * world
     value = pairs_per_step * args.steps / dt
     ms_step = dt / args.steps * 1e3
 
@@ -631,9 +734,14 @@ def main():
             "ms_per_step_median": round(float(np.median(step_ms)), 3),
             "ms_per_step_min_max": [round(float(step_ms.min()), 3), round(float(step_ms.max()), 3)],
             "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
+            "scaling": "strong" if pair_sharded else "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
             "config": dict(wl.config(), math=args.math,
-                           parallelism="dp%d (pair batches, RCCL all-gather of records)" % world,
+                           parallelism=("pairs%d (one scene per step: fragments and pair batch sharded over %d "
+                                        "ranks, %s all-gather of samples and records)"
+                                        % (world, world, "RCCL" if backend == "nccl" else backend)
+                                        if pair_sharded else
+                                        "dp%d (one scene per rank, %s all-gather of records)"
+                                        % (world, "RCCL" if backend == "nccl" else backend)),
                            schedule=("3-stream pipeline over consecutive scenes: voxelisation + coordinate levels of "
                                      "scene k+1, FCGF + feature NN of scene k, OANet + Procrustes of scene k-1; every "
                                      "timed step runs every stage in full"

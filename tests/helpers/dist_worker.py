@@ -1,0 +1,58 @@
+"""One rank of the multi-process sharded-registration GPU test (tests/test_gpu_distributed.py): the real OANet
+(RegBlock size) through lib.distributed.register_pairs_sharded on cuda:0, gloo process group (several ranks share
+the box's one GPU; gloo moves host tensors, so lib.distributed stages the collectives through host memory).
+Writes this rank's gathered records to <out>/rec_<rank>.npy.
+
+usage: RANK=r WORLD_SIZE=w MASTER_ADDR=127.0.0.1 MASTER_PORT=p python tests/helpers/dist_worker.py <guard> <out>"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+for p in (os.path.join(ROOT, "3d_multiview_reg_amd"), ROOT, os.path.join(ROOT, "tests", "golden"), HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def case(guard, dev):
+    """the shared input: 70 pairs x 1000 correspondences; pairs 32-63 are gross outliers and the output bias is
+    lowered, so the zero-row guard fires for them (their positive-weight count is 0) — all on rank 0 at world 2
+    (rank 0 holds pairs 0-63, rank 1 pairs 64-69).  guard 'scene': eval mode (the guard over the whole batch);
+    'group': train mode (BatchNorm statistics and guard per 32-pair group, the benchmark's loader batches)."""
+    from lib.filtering.oanet import OANet
+    from synth import synth_state, synth_correspondences
+    cfg = {"misc": {"net_depth": 12, "clusters": 500, "iter_num": 1, "net_channel": 128, "use_gpu": True,
+                    "normalize_weights": True}, "data": {"use_mutuals": 0}}
+    net = OANet(cfg)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    st = synth_state(shapes, seed=7, overrides={"reg_init.output.bias": [-3.0]})
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    net = net.to(dev).train(guard == "group")
+    xs, _, _ = synth_correspondences(70, 1000, seed=29)
+    xs[32:64, :, 3:] = xs[32:64, :, :3] + 5.0
+    return net, torch.from_numpy(xs).unsqueeze(1).to(dev)
+
+
+def main():
+    guard, out = sys.argv[1], sys.argv[2]
+    import torch.distributed as dist
+    from lib import distributed as D
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net, X = case(guard, dev)
+        with torch.no_grad():
+            rec = D.register_pairs_sharded(net, {"xs": X}, world, rank, guard=guard)
+        torch.cuda.synchronize()
+        np.save(os.path.join(out, "rec_%d.npy" % rank), rec.cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -45,6 +45,7 @@ class _StubFilter(torch.nn.Module):
 
     def __init__(self):
         super().__init__()
+        self.eval()                      # scene mode shards eval-mode forwards only
         self.guard_group = 0
         self.guard_sync = None
         self.seen = []

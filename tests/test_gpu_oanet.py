@@ -270,6 +270,39 @@ def test_oanet_external_guard_equals_internal(gpu, ovr):
         assert np.all(outs[0]["logits"][0].cpu().numpy() < 0)
 
 
+def test_oanet_guard_fired_by_another_rank(gpu):
+    """Scene-mode sharding when the guard's reason lives on ANOTHER rank: this rank's pairs all have positive
+    weights, the all-reduced bit is 1, and lib.distributed.scene_guard_sync forces the first local count to 0.
+    Every local pair must then carry + 1/N (oanet.py:177-178) and each block's R, t must be the weighted Kabsch of
+    those guarded weights (oracle/kabsch.py), in both blocks."""
+    import torch
+    from oracle.kabsch import kabsch
+
+    def forced(gp):   # scene_guard_sync's rewrite with the remote bit set
+        g = gp.clone()
+        g[:1] = 0
+        return g
+    xs, _, _ = synth_correspondences(4, 900, seed=81)
+    net = _oanet(128, 500, 9, gpu, which="full")
+    outs = []
+    for sync in (None, forced):
+        net.guard_sync = sync
+        with torch.no_grad():
+            outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    net.guard_sync = None
+    plain, f = outs
+    s0 = plain["scores"][0].cpu().numpy()
+    assert (s0 > 0).any(axis=1).all()                      # no zero row of its own: only the remote bit fires
+    inv_n = np.float32(1.0 / 900)
+    np.testing.assert_allclose(f["scores"][0].cpu().numpy(), s0 + inv_n, rtol=0, atol=1e-7)
+    for i in range(2):
+        w = f["scores"][i].cpu().numpy()
+        assert np.all(w >= inv_n * np.float32(0.999)), i
+        Ro, to, _, _ = kabsch(xs[..., :3], xs[..., 3:], w)
+        np.testing.assert_allclose(f["rot_est"][i].cpu().numpy(), Ro, atol=1e-5)
+        np.testing.assert_allclose(f["trans_est"][i].cpu().numpy(), to, atol=1e-5)
+
+
 def test_oanet_bn_groups_equal_batches(gpu):
     """bn_group = guard_group = 32 (train mode): one forward over 70 pairs equals the reference benchmark's three
     loader batches (32, 32, 6) run one by one — BatchNorm statistics and the zero-row guard per batch (the second
