@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mvreg.h"
+
 namespace mvr {
 
 enum Pro : int {
@@ -67,6 +69,14 @@ struct GemmArgs {
   // (stream-ordered); the split-fp16 pass sets it when an operand leaves the fp16 window and the guarded split-bf16
   // pass then recomputes every output.  Null: split-bf16 only.
   int* flag;
+  // InstanceNorm fold of the output fused into the producer (pconv only, stats_mode ST_ROW, split-bf16 launches):
+  // the workgroup that completes a pair's statistics (a per-pair arrival counter, fin_cnt[b], zeroed by the
+  // caller) merges them like in_finalize_kernel and writes the fold for the next conv's prologue:
+  // fin_sc/fin_sh [b*fin_ld + m] (eval; fin_sc2/fin_sh2 with fin_bn2 / fin_eps2 when set: a second fold of the
+  // same statistics) or (mean, var) into fin_mv [b*M + m] (fin_train).  launch_gemm sets *fin_done when it did.
+  int* fin_cnt; float fin_eps; mvr_bn_p fin_bn; float* fin_sc; float* fin_sh; int64_t fin_ld;
+  float fin_eps2; mvr_bn_p fin_bn2; float* fin_sc2; float* fin_sh2;
+  int fin_train; float2* fin_mv; int* fin_done;
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the

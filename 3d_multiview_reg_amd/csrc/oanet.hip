@@ -267,7 +267,8 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
-int g_oan_fused = 5;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 2 conv1 folded into the first PointCN
+int g_oan_fused = 13;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 2 conv1 folded into the first PointCN,
+                        // bit 3 InstanceNorm folds finished in their producer's last-arriving workgroups
                        // (point-conv XI variants); bit 1 is unused
 int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B timing)
 
@@ -352,12 +353,28 @@ struct Plan {
   size_t uimg_bytes;
   size_t bytes;
   float *X11, *XA, *T1, *E, *XD, *O1, *O2, *sc, *sh, *scK, *shK, *fac, *W1, *W8;
+  float *sc2, *sh2;      // the second fold buffer: a producer with a fused finalize writes the fold its consumer
+                         // reads while its own prologue still reads the first (Ctx::fsc)
+  float *scU, *shU;      // diff_unpool's fold of x1_1 (up1's IN + BN, oanet.py:118-119)
+  int* fcnt;             // FIN_SLOTS x P arrival counters of the fused finalizes (zeroed at the block's start)
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
   int* flags;            // FLAG_SLOTS range flags of the split-fp16 launches (zeroed at the block's start)
 };
 
 // one flag word per guarded split-fp16 launch of a block forward, assigned in launch order (a block issues ~30)
 constexpr int FLAG_SLOTS = 128;
+// arrival counters per fused finalize of a block forward (a block fuses <= 14 for 3 half layers)
+constexpr int FIN_SLOTS = 32;
+
+// the InstanceNorm fold a producer's last-arriving workgroups should write for the next conv's prologue
+struct FoldReq {
+  float eps;
+  mvr_bn_p bn;
+  float eps2 = 0.f;       // optional second fold of the same statistics (x1_1: down1's and up1's)
+  mvr_bn_p bn2{};
+  float* sc2 = nullptr;
+  float* sh2 = nullptr;
+};
 
 // Activations [P][C][Np] over points and [P][C][Kp] over clusters, rows padded to a multiple of 32
 // floats: 128-byte rows, so that row segments written by the epilogues cover whole cache lines
@@ -383,6 +400,11 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.O2 = w.take<float>(PK * C);
   pl.sc = w.take<float>((size_t)P * 2 * C);
   pl.sh = w.take<float>((size_t)P * 2 * C);
+  pl.sc2 = w.take<float>((size_t)P * 2 * C);
+  pl.sh2 = w.take<float>((size_t)P * 2 * C);
+  pl.scU = w.take<float>((size_t)P * C);
+  pl.shU = w.take<float>((size_t)P * C);
+  pl.fcnt = w.take<int>((size_t)FIN_SLOTS * P);
   pl.scK = w.take<float>((size_t)P * pl.Kp);   // train-mode BN over clusters: per pair (its group's statistics)
   pl.shK = w.take<float>((size_t)P * pl.Kp);
   size_t nf = (size_t)P * TN * pl.Kp;
@@ -419,6 +441,10 @@ struct Ctx {
   bool f16;   // split-fp16 launches enabled (flags zeroed)
   int err = 0;
   int nflag = 0;
+  int nfin = 0;   // fused finalizes issued (counter slots used)
+  int fcur = 0;   // the fold buffer the next prologue reads: 0 = pl.sc / pl.sh, 1 = pl.sc2 / pl.sh2
+  float* sc() const { return fcur ? pl.sc2 : pl.sc; }
+  float* sh() const { return fcur ? pl.sh2 : pl.sh; }
   // the next launch's own zeroed flag word, or null (split-bf16 only) when split-fp16 is off or the slots are used up
   int* flag() { return f16 && nflag < FLAG_SLOTS ? pl.flags + nflag++ : nullptr; }
   void chk(int e) {
@@ -430,7 +456,7 @@ struct Ctx {
 
   // IN(eps)+BN fold of activation `a` -> sc / sh ([P][a.C], default pl.sc / pl.sh)
   void finalize_in(const Act& a, float eps, const mvr_bn_p& bn, float* sc = nullptr, float* sh = nullptr) {
-    if (!sc) { sc = pl.sc; sh = pl.sh; }
+    if (!sc) { sc = this->sc(); sh = this->sh(); }
     const int bs = a.C >= 256 ? 256 : (a.C + 63) & ~63;
     const int G = 1024 / bs < 4 ? 1024 / bs : 4;   // tile groups per channel
     dim3 grid((a.C + bs - 1) / bs, pl.P);
@@ -452,9 +478,20 @@ struct Ctx {
   float* h_scores = nullptr;
   int32_t* h_pos = nullptr;
 
-  void conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
-            const float* w_padded = nullptr, bool no_store = false) {
+  // train mode after a fused finalize (mv holds the pairs' (mean, var)): the BatchNorm batch statistics
+  void bn_train_from_mv(int C, float eps, const mvr_bn_p& bn, float* sc, float* sh) {
+    hipLaunchKernelGGL(in_bn_train_kernel, dim3((C + 255) / 256, ngroups()), dim3(256), 0, s, pl.mv, pl.P, bn_group, C,
+                       eps, bn, sc, sh, (int64_t)C);
+    chk_launch();
+  }
+
+  // returns true when the launch also wrote the requested fold of its output (`fold`, ST_ROW only): the next
+  // conv's prologue then reads it (fcur flipped); false: the caller runs finalize_in
+  bool conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
+            const float* w_padded = nullptr, bool no_store = false, const FoldReq* fold = nullptr) {
     GemmArgs g{};
+    int done = 0;
+    if (fold) fuse(g, *fold, &done);
     if (head) {
       g.head_w = head->weight; g.head_bp = head->bias;
       g.logits = h_logits; g.scores = h_scores; g.pos = h_pos;
@@ -467,34 +504,62 @@ struct Ctx {
     g.C = out.p; g.sCb = out.ps; g.ldc = out.ld;
     if (res) { g.R = res->p; g.sRb = res->ps; g.has_res = 1; }
     g.bias = cv.bias; g.bias_mode = cv.bias ? BIAS_M : BIAS_NONE;
-    if (pro) { g.pro = PRO_B_K; g.psc = pl.sc; g.psh = pl.sh; g.sPb = in.C; }
+    if (pro) { g.pro = PRO_B_K; g.psc = sc(); g.psh = sh(); g.sPb = in.C; }
     g.stats_mode = stats_mode;
     g.stats = out.st; g.st_ld = out.st_ld; g.st_off = out.st_off;
     g.prof_kind = (in.L == pl.Kc && out.L == pl.Kc) ? PK_OAFILTER : (out.C == pl.Kc ? PK_EMBED : PK_CONV_PTS);
     g.flag = flag();
     chk(launch_gemm(g, s));
+    return fused(g, fold, done, out.C);
   }
 
-  // PointCN (oanet.py:18-43) from x to y (y may be x); sets the statistics tile width of y
-  void pointcn(const mvr_pointcn_p& pc, const Act& x, Act& y) {
-    finalize_in(x, 1e-5f, pc.bn1);
+  // request the fold in a producer's launch (counter slot, target buffers); zero when out of slots
+  void fuse(GemmArgs& g, const FoldReq& f, int* done) {
+    if (!(g_oan_fused & 8) || nfin >= FIN_SLOTS) return;
+    g.fin_cnt = pl.fcnt + (size_t)nfin * pl.P;
+    g.fin_eps = f.eps; g.fin_bn = f.bn;
+    g.fin_sc = fcur ? pl.sc : pl.sc2; g.fin_sh = fcur ? pl.sh : pl.sh2; g.fin_ld = 128;
+    g.fin_eps2 = f.eps2; g.fin_bn2 = f.bn2; g.fin_sc2 = f.sc2; g.fin_sh2 = f.sh2;
+    g.fin_train = train; g.fin_mv = pl.mv;
+    g.fin_done = done;
+  }
+  // after the launch: did it take the fold?  (flip the fold buffers; train mode: the batch statistics)
+  bool fused(const GemmArgs& g, const FoldReq* f, int done, int C) {
+    if (!f || !g.fin_cnt) return false;
+    ++nfin;   // the slot is spent either way (its counters may have been touched)
+    if (!done) return false;
+    fcur ^= 1;
+    if (train) {
+      bn_train_from_mv(C, f->eps, f->bn, sc(), sh());
+      if (f->sc2) bn_train_from_mv(C, f->eps2, f->bn2, f->sc2, f->sh2);
+    }
+    return true;
+  }
+
+  // PointCN (oanet.py:18-43) from x to y (y may be x); sets the statistics tile width of y.  x_folded: x's
+  // fold is already in sc() (its producer's fused finalize).  next: the fold of y its conv7 should fuse (the
+  // next consumer's); returns whether it did
+  bool pointcn(const mvr_pointcn_p& pc, const Act& x, Act& y, const FoldReq* next = nullptr, bool x_folded = false) {
+    if (!x_folded) finalize_in(x, 1e-5f, pc.bn1);
     Act t{pl.T1, (int64_t)y.C * pl.Np, pl.Np, y.C, pl.N, pl.stT, y.C, 0};
     const bool sc = pc.shortcut.weight != nullptr;
     y.tw0 = 128;
     y.csplit = 1 << 30;
     const mvr_conv_p* hd = head;   // the head goes with conv7 only
     head = nullptr;
-    dbg_hash(pl.sc, pl.P, 1, x.C, x.C, 0, s);
-    dbg_hash(pl.sh, pl.P, 1, x.C, x.C, 0, s);
+    dbg_hash(this->sc(), pl.P, 1, x.C, x.C, 0, s);
+    dbg_hash(this->sh(), pl.P, 1, x.C, x.C, 0, s);
     if (sc) conv(pc.shortcut, x, false, y, nullptr, ST_NONE);
-    conv(pc.conv3, x, true, t, nullptr, ST_ROW);
+    const FoldReq f5{1e-5f, pc.bn5};
+    const bool tf = conv(pc.conv3, x, true, t, nullptr, ST_ROW, nullptr, false, &f5);
     const int TNn = (pl.N + 127) / 128;
     dbg_hash(reinterpret_cast<const float*>(pl.stT), pl.P, 1, TNn * y.C * 2, (int64_t)TNn * y.C * 2, 0, s);
-    finalize_in(t, 1e-5f, pc.bn5);
-    dbg_hash(pl.sc, pl.P, 1, y.C, y.C, 0, s);
-    dbg_hash(pl.sh, pl.P, 1, y.C, y.C, 0, s);
+    if (!tf) finalize_in(t, 1e-5f, pc.bn5);
+    dbg_hash(this->sc(), pl.P, 1, y.C, y.C, 0, s);
+    dbg_hash(this->sh(), pl.P, 1, y.C, y.C, 0, s);
     head = hd;
-    conv(pc.conv7, t, true, y, sc ? &y : &x, hd ? ST_NONE : ST_ROW, nullptr, hd && head_only);
+    const bool yf = conv(pc.conv7, t, true, y, sc ? &y : &x, hd ? ST_NONE : ST_ROW, nullptr, hd && head_only,
+                         hd ? nullptr : next);
     head = nullptr;
     if (!hd) {
       dbg_hash(y.p, pl.P, y.C, pl.N, y.ps, y.ld, s);
@@ -502,12 +567,14 @@ struct Ctx {
       dbg_hash(reinterpret_cast<const float*>(y.st + y.st_off), pl.P * TNn, 1, 2 * y.C, y.st_ld * 2, 0, s);
       dbg_dump(y.st, (size_t)pl.P * TNn * y.st_ld * sizeof(float2), s);
     }
+    return yf;
   }
 
-  void oafilter(const mvr_oafilter_p& f, const Act& xd) {
+  // OAFilter (oanet.py:56-93), in place on xd; x_folded / next as for pointcn (conv3 fuses next's fold)
+  bool oafilter(const mvr_oafilter_p& f, const Act& xd, const FoldReq* next = nullptr, bool x_folded = false) {
     const int C = pl.C, Kc = pl.Kc;
     const int64_t Kp = pl.Kp;
-    finalize_in(xd, 1e-3f, f.bn1);
+    if (!x_folded) finalize_in(xd, 1e-3f, f.bn1);
     Act o1{pl.O1, (int64_t)C * Kp, Kp, C, Kc, pl.stcol, Kc, 0};
     conv(f.conv1, xd, true, o1, nullptr, train ? ST_COL : ST_NONE);
     if (train) {
@@ -533,7 +600,7 @@ struct Ctx {
     g.flag = flag();
     chk(launch_gemm(g, s));
     finalize_in(o2, 1e-3f, f.bn3);
-    conv(f.conv3, o2, true, xd, &xd, ST_ROW);  // in place: out = conv3(...) + x
+    return conv(f.conv3, o2, true, xd, &xd, ST_ROW, nullptr, false, next);  // in place: out = conv3(...) + x
   }
 
   // softmax partials [P][T][L] -> factors pl.fac [P][T][ld]
@@ -557,7 +624,7 @@ extern "C" int mvr_set_pool_split(int on) {
 
 extern "C" int mvr_set_oan_fused(int on) {
   const int prev = g_oan_fused;
-  g_oan_fused = on & 5;
+  g_oan_fused = on & 13;
   return prev;
 }
 
@@ -581,6 +648,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (workspace_bytes < pl.bytes) return MVR_EINVAL;
   Ctx cx{pl, s, bn_train ? 1 : 0, bn_train > 1 ? std::min(bn_train, P) : P, g_gemm_h || g_pconv_h};
   if (cx.f16 && hipMemsetAsync(pl.flags, 0, sizeof(int) * FLAG_SLOTS, s) != hipSuccess) return MVR_ELAUNCH;
+  if ((g_oan_fused & 8) && hipMemsetAsync(pl.fcnt, 0, sizeof(int) * FIN_SLOTS * P, s) != hipSuccess)
+    return MVR_ELAUNCH;
   const int64_t Np = pl.Np, Kp = pl.Kp;
   const int64_t CN = (int64_t)C * Np;
   const int TN = gemm_ntiles(N);
@@ -606,12 +675,17 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   f3.B = input; f3.sBb = in_pstride; f3.ldb = ld;
   f3.C = pl.T1; f3.sCb = CN; f3.ldc = Np;
   f3.bias = blk->l1_1[0].conv3.bias; f3.bias_mode = f3.bias ? BIAS_M : BIAS_NONE;
-  f3.pro = PRO_B_K; f3.psc = pl.sc; f3.psh = pl.sh; f3.sPb = C;
+  f3.pro = PRO_B_K; f3.sPb = C;
   f3.stats_mode = ST_ROW; f3.stats = pl.stT; f3.st_ld = C; f3.st_off = 0;
   f3.xin = 1; f3.xci = Cin; f3.xw = pl.W8; f3.xb = blk->conv1.bias; f3.xld = ld;
   f3.prof_kind = PK_CONV_PTS;
   const bool fold1 = (g_oan_fused & 4) && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
                      pconv_covers(f3);
+  // folds the last l1_1 conv fuses: down1's IN(1e-3) + BN for diff_pool, and up1's into scU for diff_unpool
+  FoldReq fx11{1e-3f, blk->down_bn};
+  fx11.eps2 = 1e-3f; fx11.bn2 = blk->up_bn; fx11.sc2 = pl.scU; fx11.sh2 = pl.shU;
+  const FoldReq fnext1{1e-5f, H > 1 ? blk->l1_1[1].bn1 : mvr_bn_p{}};
+  bool yfold = false;   // the current point activation's fold is already in cx.sc() (fused by its producer)
   if (fold1) {
     const int n8 = C * 8;
     hipLaunchKernelGGL(pad_cols_kernel, dim3((n8 + 255) / 256), dim3(256), 0, s, blk->conv1.weight, C, Cin, 8, pl.W8);
@@ -620,15 +694,19 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     cx.chk_launch();
     dbg_hash(reinterpret_cast<const float*>(pl.stA), P, 1, TN * C * 2, (int64_t)TN * C * 2, 0, s);
     cx.finalize_in(xa, 1e-5f, blk->l1_1[0].bn1);   // xa.st = pl.stA: the partials just written
-    dbg_hash(pl.sc, P, 1, C, C, 0, s);
-    dbg_hash(pl.sh, P, 1, C, C, 0, s);
+    dbg_hash(cx.sc(), P, 1, C, C, 0, s);
+    dbg_hash(cx.sh(), P, 1, C, C, 0, s);
+    f3.psc = cx.sc(); f3.psh = cx.sh();
     f3.flag = cx.flag();
+    const FoldReq f5{1e-5f, blk->l1_1[0].bn5};
+    int f3done = 0;
+    cx.fuse(f3, f5, &f3done);
     cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
     Act t{pl.T1, CN, Np, C, N, pl.stT, C, 0};
     dbg_hash(reinterpret_cast<const float*>(pl.stT), P, 1, TN * C * 2, (int64_t)TN * C * 2, 0, s);
-    cx.finalize_in(t, 1e-5f, blk->l1_1[0].bn5);
-    dbg_hash(pl.sc, P, 1, C, C, 0, s);
-    dbg_hash(pl.sh, P, 1, C, C, 0, s);
+    if (!cx.fused(f3, &f5, f3done, C)) cx.finalize_in(t, 1e-5f, blk->l1_1[0].bn5);
+    dbg_hash(cx.sc(), P, 1, C, C, 0, s);
+    dbg_hash(cx.sh(), P, 1, C, C, 0, s);
     Act& y = (H == 1) ? x11top : xa;
     GemmArgs f7{};
     f7.math = MATH_BF16X3; f7.M = C; f7.N = N; f7.K = C; f7.batch = P;
@@ -637,30 +715,37 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     f7.C = y.p; f7.sCb = y.ps; f7.ldc = y.ld;
     f7.R = input; f7.sRb = in_pstride; f7.has_res = 1;
     f7.bias = blk->l1_1[0].conv7.bias; f7.bias_mode = f7.bias ? BIAS_M : BIAS_NONE;
-    f7.pro = PRO_B_K; f7.psc = pl.sc; f7.psh = pl.sh; f7.sPb = C;
+    f7.pro = PRO_B_K; f7.psc = cx.sc(); f7.psh = cx.sh(); f7.sPb = C;
     f7.stats_mode = ST_ROW; f7.stats = y.st; f7.st_ld = y.st_ld; f7.st_off = y.st_off;
     f7.xin = 2; f7.xci = Cin; f7.xw = pl.W8; f7.xb = blk->conv1.bias; f7.xld = ld;
     f7.prof_kind = PK_CONV_PTS;
     f7.flag = cx.flag();
+    int f7done = 0;
+    const FoldReq* n7 = (H == 1) ? &fx11 : &fnext1;
+    cx.fuse(f7, *n7, &f7done);
     cx.chk(launch_gemm(f7, s));   // conv7 of l1_1[0] + x (recomputed)
+    yfold = cx.fused(f7, n7, f7done, C);
     dbg_hash(pl.T1, P, C, N, CN, Np, s);
     dbg_hash(y.p, P, C, N, y.ps, y.ld, s);
   } else {
     cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW, w1);
   }
-  // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C))
+  // l1_1: PointCN x H (in place on XA; the last one writes x1_1 into X11 rows [0,C)); each conv7 fuses the fold
+  // its consumer needs: the next PointCN's first IN + BN, after the last one down1's (and up1's, kept in scU)
   for (int i = fold1 ? 1 : 0; i < H; ++i) {
     Act& yo = (i == H - 1) ? x11top : xa;
-    cx.pointcn(blk->l1_1[i], xa, yo);
+    const FoldReq fn{1e-5f, i + 1 < H ? blk->l1_1[i + 1].bn1 : mvr_bn_p{}};
+    yfold = cx.pointcn(blk->l1_1[i], xa, yo, i == H - 1 ? &fx11 : &fn, yfold);
     dbg_hash(pl.T1, P, C, N, CN, Np, s);
     dbg_hash(yo.p, P, C, N, yo.ps, yo.ld, s);
   }
+  const bool up_folded = yfold;   // scU holds up1's fold of x1_1 too
 
   // diff_pool (oanet.py:96-110): E = exp(embed - tile max) over points, x_down = x . softmax(E)^T
-  cx.finalize_in(x11top, 1e-3f, blk->down_bn);
+  if (!yfold) cx.finalize_in(x11top, 1e-3f, blk->down_bn);
   Act xd{pl.XD, (int64_t)C * Kp, Kp, C, Kc, pl.stD, C, 0};
   if (pl.fused) {
-    cx.chk(mvr_oan_diff_pool_ws(pl.X11, 2 * CN, Np, pl.sc, pl.sh, C, blk->down_conv.weight, blk->down_conv.bias, P,
+    cx.chk(mvr_oan_diff_pool_ws(pl.X11, 2 * CN, Np, cx.sc(), cx.sh(), C, blk->down_conv.weight, blk->down_conv.bias, P,
                                 C, N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD), C, 0,
                                 g_pool_split ? pl.uimg : nullptr, pl.uimg_bytes, s));
   } else {
@@ -680,16 +765,18 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     cx.chk(launch_gemm(g, s));
   }
   dbg_hash(pl.XD, P, C, Kc, (int64_t)C * Kp, Kp, s);
-  // l2: OAFilter x H (in place on XD)
+  // l2: OAFilter x H (in place on XD); conv3 fuses the next OAFilter's first IN + BN
+  bool xdfold = false;
   for (int i = 0; i < H; ++i) {
-    cx.oafilter(blk->l2[i], xd);
+    const FoldReq fn{1e-3f, i + 1 < H ? blk->l2[i + 1].bn1 : mvr_bn_p{}};
+    xdfold = cx.oafilter(blk->l2[i], xd, i + 1 < H ? &fn : nullptr, xdfold);
     dbg_hash(pl.XD, P, C, Kc, (int64_t)C * Kp, Kp, s);
   }
 
   // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C): softmax over clusters
-  cx.finalize_in(x11top, 1e-3f, blk->up_bn);
+  if (!up_folded) cx.finalize_in(x11top, 1e-3f, blk->up_bn, pl.scU, pl.shU);
   if (pl.fused) {
-    cx.chk(mvr_oan_diff_unpool(pl.X11, 2 * CN, Np, pl.sc, pl.sh, C, blk->up_conv.weight, blk->up_conv.bias, pl.XD,
+    cx.chk(mvr_oan_diff_unpool(pl.X11, 2 * CN, Np, pl.scU, pl.shU, C, blk->up_conv.weight, blk->up_conv.bias, pl.XD,
                                (int64_t)C * Kp, Kp, P, C, N, Kc, pl.X11 + CN, 2 * CN, Np,
                                reinterpret_cast<float*>(pl.st11), 2 * C, C, pl.uimg, pl.uimg_bytes, s));
   } else {
@@ -724,13 +811,15 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   probe.has_res = 1; probe.bias_mode = BIAS_M; probe.head_w = blk->output.weight;
   probe.no_store = latent ? 0 : 1;   // a block whose activation is not returned keeps only the head's output
   const bool fuse_head = pconv_covers(probe);   // (that PointCN then stays on the conv3 + conv7 pair)
+  bool ofold = false;
   for (int i = 0; i < H; ++i) {
     if (fuse_head && i == H - 1) {
       cx.head = &blk->output;
       cx.head_only = latent == nullptr;
       cx.h_logits = logits; cx.h_scores = scores; cx.h_pos = guard_pos;
     }
-    cx.pointcn(blk->l1_2[i], i == 0 ? x11 : out, out);
+    const FoldReq fn{1e-5f, i + 1 < H ? blk->l1_2[i + 1].bn1 : mvr_bn_p{}};
+    ofold = cx.pointcn(blk->l1_2[i], i == 0 ? x11 : out, out, i + 1 < H ? &fn : nullptr, i > 0 && ofold);
     dbg_hash(pl.T1, P, C, N, CN, Np, s);
     if (latent || i < H - 1) dbg_hash(out.p, P, C, N, out.ps, out.ld, s);
   }

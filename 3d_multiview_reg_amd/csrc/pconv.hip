@@ -78,7 +78,111 @@ struct PcArgs {
   int64_t rld;                                  // XI & 2: row stride of the block input R
   int* range; const int* guard; int epoch;      // split-fp16: the caller's zeroed flag word, set to epoch (1) when an
                                                 // activation is out of range; split-bf16 re-run: return unless *guard == epoch
+  // the output's InstanceNorm fold, finished by the workgroup that completes a pair's statistics (GemmArgs fin_*)
+  int* fcnt; float feps; mvr_bn_p fbn; float* fsc; float* fsh; int64_t fld;
+  float feps2; mvr_bn_p fbn2; float* fsc2; float* fsh2; int ftrain; float2* fmv;
 };
+
+// (sc, sh) of IN(eps) + BN(eval) from the pooled (mean, var): in_finalize_kernel's arithmetic
+__device__ __forceinline__ void fold_write(const mvr_bn_p& bn, float eps, double mean, double var, float* sc, float* sh,
+                                           int64_t at, int c) {
+  const float rin = (float)(1.0 / sqrt(var + (double)eps));
+  float g = 1.f, b = 0.f, rm = 0.f, rs = 1.f;
+  if (bn.gamma) {
+    g = bn.gamma[c];
+    b = bn.beta[c];
+    rm = bn.mean[c];
+    rs = 1.f / sqrtf(bn.var[c] + 1e-5f);
+  }
+  const float gs = g * rs;
+  sc[at] = rin * gs;
+  sh[at] = (float)((double)b - (mean * (double)rin + (double)rm) * (double)gs);
+}
+
+// Fused InstanceNorm finalize of pair p (the caller is the workgroup whose counter arrival completed the pair's
+// statistics, behind an agent-scope acquire): the 128 channels' partials of its T = ngrp 128-point tiles merged
+// exactly as in_finalize_kernel does for 128 channels (4 tile groups t = g, g + 4, ..., their double partials
+// combined in group order; Chan's merge), so the fold is bit-identical to the separate launch's.
+// red: 4 x 128 doubles of LDS scratch; threads 0..255 take part, every thread of the workgroup reaches the barriers.
+__device__ void fin_pair(const PcArgs& a, int p, double* red, int tid) {
+  const int T = a.ngrp, L = a.N, c = tid & 127, g0 = 2 * ((tid >> 7) & 1);
+  const bool act = tid < 256;
+  const float2* sp = a.stats + (int64_t)p * T * a.st_ld + a.st_off + c;
+  if (act) {
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll 4
+    for (int t = g0; t < T; t += 4) t0 += (double)sp[(int64_t)t * a.st_ld].x;
+#pragma unroll 4
+    for (int t = g0 + 1; t < T; t += 4) t1 += (double)sp[(int64_t)t * a.st_ld].x;
+    red[g0 * 128 + c] = t0;
+    red[(g0 + 1) * 128 + c] = t1;
+  }
+  __syncthreads();
+  double tot = 0.0;
+  for (int j = 0; j < 4; ++j) tot += red[j * 128 + c];
+  const double mean = tot / L, rtw = 1.0 / 128;
+  double m2[2] = {0.0, 0.0};
+  if (act) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll 4
+      for (int t = g0 + u; t < T; t += 4) {
+        const float2 v = sp[(int64_t)t * a.st_ld];
+        const int nv = min(128, L - 128 * t);
+        const double d = (double)v.x * (nv == 128 ? rtw : 1.0 / nv) - mean;
+        m2[u] += (double)v.y + d * d * nv;
+      }
+    }
+  }
+  __syncthreads();   // every group has read the sums
+  if (act) {
+    red[g0 * 128 + c] = m2[0];
+    red[(g0 + 1) * 128 + c] = m2[1];
+  }
+  __syncthreads();
+  if (tid < 128) {
+    double m = 0.0;
+    for (int j = 0; j < 4; ++j) m += red[j * 128 + c];
+    const double var = fmax(m / L, 0.0);
+    if (a.ftrain) {
+      a.fmv[(int64_t)p * PC + c] = make_float2((float)mean, (float)var);
+    } else {
+      fold_write(a.fbn, a.feps, mean, var, a.fsc, a.fsh, (int64_t)p * a.fld + c, c);
+      if (a.fsc2) fold_write(a.fbn2, a.feps2, mean, var, a.fsc2, a.fsh2, (int64_t)p * a.fld + c, c);
+    }
+  }
+  __syncthreads();   // red is reused by the next pair
+}
+
+// lastp: 32 x YLD ints of LDS scratch ([0] count, [1..] the pairs this workgroup completes), red: fin_pair's
+__device__ void fin_tail(const PcArgs& a, int* lastp, double* red, int tid) {
+  const int64_t G = a.groups;
+  const int64_t g0 = G * blockIdx.x / gridDim.x, g1 = G * (blockIdx.x + 1) / gridDim.x;
+  if (g0 >= g1) return;   // uniform (such a workgroup returned before its main loop anyway)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int nl = 0;
+    const int pfirst = (int)(g0 / a.ngrp), plast = (int)((g1 - 1) / a.ngrp);
+    for (int p = pfirst; p <= plast; ++p) {
+      const int64_t lo = g0 > (int64_t)p * a.ngrp ? g0 : (int64_t)p * a.ngrp;
+      const int64_t hi = g1 < (int64_t)(p + 1) * a.ngrp ? g1 : (int64_t)(p + 1) * a.ngrp;
+      const int n = (int)(hi - lo);
+      const int old = __hip_atomic_fetch_add(a.fcnt + p, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old + n == a.ngrp && nl < 32 * YLD - 1) lastp[1 + nl++] = p;
+    }
+    lastp[0] = nl;
+    if (nl) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  const int nl = lastp[0];
+  for (int i = 0; i < nl; ++i) fin_pair(a, lastp[1 + i], red, tid);
+}
 
 #define PC_FENCE() __builtin_amdgcn_sched_barrier(0)
 
@@ -609,6 +713,18 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
   }
   if (H && __any(xbad || (xmx > 0.f && xmx < 0.125f)) && lane == 0) atomicExch(a.range, a.epoch);
+  if constexpr (STATS && !H) {
+    // Fused finalize (a.fcnt): publish this workgroup's statistics partials (every wave drains its stores, one
+    // agent-scope release), add its tile count to each of its pairs' arrival counters; the workgroup completing
+    // a pair acquires and merges that pair's partials (the in-launch reduction recipe of
+    // cdna_hip_programming.md: correct for any spread of a pair's tiles over XCDs).  The arguments are re-read
+    // here through an opaque kernarg pointer and the range recomputed, so none of it stays live (in SGPRs)
+    // across the main loop.  Scratch: ys (free now).
+    const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    const PcArgs& A = *reinterpret_cast<const PcArgs*>(ka);
+    if (A.fcnt) fin_tail(A, reinterpret_cast<int*>(&ys[0][0]), reinterpret_cast<double*>(&ys[1][0]), tid);
+  }
 }
 
 }  // namespace
@@ -666,10 +782,21 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   // head launches (their positive counts are atomics) nor where the output overwrites the residual in place
   // (the re-run needs the residual intact).  Which arithmetic a launch takes depends on its arguments and
   // operand values only (no process state: no launch counters, no address-range tests).
-  const bool h1 = g_pconv_h && g.flag && !head && !(g.has_res && g.R == g.C);
+  // (the same alias test as gemm.hip's launch_t: the re-run needs every input intact)
+  const bool h1 = g_pconv_h && g.flag && !head && !(g.C == g.A || g.C == g.B || (g.has_res && g.R == g.C));
   if (h1) {
     a.range = g.flag;
     a.epoch = 1;
+  }
+  // the output's InstanceNorm fold in the last-arriving workgroup of each pair (split-bf16 launches only: the
+  // split-fp16 pass and its guarded re-run would both arrive)
+  if (g.fin_cnt && st && !h1 && !head) {
+    if (!g.fin_train && (!g.fin_sc || !g.fin_sh)) return MVR_EINVAL;
+    if (g.fin_train && !g.fin_mv) return MVR_EINVAL;
+    a.fcnt = g.fin_cnt; a.feps = g.fin_eps; a.fbn = g.fin_bn; a.fsc = g.fin_sc; a.fsh = g.fin_sh; a.fld = g.fin_ld;
+    a.feps2 = g.fin_eps2; a.fbn2 = g.fin_bn2; a.fsc2 = g.fin_sc2; a.fsh2 = g.fin_sh2;
+    a.ftrain = g.fin_train; a.fmv = g.fin_mv;
+    if (g.fin_done) *g.fin_done = 1;
   }
 #define MVR_PCL(THREADS, ...)                                                   \
   do {                                                                          \

@@ -60,7 +60,9 @@ __device__ __forceinline__ int lattice_sub(uint64_t key, int t) {
 
 // lookup in a lattice table (t >= 0): the home bucket's 8 keys in one round trip (4 x 16-byte loads).  The insert
 // probed from slot lattice_sub of the home bucket onwards, so an empty slot at or after it in the home bucket, or
-// anywhere in a later bucket, that the key is not before proves it absent (slots never empty again)
+// anywhere in a later bucket, that the key is not before proves it absent (slots never empty again).  This relies on
+// no insert wrapping all the way round the table back into its home bucket's lower slots: hash_table_bytes sizes
+// every table at >= 2 slots per key (load <= 1/2), so a probe run never spans the table.
 __device__ __forceinline__ int64_t hash_find_bucket(const HashView& h, uint64_t key, int t) {
   uint64_t b = hash_home(h, key, t);
   int from = lattice_sub(key, t);
@@ -297,7 +299,11 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
   const int r = ks / 2;
   const int dx = k % ks - r, dy = (k / ks) % ks - r, dz = k / (ks * ks) - r;
   const int4 c = oc[o];
-  const int t = h.hdr[0];   // uniform: the table's home mode
+  int t = h.hdr[0];         // uniform: the table's home mode (-1 hashed, 0..15 lattice of stride 2^t)
+  if (t < -1 || t > 15) {   // not a table hash_build wrote: no neighbour can be proven present
+    nbr[e] = -1;
+    return;
+  }
   const int64_t v =
       hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step, c.w + sign * dz * step), t);
   nbr[e] = (int32_t)v;

@@ -133,13 +133,17 @@ def knn_point(k, pos1, pos2):
     """utils.py:274-299: (squared distances, indices) [b, m, k] of the k nearest pos1 [b, n, 3] points for each pos2
     [b, m, 3] point, nearest first.  k = 1 (the reference's only use, extract_mutuals) is csrc/knn.hip mvr_knn1 in
     the reference's fp32 arithmetic without materialising the [b, m, n, 3] repeats; k > 1 evaluates the same
-    expression in query chunks with torch.topk on the device."""
+    expression in query chunks with torch.topk on the device.
+    Device contract: pos1 on the HIP device (the op has no CPU path; CPU inputs raise), pos2 moved to it; results
+    on that device.  NaN: a NaN distance is never selected by k = 1 (strict '<' scan; an all-NaN row returns
+    index 0 and distance inf) where the reference's topk would return it; k > 1 keeps topk's NaN ordering."""
     N.require_hip(pos1)
+    pos2 = pos2.to(pos1.device)
     B, n, _ = pos1.shape
     m = pos2.shape[1]
     if k == 1:
         p1, s1b, s1r = _rows3(pos1)
-        p2, s2b, s2r = _rows3(pos2.to(pos1.device))
+        p2, s2b, s2r = _rows3(pos2)
         d = torch.empty(B, m, 1, dtype=torch.float32, device=pos1.device)
         idx = torch.empty(B, m, 1, dtype=torch.int64, device=pos1.device)
         if B and m:
@@ -162,7 +166,7 @@ def extract_mutuals(x1, x2, x1_soft_matches, x2_soft_matches, threshold=0.05):
     """utils.py:822-848: mutuals [b, n] float32, 1 where x1[i]'s soft match, snapped to its nearest x2 point j, maps
     back (x2_soft_matches[j]) to within `threshold` of x1[i].  One csrc/knn.hip mvr_mutuals launch (NN search,
     gather and threshold fused).  The reference fills a host tensor from a device mask (which fails for CUDA
-    inputs); the flags stay on the inputs' device here."""
+    inputs); the flags stay on the inputs' device here (x1 on the HIP device; CPU inputs raise — INTEGRATION.md)."""
     N.require_hip(x1)
     B, Np, _ = x1.shape
     dev = x1.device

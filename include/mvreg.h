@@ -10,6 +10,13 @@
  *     re-entrant, and thread-safe across distinct streams/devices;
  *   - strides are in ELEMENTS.
  *
+ * Process-wide settings: every mvr_set_* entry point (operand maths, kernel variants, A/B switches) writes ONE
+ * process-global value of the library, read by the host side of each later call when it builds its launches.
+ * They are not per stream, per thread or per call.  Set them once, before any thread issues work, and leave
+ * them: two threads selecting different settings race (a call sees whichever value was last written), and a
+ * change never affects launches already enqueued.  The defaults are the fp32-equivalent paths the parity tests
+ * pin; the Python mirror sets them only through lib._native.set_math, before the first forward.
+ *
  * Each entry point names the reference interface it replaces
  * (paths relative to the reference repo).
  */
@@ -141,7 +148,10 @@ size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels
  *   bit 0: diff_pool / diff_unpool as the fused attention kernels (mvr_oan_diff_pool / _unpool) when
  *          channels == 128 and clusters <= 1024 (else embedding GEMM + softmax factors + pooling GEMM);
  *   bit 2: the block's conv1 (in_channels <= 8 -> 128) folded into the first PointCN's point convs;
- *   bit 1 is unused (ignored).  Default 5.
+ *   bit 3: InstanceNorm folds (the next conv's IN + BN scale / shift) finished inside the producing point conv
+ *          by the workgroup whose arrival completes a pair's statistics, instead of a separate finalize launch
+ *          (bit-identical results: the same merge order);
+ *   bit 1 is unused (ignored).  Default 13.
  * Returns the previous value. */
 int mvr_set_oan_fused(int on);
 /* Key-split diff_pool launches inside mvr_oan_block_forward (mvr_oan_diff_pool_ws): 1 (default) on, 0 off

@@ -404,3 +404,34 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
             r32, r64 = o32[k][i], o64[k][i]
             bound = np.maximum(1e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
             assert (dist(f, r64) <= bound).all(), (i, k, dist(f, r64), dist(m, r64), dist(r32, r64))
+
+
+@pytest.mark.parametrize("P,npts,train", [(37, 1234, False), (70, 1500, True), (600, 100, False), (3, 5000, False)])
+def test_oanet_fused_finalize_bit_identical(gpu, P, npts, train):
+    """InstanceNorm folds finished inside their producing point conv (the workgroup whose arrival completes a
+    pair's statistics merges them, mvr_set_oan_fused bit 3) vs the separate in_finalize launches: the same
+    merge order in both, so every output is bit-identical — eval and train-mode BatchNorm (32-pair groups), a
+    ragged point count, one statistics tile per pair with more pairs than resident workgroups (a workgroup then
+    completes several pairs), and few pairs (a pair's tiles spread over many workgroups)."""
+    import torch
+    from lib import _native as NV
+    from test_gpu_oanet import _oanet
+    from synth import synth_correspondences
+    xs, _, _ = synth_correspondences(P, npts, seed=5)
+    net = _oanet(128, 500, 7, gpu, train=train, which="full")
+    if train:
+        net.bn_group = net.guard_group = 32
+    L = NV.lib()
+    prev = L.mvr_set_oan_fused(13)
+    outs = []
+    try:
+        for f in (13, 5):
+            L.mvr_set_oan_fused(f)
+            with torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    finally:
+        L.mvr_set_oan_fused(prev)
+    a, b = outs
+    for k in ("logits", "scores", "rot_est", "trans_est"):
+        for i in range(2):
+            assert torch.equal(a[k][i], b[k][i]), (k, i, (a[k][i] - b[k][i]).abs().max().item())
