@@ -325,23 +325,26 @@ struct BrickView {
 
 __device__ __forceinline__ int brick_cell(int x, int y, int z) { return (x & 3) | ((y & 3) << 2) | ((z & 3) << 4); }
 
-__global__ void brick_insert_kernel(const int4* __restrict__ c, int64_t M, HashView h) {
+// A set at tensor stride 2^t (coordinates multiples of 2^t): cells are coordinates >> t, bricks 4 cells a side
+// (brick coordinates >> (t + 2)); t = 0 for the voxel set itself.
+__global__ void brick_insert_kernel(const int4* __restrict__ c, int64_t M, HashView h, int t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < M) {
     const int4 v = c[i];
-    hash_insert_min(h, pack_key(v.x, v.y >> 2, v.z >> 2, v.w >> 2), (int32_t)i);
+    hash_insert_min(h, pack_key(v.x, v.y >> (t + 2), v.z >> (t + 2), v.w >> (t + 2)), (int32_t)i);
   }
 }
 
 // representatives (the minimum row of each brick) draw brick ids; wave-aggregated counter
 __global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView h, int32_t* count,
-                                 int32_t* slot_of, int4* bcoord) {
+                                 int32_t* slot_of, int4* bcoord, int t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t sl = -1;
   bool rep = false;
+  int4 v = make_int4(0, 0, 0, 0);
   if (i < M) {
-    const int4 v = c[i];
-    sl = hash_slot(h, pack_key(v.x, v.y >> 2, v.z >> 2, v.w >> 2));
+    v = c[i];
+    sl = hash_slot(h, pack_key(v.x, v.y >> (t + 2), v.z >> (t + 2), v.w >> (t + 2)));
     rep = sl >= 0 && h.vals[sl] == (int32_t)i;
     slot_of[i] = (int32_t)sl;
   }
@@ -351,17 +354,26 @@ __global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView
   if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
   base = __shfl(base, 0, 64);
   if (rep) h.vals[sl] = base + __popcll(m & ((1ULL << lane) - 1));
-  if (rep) bcoord[h.vals[sl]] = make_int4(c[i].x, c[i].y >> 2, c[i].z >> 2, c[i].w >> 2);
+  if (rep) bcoord[h.vals[sl]] = make_int4(v.x, v.y >> (t + 2), v.z >> (t + 2), v.w >> (t + 2));
+}
+
+// the row slots of the bricks in use (count of them) to -1: the pool is sized for one brick per row, but a
+// surface fills ~1/10 of that — clearing only the used bricks is ~10x fewer bytes than clearing the pool
+__global__ void brick_rows_init_kernel(int32_t* rows, const int32_t* __restrict__ count) {
+  const int64_t n = (int64_t)count[0] * 16;   // int4 granules
+  int4* r = reinterpret_cast<int4*>(rows);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    r[i] = make_int4(-1, -1, -1, -1);
 }
 
 __global__ void brick_fill_kernel(const int4* __restrict__ c, int64_t M, HashView h, const int32_t* __restrict__ slot_of,
-                                  int32_t* rows) {
+                                  int32_t* rows, int t) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const int4 v = c[i];
   const int sl = slot_of[i];
   if (sl < 0) return;
-  rows[(int64_t)h.vals[sl] * 64 + brick_cell(v.y, v.z, v.w)] = (int32_t)i;
+  rows[(int64_t)h.vals[sl] * 64 + brick_cell(v.y >> t, v.z >> t, v.w >> t)] = (int32_t)i;
 }
 
 // ------------------------------------------------------------------ conv1: Cin = 1, large stencil
@@ -671,6 +683,76 @@ __global__ void offset_mask_kernel(const int32_t* __restrict__ nbr, const int4* 
   rows[o] = (int32_t)o;
 }
 
+// 3^3 kernel map over the input set's brick map (stride 2^tin): one thread per output row.  The 27 neighbours
+// c + sign * d * step lie in at most 2 bricks per axis, so the row resolves <= 8 brick ids (one hash probe each,
+// in a table of ~M / 10 bricks) and reads each neighbour's row from its brick's 64-slot array — instead of 27
+// probes of the per-voxel coordinate table.  A neighbour off the input lattice (transposed maps: c - d s not a
+// multiple of 2^tin) is absent.  Same nbr[o][k] (k = (dx+1) + 3 (dy+1) + 9 (dz+1)) as kernel_map_kernel; with
+// `keys` it also writes the row's mvr_kernel_map_order sort key (active-offset mask, fragment, Morton code of
+// c / kstep), so the order needs no second pass over the table.
+__device__ __forceinline__ int brick_id_of(const HashView& h, int b, int bx, int by, int bz) {
+  const int64_t sl = hash_slot(h, pack_key(b, bx, by, bz));
+  return sl >= 0 ? h.vals[sl] : -1;
+}
+__global__ __launch_bounds__(256) void kernel_map_brick_kernel(const int4* __restrict__ oc, int64_t Mo, BrickView bv,
+                                                               int tin, int step, int sign, int32_t* __restrict__ nbr,
+                                                               uint64_t* __restrict__ keys, int kstep) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= Mo) return;
+  const int4 c = oc[o];
+  const int tb = tin + 2, amask = (1 << tin) - 1;
+  int n[3][3];   // [axis][d + 1]: neighbour coordinate
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    n[0][d] = c.y + sign * (d - 1) * step;
+    n[1][d] = c.z + sign * (d - 1) * step;
+    n[2][d] = c.w + sign * (d - 1) * step;
+  }
+  int lo[3], two[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int b0 = n[a][0] >> tb, b2 = n[a][2] >> tb;   // monotone in d: the extremes are d = -1 and d = +1
+    lo[a] = min(b0, b2);
+    two[a] = b0 != b2;
+  }
+  int id[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int ix = q & 1, iy = (q >> 1) & 1, iz = q >> 2;
+    id[q] = ((ix && !two[0]) || (iy && !two[1]) || (iz && !two[2]))
+                ? -1 : brick_id_of(bv.h, c.x, lo[0] + ix, lo[1] + iy, lo[2] + iz);
+  }
+  uint32_t m = 0;
+  int32_t* dst = nbr + o * 27;
+#pragma unroll
+  for (int dz = 0; dz < 3; ++dz)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int x = n[0][dx], y = n[1][dy], z = n[2][dz];
+        const int q = ((x >> tb) != lo[0]) | (((y >> tb) != lo[1]) << 1) | (((z >> tb) != lo[2]) << 2);
+        int bid = id[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) bid = q == j ? id[j] : bid;   // register select, no indexed scratch
+        const bool ok = bid >= 0 && ((x | y | z) & amask) == 0;
+        const int row = ok ? bv.rows[(int64_t)bid * 64 + brick_cell(x >> tin, y >> tin, z >> tin)] : -1;
+        const int k = dx + 3 * dy + 9 * dz;
+        dst[k] = row;
+        m |= (row >= 0 ? 1u : 0u) << k;
+      }
+  if (keys) {
+    const uint32_t l = ((uint32_t)c.x & 31u) << 27 | spread3((uint32_t)(c.y / kstep)) << 2 |
+                       spread3((uint32_t)(c.z / kstep)) << 1 | spread3((uint32_t)(c.w / kstep));
+    keys[o] = (uint64_t)m << 32 | l;
+  }
+}
+
+__global__ void iota_kernel(int32_t* v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (int32_t)i;
+}
+
 }  // namespace mvr
 
 using namespace mvr;
@@ -794,22 +876,31 @@ static BrickView brick_view(void* ws, int64_t M) {
 
 extern "C" size_t mvr_brick_map_bytes(int64_t M) { return brick_map_bytes(M); }
 
-extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (!coords || M < 0 || !ws || ws_bytes < brick_map_bytes(M)) return MVR_EINVAL;
+extern "C" int mvr_brick_map_build_stride(const int32_t* coords, int64_t M, int stride, void* ws, size_t ws_bytes,
+                                          hipStream_t s) {
+  if (!coords || M < 0 || !ws || ws_bytes < brick_map_bytes(M) || stride <= 0 || (stride & (stride - 1)) ||
+      stride > (1 << 12))
+    return MVR_EINVAL;
+  const int t = __builtin_ctz((unsigned)stride);
   BrickView v = brick_view(ws, M);
   int32_t* slot_of = v.rows + (M > 0 ? M : 1) * 64;
-  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)v.h.cap * 12 + M * 300.0, s);
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)v.h.cap * 12 + M * 40.0, s);
   if (hipMemsetAsync(v.count, 0, 16, s) != hipSuccess) return MVR_ELAUNCH;
-  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)v.h.cap)), dim3(256), 0, s, v.h);
+  hipLaunchKernelGGL(hash_clear_kernel, dim3(nblk((int64_t)v.h.cap)), dim3(256), 0, s, v.h, -1);
   if (M > 0) {
-    if (hipMemsetAsync(v.rows, 0xff, (size_t)M * 64 * 4, s) != hipSuccess) return MVR_ELAUNCH;
     const int4* c = reinterpret_cast<const int4*>(coords);
-    hipLaunchKernelGGL(brick_insert_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h);
-    hipLaunchKernelGGL(brick_ids_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, v.count, slot_of, v.bcoord);
-    hipLaunchKernelGGL(brick_fill_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, slot_of, v.rows);
+    hipLaunchKernelGGL(brick_insert_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, t);
+    hipLaunchKernelGGL(brick_ids_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, v.count, slot_of, v.bcoord, t);
+    hipLaunchKernelGGL(brick_rows_init_kernel, dim3((unsigned)std::min<int64_t>(1024, nblk(M * 16))), dim3(256), 0, s,
+                       v.rows, v.count);
+    hipLaunchKernelGGL(brick_fill_kernel, dim3(nblk(M)), dim3(256), 0, s, c, M, v.h, slot_of, v.rows, t);
   }
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, size_t ws_bytes, hipStream_t s) {
+  return mvr_brick_map_build_stride(coords, M, 1, ws, ws_bytes, s);
 }
 
 extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
@@ -868,6 +959,50 @@ extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) {
   const size_t n = (size_t)(Mo > 0 ? Mo : 1);
   return order_sort_bytes(Mo) + n * 20 + 3 * 256;
 }
+// 3^3 kernel maps over brick maps (kernel_map_brick_kernel): in_bricks = mvr_brick_map_build_stride of the Min
+// input coordinates at tensor stride in_stride; neighbour of output c at offset d: c + d step (transposed:
+// c - d step).  order_keys (optional, uint64 [Mout]): the rows' sort keys for mvr_kernel_map_order_keys
+// (out_stride: the output set's tensor stride, for the Morton code).
+extern "C" int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, int out_stride, const void* in_bricks,
+                                     int64_t Min, size_t in_bricks_bytes, int in_stride, int step, int transposed,
+                                     int32_t* nbr, uint64_t* order_keys, hipStream_t s) {
+  if (!out_coords || Mout < 0 || !in_bricks || Min < 0 || in_bricks_bytes < brick_map_bytes(Min) || step <= 0 ||
+      in_stride <= 0 || (in_stride & (in_stride - 1)) || in_stride > (1 << 12) || out_stride <= 0 || !nbr)
+    return MVR_EINVAL;
+  if (Mout == 0) return MVR_OK;
+  BrickView v = brick_view(const_cast<void*>(in_bricks), Min);
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mout * (16 + 27 * 4 + 8 * 12 + (order_keys ? 8 : 0)), s);
+  hipLaunchKernelGGL(kernel_map_brick_kernel, dim3(nblk(Mout)), dim3(256), 0, s,
+                     reinterpret_cast<const int4*>(out_coords), Mout, v, __builtin_ctz((unsigned)in_stride), step,
+                     transposed ? -1 : 1, nbr, order_keys, out_stride);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+// the row order from precomputed keys (mvr_kernel_map_bricks' order_keys): the same stable LSD radix sort as
+// mvr_kernel_map_order over the same keys.  keys is not modified.  Workspace: mvr_kernel_map_order_bytes(Mo).
+extern "C" int mvr_kernel_map_order_keys(const uint64_t* keys, int64_t Mo, int K, int32_t* perm, void* ws,
+                                         size_t ws_bytes, hipStream_t s) {
+  if (!keys || !perm || Mo < 0 || K <= 0 || K > 32 || !ws || ws_bytes < mvr_kernel_map_order_bytes(Mo) ||
+      Mo > 0x7fffffff)
+    return MVR_EINVAL;
+  if (Mo == 0) return MVR_OK;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mo * 32, s);
+  char* p = reinterpret_cast<char*>(ws);
+  auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
+  take((size_t)Mo * 8);   // (mvr_kernel_map_order's key buffer: unused here)
+  uint64_t* kout = reinterpret_cast<uint64_t*>(take((size_t)Mo * 8));
+  int32_t* vin = reinterpret_cast<int32_t*>(take((size_t)Mo * 4));
+  size_t tmp = order_sort_bytes(Mo);
+  if (!tmp) return MVR_ELAUNCH;
+  void* tbuf = take(tmp);
+  hipLaunchKernelGGL(iota_kernel, dim3(nblk(Mo)), dim3(256), 0, s, vin, Mo);
+  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, keys, kout, vin, perm, (int)Mo, 0, 32 + K, s) != hipSuccess)
+    return MVR_ELAUNCH;
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
 extern "C" int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mo, int K,
                                     int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s) {
   if (!nbr || !perm || Mo < 0 || K <= 0 || K > 32 || !ws || ws_bytes < mvr_kernel_map_order_bytes(Mo) ||

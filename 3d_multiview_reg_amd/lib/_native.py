@@ -113,12 +113,15 @@ _SIGS = {
     "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
     "mvr_kernel_map_order_bytes": (c_size, [c_i64]),
     "mvr_kernel_map_order": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
+    "mvr_kernel_map_bricks": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_size, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "mvr_kernel_map_order_keys": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
                            c_int, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "mvr_spconv_wimage_bytes": (c_size, [c_int, c_int, c_int]),
     "mvr_spconv_wimage": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_size, c_vp]),
     "mvr_brick_map_bytes": (c_size, [c_i64]),
     "mvr_brick_map_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),
+    "mvr_brick_map_build_stride": (c_int, [c_vp, c_i64, c_int, c_vp, c_size, c_vp]),
     "mvr_spconv_c1": (c_int, [c_vp, c_i64, c_vp, c_i64, c_size, c_vp, c_int, c_int, c_vp, c_int, BnP, c_float, c_int,
                               c_vp, c_i64, c_vp]),
     "mvr_l2norm_rows": (c_int, [c_vp, c_i64, c_int, c_i64, c_vp]),

@@ -8,10 +8,16 @@ ME 0.4 itself stored the batch index last).  Every coordinate set, hash table
 and kernel map lives in HBM and is cached on the CoordinateManager shared by all
 tensors of one forward pass.
 """
+import os
+
 import numpy as np
 import torch
 
 from lib import _native as N
+
+# 3^3 kernel maps over brick maps (csrc/sparse.hip kernel_map_brick_kernel); MVR_BRICK_MAPS=0 resolves them over
+# the per-level coordinate tables instead (A/B timing; identical maps)
+BRICK_MAPS = os.environ.get("MVR_BRICK_MAPS", "1") == "1"
 
 
 class CoordinateManager:
@@ -25,6 +31,7 @@ class CoordinateManager:
         self.bricks = {}
         self.maps = {}
         self.orders = {}
+        self.order_keys = {}
 
     def coords_at(self, s):
         if s not in self.coords:
@@ -52,19 +59,34 @@ class CoordinateManager:
         return self.tables[s]
 
     def brick_map(self, s):
-        """4x4x4 brick map of the stride-s set (large-stencil neighbourhoods, csrc/sparse.hip)."""
+        """4x4x4 brick map of the stride-s set (cells = coordinates / s; csrc/sparse.hip): the neighbourhood
+        structure of the 3^3 kernel maps and of conv1's 7^3 stencil."""
         if s not in self.bricks:
             c = self.coords_at(s)
             L = N.lib()
             nb = L.mvr_brick_map_bytes(c.shape[0])
             t = torch.empty(nb, dtype=torch.uint8, device=self.device)
-            N.check(L.mvr_brick_map_build(N.ptr(c), c.shape[0], N.ptr(t), nb, N.stream()), "mvr_brick_map_build")
+            N.check(L.mvr_brick_map_build_stride(N.ptr(c), c.shape[0], s, N.ptr(t), nb, N.stream()),
+                    "mvr_brick_map_build_stride")
             self.bricks[s] = t
         return self.bricks[s]
 
     def kernel_map(self, kind, s, ks=3):
-        """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed)."""
+        """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed).
+        3^3 maps are resolved over the input level's brick map (mvr_kernel_map_bricks, which also writes the
+        rows' order keys for kernel_map_order); other sizes over the level's coordinate table."""
         key = (kind, s, ks)
+        if key not in self.maps and ks == 3 and BRICK_MAPS:
+            out_s, in_s, tr = {"s1": (s, s, 0), "down": (2 * s, s, 0), "up": (s, 2 * s, 1)}[kind]
+            out_c, in_c = self.coords_at(out_s), self.coords_at(in_s)
+            bricks = self.brick_map(in_s)
+            nbr = torch.empty(out_c.shape[0], 27, dtype=torch.int32, device=self.device)
+            keys = torch.empty(out_c.shape[0], dtype=torch.int64, device=self.device)
+            N.check(N.lib().mvr_kernel_map_bricks(N.ptr(out_c), out_c.shape[0], out_s, N.ptr(bricks), in_c.shape[0],
+                                                  bricks.numel(), in_s, s, tr, N.ptr(nbr), N.ptr(keys), N.stream()),
+                    "mvr_kernel_map_bricks")
+            self.maps[key] = nbr
+            self.order_keys[key] = keys
         if key not in self.maps:
             if kind == "s1":
                 out_c, tab, tr = self.coords_at(s), self.table(s), 0
@@ -92,9 +114,14 @@ class CoordinateManager:
             L = N.lib()
             ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr.shape[0]), self.device)
             perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.device)
-            N.check(L.mvr_kernel_map_order(N.ptr(nbr), N.ptr(out_c), 2 * s if kind == "down" else s, nbr.shape[0],
-                                           nbr.shape[1], N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
-                    "mvr_kernel_map_order")
+            if key in self.order_keys:   # keys written by the brick kernel map
+                N.check(L.mvr_kernel_map_order_keys(N.ptr(self.order_keys.pop(key)), nbr.shape[0], nbr.shape[1],
+                                                    N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
+                        "mvr_kernel_map_order_keys")
+            else:
+                N.check(L.mvr_kernel_map_order(N.ptr(nbr), N.ptr(out_c), 2 * s if kind == "down" else s,
+                                               nbr.shape[0], nbr.shape[1], N.ptr(perm), N.ptr(ws), ws.numel(),
+                                               N.stream()), "mvr_kernel_map_order")
             self.orders[key] = perm
         return self.orders[key]
 
@@ -137,7 +164,9 @@ def voxelize(points_list, voxel_size, device, distinct_hint=None):
     pts = [torch.as_tensor(np.asarray(p, dtype=np.float32)) if not torch.is_tensor(p) else p.float() for p in points_list]
     B = len(pts)
     n = [int(p.shape[0]) for p in pts]
-    xyz = torch.cat(pts, 0).to(device).contiguous()
+    xyz = _adjacent_views(pts, device)
+    if xyz is None:
+        xyz = torch.cat(pts, 0).to(device).contiguous()
     off = torch.tensor(np.concatenate([[0], np.cumsum(n)]), dtype=torch.int64).pin_memory().to(device, non_blocking=True)
     total = int(sum(n))
     L = N.lib()
@@ -165,6 +194,37 @@ def voxelize(points_list, voxel_size, device, distinct_hint=None):
     xyz_down = torch.empty(M, 3, device=device)
     N.check(L.mvr_gather_rows(N.ptr(xyz), 3, N.ptr(sel), M, N.ptr(xyz_down), N.stream()), "mvr_gather_rows")
     return coords, sel, [int(v) for v in c[1:1 + B]], xyz_down
+
+
+def fragment_views(points_list, device):
+    """The fragments copied once into ONE contiguous device buffer, returned as views of it: voxelize() then
+    reads them in place (no per-call concatenation of the raw points)."""
+    pts = [torch.as_tensor(np.asarray(p, dtype=np.float32)) if not torch.is_tensor(p) else p.float() for p in points_list]
+    buf = torch.cat([p.reshape(-1, 3).to(device) for p in pts], 0).contiguous()
+    views, o = [], 0
+    for p in pts:
+        views.append(buf[o:o + p.shape[0]])
+        o += p.shape[0]
+    return views
+
+
+def _adjacent_views(pts, device):
+    """the [sum n, 3] tensor the fragments already form when they are consecutive row ranges of one contiguous
+    buffer on `device` (fragment_views), else None"""
+    if not pts:
+        return None
+    dev = torch.device(device)
+    first = pts[0]
+    if first.device.type != dev.type or (dev.index is not None and first.device.index != dev.index):
+        return None
+    ptr = first.data_ptr()
+    for p in pts:
+        if p.device != first.device or p.dim() != 2 or p.shape[1] != 3 or p.dtype != torch.float32 or \
+                not p.is_contiguous() or p.data_ptr() != ptr:
+            return None
+        ptr += p.numel() * 4
+    total = sum(int(p.shape[0]) for p in pts)
+    return first.new_empty(0).set_(first.untyped_storage(), first.storage_offset(), (total, 3), (3, 1))
 
 
 _VOX_HINT = {}   # per device: voxel-count estimate for the next voxelize() table (the last call's count + 50 %)

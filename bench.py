@@ -141,6 +141,7 @@ class SceneWorkload:
     def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025, samp="rand", shard="scenes", world=1,
                  groups=None):
         import lib.config
+        from lib.sparse import fragment_views
         from synth import synth_scene_fragments
         cfg = oanet_cfg()
         cfg["method"]["descriptor_module"] = "fcgf"
@@ -168,9 +169,9 @@ class SceneWorkload:
             self.p0, self.p1 = D.shard_pairs(self.pairs, world, rank, group=1)
             self.pair_block = pair_index(n_frag, dev)[self.p0:self.p1].contiguous()
             self.pg_counts, self.pg_samples, self.pg_filter = groups
-            self.raw = [torch.from_numpy(f).to(dev) for f in self.frags[self.f0:self.f1]]
+            self.raw = fragment_views(self.frags[self.f0:self.f1], dev)
         else:
-            self.raw = [torch.from_numpy(f).to(dev) for f in self.frags]     # resident in HBM
+            self.raw = fragment_views(self.frags, dev)     # resident in HBM, one buffer (voxelize reads it in place)
 
     def prepare(self):
         """voxelise (prepare_data on the GPU) and build the strided coordinate sets of the sparse input: every

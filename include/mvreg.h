@@ -376,6 +376,20 @@ int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table
 size_t mvr_kernel_map_order_bytes(int64_t Mout);
 int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mout, int K, int32_t* perm,
                          void* workspace, size_t workspace_bytes, mvr_stream_t stream);
+/* 3^3 kernel map (the same nbr[o][k] as mvr_kernel_map with ksize 3) over the INPUT set's brick map
+ * (mvr_brick_map_build_stride of its Min coordinates at tensor stride in_stride, a power of two): neighbour of
+ * out_coords[o] at offset d = out + d*step (transposed: out - d*step; a neighbour off the input lattice is absent).
+ * One thread per output row resolves the <= 8 bricks its 27 neighbours fall in.  order_keys (optional, uint64
+ * [Mout]): each row's sort key of mvr_kernel_map_order (active-offset mask, then fragment and Morton code of
+ * out_coords / out_stride), for mvr_kernel_map_order_keys.  Replaces the per-voxel table probes of the ME
+ * CoordinateManager's kernel maps (fcgf.py:118-227). */
+int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, int out_stride, const void* in_bricks, int64_t Min,
+                          size_t in_bricks_bytes, int in_stride, int step, int transposed, int32_t* nbr,
+                          uint64_t* order_keys, mvr_stream_t stream);
+/* mvr_kernel_map_order from mvr_kernel_map_bricks' order_keys (the same stable sort of the same keys: the same
+ * perm).  Workspace: mvr_kernel_map_order_bytes(Mout). */
+int mvr_kernel_map_order_keys(const uint64_t* order_keys, int64_t Mout, int K, int32_t* perm, void* workspace,
+                              size_t workspace_bytes, mvr_stream_t stream);
 /* MinkowskiConvolution forward, gather-GEMM over the neighbour table (nbr NULL & K==1:
  * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
  * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
@@ -408,10 +422,14 @@ int mvr_set_spconv_math(int h);
    Returns the previous setting. */
 int mvr_set_spconv_xcd(int on);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
- * neighbourhood structure of the large-stencil conv below.  Workspace: mvr_brick_map_bytes(M). */
+ * neighbourhood structure of the large-stencil conv below and of mvr_kernel_map_bricks.  Workspace:
+ * mvr_brick_map_bytes(M).  _stride: a set at tensor stride `stride` (a power of two, coordinates multiples of it):
+ * cells are coordinates / stride; mvr_brick_map_build = stride 1. */
 size_t mvr_brick_map_bytes(int64_t M);
 int mvr_brick_map_build(const int32_t* coords, int64_t M, void* workspace, size_t workspace_bytes,
                         mvr_stream_t stream);
+int mvr_brick_map_build_stride(const int32_t* coords, int64_t M, int stride, void* workspace, size_t workspace_bytes,
+                               mvr_stream_t stream);
 /* single-input-channel conv with a large stencil (FCGF conv1, 7^3) over the input set's brick map
  * (in_bricks built from the Min input coordinates; input cell = coordinate / step).
  * out_coords NULL: the output set is the input set itself (Mout == Min, step 1, ksize 7; output row o =

@@ -114,6 +114,44 @@ def test_lattice_table_kernel_maps_dense_and_sparse(gpu, stride):
                 dx, dy, dz = k % 3 - 1, (k // 3) % 3 - 1, k // 9 - 1
                 ref[o, k] = index.get((b, x + sg * dx * stride, y + sg * dy * stride, z + sg * dz * stride), -1)
         np.testing.assert_array_equal(maps[0], ref)
+        # the brick-map kernel map over the same set (mvr_kernel_map_bricks): the same table
+        nbb = L.mvr_brick_map_bytes(M)
+        br = torch.empty(nbb, dtype=torch.uint8, device=gpu)
+        N.check(L.mvr_brick_map_build_stride(N.ptr(cd), M, stride, N.ptr(br), nbb, N.stream()), "bricks")
+        nbr = torch.empty(M, 27, dtype=torch.int32, device=gpu)
+        N.check(L.mvr_kernel_map_bricks(N.ptr(cd), M, stride, N.ptr(br), M, nbb, stride, stride, tr, N.ptr(nbr), None,
+                                        N.stream()), "brick map")
+        np.testing.assert_array_equal(nbr.cpu().numpy(), ref)
+
+
+def test_brick_kernel_maps_equal_table_maps(gpu, frags):
+    """All ten 3^3 kernel maps of FCGF (s1 at strides 1-8, down 1-4, up 1-4) over the input level's brick map
+    (mvr_kernel_map_bricks) equal the maps over the level's lattice coordinate table (mvr_kernel_map), and the row
+    orders from the brick kernel's keys (mvr_kernel_map_order_keys) equal mvr_kernel_map_order's"""
+    import torch
+    from lib import _native as N
+    from lib.sparse import voxelize, CoordinateManager
+    L = N.lib()
+    c, _, counts, _ = voxelize(frags, 0.025, gpu)
+    cm = CoordinateManager(c, len(counts))
+    maps = [("s1", s) for s in (1, 2, 4, 8)] + [(k, s) for k in ("down", "up") for s in (1, 2, 4)]
+    for kind, s in maps:
+        nbr_b = cm.kernel_map(kind, s)
+        perm_b = cm.kernel_map_order(kind, s)
+        out_s, in_s, tr = {"s1": (s, s, 0), "down": (2 * s, s, 0), "up": (s, 2 * s, 1)}[kind]
+        out_c, in_c = cm.coords_at(out_s), cm.coords_at(in_s)
+        nb = L.mvr_hash_table_bytes(in_c.shape[0])
+        tab = torch.empty(nb, dtype=torch.uint8, device=gpu)
+        N.check(L.mvr_hash_build_lattice(N.ptr(in_c), in_c.shape[0], in_s, N.ptr(tab), nb, N.stream()), "table")
+        nbr_t = torch.empty_like(nbr_b)
+        N.check(L.mvr_kernel_map(N.ptr(out_c), out_c.shape[0], N.ptr(tab), nb, 3, s, tr, N.ptr(nbr_t), N.stream()),
+                "map")
+        assert torch.equal(nbr_b, nbr_t), (kind, s)
+        ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr_t.shape[0]), gpu)
+        perm_t = torch.empty_like(perm_b)
+        N.check(L.mvr_kernel_map_order(N.ptr(nbr_t), N.ptr(out_c), out_s, nbr_t.shape[0], 27, N.ptr(perm_t), N.ptr(ws),
+                                       ws.numel(), N.stream()), "order")
+        assert torch.equal(perm_b, perm_t), (kind, s)
 
 
 def test_fcgf_forward_matches_oracle(gpu, frags):
