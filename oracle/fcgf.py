@@ -13,9 +13,59 @@ parity is "unpinned" (DESIGN.md §Oracle):
     input tensor stride; transposed conv: input = output - off * s_out;
   * weights: conv '.kernel' [K, Cin, Cout] (ME 0.4), BatchNorm1d eval (eps 1e-5).
 """
+import ctypes
+import os
+
 import numpy as np
 
 KEY_BIAS = 1 << 16
+_C = None
+
+
+def _clib():
+    """oracle/build/libmvoracle.so (oracle/csrc/sparse_conv.c, C + OpenMP: built by __graft_entry__.build() or
+    `make -C oracle`): the kernel map and sparse conv of this module for the host-core CPU baseline"""
+    global _C
+    if _C is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libmvoracle.so")
+        L = ctypes.CDLL(path)
+        vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        L.mvo_kernel_map.argtypes = [vp, i64, vp, i64, ci, ci, ci, vp]
+        L.mvo_sparse_conv.argtypes = [vp, i64, ci, vp, i64, ci, vp, ci, vp, vp]
+        L.mvo_set_threads.argtypes = [ci]
+        _C = L
+    return _C
+
+
+def set_threads(n):
+    """OpenMP threads of the C backend; returns the previous maximum"""
+    return _clib().mvo_set_threads(int(n))
+
+
+def kernel_map_c(out_coords, in_coords, ks, step, transposed=False):
+    """kernel_map() in C (hash of the input set instead of the sorted-key table): the same nbr"""
+    oc = np.ascontiguousarray(out_coords, dtype=np.int32)
+    ic = np.ascontiguousarray(in_coords, dtype=np.int32)
+    nbr = np.empty((len(oc), ks ** 3), dtype=np.int64)
+    rc = _clib().mvo_kernel_map(ic.ctypes.data, len(ic), oc.ctypes.data, len(oc), ks, step, int(transposed),
+                                nbr.ctypes.data)
+    if rc:
+        raise RuntimeError("mvo_kernel_map failed (%d)" % rc)
+    return nbr
+
+
+def sparse_conv_c(feat, nbr, W, bias=None):
+    """sparse_conv() in C + OpenMP (fp32, per output row in the order k, ci)"""
+    f = np.ascontiguousarray(feat, dtype=np.float32)
+    n = np.ascontiguousarray(nbr, dtype=np.int64)
+    w = np.ascontiguousarray(W, dtype=np.float32)
+    b = None if bias is None else np.ascontiguousarray(np.asarray(bias, np.float32).reshape(-1))
+    out = np.empty((n.shape[0], w.shape[2]), dtype=np.float32)
+    rc = _clib().mvo_sparse_conv(f.ctypes.data, f.shape[0], f.shape[1], n.ctypes.data, n.shape[0], n.shape[1],
+                                 w.ctypes.data, w.shape[2], None if b is None else b.ctypes.data, out.ctypes.data)
+    if rc:
+        raise RuntimeError("mvo_sparse_conv failed (%d)" % rc)
+    return out
 
 
 def pack(c):
@@ -109,64 +159,69 @@ def relu(x):
 
 
 class Levels:
-    """Coordinate sets, tables and kernel maps for strides 1, 2, 4, 8 of a batch."""
+    """Coordinate sets, tables and kernel maps for strides 1, 2, 4, 8 of a batch (backend "c": the maps by
+    oracle/csrc/sparse_conv.c)."""
 
-    def __init__(self, coords0):
+    def __init__(self, coords0, backend="numpy"):
         self.coords = [np.asarray(coords0, np.int32)]
         for l in range(1, 4):
             self.coords.append(downsample(self.coords[-1], 2 ** l))
-        self.tables = [Table(c) for c in self.coords]
+        self.backend = backend
+        self.tables = [Table(c) for c in self.coords] if backend == "numpy" else None
         self._maps = {}
 
     def nbr(self, kind, l):
         key = (kind, l)
         if key not in self._maps:
-            if kind == "s1":      # 3^3 at level l
-                m = kernel_map(self.coords[l], self.tables[l], 3, 2 ** l)
-            elif kind == "down":  # level l -> l+1
-                m = kernel_map(self.coords[l + 1], self.tables[l], 3, 2 ** l)
-            elif kind == "up":    # level l+1 -> l (transposed)
-                m = kernel_map(self.coords[l], self.tables[l + 1], 3, 2 ** l, transposed=True)
-            elif kind == "k7":
-                m = kernel_map(self.coords[0], self.tables[0], 7, 1)
+            # (output level, input level, ks, step, transposed)
+            o, i, ks, step, tr = {"s1": (l, l, 3, 2 ** l, False), "down": (l + 1, l, 3, 2 ** l, False),
+                                  "up": (l, l + 1, 3, 2 ** l, True), "k7": (0, 0, 7, 1, False)}[kind]
+            if self.backend == "c":
+                m = kernel_map_c(self.coords[o], self.coords[i], ks, step, tr)
+            else:
+                m = kernel_map(self.coords[o], self.tables[i], ks, step, tr)
             self._maps[key] = m
         return self._maps[key]
 
 
-def block(x, st, pre, lv, l):
+def block(x, st, pre, lv, l, conv=None):
     """BasicBlockBN (fcgf.py:23-67): relu(bn1(conv1 x)) -> bn2(conv2) + x -> relu."""
+    conv = conv or sparse_conv
     n = lv.nbr("s1", l)
-    o = relu(bn(sparse_conv(x, n, st[pre + ".conv1.kernel"]), st, pre + ".norm1"))
-    o = bn(sparse_conv(o, n, st[pre + ".conv2.kernel"]), st, pre + ".norm2")
+    o = relu(bn(conv(x, n, st[pre + ".conv1.kernel"]), st, pre + ".norm1"))
+    o = bn(conv(o, n, st[pre + ".conv2.kernel"]), st, pre + ".norm2")
     return relu(o + x)
 
 
-def fcgf_forward(st, coords0, feats0, normalize=True):
+def fcgf_forward(st, coords0, feats0, normalize=True, backend="numpy"):
     """fcgf.py:229-280 (eval).  st: state dict of numpy arrays (ME 0.4 key names).
-    coords0 int [M,4], feats0 [M,1] -> F [M,32] (+ the Levels used)."""
+    coords0 int [M,4], feats0 [M,1] -> F [M,32] (+ the Levels used).  backend "c": kernel maps and sparse convs
+    in C + OpenMP (oracle/csrc/sparse_conv.c; the CPU baseline's FCGF leg), else numpy."""
     st = {k: np.asarray(v, np.float32) for k, v in st.items() if not k.endswith("num_batches_tracked")}
-    lv = Levels(coords0)
+    lv = Levels(coords0, backend)
+    sparse_conv = sparse_conv_c if backend == "c" else globals()["sparse_conv"]
+    blk = lambda x, pre, l: block(x, st, pre, lv, l, sparse_conv)   # noqa: E731
     f = np.asarray(feats0, np.float32)
     s1 = bn(sparse_conv(f, lv.nbr("k7", 0), st["conv1.kernel"]), st, "norm1")
-    s1 = block(s1, st, "block1", lv, 0)
+    s1 = blk(s1, "block1", 0)
     out = relu(s1)
     s2 = bn(sparse_conv(out, lv.nbr("down", 0), st["conv2.kernel"]), st, "norm2")
-    s2 = block(s2, st, "block2", lv, 1)
+    s2 = blk(s2, "block2", 1)
     out = relu(s2)
     s4 = bn(sparse_conv(out, lv.nbr("down", 1), st["conv3.kernel"]), st, "norm3")
-    s4 = block(s4, st, "block3", lv, 2)
+    s4 = blk(s4, "block3", 2)
     out = relu(s4)
     s8 = bn(sparse_conv(out, lv.nbr("down", 2), st["conv4.kernel"]), st, "norm4")
-    s8 = block(s8, st, "block4", lv, 3)
+    s8 = blk(s8, "block4", 3)
     out = relu(s8)
     out = bn(sparse_conv(out, lv.nbr("up", 2), st["conv4_tr.kernel"]), st, "norm4_tr")
-    out = relu(block(out, st, "block4_tr", lv, 2))
+    out = relu(blk(out, "block4_tr", 2))
     out = np.concatenate([out, s4], axis=1)
     out = bn(sparse_conv(out, lv.nbr("up", 1), st["conv3_tr.kernel"]), st, "norm3_tr")
-    out = relu(block(out, st, "block3_tr", lv, 1))
+    out = relu(blk(out, "block3_tr", 1))
     out = np.concatenate([out, s2], axis=1)
     out = bn(sparse_conv(out, lv.nbr("up", 0), st["conv2_tr.kernel"]), st, "norm2_tr")
-    out = relu(block(out, st, "block2_tr", lv, 0))
+    out = relu(blk(out, "block2_tr", 0))
     out = np.concatenate([out, s1], axis=1)
     out = relu(out @ st["conv1_tr.kernel"][0])
     out = out @ st["final.kernel"][0] + st["final.bias"].reshape(1, -1)

@@ -90,3 +90,24 @@ def test_demo_pair_voxel_counts():
     pcs = [read_ply_xyz(os.path.join(d, "cloud_bin_%d.ply" % k)) for k in range(2)]
     _, _, counts = voxelize(pcs, 0.025)
     assert list(counts) == [18977, 19082]
+
+
+def test_c_backend_equals_numpy_oracle():
+    """oracle/csrc/sparse_conv.c (the CPU baseline's FCGF leg, C + OpenMP) against the numpy restatement: the same
+    kernel maps (all kinds, 7^3 included) and features to fp32 rounding on a real fragment"""
+    import os
+    import subprocess
+    from synth import synth_scene_fragments, synth_state
+    from oracle.fcgf import voxelize, fcgf_forward, fcgf_state_shapes
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if not os.path.exists(os.path.join(root, "oracle", "build", "libmvoracle.so")):
+        subprocess.run(["make", "-C", os.path.join(root, "oracle")], check=True)
+    frags, _ = synth_scene_fragments(2, seed=43, n_pts=40000)
+    c, _, _ = voxelize(frags, 0.025)
+    st = synth_state(fcgf_state_shapes(), seed=3)
+    ones = np.ones((len(c), 1), np.float32)
+    Fn, lvn = fcgf_forward(st, c, ones)
+    Fc, lvc = fcgf_forward(st, c, ones, backend="c")
+    for kind, l in (("s1", 0), ("s1", 3), ("down", 0), ("down", 2), ("up", 0), ("up", 2), ("k7", 0)):
+        np.testing.assert_array_equal(lvn.nbr(kind, l), lvc.nbr(kind, l), err_msg="%s %d" % (kind, l))
+    np.testing.assert_allclose(Fc, Fn, atol=2e-6)
