@@ -26,6 +26,10 @@
 //
 // Roofline: 4 * C * clusters * points flops per pair on the split MFMA (6 bf16 MFMAs per fp32
 // product: 16 * 157.3 / 6 = 419 TF/s fp32-equivalent); HBM traffic ~ x once + the output.
+#include <algorithm>
+#include <functional>
+#include <vector>
+
 #include "common.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
@@ -226,7 +230,8 @@ struct PoolArgs {
   int P, N, Kc, nqb;                               // nqb = ceil(Kc / 256) query blocks
   float* out; int64_t ops, old;                    // x_down [P][128][old]
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(Kc/128)][st_ld] (+ st_off + c), nullable
-  int nks;                                         // key splits per (pair, query block); 1: none
+  int nks;                                         // key splits per (pair, query block) of the split tail; 1: none
+  int g0;                                          // nks > 1: pair octets [0, g0) unsplit, the rest split (the tail)
   float* part; int* cnt;                           // nks > 1: per-split (O, m, l) slabs, arrival tickets
   int* range;                                      // H = 1: set when an operand is outside the fp16 range
   const int* guard;                                // H = 0 re-run: return unless *guard is set
@@ -263,14 +268,17 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_attn_reruns, 1);
   }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
-  int p, jb, ks = 0;
-  if (a.nks > 1) {   // the splits of one (pair, query block) are blocks b, b + 8, ..: one XCD, adjacent
-    const int b = blockIdx.x, x = b & 7;
+  int p, jb, ks = 0, nks = 1;
+  const int nb0 = 8 * a.nqb * a.g0;   // blocks of the unsplit pair octets (nks > 1)
+  if (a.nks > 1 && (int)blockIdx.x >= nb0) {
+    // the split tail: the splits of one (pair, query block) are blocks b, b + 8, ..: one XCD, adjacent
+    const int b = blockIdx.x - nb0, x = b & 7;
     int t = b >> 3;
-    ks = t % a.nks;
-    t /= a.nks;
+    nks = a.nks;
+    ks = t % nks;
+    t /= nks;
     jb = t % a.nqb;
-    p = (t / a.nqb) * 8 + x;
+    p = (a.g0 + t / a.nqb) * 8 + x;
   } else {
     pair_block(a.nqb, p, jb);
   }
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   const float* X = a.X + (int64_t)p * a.xps;
   const int N = a.N;
   const int nkb = (N + AKB - 1) / AKB;
-  const int kb0 = nkb * ks / a.nks, kb1 = nkb * (ks + 1) / a.nks;   // this split's key blocks
+  const int kb0 = nkb * ks / nks, kb1 = nkb * (ks + 1) / nks;   // this split's key blocks
   const int nlast = ((N + 3) & ~3) - 4;   // last readable 4-key group of a row
 
   // raw tile kb -> xraw[kb & 1] as [c][32] fp32 rows: wave w moves rows 16 w .. 16 w + 15 in two
@@ -487,11 +495,11 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     }
     if (__any(bad) && lane == 0) atomicOr(a.range, 1);
   }
-  if (a.nks > 1) {
+  if (nks > 1) {
     // publish this split's (O, m, l); the last split to arrive merges all of them (counter hand-off:
     // plain stores, agent-scope release before the ticket, agent-scope acquire by the reducer)
     const int64_t slot = (int64_t)p * a.nqb + jb;
-    float* mine = a.part + (slot * a.nks + ks) * PSLAB + tid;
+    float* mine = a.part + (slot * nks + ks) * PSLAB + tid;
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -507,7 +515,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       const int tk = __hip_atomic_fetch_add(a.cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // tickets are not reset between the fp16 launch and its guarded re-run: the last split of a slot
       // draws nks - 1 modulo nks
-      const bool last = tk % a.nks == a.nks - 1;
+      const bool last = tk % nks == nks - 1;
       flag[0] = last;
       if (last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -519,8 +527,8 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     // merge the splits in split order (whichever arrived last: the result does not depend on arrival order)
     const floatx16 own[4] = {O[0], O[1], O[2], O[3]};
     const float mown = m, lown = l;
-    for (int o = 0; o < a.nks; ++o) {
-      const float* th = a.part + (slot * a.nks + o) * PSLAB + tid;
+    for (int o = 0; o < nks; ++o) {
+      const float* th = a.part + (slot * nks + o) * PSLAB + tid;
       const float m2 = o == ks ? mown : th[64 * ATHREADS], l2 = o == ks ? lown : th[65 * ATHREADS];
       if (o == 0) {
 #pragma unroll
@@ -1068,22 +1076,52 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
 }
 
 // Key splits of the pool launch: with one 512-thread workgroup per CU, P x ceil(Kc / 256) workgroups
-// leave a partial last round (435 pairs: 880 workgroups = 3.44 rounds of 256); splitting the keys
-// (points) of every (pair, query block) shortens the rounds.  Picks nks in {1, 2, 4} minimising
-// rounds / nks (ties: fewer splits), with >= 8 key blocks per split.
-static int pool_splits(int P, int nqb, int N) {
+// leave a partial last round (435 pairs: 880 workgroups = 3.44 rounds of 256).  Splitting the keys (points) of
+// a (pair, query block) into k parts shortens the rounds, but every split unit writes an (O, m, l) slab that the
+// last one reads back (135 KB each).  So only a TAIL is split: the pair octets [0, g0) run whole, the rest in k
+// parts, dispatched after them.  Candidates (k in {1, 2, 4} with >= 8 key blocks per part; g0 = every octet, no
+// octet, or the most octets whose whole units fill complete rounds) are ranked by the makespan of the dispatch
+// order on `cus` slots (a unit = 1, a part = 1 / k), ties to fewer slabs.  A function of the shape and the
+// device's CU count only.
+struct PoolSplit { int nks, g0; };
+static double pool_makespan(int64_t full, int64_t parts, int k, int cus) {
+  // greedy in dispatch order: the whole units first, then the parts, each to the earliest free slot
+  std::vector<double> slot((size_t)cus, 0.0);
+  std::make_heap(slot.begin(), slot.end(), std::greater<double>());
+  auto put = [&](double d) {
+    std::pop_heap(slot.begin(), slot.end(), std::greater<double>());
+    slot.back() += d;
+    std::push_heap(slot.begin(), slot.end(), std::greater<double>());
+  };
+  for (int64_t i = 0; i < full; ++i) put(1.0);
+  for (int64_t i = 0; i < parts; ++i) put(1.0 / k);
+  return *std::max_element(slot.begin(), slot.end());
+}
+static PoolSplit pool_splits(int P, int nqb, int N) {
   int dev = 0, cus = 0;   // the current device's CU count (an attribute query, no process state)
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
-  const int64_t wg = (int64_t)((P + 7) / 8) * 8 * nqb;
+  const int G = (P + 7) / 8;                 // pair octets
+  const int64_t per = 8LL * nqb;             // workgroups of one octet, unsplit
   const int nkb = (N + AKB - 1) / AKB;
-  int best = 1;
-  double tbest = (double)((wg + cus - 1) / cus);
+  PoolSplit best{1, G};
+  double tbest = pool_makespan(per * G, 0, 1, cus);
+  int64_t slabs_best = 0;
   for (int k = 2; k <= 4; k *= 2) {
     if (nkb < 8 * k) break;
-    const double t = (double)((wg * k + cus - 1) / cus) / k;
-    if (t < tbest - 1e-9) { tbest = t; best = k; }
+    const int gfill = (int)(((per * G) / cus) * cus / per);   // most whole octets in complete rounds
+    const int cands[3] = {0, gfill, G};
+    for (int g0 : cands) {
+      if (g0 >= G) continue;
+      const int64_t parts = per * k * (G - g0);
+      const double t = pool_makespan(per * g0, parts, k, cus);
+      if (t < tbest - 1e-9 || (t < tbest + 1e-9 && parts < slabs_best)) {
+        tbest = t;
+        best = PoolSplit{k, g0};
+        slabs_best = parts;
+      }
+    }
   }
   return best;
 }
@@ -1140,9 +1178,11 @@ extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x
   // mvr_oan_diff_pool_workspace_bytes is an error rather than a silently different split (and summation order)
   if (workspace) {
     if (!al16(workspace) || workspace_bytes < pool_ws_bytes(P, clusters, 4)) return MVR_EINVAL;
-    const int k = pool_splits(P, a.nqb, N);
+    const PoolSplit ps = pool_splits(P, a.nqb, N);
+    const int k = ps.nks;
     if (k > 1) {
       a.nks = k;
+      a.g0 = ps.g0;
       a.part = reinterpret_cast<float*>(workspace);
       a.cnt = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + slots * (size_t)k * PSLAB * 4);
     }
@@ -1159,7 +1199,8 @@ extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x
   const double fl = 4.0 * AC * clusters * (double)N * P;
   const double by = 4.0 * AC * ((double)N + clusters) * P;
   ProfScope prof(PK_POOL, fl, by, stream);
-  const int grid = ((P + 7) / 8) * 8 * a.nqb * a.nks;
+  const int G = (P + 7) / 8;
+  const int grid = a.nks > 1 ? 8 * a.nqb * (a.g0 + a.nks * (G - a.g0)) : G * 8 * a.nqb;
   if (range) {   // split-fp16, then the split-bf16 re-run that returns at once unless an operand was out of range
     a.range = range;
     hipLaunchKernelGGL(oan_pool_kernel<1>, dim3(grid), dim3(ATHREADS), 0, stream, a);

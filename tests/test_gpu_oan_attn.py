@@ -56,11 +56,14 @@ def math(request):
 
 
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (41, 700, 300)])
+@pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (41, 700, 300),
+                                    (300, 600, 500)])
 def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
     """split: mvr_oan_diff_pool_ws with a workspace (points split over 2-4 workgroups per (pair, cluster
-    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  The split-fp16 math
-    needs the workspace's flag word: without one the launch is split-bf16."""
+    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  300 pairs x 500 clusters
+    (608 whole workgroups on 256 CUs): only the tail past the two complete rounds is split (pair octets 32-37),
+    the rest runs whole.  The split-fp16 math needs the workspace's flag word: without one the launch is
+    split-bf16."""
     import torch
     from lib import _native as NV
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 1000 + N)
