@@ -959,6 +959,13 @@ extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) {
   const size_t n = (size_t)(Mo > 0 ? Mo : 1);
   return order_sort_bytes(Mo) + n * 20 + 3 * 256;
 }
+static int g_spconv_order = 0;
+extern "C" int mvr_set_spconv_order(int mode) {
+  const int prev = g_spconv_order;
+  g_spconv_order = mode == 1 ? 1 : 0;
+  return prev;
+}
+
 // 3^3 kernel maps over brick maps (kernel_map_brick_kernel): in_bricks = mvr_brick_map_build_stride of the Min
 // input coordinates at tensor stride in_stride; neighbour of output c at offset d: c + d step (transposed:
 // c - d step).  order_keys (optional, uint64 [Mout]): the rows' sort keys for mvr_kernel_map_order_keys
@@ -997,7 +1004,9 @@ extern "C" int mvr_kernel_map_order_keys(const uint64_t* keys, int64_t Mo, int K
   if (!tmp) return MVR_ELAUNCH;
   void* tbuf = take(tmp);
   hipLaunchKernelGGL(iota_kernel, dim3(nblk(Mo)), dim3(256), 0, s, vin, Mo);
-  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, keys, kout, vin, perm, (int)Mo, 0, 32 + K, s) != hipSuccess)
+  // g_spconv_order 1: the fragment + Morton bits only (spatially compact tiles, larger offset unions; A/B timing)
+  const int end_bit = g_spconv_order == 1 ? 32 : 32 + K;
+  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, keys, kout, vin, perm, (int)Mo, 0, end_bit, s) != hipSuccess)
     return MVR_ELAUNCH;
   MVR_CHECK_LAUNCH();
   return MVR_OK;

@@ -390,6 +390,10 @@ int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, int out_strid
  * perm).  Workspace: mvr_kernel_map_order_bytes(Mout). */
 int mvr_kernel_map_order_keys(const uint64_t* order_keys, int64_t Mout, int K, int32_t* perm, void* workspace,
                               size_t workspace_bytes, mvr_stream_t stream);
+/* row order of mvr_kernel_map_order_keys (process-wide): 0 (default) active-offset mask, then fragment and Morton
+ * code; 1 fragment and Morton code only (spatially compact tiles whose offset unions are larger; A/B timing).
+ * Returns the previous setting. */
+int mvr_set_spconv_order(int mode);
 /* MinkowskiConvolution forward, gather-GEMM over the neighbour table (nbr NULL & K==1:
  * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
  * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
