@@ -142,3 +142,64 @@ def test_pack_unpack_roundtrip():
     np.testing.assert_allclose(t2, t.numpy())
     np.testing.assert_allclose(conf, (sc > 0.5).float().mean(1).numpy())
     assert flag.all()
+
+
+def _worker_own_block(rank, world, port, P, q):
+    """each rank holds only its own block of the filtering input (the bench's pair-sharded scene: a rank matches
+    only its pairs) and says where it starts"""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s, e = D.shard_pairs(P, world, rank, group=1)
+        xs = _xs(P, zero_pair=P - 3)[s:e]
+        rec = D.register_pairs_sharded(_StubFilter(), {"xs": xs, "num_pairs": P}, world, rank, group=1,
+                                       guard="scene", first_pair=s)
+        q.put((rank, rec.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_register_sharded_own_block_gloo_world2():
+    """first_pair mode (the input holds only this rank's block, balanced single-pair groups): the gathered records
+    equal one rank over the whole batch, the scene guard firing from the last rank's zero pair"""
+    P, world = 45, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_own_block, args=(r, world, port, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = D.register_pairs_sharded(_StubFilter(), {"xs": _xs(P, zero_pair=P - 3)}, 1, 0, group=1, guard="scene").numpy()
+    for _, rec in res:
+        np.testing.assert_array_equal(rec, ref)
+
+
+def test_register_sharded_contract_errors():
+    """scene guard over a train-mode (batch-statistics) forward would need the BatchNorm moments of every rank:
+    refused; a block that is not the rank's shard: refused"""
+    stub = _StubFilter()
+    stub.train()
+    with pytest.raises(ValueError):
+        D.register_pairs_sharded(stub, {"xs": _xs(8)}, 1, 0, guard="scene")
+    stub.eval()
+    with pytest.raises(ValueError):
+        D.register_pairs_sharded(stub, {"xs": _xs(8)[:5], "num_pairs": 8}, 1, 0, guard="scene", first_pair=2)
+
+
+def test_register_sharded_group_mode_sets_bn_groups():
+    """group mode runs the filter with guard and BatchNorm groups of `group` pairs (the benchmark's loader
+    batches) and restores the filter's settings afterwards"""
+    class Spy(_StubFilter):
+        def filter_correspondences(self, d):
+            self.during = (self.guard_group, self.bn_group)
+            return super().filter_correspondences(d)
+    s = Spy()
+    s.bn_group = 0
+    D.register_pairs_sharded(s, {"xs": _xs(40)}, 1, 0, guard="group")
+    assert s.during == (D.GROUP, D.GROUP)
+    assert (s.guard_group, s.bn_group) == (0, 0)
