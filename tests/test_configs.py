@@ -69,3 +69,22 @@ def test_harness_reads_method_yaml_from_cwd(monkeypatch):
         B.load_model("OANet", None)
     m2 = B.load_model("Anything", None, cfg_path=os.path.join(GOLDEN, CONFIGS[1]))
     assert m2.precomputed_desc
+
+
+def test_scripts_utils_host_helpers(tmp_path):
+    """scripts/utils.py's host helpers (reference :16-41, :125-145)"""
+    import numpy as np
+    import torch
+    from scripts.utils import read_txt, ensure_dir, transform_point_cloud
+    d = tmp_path / "a" / "b"
+    ensure_dir(str(d))
+    ensure_dir(str(d))
+    (d / "x.txt").write_text(" one \ntwo\n")
+    assert read_txt(str(d / "x.txt")) == ["one", "two"]
+    r = np.random.RandomState(0)
+    x = r.rand(7, 3)
+    R = np.linalg.qr(r.rand(3, 3))[0]
+    t = r.rand(3, 1)
+    np.testing.assert_allclose(transform_point_cloud(x, R, t), x @ R.T + t.T)
+    xt = transform_point_cloud(torch.from_numpy(x), torch.from_numpy(R), torch.from_numpy(t), data_type="torch")
+    np.testing.assert_allclose(xt.numpy(), x @ R.T + t.T)

@@ -128,3 +128,33 @@ def test_pairwise_demo_reference_pair(gpu, tmp_path, monkeypatch):
     assert keys.tolist() == [["0", "1", "True"]]
     np.testing.assert_allclose(traj[0], T, atol=1e-9)
     np.testing.assert_allclose(T[:3, :3] @ T[:3, :3].T, np.eye(3), atol=1e-5)
+
+
+def test_extract_features_reference_helper(gpu):
+    """scripts/utils.py extract_features (reference :44-122) on the reference's demo cloud: the kept points are
+    the first-occurrence voxel representatives (18,977 at 0.025 m), the features equal FCGFNet on
+    lib.sparse.voxelize's batch of the same cloud, unit norm; rgb inputs are refused (one input channel)"""
+    import torch
+    from lib.descriptor.fcgf import FCGFNet
+    from lib.ply import read_ply_xyz
+    from lib.sparse import voxelize, SparseTensor
+    from scripts.utils import extract_features, transform_point_cloud, read_txt
+    from synth import synth_state
+    xyz = read_ply_xyz(os.path.join(DEMO, "cloud_bin_0.ply"))
+    net = FCGFNet()
+    st = synth_state({k: tuple(v.shape) for k, v in net.state_dict().items()}, seed=3)
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    net = net.to(gpu)
+    with torch.no_grad():
+        pts, F = extract_features(net, xyz, voxel_size=0.025, device=gpu)
+        c, sel, _, _ = voxelize([np.ascontiguousarray(xyz, dtype=np.float32)], 0.025, gpu)
+        F2 = net(SparseTensor(torch.ones(c.shape[0], 1, device=gpu), coords=c, batch_size=1).to(gpu)).F
+    assert pts.shape == (18977, 3) and F.shape == (18977, 32)
+    np.testing.assert_array_equal(pts, xyz[sel.cpu().numpy()])
+    assert torch.equal(F, F2)
+    np.testing.assert_allclose(F.norm(dim=1).cpu().numpy(), 1.0, atol=1e-5)
+    with pytest.raises(NotImplementedError):
+        extract_features(net, xyz[:100], rgb=np.zeros((100, 3)), voxel_size=0.025, device=gpu)
+    R, t = np.eye(3), np.ones((3, 1))
+    np.testing.assert_allclose(transform_point_cloud(xyz[:5], R, t), xyz[:5] + 1.0)
+    assert read_txt(os.path.join(GOLDEN, "configs", "pairwise_registration", "eval", "RegBlock.yaml"))[0] == "method:"
