@@ -202,3 +202,44 @@ def test_kernel_map_order_mask_then_morton(gpu, frags):
         lo = ((out_c[:, 0] & 31) << 27) | (spread(q[:, 0] & 511) << 2) | (spread(q[:, 1] & 511) << 1) | spread(q[:, 2] & 511)
         key = (mask << 32) | lo
         assert np.array_equal(perm, np.argsort(key, kind="stable"))
+
+
+def test_brick_kernel_map_edge_cases(gpu):
+    """mvr_kernel_map_bricks / mvr_brick_map_build_stride: an empty input set (every neighbour absent), an empty
+    output set (no launch), negative coordinates across brick boundaries, a transposed map whose neighbours are off
+    the coarse lattice for odd cells, and the argument checks"""
+    import torch
+    from lib import _native as N
+    L = N.lib()
+    # empty input set
+    oc = torch.tensor([[0, 0, 0, 0], [0, -1, 5, -9]], dtype=torch.int32, device=gpu)
+    nbb = L.mvr_brick_map_bytes(0)
+    br = torch.empty(nbb, dtype=torch.uint8, device=gpu)
+    N.check(L.mvr_brick_map_build_stride(N.ptr(oc), 0, 1, N.ptr(br), nbb, N.stream()), "empty bricks")
+    nbr = torch.zeros(2, 27, dtype=torch.int32, device=gpu)
+    N.check(L.mvr_kernel_map_bricks(N.ptr(oc), 2, 1, N.ptr(br), 0, nbb, 1, 1, 0, N.ptr(nbr), None, N.stream()), "map")
+    assert (nbr.cpu().numpy() == -1).all()
+    assert L.mvr_kernel_map_bricks(N.ptr(oc), 0, 1, N.ptr(br), 0, nbb, 1, 1, 0, N.ptr(nbr), None, N.stream()) == 0
+    assert L.mvr_kernel_map_bricks(N.ptr(oc), 2, 1, N.ptr(br), 0, nbb, 3, 1, 0, N.ptr(nbr), None, N.stream()) != 0
+    assert L.mvr_brick_map_build_stride(N.ptr(oc), 2, 6, N.ptr(br), L.mvr_brick_map_bytes(2), N.stream()) != 0
+    # fine set around the origin (negative coordinates, brick boundaries at multiples of 4 cells), coarse set = the
+    # stride-2 cells it covers; up map (coarse -> fine, transposed) and down map (fine -> coarse) vs brute force
+    g = np.arange(-5, 5)
+    fine = np.array([(b, x, y, z) for b in range(2) for x in g for y in g for z in (-1, 0, 3)], dtype=np.int32)
+    coarse = np.unique(np.concatenate([fine[:, :1], np.floor_divide(fine[:, 1:], 2) * 2], 1), axis=0).astype(np.int32)
+    idx = {s: {tuple(r): i for i, r in enumerate(c.tolist())} for s, c in ((1, fine), (2, coarse))}
+    tf, tc = torch.from_numpy(fine).to(gpu), torch.from_numpy(coarse).to(gpu)
+    bf, bc = (torch.empty(L.mvr_brick_map_bytes(len(c)), dtype=torch.uint8, device=gpu) for c in (fine, coarse))
+    N.check(L.mvr_brick_map_build_stride(N.ptr(tf), len(fine), 1, N.ptr(bf), bf.numel(), N.stream()), "bf")
+    N.check(L.mvr_brick_map_build_stride(N.ptr(tc), len(coarse), 2, N.ptr(bc), bc.numel(), N.stream()), "bc")
+    for name, out, o_s, br_, in_s, tr, src in (("up", tf, 1, bc, 2, 1, coarse), ("down", tc, 2, bf, 1, 0, fine)):
+        nb = torch.empty(out.shape[0], 27, dtype=torch.int32, device=gpu)
+        N.check(L.mvr_kernel_map_bricks(N.ptr(out), out.shape[0], o_s, N.ptr(br_), len(src), br_.numel(), in_s, 1, tr,
+                                        N.ptr(nb), None, N.stream()), name)
+        ref = np.full((out.shape[0], 27), -1, np.int32)
+        sg = -1 if tr else 1
+        for o, (b, x, y, z) in enumerate(out.cpu().numpy().tolist()):
+            for k in range(27):
+                dx, dy, dz = k % 3 - 1, (k // 3) % 3 - 1, k // 9 - 1
+                ref[o, k] = idx[in_s].get((b, x + sg * dx, y + sg * dy, z + sg * dz), -1)
+        np.testing.assert_array_equal(nb.cpu().numpy(), ref, err_msg=name)
