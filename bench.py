@@ -204,6 +204,7 @@ class SceneWorkload:
         sampled (xyz, descriptor) of every fragment (RCCL, ~21 MB per scene), then the feature NN of this rank's
         block of pairs only."""
         if data is None:
+            self._wait_prep()
             data = self.prepare()
         np.random.seed(self.rng_seed)
         if self.shard != "pairs":
@@ -295,6 +296,14 @@ class SceneWorkload:
         self.prepared = self.prep_pool.submit(self.prepare_on, sC) if self.prep_pool else self.prepare_on(sC)
         return rec
 
+    def _wait_prep(self):
+        """a prepare() issued from the main thread first waits for the helper thread's pending one: with
+        --shard pairs each prepare() makes a collective (the voxel counts), and one rank's two threads must not
+        interleave theirs (every rank then issues them in the same order)"""
+        p = getattr(self, "prepared", None)
+        if p is not None and hasattr(p, "result"):
+            p.result()
+
     def prepare_on(self, stream):
         """prepare() on `stream` (callable from a helper thread: the current device and stream are per thread)"""
         torch.cuda.set_device(self.dev)
@@ -380,6 +389,7 @@ class SceneWorkload:
         from the scene's kernel maps: FLOPs = 2 Cin Cout per (input, output) pair of every conv; compulsory bytes =
         input rows + output rows (+ residual rows) + weights + the neighbour table, fp32 / int32.  (Host syncs:
         call outside the timed region.)"""
+        self._wait_prep()
         data = self.prepare()
         cm = data["sinput0_coords_manager"]
         M = {s: int(cm.coords_at(s).shape[0]) for s in (1, 2, 4, 8)}
