@@ -1084,6 +1084,7 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
 // order on `cus` slots (a unit = 1, a part = 1 / k), ties to fewer slabs.  A function of the shape and the
 // device's CU count only.
 struct PoolSplit { int nks, g0; };
+int g_pool_tail = 0;   // mvr_set_pool_tail: 1 split only the tail (below); 0 every (pair, block) or none (round 3)
 static double pool_makespan(int64_t full, int64_t parts, int k, int cus) {
   // greedy in dispatch order: the whole units first, then the parts, each to the earliest free slot
   std::vector<double> slot((size_t)cus, 0.0);
@@ -1113,7 +1114,7 @@ static PoolSplit pool_splits(int P, int nqb, int N) {
     const int gfill = (int)(((per * G) / cus) * cus / per);   // most whole octets in complete rounds
     const int cands[3] = {0, gfill, G};
     for (int g0 : cands) {
-      if (g0 >= G) continue;
+      if (g0 >= G || (g0 > 0 && !g_pool_tail)) continue;
       const int64_t parts = per * k * (G - g0);
       const double t = pool_makespan(per * g0, parts, k, cus);
       if (t < tbest - 1e-9 || (t < tbest + 1e-9 && parts < slabs_best)) {
@@ -1130,6 +1131,12 @@ static PoolSplit pool_splits(int P, int nqb, int N) {
 static size_t pool_ws_bytes(int P, int clusters, int nks) {
   const size_t slots = (size_t)P * ((clusters + AQ - 1) / AQ);
   return (nks > 1 ? slots * ((size_t)nks * PSLAB * 4 + 4) : 0) + 512;
+}
+
+extern "C" int mvr_set_pool_tail(int on) {
+  const int prev = g_pool_tail;
+  g_pool_tail = on ? 1 : 0;
+  return prev;
 }
 
 extern "C" size_t mvr_oan_diff_pool_workspace_bytes(int P, int channels, int clusters) {

@@ -267,8 +267,12 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
-int g_oan_fused = 13;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 2 conv1 folded into the first PointCN,
-                        // bit 3 InstanceNorm folds finished in their producer's last-arriving workgroups
+#ifndef OAN_FUSED_DEFAULT
+#define OAN_FUSED_DEFAULT 5
+#endif
+int g_oan_fused = OAN_FUSED_DEFAULT;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 2 conv1 folded into the first
+                                       // PointCN, bit 3 InstanceNorm folds finished in their producer's
+                                       // last-arriving workgroups
                        // (point-conv XI variants); bit 1 is unused
 int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B timing)
 

@@ -15,9 +15,9 @@ import torch
 
 from lib import _native as N
 
-# 3^3 kernel maps over brick maps (csrc/sparse.hip kernel_map_brick_kernel); MVR_BRICK_MAPS=0 resolves them over
-# the per-level coordinate tables instead (A/B timing; identical maps)
-BRICK_MAPS = os.environ.get("MVR_BRICK_MAPS", "1") == "1"
+# 3^3 kernel maps over brick maps (csrc/sparse.hip kernel_map_brick_kernel) with MVR_BRICK_MAPS=1, else over the
+# per-level coordinate tables (identical maps; A/B timing)
+BRICK_MAPS = os.environ.get("MVR_BRICK_MAPS", "0") == "1"
 
 
 class CoordinateManager:

@@ -151,12 +151,15 @@ size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels
  *   bit 3: InstanceNorm folds (the next conv's IN + BN scale / shift) finished inside the producing point conv
  *          by the workgroup whose arrival completes a pair's statistics, instead of a separate finalize launch
  *          (bit-identical results: the same merge order);
- *   bit 1 is unused (ignored).  Default 13.
+ *   bit 1 is unused (ignored).  Default 5 (bit 3 until validated on the device; 13 with it).
  * Returns the previous value. */
 int mvr_set_oan_fused(int on);
 /* Key-split diff_pool launches inside mvr_oan_block_forward (mvr_oan_diff_pool_ws): 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */
 int mvr_set_pool_split(int on);
+/* How mvr_oan_diff_pool_ws splits (process-wide): 0 every (pair, cluster block) in k parts or none; 1 only the
+ * launch's tail past its complete rounds (fewer partial slabs, the same makespan).  Returns the previous setting. */
+int mvr_set_pool_tail(int on);
 
 /* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
  * a multiple of 4, input 16-byte aligned, padding columns [N, ld) finite (zero).

@@ -47,7 +47,12 @@ def test_voxelize_hint_sized_table_matches_oracle(gpu, frags, hint):
     np.testing.assert_array_equal(sel2.cpu().numpy(), osel)
 
 
-def test_strided_sets_and_kernel_maps_match_oracle(gpu, frags):
+@pytest.mark.parametrize("bricks", [False, True])
+def test_strided_sets_and_kernel_maps_match_oracle(gpu, frags, bricks, monkeypatch):
+    """every level's coordinate set and the 3^3 kernel maps (over the coordinate tables, and over brick maps:
+    mvr_kernel_map_bricks) equal the oracle's"""
+    import lib.sparse
+    monkeypatch.setattr(lib.sparse, "BRICK_MAPS", bricks)
     from lib.sparse import voxelize, CoordinateManager
     from oracle.fcgf import Levels
     c, _, counts, _ = voxelize(frags, 0.025, gpu)
@@ -124,13 +129,15 @@ def test_lattice_table_kernel_maps_dense_and_sparse(gpu, stride):
         np.testing.assert_array_equal(nbr.cpu().numpy(), ref)
 
 
-def test_brick_kernel_maps_equal_table_maps(gpu, frags):
+def test_brick_kernel_maps_equal_table_maps(gpu, frags, monkeypatch):
     """All ten 3^3 kernel maps of FCGF (s1 at strides 1-8, down 1-4, up 1-4) over the input level's brick map
     (mvr_kernel_map_bricks) equal the maps over the level's lattice coordinate table (mvr_kernel_map), and the row
     orders from the brick kernel's keys (mvr_kernel_map_order_keys) equal mvr_kernel_map_order's"""
     import torch
+    import lib.sparse
     from lib import _native as N
     from lib.sparse import voxelize, CoordinateManager
+    monkeypatch.setattr(lib.sparse, "BRICK_MAPS", True)
     L = N.lib()
     c, _, counts, _ = voxelize(frags, 0.025, gpu)
     cm = CoordinateManager(c, len(counts))

@@ -55,17 +55,20 @@ def math(request):
     NV.lib().mvr_set_attn_math(prev)
 
 
-@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("split", [False, True, "tail"])
 @pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (41, 700, 300),
                                     (300, 600, 500)])
 def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
     """split: mvr_oan_diff_pool_ws with a workspace (points split over 2-4 workgroups per (pair, cluster
-    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  300 pairs x 500 clusters
-    (608 whole workgroups on 256 CUs): only the tail past the two complete rounds is split (pair octets 32-37),
-    the rest runs whole.  The split-fp16 math needs the workspace's flag word: without one the launch is
-    split-bf16."""
+    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  "tail"
+    (mvr_set_pool_tail(1)): at 300 pairs x 500 clusters (608 whole workgroups on 256 CUs) only the tail past the
+    two complete rounds is split (pair octets 32-37), the rest runs whole.  The split-fp16 math needs the
+    workspace's flag word: without one the launch is split-bf16."""
     import torch
     from lib import _native as NV
+    if split == "tail" and P < 300:
+        pytest.skip("the tail split differs from the uniform one only past a complete round of workgroups")
+    prev_tail = NV.lib().mvr_set_pool_tail(1 if split == "tail" else 0)
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 1000 + N)
     xd, e = _embed(x, sc, sh, W, b, N)
     ref = (xd @ torch.softmax(e, dim=2).transpose(1, 2)).numpy()          # oanet.py:106-110
@@ -88,6 +91,7 @@ def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
         assert L.mvr_oan_diff_pool(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
                                    P, C, N, Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.stream()) == 0
     torch.cuda.synchronize()
+    NV.lib().mvr_set_pool_tail(prev_tail)
     o = out.cpu().numpy()
     scale = np.abs(ref).max()
     np.testing.assert_allclose(o[:, :, :Kc], ref, atol=2e-5 * scale, rtol=0)
