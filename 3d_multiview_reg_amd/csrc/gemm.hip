@@ -942,6 +942,305 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(KArgs ka) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// OAFilter conv2 (oanet.py:72-81, the 1x1 conv over clusters run on the transpose, oanet.hip oafilter):
+//   C[b](m, n) = sum_k relu(A[b](m, k) sc[b][k] + sh[b][k]) W(n, k) + bias[n] + R[b](m, n),   m < 128
+// with W [N][K] shared by every pair and per-128-column row statistics (ST_ROW).  Split once: the generic kernel
+// above re-splits every A element in the two waves that share its rows and every B element in the two that share
+// its columns, per stage; here
+//   * W is split into its three bf16 planes once per launch (oaf_w_image_kernel, 1.5 MB for 500 x 500), in the
+//     exact LDS image order, and staged by LDS-DMA;
+//   * the A slab of a stage is loaded into registers one stage ahead (fp32, 32 B per thread), folded (BN + ReLU)
+//     and split by the whole workgroup, each element once, into three LDS planes — in the middle of the previous
+//     stage's MFMAs;
+//   * one 512-thread workgroup per CU computes a 128 x 256 tile (8 waves of 64 x 64): A is read once per 256
+//     columns, and the MFMA fragments come straight from the planes by ds_read_b128.
+// Planes are [rows][32 k] bf16 (64-byte rows) with the 16-byte chunk c of row r stored at c ^ ((r >> 2) & 3):
+// every ds_read_b128 lane group (MI355X_MICROARCH §LDS) then covers 16 distinct 16-byte slots of the 256-byte
+// bank row.  K % 4 == 0 (the PRO_A_K contract); M == 128.
+constexpr int C2_BN = 256, C2_BK = 32, C2_THREADS = 512;
+constexpr int C2_APL = 128 * C2_BK;                  // bf16 per A plane and stage (8 KB)
+constexpr int C2_BPL = C2_BN * C2_BK;                // bf16 per B plane and stage (16 KB)
+constexpr int C2_SLOT = 3 * (C2_APL + C2_BPL);       // bf16 per stage slot (72 KB)
+
+__host__ __device__ inline int c2_npad(int N) { return (N + C2_BN - 1) / C2_BN * C2_BN; }
+__host__ __device__ inline int c2_nks(int K) { return (K + C2_BK - 1) / C2_BK; }
+
+int64_t oaf_conv2_image_bytes(int N, int K) {
+  if (N <= 0 || K <= 0) return 0;
+  return (int64_t)3 * c2_nks(K) * c2_npad(N) * C2_BK * 2;
+}
+
+// img[p][ks][n][32]: plane p (h, m, l) of W(n, 32 ks + 8c + e) at chunk position c ^ ((n >> 2) & 3), element e;
+// zero past N and K.  One thread per (ks, n, c).
+__global__ void oaf_w_image_kernel(const float* __restrict__ W, int N, int K, int64_t ldw, int Npad, int nks,
+                                   uint16_t* __restrict__ img) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)nks * Npad * 4) return;
+  const int c = (int)(i & 3);
+  const int n = (int)((i >> 2) % Npad), ks = (int)((i >> 2) / Npad);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 32 * ks + 8 * c + e;
+    v[e] = (n < N && k < K) ? W[(int64_t)n * ldw + k] : 0.f;
+  }
+  u32x4 H, Mm, L;
+  split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), H, Mm, L);
+  const int64_t plane = (int64_t)nks * Npad * C2_BK;
+  const int64_t o = ((int64_t)ks * Npad + n) * C2_BK + 8 * (c ^ ((n >> 2) & 3));
+  *reinterpret_cast<u32x4*>(img + o) = H;
+  *reinterpret_cast<u32x4*>(img + plane + o) = Mm;
+  *reinterpret_cast<u32x4*>(img + 2 * plane + o) = L;
+}
+
+__global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, const uint16_t* __restrict__ img) {
+  __shared__ __attribute__((aligned(16))) uint16_t sm[2 * C2_SLOT];
+  __shared__ float2 red[4 * 128];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;             // 64-row half, 64-column quarter of the tile
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int N = g.N, K = g.K;
+  const int N4 = (N + 3) & ~3;
+  const int ntn = (N + C2_BN - 1) / C2_BN, ntn128 = (N + 127) / 128;
+  const int Npad = ntn * C2_BN, nks = c2_nks(K);
+  const int ntiles = ntn * g.batch;
+  const int G = gridDim.x, slot = xcd_slot();
+  const int my_tiles = (ntiles - slot + G - 1) / G;
+  const int S = my_tiles * nks;
+  if (S <= 0) return;
+
+  // A staging: thread -> row am, 8 k from 8 ac (32 bytes of fp32 per stage)
+  const int am = tid >> 2, ac = tid & 3;
+  const int apos = am * C2_BK + 8 * (ac ^ ((am >> 2) & 3));
+  float4 ra0, ra1, rs0, rs1, rh0, rh1;
+  auto issue_a = [&](int gs) {
+    const int t = slot + (gs / nks) * G, ks = gs % nks;
+    const int b = t / ntn;
+    const int k = ks * C2_BK + 8 * ac;
+    const int k0 = min(k, K - 4), k1 = min(k + 4, K - 4);   // clamped into the row; zeroed past K at the fold
+    const float* Ar = g.A + (int64_t)b * g.sAb + (int64_t)am * g.lda;
+    const float* ps = g.psc + (int64_t)b * g.sPb;
+    const float* ph = g.psh + (int64_t)b * g.sPb;
+    ra0 = *reinterpret_cast<const float4*>(Ar + k0);
+    ra1 = *reinterpret_cast<const float4*>(Ar + k1);
+    rs0 = *reinterpret_cast<const float4*>(ps + k0);
+    rs1 = *reinterpret_cast<const float4*>(ps + k1);
+    rh0 = *reinterpret_cast<const float4*>(ph + k0);
+    rh1 = *reinterpret_cast<const float4*>(ph + k1);
+  };
+  auto store_a = [&](int gs) {   // fold + split the registers of stage gs into its slot's A planes
+    const int k = (gs % nks) * C2_BK + 8 * ac;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = k + e < K ? fmaxf(fmaf(f4(ra0, e), f4(rs0, e), f4(rh0, e)), 0.f) : 0.f;
+      v[4 + e] = k + 4 + e < K ? fmaxf(fmaf(f4(ra1, e), f4(rs1, e), f4(rh1, e)), 0.f) : 0.f;
+    }
+    u32x4 H, Mm, L;
+    split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), H, Mm, L);
+    uint16_t* As = sm + (gs & 1) * C2_SLOT;
+    *reinterpret_cast<u32x4*>(As + apos) = H;
+    *reinterpret_cast<u32x4*>(As + C2_APL + apos) = Mm;
+    *reinterpret_cast<u32x4*>(As + 2 * C2_APL + apos) = L;
+  };
+  // B staging: the 3 planes x 16 KB of a stage are 48 one-KB LDS-DMA pieces, 6 per wave
+  auto issue_b = [&](int gs) {
+    const int t = slot + (gs / nks) * G, ks = gs % nks;
+    const int tn = t % ntn;
+    uint16_t* Bs = sm + (gs & 1) * C2_SLOT + 3 * C2_APL;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const int idx = 6 * wid + q, p = idx >> 4, seg = idx & 15;
+      const uint32_t off =
+          (uint32_t)((((int64_t)p * nks + ks) * Npad + (int64_t)tn * C2_BN) * C2_BK * 2) + 1024u * seg + 16u * lane;
+      glds16s(img, off, lds_addr(Bs + p * C2_BPL + 512 * seg));
+    }
+  };
+
+  floatx16 acc[2][2];
+  const int t4 = lane & 3, p8 = l32 >> 2;
+  const bool h1 = (t4 & 1) != 0, h2 = (t4 & 2) != 0;
+
+  issue_a(0);
+  store_a(0);
+  issue_b(0);
+  if (S > 1) issue_a(1);
+  if (S > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // B(0) landed; A(1) (6 loads, younger) in flight
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int gs = 0; gs < S; ++gs) {
+    const int ks = gs % nks;
+    lds_barrier();   // stage gs's A planes written and its B planes landed (each wave waited its own DMA);
+                     // every wave has finished reading slot (gs + 1) & 1 (stage gs - 1)
+    if (ks == 0) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
+    }
+    const uint16_t* As = sm + (gs & 1) * C2_SLOT;
+    const uint16_t* Bs = As + 3 * C2_APL;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int cc = 2 * st + kh;   // 16-byte chunk of k 16 st + 8 kh .. + 7
+      bx::Frag fa[2], fb[2];
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int r = wm * 64 + ii * 32 + l32;
+        const int o = r * C2_BK + 8 * (cc ^ ((r >> 2) & 3));
+        fa[ii].h = *reinterpret_cast<const bf16x8*>(As + o);
+        fa[ii].m = *reinterpret_cast<const bf16x8*>(As + C2_APL + o);
+        fa[ii].l = *reinterpret_cast<const bf16x8*>(As + 2 * C2_APL + o);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn * 64 + j * 32 + l32;
+        const int o = r * C2_BK + 8 * (cc ^ ((r >> 2) & 3));
+        fb[j].h = *reinterpret_cast<const bf16x8*>(Bs + o);
+        fb[j].m = *reinterpret_cast<const bf16x8*>(Bs + C2_BPL + o);
+        fb[j].l = *reinterpret_cast<const bf16x8*>(Bs + 2 * C2_BPL + o);
+      }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[ii][j] = bx::mfma6(fa[ii], fb[j], acc[ii][j]);
+      if (st == 0 && gs + 1 < S) {
+        // stage gs + 1: fold + split A into the other slot (free since the barrier), its B by DMA, and the next
+        // A registers (issued after the DMA, so that vmcnt(6) below waits for the DMA only)
+        store_a(gs + 1);
+        issue_b(gs + 1);
+        if (gs + 2 < S) issue_a(gs + 2);
+      }
+    }
+    if (ks == nks - 1) {
+      // ------------------------------------------------------------ epilogue of the tile (row path of tile_epilogue)
+      const int t = slot + (gs / nks) * G;
+      const int b = t / ntn, tn = t % ntn;
+      const int n0 = tn * C2_BN, nb0 = n0 + wn * 64;
+      const int nw = min(max(N - nb0, 0), 64);
+      const float rnw = nw > 0 ? 1.f / (float)nw : 0.f;
+      bool cok[2][4], sok[2];
+      float bn[2][4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int gn = nb0 + j * 32 + 4 * p8;
+        sok[j] = gn < N4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          cok[j][u] = gn + u < N;
+          bn[j][u] = cok[j][u] ? g.bias[gn + u] : 0.f;
+        }
+      }
+      float* Cb = g.C + (int64_t)b * g.sCb;
+      const float* Rb = g.R + (int64_t)b * g.sRb;
+      float4 w[2][2][4];
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gm = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int gn = min(nb0 + j * 32 + 4 * p8, N4 - 4);
+            w[ii][j][q] = *reinterpret_cast<const float4*>(Rb + (int64_t)gm * g.ldc + gn);
+          }
+        }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gm = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            float a0 = acc[ii][j][4 * q], a1 = acc[ii][j][4 * q + 1], a2 = acc[ii][j][4 * q + 2],
+                  a3 = acc[ii][j][4 * q + 3];
+            quad_transpose(a0, a1, a2, a3, h1, h2);
+            const float4 x = make_float4(a0 + bn[j][0] + w[ii][j][q].x, a1 + bn[j][1] + w[ii][j][q].y,
+                                         a2 + bn[j][2] + w[ii][j][q].z, a3 + bn[j][3] + w[ii][j][q].w);
+            w[ii][j][q] = x;
+            if (sok[j]) *reinterpret_cast<float4*>(Cb + (int64_t)gm * g.ldc + nb0 + j * 32 + 4 * p8) = x;
+          }
+        }
+        float s1[4], s2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          s1[q] = 0.f;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s1[q] += cok[j][u] ? f4(w[ii][j][q], u) : 0.f;
+          s1[q] = sum8_p8(s1[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float mu = s1[q] * rnw;
+          s2[q] = 0.f;
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float d = cok[j][u] ? f4(w[ii][j][q], u) - mu : 0.f;
+              s2[q] = fmaf(d, d, s2[q]);
+            }
+          s2[q] = sum8_p8(s2[q]);
+        }
+        if (p8 == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            red[wn * 128 + wm * 64 + ii * 32 + 8 * q + 4 * kh + t4] = make_float2(s1[q], s2[q]);
+        }
+      }
+      lds_barrier();
+      if (tid < 256) {   // merge the two 64-column waves of each 128-column statistics tile (Chan)
+        const int half = tid >> 7, row = tid & 127;
+        const int n0h = n0 + 128 * half;
+        if (n0h < N) {
+          const float2 x = red[(2 * half) * 128 + row], c = red[(2 * half + 1) * 128 + row];
+          const int na = min(N - n0h, 64), nb = min(max(N - n0h - 64, 0), 64);
+          float2 o = x;
+          if (nb > 0) {
+            const float d = c.x / (float)nb - x.x / (float)na;
+            o = make_float2(x.x + c.x, x.y + c.y + d * d * ((float)na * (float)nb / (float)(na + nb)));
+          }
+          g.stats[((int64_t)b * ntn128 + 2 * tn + half) * g.st_ld + g.st_off + row] = o;
+        }
+      }
+      // (red is next written in the next tile's epilogue, after at least one stage barrier)
+    }
+    if (gs + 1 < S) {
+      // B(gs + 1) landed, A(gs + 2) (6 loads, younger) in flight; loads retire in order.  After an epilogue its
+      // stores are outstanding too (not ordered with the loads): drain everything.
+      if (gs + 2 < S && ks != nks - 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+}
+
+int g_oaf_conv2 = 0;   // mvr_set_oaf_conv2
+
+static bool oaf_conv2_covers(const GemmArgs& g) {
+  return g.wimg && g.M == 128 && g.pro == PRO_A_K && g.bkc == 1 && g.sBb == 0 && g.bias_mode == BIAS_N &&
+         g.stats_mode == ST_ROW && g.has_res && !g.no_store && !g.head_w && !g.xin && g.K % 4 == 0 &&
+         g.wimg_bytes >= oaf_conv2_image_bytes(g.N, g.K) && (reinterpret_cast<uintptr_t>(g.wimg) & 15) == 0 &&
+         (int64_t)c2_nks(g.K) * c2_npad(g.N) * C2_BK * 2 * 3 < ((int64_t)1 << 31);
+}
+
+static int launch_oaf_conv2(const GemmArgs& g, hipStream_t s) {
+  const int Npad = c2_npad(g.N), nks = c2_nks(g.K);
+  const int64_t nthr = (int64_t)nks * Npad * 4;
+  hipLaunchKernelGGL(oaf_w_image_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, g.B, g.N, g.K, g.ldb,
+                     Npad, nks, g.wimg);
+  MVR_CHECK_LAUNCH();
+  const long long tiles = (long long)(Npad / C2_BN) * g.batch;
+  const unsigned wgs = (unsigned)(tiles < 256 ? tiles : 256);   // one 144-KB-LDS workgroup per CU
+  hipLaunchKernelGGL(oaf_conv2_kernel, dim3(wgs), dim3(C2_THREADS), 0, s, g, (const uint16_t*)g.wimg);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
 #ifndef GEMM_F16_DEFAULT
 #define GEMM_F16_DEFAULT 0
 #endif
@@ -968,7 +1267,7 @@ static void launch_t(const KArgs& ka0, long long tiles, hipStream_t s) {
 
 static inline bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-int launch_gemm(const GemmArgs& g, hipStream_t s) {
+static int launch_gemm_impl(const GemmArgs& g, hipStream_t s, bool conv2) {
   if (g.M <= 0 || g.N <= 0 || g.batch <= 0) return MVR_OK;
   if (!g.A || !g.B || (!g.C && !g.no_store) || g.K <= 0) return MVR_EINVAL;
   // no_store: statistics only (row statistics), or the output head only (point-conv kernel)
@@ -1004,6 +1303,7 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
   }
   ProfScope prof(g.prof_kind, fl, by, s);
   if (pconv_covers(g)) return launch_pconv(g, s);
+  if (conv2 && oaf_conv2_covers(g)) return launch_oaf_conv2(g, s);
   if (g.head_w) return MVR_EINVAL;   // the fused head exists on the point-conv kernel only
   // Dispatch only the combinations the OANet schedule uses (oanet.hip).
 #define MVR_CASE(P, BKC_, BI, ST, RS)                                                                     \
@@ -1028,6 +1328,8 @@ int launch_gemm(const GemmArgs& g, hipStream_t s) {
 #undef MVR_CASE
   return MVR_EINVAL;
 }
+
+int launch_gemm(const GemmArgs& g, hipStream_t s) { return launch_gemm_impl(g, s, g_oaf_conv2 != 0); }
 
 }  // namespace mvr
 
@@ -1064,6 +1366,38 @@ extern "C" int mvr_gemm_trace(unsigned long long* out, int reset) {
   return 0;
 }
 #endif
+
+// C-ABI: the OAFilter conv2 launch on the split-once kernel whatever mvr_set_oaf_conv2 says (tests): W [N][K]
+// (row stride ldw) shared by every pair, A folded by (psc, psh) per k, bias per n, residual R, row statistics per
+// 128-column tile; img: img_bytes >= mvr_oaf_conv2_image_bytes(N, K) of scratch.  MVR_EINVAL when the shape is not
+// the kernel's (M != 128, K % 4 != 0, a null operand).
+extern "C" int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda,
+                                 const float* W, int64_t ldw, float* C, int64_t sCb, int64_t ldc, const float* R,
+                                 int64_t sRb, const float* bias, const float* psc, const float* psh, int64_t sPb,
+                                 float* stats, int64_t st_ld, void* img, int64_t img_bytes, hipStream_t stream) {
+  mvr::GemmArgs g{};
+  g.math = mvr::MATH_BF16X3;
+  g.M = M; g.N = N; g.K = K; g.batch = batch;
+  g.A = A; g.sAb = sAb; g.lda = lda;
+  g.B = W; g.sBb = 0; g.ldb = ldw; g.bkc = 1;
+  g.C = C; g.sCb = sCb; g.ldc = ldc;
+  g.R = R; g.sRb = sRb; g.has_res = 1;
+  g.bias = bias; g.bias_mode = mvr::BIAS_N;
+  g.psc = psc; g.psh = psh; g.sPb = sPb; g.pro = mvr::PRO_A_K;
+  g.stats = reinterpret_cast<float2*>(stats); g.st_ld = st_ld; g.stats_mode = mvr::ST_ROW;
+  g.wimg = static_cast<uint16_t*>(img); g.wimg_bytes = img_bytes;
+  if (!R || !bias || !psc || !psh || !stats || !img || M != 128 || K % 4) return MVR_EINVAL;
+  if (!mvr::oaf_conv2_covers(g)) return MVR_EINVAL;
+  return mvr::launch_gemm_impl(g, stream, true);
+}
+
+extern "C" size_t mvr_oaf_conv2_image_bytes(int N, int K) { return (size_t)mvr::oaf_conv2_image_bytes(N, K); }
+
+extern "C" int mvr_set_oaf_conv2(int on) {
+  const int prev = mvr::g_oaf_conv2;
+  mvr::g_oaf_conv2 = on ? 1 : 0;
+  return prev;
+}
 
 extern "C" int mvr_set_gemm_f16(int on) {
   const int prev = mvr::g_gemm_h;

@@ -77,6 +77,10 @@ struct GemmArgs {
   int* fin_cnt; float fin_eps; mvr_bn_p fin_bn; float* fin_sc; float* fin_sh; int64_t fin_ld;
   float fin_eps2; mvr_bn_p fin_bn2; float* fin_sc2; float* fin_sh2;
   int fin_train; float2* fin_mv; int* fin_done;
+  // OAFilter conv2 shape (M = 128, PRO_A_K, B = weights [N][K] shared by every pair, BIAS_N, ST_ROW, residual) with
+  // mvr_set_oaf_conv2 on: scratch for the weights' split-bf16 image (oaf_conv2_image_bytes(N, K) bytes, written
+  // by the launch), which routes it to the split-once kernel (gemm.hip oaf_conv2_kernel).  Null: generic kernel.
+  uint16_t* wimg; int64_t wimg_bytes;
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the
@@ -94,7 +98,11 @@ int launch_gemm(const GemmArgs& g, hipStream_t stream);
 bool pconv_covers(const GemmArgs& g);   // head fields set: only pconv can run it
 int launch_pconv(const GemmArgs& g, hipStream_t stream);
 
-inline int gemm_ntiles(int N) { return (N + GEMM_BN - 1) / GEMM_BN; }
+// bytes of the weights' split-bf16 image the OAFilter conv2 kernel reads (GemmArgs.wimg)
+int64_t oaf_conv2_image_bytes(int N, int K);
+extern int g_oaf_conv2;      // mvr_set_oaf_conv2
+
+inline int gemm_ntiles(int N){ return (N + GEMM_BN - 1) / GEMM_BN; }
 inline int gemm_mtiles(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }
 inline int64_t round4(int64_t x) { return (x + 3) & ~(int64_t)3; }
 inline int64_t round32(int64_t x) { return (x + 31) & ~(int64_t)31; }

@@ -363,6 +363,8 @@ struct Plan {
   int* fcnt;             // FIN_SLOTS x P arrival counters of the fused finalizes (zeroed at the block's start)
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
   int* flags;            // FLAG_SLOTS range flags of the split-fp16 launches (zeroed at the block's start)
+  uint16_t* w2img;       // OAFilter conv2's weight image (mvr_set_oaf_conv2; rewritten by every conv2 launch)
+  int64_t w2img_bytes;
 };
 
 // one flag word per guarded split-fp16 launch of a block forward, assigned in launch order (a block issues ~30)
@@ -432,6 +434,8 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   pl.mv = w.take<float2>((size_t)P * 2 * C);
   pl.stcol = w.take<float2>((size_t)P * MC * Kc);
   pl.flags = w.take<int>(FLAG_SLOTS);
+  pl.w2img_bytes = oaf_conv2_image_bytes(Kc, Kc);
+  pl.w2img = w.take<uint16_t>((size_t)pl.w2img_bytes / 2);
   pl.bytes = w.off + 256;
   return pl;
 }
@@ -602,6 +606,7 @@ struct Ctx {
     g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
     g.prof_kind = PK_OAFILTER;
     g.flag = flag();
+    g.wimg = pl.w2img; g.wimg_bytes = pl.w2img_bytes;   // the split-once kernel when mvr_set_oaf_conv2 is on
     chk(launch_gemm(g, s));
     finalize_in(o2, 1e-3f, f.bn3);
     return conv(f.conv3, o2, true, xd, &xd, ST_ROW, nullptr, false, next);  // in place: out = conv3(...) + x

@@ -57,6 +57,10 @@ _SIGS = {
     "mvr_gemm_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_int, c_vp, c_i64,
                              c_i64, c_vp, c_i64, c_vp, c_int, c_vp, c_vp, c_i64, c_i64, c_int, c_vp, c_i64, c_int,
                              c_int, c_int, c_vp, c_vp]),
+    "mvr_oaf_conv2_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
+                                  c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
+    "mvr_oaf_conv2_image_bytes": (c_size, [c_int, c_int]),
+    "mvr_set_oaf_conv2": (c_int, [c_int]),
     "mvr_set_pconv": (c_int, [c_int]),
     "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),

@@ -104,6 +104,20 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
    (in place).  0 (default) off, 1 on.  Returns the previous setting.  The choice never depends on process state
    (launch counts, buffer addresses). */
 int mvr_set_gemm_f16(int on);
+/* OAFilter conv2 (oanet.py:72-81: the 1x1 conv over the clusters on the transpose, W2 [K][K] shared by every pair):
+ * C[b](m, n) = sum_k relu(A[b](m, k) psc[b*sPb + k] + psh[b*sPb + k]) W(n, k) + bias[n] + R[b](m, n), M = 128, row
+ * statistics per 128-column tile as mvr_gemm_f32's stats_mode 1 (st_off 0), on the split-once kernel (gemm.hip
+ * oaf_conv2_kernel: W split into an image once per launch, each A element folded and split once per workgroup,
+ * 128 x 256 tiles).  img: >= mvr_oaf_conv2_image_bytes(N, K) bytes of 16-byte aligned device scratch, written by the
+ * call.  Layout as mvr_gemm_f32 (K % 4 == 0).  MVR_EINVAL when the shape is not the kernel's. */
+int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* W,
+                      int64_t ldw, float* C, int64_t sCb, int64_t ldc, const float* R, int64_t sRb, const float* bias,
+                      const float* psc, const float* psh, int64_t sPb, float* stats, int64_t st_ld, void* img,
+                      int64_t img_bytes, mvr_stream_t stream);
+size_t mvr_oaf_conv2_image_bytes(int N, int K);
+/* Run the OANet block's OAFilter conv2 launches (mvr_oan_block_forward) on that kernel: 0 (default) the generic
+ * GEMM, 1 the split-once kernel.  Process-wide; returns the previous setting. */
+int mvr_set_oaf_conv2(int on);
 /* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */

@@ -355,3 +355,77 @@ def test_gemm_rejects_bad_layout(gpu):
     # misaligned C
     assert L.mvr_gemm_f32(15, 12, 8, 1, NV.ptr(A), 0, 8, NV.ptr(B), 0, 16, 0, NV.ptr(C[0, 1:]), 0, 16, None, 0,
                           None, 0, None, None, 0, 0, 0, None, 0, 0, 0, 1, NV.ptr(NV.flag_word()), NV.stream()) == -1
+
+
+@pytest.mark.parametrize("N,K,batch,shared_fold", [(500, 500, 5, False), (500, 500, 300, True), (36, 36, 3, False),
+                                                   (300, 260, 4, False), (517, 128, 3, True), (256, 4, 2, False),
+                                                   (1, 32, 2, False), (640, 500, 300, False)])
+def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
+    """OAFilter conv2 on the split-once kernel (gemm.hip oaf_conv2_kernel: weight image split once per launch, the
+    A slab folded and split once per workgroup, 128 x 256 tiles) against float64 and against the generic kernel:
+    ragged N (partial 256-column tiles, an empty second statistics half at N = 517 and 1), a K tail, K = 4, more
+    tiles than workgroups (batch 300: every workgroup runs several tiles across the stage ring), the eval-mode
+    fold shared by every pair (sPb = 0) and per-pair folds (train)."""
+    import torch
+    from lib import _native as NV
+    M = 128
+    r = np.random.RandomState(N * 7 + K + batch)
+    K4, N4 = r4(K), r4(N)
+    A = r.standard_normal((batch, M, K)).astype(np.float32)
+    W = (r.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32)
+    Rm = r.standard_normal((batch, M, N)).astype(np.float32)
+    bias = r.standard_normal(N).astype(np.float32)
+    nf = 1 if shared_fold else batch
+    sc = r.uniform(0.5, 1.5, (nf, K)).astype(np.float32)
+    sh = r.uniform(-0.5, 0.5, (nf, K)).astype(np.float32)
+    Ad = np.maximum(A.astype(np.float64) * sc[:, None, :] + sh[:, None, :], 0)
+    Cref = Ad @ W.astype(np.float64).T + bias[None, None, :] + Rm
+    scale = np.abs(Ad) @ np.abs(W.astype(np.float64)).T + 1.0
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(gpu)   # noqa: E731
+    tA, tW, tR, tb, tsc, tsh = t(_pad(A, K4)), t(_pad(W, K4)), t(_pad(Rm, N4)), t(bias), t(sc), t(sh)
+    nT = (N + BT - 1) // BT
+    L = NV.lib()
+    img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(N, K)) // 4 + 4, device=gpu)
+    outs = []
+    for new in (True, False):
+        C = torch.full((batch, M, N4), float("nan"), device=gpu)
+        st = torch.zeros(batch, nT, M, 2, device=gpu)
+        if new:
+            rc = L.mvr_oaf_conv2_f32(M, N, K, batch, NV.ptr(tA), M * K4, K4, NV.ptr(tW), K4, NV.ptr(C), M * N4, N4,
+                                     NV.ptr(tR), M * N4, NV.ptr(tb), NV.ptr(tsc), NV.ptr(tsh), 0 if shared_fold else K,
+                                     NV.ptr(st), M, NV.ptr(img), img.numel() * 4, NV.stream())
+        else:
+            rc = L.mvr_gemm_f32(M, N, K, batch, NV.ptr(tA), M * K4, K4, NV.ptr(tW), 0, K4, 1, NV.ptr(C), M * N4, N4,
+                                NV.ptr(tR), M * N4, NV.ptr(tb), 2, NV.ptr(tsc), NV.ptr(tsh), 0 if shared_fold else K,
+                                0, 1, NV.ptr(st), M, 0, 1, 1, None, NV.stream())
+        assert rc == 0
+        torch.cuda.synchronize()
+        Cg = C.cpu().numpy().astype(np.float64)
+        assert np.all(np.isfinite(Cg)), "padding columns must be written with finite values"
+        Cg = Cg[..., :N]
+        assert np.all(np.abs(Cg - Cref) <= 1e-5 * scale), np.max(np.abs(Cg - Cref) / scale)
+        S = st.cpu().numpy().astype(np.float64)
+        for tt in range(nT):
+            blk = Cref[:, :, tt * BT:(tt + 1) * BT]
+            np.testing.assert_allclose(S[:, tt, :, 0], blk.sum(-1), rtol=1e-4, atol=1e-3)
+            dev2 = ((blk - blk.mean(-1, keepdims=True)) ** 2).sum(-1)
+            np.testing.assert_allclose(S[:, tt, :, 1], dev2, rtol=1e-4, atol=1e-3)
+        outs.append(Cg)
+    # the two kernels differ only in the MFMA k order inside a 32-k stage
+    assert np.all(np.abs(outs[0] - outs[1]) <= 2e-6 * scale), np.max(np.abs(outs[0] - outs[1]) / scale)
+
+
+def test_oaf_conv2_rejects_other_shapes(gpu):
+    import torch
+    from lib import _native as NV
+    L = NV.lib()
+    x = torch.zeros(1 << 16, device=gpu)
+    p = NV.ptr(x)
+    nb = int(L.mvr_oaf_conv2_image_bytes(64, 64))
+    assert nb == 3 * 2 * 256 * 32 * 2
+    args = lambda M, K, img_bytes: (M, 64, K, 1, p, 0, 68, p, 68, p, 0, 64, p, 0, p, p, p, 0, p, M, p,   # noqa: E731
+                                    img_bytes, NV.stream())
+    assert L.mvr_oaf_conv2_f32(*args(64, 64, nb)) == -1       # M != 128
+    assert L.mvr_oaf_conv2_f32(*args(128, 66, nb)) == -1      # K % 4
+    assert L.mvr_oaf_conv2_f32(*args(128, 64, nb - 16)) == -1  # image scratch too small
+    torch.cuda.synchronize()

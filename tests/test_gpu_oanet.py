@@ -96,7 +96,16 @@ def test_oanet_small_golden(gpu, fx, train, ovr):
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
 
-def test_oanet_full_golden(gpu):
+@pytest.fixture(params=[0, 1], ids=["conv2_generic", "conv2_split_once"])
+def conv2(request):
+    """mvr_set_oaf_conv2: the OAFilter conv2 launches on the generic GEMM or the split-once kernel"""
+    from lib import _native as NV
+    prev = NV.lib().mvr_set_oaf_conv2(request.param)
+    yield request.param
+    NV.lib().mvr_set_oaf_conv2(prev)
+
+
+def test_oanet_full_golden(gpu, conv2):
     import torch
     g = golden("oanet_full_eval.npz")
     net = _oanet(128, 500, 7, gpu, which="full")
@@ -105,7 +114,7 @@ def test_oanet_full_golden(gpu):
     _check(out, g, atol_logit=2e-3)
 
 
-def test_oanet_full_train_golden(gpu):
+def test_oanet_full_train_golden(gpu, conv2):
     """STRESS fixture (the strict bound is enforced on the well-conditioned oanet_full_train_strict.npz below).
     The benchmark's mode (scripts/benchmark_pairwise_registration.py:159-197 never calls model.eval():
     BatchNorm on the statistics of each 32-pair batch) at full size against the reference (RegBlock network,
@@ -139,7 +148,7 @@ def test_oanet_full_train_golden(gpu):
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
 
-def test_oanet_full_train_strict_golden(gpu):
+def test_oanet_full_train_strict_golden(gpu, conv2):
     """north_star's bound on the benchmark's mode: train-mode BatchNorm over one 32-pair batch, RegBlock network,
     32 pairs x 5000 correspondences, on the well-conditioned reference fixture (the reference's fp32 output sits
     within 1e-5 of its own fp64 output on every pair).  R and t within 1e-4 of the reference on EVERY pair of

@@ -21,6 +21,7 @@ CASES = {
     "pool": (C, K, N, 3, 1, 0, 1, 0),
     "unpool": (C, N, K, 3, 0, 0, 1, 0),
     "oaf_conv2": (C, K, K, 1, 1, 2, 1, 1),    # OAFilter conv2 (oanet.hip oafilter): W2 shared, bias per n, residual
+    "oaf_conv2_so": (C, K, K, 1, 1, 2, 1, 1),  # the same on the split-once kernel (mvr_oaf_conv2_f32)
     "conv_oaf1": (C, K, C, 2, 0, 1, 4, 0),    # OAFilter conv1 over the clusters: IN/BN/ReLU prologue, column stats
 }
 
@@ -55,8 +56,15 @@ def run(name, iters, math, pconv=1):
     st_ld = M if stats in (1, 2) else Nn
     L = NV.lib()
     L.mvr_set_pconv(pconv)
+    img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(Nn, Kk)) // 4 + 4, device=d) if name == "oaf_conv2_so" else None
 
     def go():
+        if img is not None:
+            rc = L.mvr_oaf_conv2_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), Kk, NV.ptr(Cout), M * Nl, Nl,
+                                     NV.ptr(R), M * Nl, NV.ptr(bvec), NV.ptr(sc), NV.ptr(sh), sPb, NV.ptr(st), st_ld,
+                                     NV.ptr(img), img.numel() * 4, NV.stream())
+            assert rc == 0
+            return
         rc = L.mvr_gemm_f32(M, Nn, Kk, P, NV.ptr(A), sAb, Kk, NV.ptr(Bt), sBb, Kk if bkc else Nl, bkc,
                             NV.ptr(Cout), M * Nl, Nl, NV.ptr(R), M * Nl, NV.ptr(bvec), bias, NV.ptr(sc),
                             NV.ptr(sh), sPb, pld, pro, NV.ptr(st), st_ld, 0, stats, math, NV.ptr(NV.flag_word()), NV.stream())
