@@ -65,6 +65,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // Which 16-byte chunk q (4 consecutive k of the 32-k stage) lane half h reads as its s4-th
@@ -1014,8 +1015,8 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   // A staging: thread -> row am, 8 k from 8 ac (32 bytes of fp32 per stage)
   const int am = tid >> 2, ac = tid & 3;
   const int apos = am * C2_BK + 8 * (ac ^ ((am >> 2) & 3));
-  float4 ra0, ra1, rs0, rs1, rh0, rh1;
-  auto issue_a = [&](int gs) {
+  f32x4 ra0, ra1, rs0, rs1, rh0, rh1;
+  auto issue_a = [&](int gs) {   // 6 loads
     const int t = slot + (gs / nks) * G, ks = gs % nks;
     const int b = t / ntn;
     const int k = ks * C2_BK + 8 * ac;
@@ -1023,33 +1024,33 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
     const float* Ar = g.A + (int64_t)b * g.sAb + (int64_t)am * g.lda;
     const float* ps = g.psc + (int64_t)b * g.sPb;
     const float* ph = g.psh + (int64_t)b * g.sPb;
-    ra0 = *reinterpret_cast<const float4*>(Ar + k0);
-    ra1 = *reinterpret_cast<const float4*>(Ar + k1);
-    rs0 = *reinterpret_cast<const float4*>(ps + k0);
-    rs1 = *reinterpret_cast<const float4*>(ps + k1);
-    rh0 = *reinterpret_cast<const float4*>(ph + k0);
-    rh1 = *reinterpret_cast<const float4*>(ph + k1);
+    ra0 = *reinterpret_cast<const f32x4*>(Ar + k0);
+    ra1 = *reinterpret_cast<const f32x4*>(Ar + k1);
+    rs0 = *reinterpret_cast<const f32x4*>(ps + k0);
+    rs1 = *reinterpret_cast<const f32x4*>(ps + k1);
+    rh0 = *reinterpret_cast<const f32x4*>(ph + k0);
+    rh1 = *reinterpret_cast<const f32x4*>(ph + k1);
   };
-  auto store_a = [&](int gs) {   // fold + split the registers of stage gs into its slot's A planes
+  auto store_a = [&](int gs, int sl) {   // fold + split the registers of stage gs into slot sl's A planes
     const int k = (gs % nks) * C2_BK + 8 * ac;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      v[e] = k + e < K ? fmaxf(fmaf(f4(ra0, e), f4(rs0, e), f4(rh0, e)), 0.f) : 0.f;
-      v[4 + e] = k + 4 + e < K ? fmaxf(fmaf(f4(ra1, e), f4(rs1, e), f4(rh1, e)), 0.f) : 0.f;
+      v[e] = k + e < K ? fmaxf(fmaf(ra0[e], rs0[e], rh0[e]), 0.f) : 0.f;
+      v[4 + e] = k + 4 + e < K ? fmaxf(fmaf(ra1[e], rs1[e], rh1[e]), 0.f) : 0.f;
     }
     u32x4 H, Mm, L;
     split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), H, Mm, L);
-    uint16_t* As = sm + (gs & 1) * C2_SLOT;
+    uint16_t* As = sm + sl * C2_SLOT;
     *reinterpret_cast<u32x4*>(As + apos) = H;
     *reinterpret_cast<u32x4*>(As + C2_APL + apos) = Mm;
     *reinterpret_cast<u32x4*>(As + 2 * C2_APL + apos) = L;
   };
   // B staging: the 3 planes x 16 KB of a stage are 48 one-KB LDS-DMA pieces, 6 per wave
-  auto issue_b = [&](int gs) {
+  auto issue_b = [&](int gs, int sl) {
     const int t = slot + (gs / nks) * G, ks = gs % nks;
     const int tn = t % ntn;
-    uint16_t* Bs = sm + (gs & 1) * C2_SLOT + 3 * C2_APL;
+    uint16_t* Bs = sm + sl * C2_SLOT + 3 * C2_APL;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const int idx = 6 * wid + q, p = idx >> 4, seg = idx & 15;
@@ -1063,24 +1064,30 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   const int t4 = lane & 3, p8 = l32 >> 2;
   const bool h1 = (t4 & 1) != 0, h2 = (t4 & 2) != 0;
 
+  // Per stage gs (one barrier): right after the barrier B(gs + 1) goes by DMA into the other slot (a whole stage to
+  // land); the A registers of gs + 1 (loaded a stage ago) are folded and split into that slot interleaved with the
+  // first k16 step's MFMAs, then the A loads of gs + 2 are issued.  The last stage does the same with clamped
+  // indices into the unused slot (branch-free: one scheduling region for the split and the MFMAs).  Loads retire in
+  // order: vmcnt(6) at the end of a stage = B(gs + 1) landed, the 6 younger A loads still in flight.
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
   issue_a(0);
-  store_a(0);
-  issue_b(0);
-  if (S > 1) issue_a(1);
-  if (S > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // B(0) landed; A(1) (6 loads, younger) in flight
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  store_a(0, 0);
+  issue_b(0, 0);
+  issue_a(min(1, S - 1));
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // B(0) landed; A(1) in flight
   for (int gs = 0; gs < S; ++gs) {
     const int ks = gs % nks;
+    const int gn = min(gs + 1, S - 1), so = (gs + 1) & 1;
     lds_barrier();   // stage gs's A planes written and its B planes landed (each wave waited its own DMA);
-                     // every wave has finished reading slot (gs + 1) & 1 (stage gs - 1)
-    if (ks == 0) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
-    }
+                     // every wave has finished reading slot so (stage gs - 1)
+    // the A registers of gs + 1 ready before the DMA is issued (a use here makes the compiler's wait precede it)
+    asm volatile("" ::"v"(ra0), "v"(ra1), "v"(rs0), "v"(rs1), "v"(rh0), "v"(rh1));
+    issue_b(gn, so);
     const uint16_t* As = sm + (gs & 1) * C2_SLOT;
     const uint16_t* Bs = As + 3 * C2_APL;
 #pragma unroll
@@ -1103,16 +1110,23 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
         fb[j].m = *reinterpret_cast<const bf16x8*>(Bs + C2_BPL + o);
         fb[j].l = *reinterpret_cast<const bf16x8*>(Bs + 2 * C2_BPL + o);
       }
+      if (st == 0) store_a(gn, so);
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[ii][j] = bx::mfma6(fa[ii], fb[j], acc[ii][j]);
-      if (st == 0 && gs + 1 < S) {
-        // stage gs + 1: fold + split A into the other slot (free since the barrier), its B by DMA, and the next
-        // A registers (issued after the DMA, so that vmcnt(6) below waits for the DMA only)
-        store_a(gs + 1);
-        issue_b(gs + 1);
-        if (gs + 2 < S) issue_a(gs + 2);
+      if (st == 0) {
+        issue_a(min(gs + 2, S - 1));
+        // 12 fragment reads, then the 24 MFMAs each followed by a share of the split (VALU, its 3 LDS writes)
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+        for (int u = 0; u < 24; ++u) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          if (u == 20) __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+          if (u == 21) __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (ks == nks - 1) {
@@ -1209,14 +1223,19 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
         }
       }
       // (red is next written in the next tile's epilogue, after at least one stage barrier)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;   // the next tile's accumulators
     }
-    if (gs + 1 < S) {
-      // B(gs + 1) landed, A(gs + 2) (6 loads, younger) in flight; loads retire in order.  After an epilogue its
-      // stores are outstanding too (not ordered with the loads): drain everything.
-      if (gs + 2 < S && ks != nks - 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // B(gs + 1) landed, A(gs + 2) (6 loads, younger) in flight.  After an epilogue its stores are outstanding too
+    // (not ordered with the loads): drain everything.
+    if (ks != nks - 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 }
 
 int g_oaf_conv2 = 0;   // mvr_set_oaf_conv2

@@ -1078,13 +1078,17 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
 // Key splits of the pool launch: with one 512-thread workgroup per CU, P x ceil(Kc / 256) workgroups
 // leave a partial last round (435 pairs: 880 workgroups = 3.44 rounds of 256).  Splitting the keys (points) of
 // a (pair, query block) into k parts shortens the rounds, but every split unit writes an (O, m, l) slab that the
-// last one reads back (135 KB each).  So only a TAIL is split: the pair octets [0, g0) run whole, the rest in k
-// parts, dispatched after them.  Candidates (k in {1, 2, 4} with >= 8 key blocks per part; g0 = every octet, no
-// octet, or the most octets whose whole units fill complete rounds) are ranked by the makespan of the dispatch
-// order on `cus` slots (a unit = 1, a part = 1 / k), ties to fewer slabs.  A function of the shape and the
-// device's CU count only.
+// last one reads back (135 KB each), and the split changes a unit's summation order.
+//  * default: every unit in 2 parts at N >= 16 key blocks (3.5 rounds instead of 4 at 435 pairs), a function of N
+//    alone, so a pair's result does not depend on the batch it came in (pair-sharded runs over any number of ranks
+//    give the one-process records bit for bit, tests/test_gpu_distributed.py);
+//  * mvr_set_pool_tail(1): only a TAIL is split: the pair octets [0, g0) run whole, the rest in k parts,
+//    dispatched after them.  Candidates (k in {1, 2, 4} with >= 8 key blocks per part; g0 = every octet, no octet,
+//    or the most octets whose whole units fill complete rounds) are ranked by the makespan of the dispatch order
+//    on `cus` slots (a unit = 1, a part = 1 / k), ties to fewer slabs: fewer slabs (224 instead of 1760 at 435
+//    pairs), but the split of a pair then depends on the batch size and the device's CU count.
 struct PoolSplit { int nks, g0; };
-int g_pool_tail = 0;   // mvr_set_pool_tail: 1 split only the tail (below); 0 every (pair, block) or none (round 3)
+int g_pool_tail = 0;   // mvr_set_pool_tail
 static double pool_makespan(int64_t full, int64_t parts, int k, int cus) {
   // greedy in dispatch order: the whole units first, then the parts, each to the earliest free slot
   std::vector<double> slot((size_t)cus, 0.0);
@@ -1099,13 +1103,14 @@ static double pool_makespan(int64_t full, int64_t parts, int k, int cus) {
   return *std::max_element(slot.begin(), slot.end());
 }
 static PoolSplit pool_splits(int P, int nqb, int N) {
+  const int nkb = (N + AKB - 1) / AKB;
+  if (!g_pool_tail) return nkb >= 16 ? PoolSplit{2, 0} : PoolSplit{1, (P + 7) / 8};
   int dev = 0, cus = 0;   // the current device's CU count (an attribute query, no process state)
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
     cus = 256;
   const int G = (P + 7) / 8;                 // pair octets
   const int64_t per = 8LL * nqb;             // workgroups of one octet, unsplit
-  const int nkb = (N + AKB - 1) / AKB;
   PoolSplit best{1, G};
   double tbest = pool_makespan(per * G, 0, 1, cus);
   int64_t slabs_best = 0;
@@ -1114,7 +1119,7 @@ static PoolSplit pool_splits(int P, int nqb, int N) {
     const int gfill = (int)(((per * G) / cus) * cus / per);   // most whole octets in complete rounds
     const int cands[3] = {0, gfill, G};
     for (int g0 : cands) {
-      if (g0 >= G || (g0 > 0 && !g_pool_tail)) continue;
+      if (g0 >= G) continue;
       const int64_t parts = per * k * (G - g0);
       const double t = pool_makespan(per * g0, parts, k, cus);
       if (t < tbest - 1e-9 || (t < tbest + 1e-9 && parts < slabs_best)) {

@@ -495,8 +495,10 @@ struct Ctx {
 
   // returns true when the launch also wrote the requested fold of its output (`fold`, ST_ROW only): the next
   // conv's prologue then reads it (fcur flipped); false: the caller runs finalize_in
+  // (pro_sc / pro_sh: the prologue's fold when it is not the current one, e.g. diff_unpool's scU / shU)
   bool conv(const mvr_conv_p& cv, const Act& in, bool pro, const Act& out, const Act* res, int stats_mode,
-            const float* w_padded = nullptr, bool no_store = false, const FoldReq* fold = nullptr) {
+            const float* w_padded = nullptr, bool no_store = false, const FoldReq* fold = nullptr,
+            const float* pro_sc = nullptr, const float* pro_sh = nullptr) {
     GemmArgs g{};
     int done = 0;
     if (fold) fuse(g, *fold, &done);
@@ -512,7 +514,7 @@ struct Ctx {
     g.C = out.p; g.sCb = out.ps; g.ldc = out.ld;
     if (res) { g.R = res->p; g.sRb = res->ps; g.has_res = 1; }
     g.bias = cv.bias; g.bias_mode = cv.bias ? BIAS_M : BIAS_NONE;
-    if (pro) { g.pro = PRO_B_K; g.psc = sc(); g.psh = sh(); g.sPb = in.C; }
+    if (pro) { g.pro = PRO_B_K; g.psc = pro_sc ? pro_sc : sc(); g.psh = pro_sh ? pro_sh : sh(); g.sPb = in.C; }
     g.stats_mode = stats_mode;
     g.stats = out.st; g.st_ld = out.st_ld; g.st_off = out.st_off;
     g.prof_kind = (in.L == pl.Kc && out.L == pl.Kc) ? PK_OAFILTER : (out.C == pl.Kc ? PK_EMBED : PK_CONV_PTS);
@@ -790,7 +792,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
                                reinterpret_cast<float*>(pl.st11), 2 * C, C, pl.uimg, pl.uimg_bytes, s));
   } else {
     Act e2{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, N, 0};
-    cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX);
+    cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX, nullptr, false, nullptr, pl.scU, pl.shU);
     const int MK = gemm_mtiles(Kc);
     cx.smx_factors(MK, N, Np);
     GemmArgs g{};

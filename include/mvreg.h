@@ -171,8 +171,11 @@ int mvr_set_oan_fused(int on);
 /* Key-split diff_pool launches inside mvr_oan_block_forward (mvr_oan_diff_pool_ws): 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */
 int mvr_set_pool_split(int on);
-/* How mvr_oan_diff_pool_ws splits (process-wide): 0 every (pair, cluster block) in k parts or none; 1 only the
- * launch's tail past its complete rounds (fewer partial slabs, the same makespan).  Returns the previous setting. */
+/* How mvr_oan_diff_pool_ws splits (process-wide): 0 (default) every (pair, cluster block) in 2 parts when N >= 512
+ * (none below), a function of N alone: a pair's result does not depend on the batch (or rank shard) it came in;
+ * 1 only the launch's tail past its complete rounds, chosen by the batch's makespan on the device's CUs (fewer
+ * partial slabs, the same makespan, but a pair's summation order then depends on the batch size).  Returns the
+ * previous setting. */
 int mvr_set_pool_tail(int on);
 
 /* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
