@@ -988,10 +988,21 @@ extern "C" int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, in
 
 // the row order from precomputed keys (mvr_kernel_map_bricks' order_keys): the same stable LSD radix sort as
 // mvr_kernel_map_order over the same keys.  keys is not modified.  Workspace: mvr_kernel_map_order_bytes(Mo).
+extern "C" int mvr_kernel_map_order_keys_bits(const uint64_t* keys, int64_t Mo, int begin_bit, int end_bit,
+                                              int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s);
 extern "C" int mvr_kernel_map_order_keys(const uint64_t* keys, int64_t Mo, int K, int32_t* perm, void* ws,
                                          size_t ws_bytes, hipStream_t s) {
-  if (!keys || !perm || Mo < 0 || K <= 0 || K > 32 || !ws || ws_bytes < mvr_kernel_map_order_bytes(Mo) ||
-      Mo > 0x7fffffff)
+  if (K <= 0 || K > 32) return MVR_EINVAL;
+  // g_spconv_order 1: the fragment + Morton bits only (spatially compact tiles, larger offset unions; A/B timing)
+  return mvr_kernel_map_order_keys_bits(keys, Mo, 0, g_spconv_order == 1 ? 32 : 32 + K, perm, ws, ws_bytes, s);
+}
+
+// the same over the key bits [begin_bit, end_bit) only (0 <= begin_bit < end_bit <= 64): e.g. [0, 32) orders by
+// fragment and Morton code alone
+extern "C" int mvr_kernel_map_order_keys_bits(const uint64_t* keys, int64_t Mo, int begin_bit, int end_bit,
+                                              int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (!keys || !perm || Mo < 0 || begin_bit < 0 || end_bit > 64 || begin_bit >= end_bit || !ws ||
+      ws_bytes < mvr_kernel_map_order_bytes(Mo) || Mo > 0x7fffffff)
     return MVR_EINVAL;
   if (Mo == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mo * 32, s);
@@ -1004,9 +1015,8 @@ extern "C" int mvr_kernel_map_order_keys(const uint64_t* keys, int64_t Mo, int K
   if (!tmp) return MVR_ELAUNCH;
   void* tbuf = take(tmp);
   hipLaunchKernelGGL(iota_kernel, dim3(nblk(Mo)), dim3(256), 0, s, vin, Mo);
-  // g_spconv_order 1: the fragment + Morton bits only (spatially compact tiles, larger offset unions; A/B timing)
-  const int end_bit = g_spconv_order == 1 ? 32 : 32 + K;
-  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, keys, kout, vin, perm, (int)Mo, 0, end_bit, s) != hipSuccess)
+  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, keys, kout, vin, perm, (int)Mo, begin_bit, end_bit, s) !=
+      hipSuccess)
     return MVR_ELAUNCH;
   MVR_CHECK_LAUNCH();
   return MVR_OK;

@@ -119,6 +119,7 @@ _SIGS = {
     "mvr_kernel_map_order": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_kernel_map_bricks": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_size, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "mvr_kernel_map_order_keys": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
+    "mvr_kernel_map_order_keys_bits": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_set_spconv_order": (c_int, [c_int]),
     "mvr_set_pool_tail": (c_int, [c_int]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,

@@ -18,6 +18,10 @@ from lib import _native as N
 # 3^3 kernel maps over brick maps (csrc/sparse.hip kernel_map_brick_kernel) with MVR_BRICK_MAPS=1, else over the
 # per-level coordinate tables (identical maps; A/B timing)
 BRICK_MAPS = os.environ.get("MVR_BRICK_MAPS", "0") == "1"
+# tiling order of the sparse convs over brick-path keys: "mask" (default) active-offset mask, then fragment and
+# Morton code; "spatial": fragment and Morton code alone for the s1 / down maps (fewer distinct rows gathered per
+# tile, larger offset unions), the mask kept for the transposed maps (whose rows use <= 8 of 27 offsets by parity)
+SPCONV_ORDER = os.environ.get("MVR_SPCONV_ORDER", "mask")
 
 
 class CoordinateManager:
@@ -114,7 +118,11 @@ class CoordinateManager:
             L = N.lib()
             ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr.shape[0]), self.device)
             perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.device)
-            if key in self.order_keys:   # keys written by the brick kernel map
+            if key in self.order_keys and SPCONV_ORDER == "spatial" and kind != "up":
+                N.check(L.mvr_kernel_map_order_keys_bits(N.ptr(self.order_keys.pop(key)), nbr.shape[0], 0, 32,
+                                                         N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
+                        "mvr_kernel_map_order_keys_bits")
+            elif key in self.order_keys:   # keys written by the brick kernel map
                 N.check(L.mvr_kernel_map_order_keys(N.ptr(self.order_keys.pop(key)), nbr.shape[0], nbr.shape[1],
                                                     N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
                         "mvr_kernel_map_order_keys")

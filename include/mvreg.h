@@ -115,8 +115,8 @@ int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A, int64_t sA
                       const float* psc, const float* psh, int64_t sPb, float* stats, int64_t st_ld, void* img,
                       int64_t img_bytes, mvr_stream_t stream);
 size_t mvr_oaf_conv2_image_bytes(int N, int K);
-/* Run the OANet block's OAFilter conv2 launches (mvr_oan_block_forward) on that kernel: 0 (default) the generic
- * GEMM, 1 the split-once kernel.  Process-wide; returns the previous setting. */
+/* Run the OANet block's OAFilter conv2 launches (mvr_oan_block_forward) on that kernel: 1 (default) the
+ * split-once kernel, 0 the generic GEMM (A/B).  Process-wide; returns the previous setting. */
 int mvr_set_oaf_conv2(int on);
 /* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
@@ -410,6 +410,10 @@ int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, int out_strid
  * perm).  Workspace: mvr_kernel_map_order_bytes(Mout). */
 int mvr_kernel_map_order_keys(const uint64_t* order_keys, int64_t Mout, int K, int32_t* perm, void* workspace,
                               size_t workspace_bytes, mvr_stream_t stream);
+/* The same over the key bits [begin_bit, end_bit) only (0 <= begin_bit < end_bit <= 64; [0, 32): fragment and
+ * Morton code alone, [0, 32 + K): the full key). */
+int mvr_kernel_map_order_keys_bits(const uint64_t* keys, int64_t Mo, int begin_bit, int end_bit, int32_t* perm,
+                                   void* ws, size_t ws_bytes, mvr_stream_t stream);
 /* row order of mvr_kernel_map_order_keys (process-wide): 0 (default) active-offset mask, then fragment and Morton
  * code; 1 fragment and Morton code only (spatially compact tiles whose offset unions are larger; A/B timing).
  * Returns the previous setting. */

@@ -57,7 +57,8 @@ def test_register_sharded_real_oanet_two_processes(gpu, tmp_path, guard):
     for r in range(world):
         rec = np.load(os.path.join(str(tmp_path), "rec_%d.npy" % r))
         np.testing.assert_array_equal(rec[:, 0], np.arange(70))
-        assert np.array_equal(rec, ref), (r, np.abs(rec - ref).max())
+        # (pairs 32-63 are degenerate for the Procrustes: whatever it returns there must match too)
+        assert np.array_equal(rec, ref, equal_nan=True), (r, np.nanmax(np.abs(rec - ref)))
     # the guard really fired, for a reason that lives on rank 0 only: pairs 32-63 have no positive logit in
     # block 0; every pair in its scope then carries + 1/N (scene: all 70, rank 1's 64-69 included; group: 32-63)
     lg = plain["logits"][0].cpu().numpy()

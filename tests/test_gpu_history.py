@@ -12,6 +12,8 @@ in-place = pointer equality, shape-only pool splits).
 These tests run the case, then disturb every piece of process state the earlier tests could leave behind
 (caching-allocator layout, grown per-stream workspaces, other streams, other network shapes, the benchmark
 harness itself), then run it again, in both operand maths, and require identical bits."""
+import os
+
 import numpy as np
 import pytest
 
@@ -44,6 +46,7 @@ def _forward(net, xs, fused):
 def _disturb(gpu, tmp_path):
     """what the earlier tests of a suite leave behind"""
     import torch
+    from conftest import GOLDEN
     import bench
     from lib import _native as NV
     from test_gpu_benchmark_harness import _scene
@@ -56,8 +59,13 @@ def _disturb(gpu, tmp_path):
         wl.step_pipelined(1)
         bench.PrecomputedWorkload(gpu, 0, 40, 3000).step()
     _scene(str(tmp_path / "redwood"), scene="iclnuim-office1", n_frag=4, n_corr=600)
-    main(["--source_path", str(tmp_path), "--dataset", "redwood", "--method", "RegBlock", "--batch_size", "32",
-          "--num_workers", "0"])
+    cwd = os.getcwd()
+    os.chdir(GOLDEN)   # the harness reads ./configs/pairwise_registration/eval/RegBlock.yaml (the reference's file)
+    try:
+        main(["--source_path", str(tmp_path), "--dataset", "redwood", "--method", "RegBlock", "--batch_size", "32",
+              "--num_workers", "0"])
+    finally:
+        os.chdir(cwd)
     torch.cuda.synchronize()
     del keep[1]
     return keep

