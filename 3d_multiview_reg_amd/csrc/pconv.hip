@@ -47,6 +47,7 @@ namespace mvr {
 #endif
 
 int g_pconv = 1;   // mvr_set_pconv: 0 routes these convs to gemm_kernel (A/B timing)
+int g_pconv_grid = 1;   // mvr_set_pconv_grid: workgroups per resident slot (1: one persistent round)
 #ifndef PCONV_MATH_DEFAULT
 #define PCONV_MATH_DEFAULT 0
 #endif
@@ -773,7 +774,9 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   a.hw = g.head_w; a.hb = g.head_bp; a.logits = g.logits; a.scores = g.scores; a.pos = g.pos;
   a.xci = g.xci; a.xw = g.xw; a.xb = g.xb; a.rld = g.xld;
   const int ks = g.K / 16;
-  const int64_t slots = ks == 8 ? 512 : 256;   // resident workgroups (2 / 1 per CU)
+  // resident workgroups (2 / 1 per CU); g_pconv_grid > 1: that many contiguous group ranges per slot, dealt by the
+  // dispatcher as slots free up (balances against another stream's kernels holding some CUs)
+  const int64_t slots = (ks == 8 ? 512 : 256) * (int64_t)g_pconv_grid;
   const int grid = (int)(a.groups < slots ? a.groups : slots);
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
   const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
@@ -852,6 +855,12 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
 extern "C" int mvr_set_pconv_math(int h) {
   const int prev = mvr::g_pconv_h;
   mvr::g_pconv_h = h ? 1 : 0;
+  return prev;
+}
+
+extern "C" int mvr_set_pconv_grid(int mul) {
+  const int prev = mvr::g_pconv_grid;
+  mvr::g_pconv_grid = mul < 1 ? 1 : (mul > 64 ? 64 : mul);
   return prev;
 }
 

@@ -62,6 +62,7 @@ _SIGS = {
     "mvr_oaf_conv2_image_bytes": (c_size, [c_int, c_int]),
     "mvr_set_oaf_conv2": (c_int, [c_int]),
     "mvr_set_pconv": (c_int, [c_int]),
+    "mvr_set_pconv_grid": (c_int, [c_int]),
     "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),

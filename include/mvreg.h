@@ -122,6 +122,10 @@ int mvr_set_oaf_conv2(int on);
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
  * (A/B timing).  Returns the previous setting. */
 int mvr_set_pconv(int on);
+/* Point-conv launch grid (process-wide): mul (1..64, default 1) workgroups per resident slot, each a contiguous
+ * range of 128-point statistics groups (1: one persistent round).  Results do not depend on it (each group's
+ * statistics come from one workgroup; the folds merge them in group order).  Returns the previous setting. */
+int mvr_set_pconv_grid(int mul);
 /* operand math of the point convs (not the output-head launches): 0 (default) split-bf16 (fp32-equivalent);
    1 split-fp16 for launches that have a range flag (see mvr_set_gemm_f16): 3 MFMAs per product, weight rows
    range-scaled, activations x 2^6 after the prologue and range-checked, with a guarded split-bf16 re-run of a

@@ -400,12 +400,12 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
             hx(o64["logits"][1]), hx(xs)), flush=True)
     for out in outs:
         for i in range(2):
-            # block 1 consumes block 0's residuals: there each logit may sit as far from fp64 as 3x the fp32
-            # oracle's own distance (a chaotic pair), at least 2e-3
+            # block 1 consumes block 0's residuals: there a pair's logits may sit as far from fp64 as 3x the fp32
+            # oracle's own largest distance on that pair (a chaotic pair), at least 2e-3
             lg = out["logits"][i].cpu().numpy()
             tol = 2e-3 + 1e-4 * np.abs(o64["logits"][i])
             if i == 1:
-                tol = np.maximum(tol, 3 * np.abs(o32["logits"][i] - o64["logits"][i]))
+                tol = np.maximum(tol, 3 * np.abs(o32["logits"][i] - o64["logits"][i]).max(1, keepdims=True))
             assert (np.abs(lg - o64["logits"][i]) <= tol).all(), (i, np.abs(lg - o64["logits"][i]).max())
             sc, ref = out["scores"][i].cpu().numpy(), o64["scores"][i]
             near = np.abs(ref - 0.5) < 1e-4
@@ -448,3 +448,33 @@ def test_oanet_fused_finalize_bit_identical(gpu, P, npts, train):
     for k in ("logits", "scores", "rot_est", "trans_est"):
         for i in range(2):
             assert torch.equal(a[k][i], b[k][i]), (k, i, (a[k][i] - b[k][i]).abs().max().item())
+
+
+@pytest.mark.parametrize("P,npts,train,fused", [(37, 1234, False, 13), (70, 1500, True, 13), (37, 1234, False, 5)])
+def test_pconv_grid_bit_identical(gpu, P, npts, train, fused):
+    """The point-conv launch grid (mvr_set_pconv_grid: several contiguous group ranges per resident slot, dealt by
+    the dispatcher) changes which workgroup computes a 128-point group, never what it computes: every output is
+    bit-identical, with and without the fused InstanceNorm folds (whose last arriver merges in group order)."""
+    import torch
+    from lib import _native as NV
+    from test_gpu_oanet import _oanet
+    from synth import synth_correspondences
+    xs, _, _ = synth_correspondences(P, npts, seed=6)
+    net = _oanet(128, 500, 7, gpu, train=train, which="full")
+    if train:
+        net.bn_group = net.guard_group = 32
+    L = NV.lib()
+    prev, prevf = L.mvr_set_pconv_grid(1), L.mvr_set_oan_fused(fused)
+    outs = []
+    try:
+        for m in (1, 3, 8):
+            L.mvr_set_pconv_grid(m)
+            with torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    finally:
+        L.mvr_set_pconv_grid(prev)
+        L.mvr_set_oan_fused(prevf)
+    for o in outs[1:]:
+        for k in ("logits", "scores", "rot_est", "trans_est"):
+            for i in range(2):
+                assert torch.equal(outs[0][k][i], o[k][i]), (k, i, (outs[0][k][i] - o[k][i]).abs().max().item())
