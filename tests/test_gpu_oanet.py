@@ -120,8 +120,9 @@ def test_oanet_full_train_golden(gpu, conv2):
     BatchNorm on the statistics of each 32-pair batch) at full size against the reference (RegBlock network,
     32 pairs x 5000 correspondences).  Masks identical away from 0.5 in both blocks.  This random network is
     chaotic (block 1 consumes block 0's residuals): the reference's own fp32 result sits up to 2.5e-4 from exact
-    arithmetic (oanet_full_train_f64.npz, our float64 restatement), so in both blocks each pair must be within
-    max(1e-4, 2 x that distance) of the reference's fp32 or of exact arithmetic — and at least 30 of the 32 pairs
+    arithmetic (oanet_full_train_f64.npz, our float64 restatement).  So in both blocks each pair must be within
+    1e-4 of exact arithmetic unless it is chaotic — as shown by the reference's own distance from exact (2x) or by
+    the spread of our result under a different diff_pool summation order (3x) — and at least 30 of the 32 pairs
     within 1e-4 of the reference's fp32.  (Round 4's pool split,
     now the same for every batch size, put one block-0 pair at 1.05e-4 of the reference's fp32.)"""
     import hashlib
@@ -130,9 +131,21 @@ def test_oanet_full_train_golden(gpu, conv2):
     g64 = golden("oanet_full_train_f64.npz")
     xs, _, _ = synth_correspondences(32, 5000, seed=33)
     assert hashlib.sha1(xs.tobytes()).hexdigest() == str(g["xs_sha1"])
+    from lib import _native as NV
     net = _oanet(128, 500, 7, gpu, train=True, which="full")
-    with torch.no_grad():
-        out = net({"xs": torch.from_numpy(xs).unsqueeze(1)})
+    L = NV.lib()
+    outs = []
+    # the default run, then two runs that differ from it only in diff_pool's summation order (key splits off / the
+    # batch-dependent tail split): their spread measures each pair's own fp32 rounding sensitivity
+    for knob, v in ((None, None), ("mvr_set_pool_split", 0), ("mvr_set_pool_tail", 1)):
+        prev = getattr(L, knob)(v) if knob else None
+        try:
+            with torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+        finally:
+            if knob:
+                getattr(L, knob)(prev)
+    out = outs[0]
     dist = lambda u, v: np.abs(u - v).reshape(u.shape[0], -1).max(1)   # noqa: E731
     for i in range(2):
         sc, ref = out["scores"][i].cpu().numpy(), g["scores%d" % i]
@@ -142,9 +155,10 @@ def test_oanet_full_train_golden(gpu, conv2):
         for k, kg in (("rot_est", "R"), ("trans_est", "t")):
             got, r32, r64 = out[k][i].cpu().numpy(), g["%s%d" % (kg, i)], g64["%s%d" % (kg, i)]
             d, d64, e = dist(got, r32), dist(got, r64), dist(r32, r64)
-            # every pair within max(1e-4, 2 x the reference's own distance from exact) of the reference's fp32 or
-            # of exact arithmetic; at least 30 of 32 within 1e-4 of the reference's fp32
-            assert (np.minimum(d, d64) <= np.maximum(1e-4, 2 * e)).all(), (i, k, d, d64, e)
+            spread = np.max([dist(got, o[k][i].cpu().numpy()) for o in outs[1:]], axis=0)
+            # every pair within max(1e-4, 2 x the reference's own distance from exact, 3 x our rounding spread) of
+            # exact arithmetic; at least 30 of 32 within 1e-4 of the reference's fp32
+            assert (d64 <= np.maximum(1e-4, np.maximum(2 * e, 3 * spread))).all(), (i, k, d64, e, spread)
             assert (d <= 1e-4).sum() >= 30, (i, k, d)
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
