@@ -1075,6 +1075,10 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
+#if GEMM_TRACE   // phases: 0 barrier, 1 A wait + DMA issue, 2 first k16 step (+ split), 3 second, 4 epilogue, 5 stage-end wait
+  unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime();
+  int prev_slot = 7;
+#endif
   issue_a(0);
   store_a(0, 0);
   issue_b(0, 0);
@@ -1083,11 +1087,14 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   for (int gs = 0; gs < S; ++gs) {
     const int ks = gs % nks;
     const int gn = min(gs + 1, S - 1), so = (gs + 1) & 1;
+    TSTAMP(0);
     lds_barrier();   // stage gs's A planes written and its B planes landed (each wave waited its own DMA);
                      // every wave has finished reading slot so (stage gs - 1)
+    TSTAMP(1);
     // the A registers of gs + 1 ready before the DMA is issued (a use here makes the compiler's wait precede it)
     asm volatile("" ::"v"(ra0), "v"(ra1), "v"(rs0), "v"(rs1), "v"(rh0), "v"(rh1));
     issue_b(gn, so);
+    TSTAMP(2);
     const uint16_t* As = sm + (gs & 1) * C2_SLOT;
     const uint16_t* Bs = As + 3 * C2_APL;
 #pragma unroll
@@ -1127,8 +1134,10 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
           if (u == 21) __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
+        TSTAMP(3);
       }
     }
+    TSTAMP(4);
     if (ks == nks - 1) {
       // ------------------------------------------------------------ epilogue of the tile (row path of tile_epilogue)
       const int t = slot + (gs / nks) * G;
@@ -1232,10 +1241,16 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
     }
     // B(gs + 1) landed, A(gs + 2) (6 loads, younger) in flight.  After an epilogue its stores are outstanding too
     // (not ordered with the loads): drain everything.
+    TSTAMP(5);
     if (ks != nks - 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
+#if GEMM_TRACE
+  TSTAMP(7);
+  if (lane == 0)
+    for (int q = 0; q < 8; ++q) atomicAdd(&g_gemm_trace[q], tr[q]);
+#endif
 }
 
 int g_oaf_conv2 = 1;   // mvr_set_oaf_conv2 (default on: 0.25 vs 0.30 ms per launch, oafilter 2.08 vs 2.38 ms per step)

@@ -93,6 +93,9 @@ def run(name, iters, math, pconv=1):
         tot = sum(buf)
         names = ["stage-wait+barrier", "ktail+lds-reads", "barrier+issue", "transform+split+mfma",
                  "refill(late)/loop", "tile_of", "epilogue", "tail"]
+        if name == "oaf_conv2_so":   # the split-once kernel's phases (gemm.hip oaf_conv2_kernel)
+            names = ["barrier", "A-wait+DMA-issue", "k16 step 0 + split", "k16 step 1", "epilogue", "stage-end wait",
+                     "-", "prologue/tail"]
         print("   phase shares (wave-cycles, one launch): " +
               ", ".join("%s %.1f%%" % (names[q], 100.0 * buf[q] / max(tot, 1)) for q in range(8)), flush=True)
 
