@@ -497,44 +497,40 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   }
   if (nks > 1) {
     // publish this split's (O, m, l); the last split to arrive merges all of them (counter hand-off:
-    // plain stores, agent-scope release before the ticket, agent-scope acquire by the reducer)
+    // device-coherent stores, each lane's complete before the ticket, device-coherent loads by the reducer — no
+    // agent-scope fences, whose L2 write-back / invalidation cost every workgroup on the XCD its cached lines)
     const int64_t slot = (int64_t)p * a.nqb + jb;
     float* mine = a.part + (slot * nks + ks) * PSLAB + tid;
+    auto st_c = [](float* q, float v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mine[(16 * cb + r) * ATHREADS] = O[cb][r];
-    mine[64 * ATHREADS] = m;
-    mine[65 * ATHREADS] = l;
+      for (int r = 0; r < 16; ++r) st_c(mine + (16 * cb + r) * ATHREADS, O[cb][r]);
+    st_c(mine + 64 * ATHREADS, m);
+    st_c(mine + 65 * ATHREADS, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(xraw);   // the raw-tile ring is drained
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int tk = __hip_atomic_fetch_add(a.cnt + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // tickets are not reset between the fp16 launch and its guarded re-run: the last split of a slot
       // draws nks - 1 modulo nks
-      const bool last = tk % nks == nks - 1;
-      flag[0] = last;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      flag[0] = tk % nks == nks - 1;
     }
     __syncthreads();
     if (!flag[0]) return;   // uniform
     // merge the splits in split order (whichever arrived last: the result does not depend on arrival order)
     const floatx16 own[4] = {O[0], O[1], O[2], O[3]};
     const float mown = m, lown = l;
+    auto ld_c = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     for (int o = 0; o < nks; ++o) {
       const float* th = a.part + (slot * nks + o) * PSLAB + tid;
-      const float m2 = o == ks ? mown : th[64 * ATHREADS], l2 = o == ks ? lown : th[65 * ATHREADS];
+      const float m2 = o == ks ? mown : ld_c(th + 64 * ATHREADS), l2 = o == ks ? lown : ld_c(th + 65 * ATHREADS);
       if (o == 0) {
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) O[cb][r] = o == ks ? own[cb][r] : th[(16 * cb + r) * ATHREADS];
+          for (int r = 0; r < 16; ++r) O[cb][r] = o == ks ? own[cb][r] : ld_c(th + (16 * cb + r) * ATHREADS);
         m = m2;
         l = l2;
         continue;
@@ -545,7 +541,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          O[cb][r] = O[cb][r] * f1 + (o == ks ? own[cb][r] : th[(16 * cb + r) * ATHREADS]) * f2;
+          O[cb][r] = O[cb][r] * f1 + (o == ks ? own[cb][r] : ld_c(th + (16 * cb + r) * ATHREADS)) * f2;
       l = l * f1 + l2 * f2;
       m = mn;
     }

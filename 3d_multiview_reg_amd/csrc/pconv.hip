@@ -101,10 +101,15 @@ __device__ __forceinline__ void fold_write(const mvr_bn_p& bn, float eps, double
 }
 
 // Fused InstanceNorm finalize of pair p (the caller is the workgroup whose counter arrival completed the pair's
-// statistics, behind an agent-scope acquire): the 128 channels' partials of its T = ngrp 128-point tiles merged
+// statistics): the 128 channels' partials of its T = ngrp 128-point tiles (read with device-coherent loads: the
+// producers wrote them with device-coherent stores, so no L2 write-back or invalidation is needed) merged
 // exactly as in_finalize_kernel does for 128 channels (4 tile groups t = g, g + 4, ..., their double partials
 // combined in group order; Chan's merge), so the fold is bit-identical to the separate launch's.
 // red: 4 x 128 doubles of LDS scratch; threads 0..255 take part, every thread of the workgroup reaches the barriers.
+__device__ __forceinline__ float2 ld_coherent(const float2* q) {
+  return __builtin_bit_cast(float2, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(q), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
 __device__ void fin_pair(const PcArgs& a, int p, double* red, int tid) {
   const int T = a.ngrp, L = a.N, c = tid & 127, g0 = 2 * ((tid >> 7) & 1);
   const bool act = tid < 256;
@@ -112,9 +117,9 @@ __device__ void fin_pair(const PcArgs& a, int p, double* red, int tid) {
   if (act) {
     double t0 = 0.0, t1 = 0.0;
 #pragma unroll 4
-    for (int t = g0; t < T; t += 4) t0 += (double)sp[(int64_t)t * a.st_ld].x;
+    for (int t = g0; t < T; t += 4) t0 += (double)ld_coherent(sp + (int64_t)t * a.st_ld).x;
 #pragma unroll 4
-    for (int t = g0 + 1; t < T; t += 4) t1 += (double)sp[(int64_t)t * a.st_ld].x;
+    for (int t = g0 + 1; t < T; t += 4) t1 += (double)ld_coherent(sp + (int64_t)t * a.st_ld).x;
     red[g0 * 128 + c] = t0;
     red[(g0 + 1) * 128 + c] = t1;
   }
@@ -128,7 +133,7 @@ __device__ void fin_pair(const PcArgs& a, int p, double* red, int tid) {
     for (int u = 0; u < 2; ++u) {
 #pragma unroll 4
       for (int t = g0 + u; t < T; t += 4) {
-        const float2 v = sp[(int64_t)t * a.st_ld];
+        const float2 v = ld_coherent(sp + (int64_t)t * a.st_ld);
         const int nv = min(128, L - 128 * t);
         const double d = (double)v.x * (nv == 128 ? rtw : 1.0 / nv) - mean;
         m2[u] += (double)v.y + d * d * nv;
@@ -160,11 +165,12 @@ __device__ void fin_tail(const PcArgs& a, int* lastp, double* red, int tid) {
   const int64_t G = a.groups;
   const int64_t g0 = G * blockIdx.x / gridDim.x, g1 = G * (blockIdx.x + 1) / gridDim.x;
   if (g0 >= g1) return;   // uniform (such a workgroup returned before its main loop anyway)
+  // every lane's statistics stores (device-coherent) complete before the arrival: no agent-scope release fence,
+  // whose L2 write-back (buffer_wbl2) and, on the acquire side, L2 invalidation (buffer_inv) cost every workgroup
+  // of the launch and every other kernel on the XCD their cached lines
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int nl = 0;
     const int pfirst = (int)(g0 / a.ngrp), plast = (int)((g1 - 1) / a.ngrp);
     for (int p = pfirst; p <= plast; ++p) {
@@ -175,10 +181,6 @@ __device__ void fin_tail(const PcArgs& a, int* lastp, double* red, int tid) {
       if (old + n == a.ngrp && nl < 32 * YLD - 1) lastp[1 + nl++] = p;
     }
     lastp[0] = nl;
-    if (nl) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   const int nl = lastp[0];
@@ -587,8 +589,16 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
         }
         if ((lane & 7) == 0) {
           float2* st = a.stats + ((int64_t)c.p * a.ngrp + c.kc / GRP) * a.st_ld + a.st_off + 32 * w + erow;
+          if (a.fcnt) {   // read back in this launch by the pair's last arriver (fin_pair): device-coherent stores
 #pragma unroll
-          for (int q = 0; q < 4; ++q) st[8 * q] = make_float2(ls[q], lss[q]);
+            for (int q = 0; q < 4; ++q)
+              __hip_atomic_store(reinterpret_cast<unsigned long long*>(st + 8 * q),
+                                 __builtin_bit_cast(unsigned long long, make_float2(ls[q], lss[q])), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) st[8 * q] = make_float2(ls[q], lss[q]);
+          }
         }
       }
     }
