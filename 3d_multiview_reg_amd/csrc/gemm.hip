@@ -963,6 +963,7 @@ constexpr int C2_BN = 256, C2_BK = 32, C2_THREADS = 512;
 constexpr int C2_APL = 128 * C2_BK;                  // bf16 per A plane and stage (8 KB)
 constexpr int C2_BPL = C2_BN * C2_BK;                // bf16 per B plane and stage (16 KB)
 constexpr int C2_SLOT = 3 * (C2_APL + C2_BPL);       // bf16 per stage slot (72 KB)
+constexpr int C2_KMAX = 512;                         // largest K (the per-tile fold vectors live in LDS)
 
 __host__ __device__ inline int c2_npad(int N) { return (N + C2_BN - 1) / C2_BN * C2_BN; }
 __host__ __device__ inline int c2_nks(int K) { return (K + C2_BK - 1) / C2_BK; }
@@ -998,6 +999,7 @@ __global__ void oaf_w_image_kernel(const float* __restrict__ W, int N, int K, in
 __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, const uint16_t* __restrict__ img) {
   __shared__ __attribute__((aligned(16))) uint16_t sm[2 * C2_SLOT];
   __shared__ float2 red[4 * 128];
+  __shared__ __attribute__((aligned(16))) float fsv[2][2][C2_KMAX + C2_BK];   // [tile parity][scale | shift][k]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 2, wn = wid & 3;             // 64-row half, 64-column quarter of the tile
@@ -1015,24 +1017,34 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   // A staging: thread -> row am, 8 k from 8 ac (32 bytes of fp32 per stage)
   const int am = tid >> 2, ac = tid & 3;
   const int apos = am * C2_BK + 8 * (ac ^ ((am >> 2) & 3));
-  f32x4 ra0, ra1, rs0, rs1, rh0, rh1;
-  auto issue_a = [&](int gs) {   // 6 loads
+  f32x4 ra0, ra1;
+  auto issue_a = [&](int gs) {   // 2 loads
     const int t = slot + (gs / nks) * G, ks = gs % nks;
     const int b = t / ntn;
     const int k = ks * C2_BK + 8 * ac;
     const int k0 = min(k, K - 4), k1 = min(k + 4, K - 4);   // clamped into the row; zeroed past K at the fold
     const float* Ar = g.A + (int64_t)b * g.sAb + (int64_t)am * g.lda;
-    const float* ps = g.psc + (int64_t)b * g.sPb;
-    const float* ph = g.psh + (int64_t)b * g.sPb;
     ra0 = *reinterpret_cast<const f32x4*>(Ar + k0);
     ra1 = *reinterpret_cast<const f32x4*>(Ar + k1);
-    rs0 = *reinterpret_cast<const f32x4*>(ps + k0);
-    rs1 = *reinterpret_cast<const f32x4*>(ps + k1);
-    rh0 = *reinterpret_cast<const f32x4*>(ph + k0);
-    rh1 = *reinterpret_cast<const f32x4*>(ph + k1);
+  };
+  // the fold vectors (scale, shift per k) of this workgroup's tile i -> LDS parity i & 1: one float4 per thread
+  // (2 K / 4 <= 256 threads), loaded a stage before it is stored
+  const int q4 = K / 4;
+  f32x4 fv;
+  auto load_fold = [&](int i) {
+    const int b = (slot + min(i, my_tiles - 1) * G) / ntn;
+    if (tid < 2 * q4)
+      fv = *reinterpret_cast<const f32x4*>((tid < q4 ? g.psc : g.psh) + (int64_t)b * g.sPb + 4 * (tid < q4 ? tid : tid - q4));
+  };
+  auto store_fold = [&](int i) {
+    if (tid < 2 * q4) *reinterpret_cast<f32x4*>(&fsv[i & 1][tid < q4 ? 0 : 1][4 * (tid < q4 ? tid : tid - q4)]) = fv;
   };
   auto store_a = [&](int gs, int sl) {   // fold + split the registers of stage gs into slot sl's A planes
     const int k = (gs % nks) * C2_BK + 8 * ac;
+    const float* fs = fsv[(gs / nks) & 1][0] + k;
+    const float* fh = fsv[(gs / nks) & 1][1] + k;
+    const f32x4 rs0 = *reinterpret_cast<const f32x4*>(fs), rs1 = *reinterpret_cast<const f32x4*>(fs + 4);
+    const f32x4 rh0 = *reinterpret_cast<const f32x4*>(fh), rh1 = *reinterpret_cast<const f32x4*>(fh + 4);
     float v[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -1068,7 +1080,7 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   // land); the A registers of gs + 1 (loaded a stage ago) are folded and split into that slot interleaved with the
   // first k16 step's MFMAs, then the A loads of gs + 2 are issued.  The last stage does the same with clamped
   // indices into the unused slot (branch-free: one scheduling region for the split and the MFMAs).  Loads retire in
-  // order: vmcnt(6) at the end of a stage = B(gs + 1) landed, the 6 younger A loads still in flight.
+  // order: vmcnt(2) at the end of a stage = B(gs + 1) landed, the 2 younger A loads still in flight.
 #pragma unroll
   for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
@@ -1079,21 +1091,49 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime();
   int prev_slot = 7;
 #endif
+  load_fold(0);
+  store_fold(0);
   issue_a(0);
+  __syncthreads();
   store_a(0, 0);
   issue_b(0, 0);
   issue_a(min(1, S - 1));
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // B(0) landed; A(1) in flight
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // B(0) landed; A(1) in flight
+  float4 w[2][2][4];   // the residual of the tile's output, loaded at the start of its last stage
   for (int gs = 0; gs < S; ++gs) {
-    const int ks = gs % nks;
+    const int ks = gs % nks, ti = gs / nks;
     const int gn = min(gs + 1, S - 1), so = (gs + 1) & 1;
     TSTAMP(0);
     lds_barrier();   // stage gs's A planes written and its B planes landed (each wave waited its own DMA);
-                     // every wave has finished reading slot so (stage gs - 1)
+                     // every wave has finished reading slot so (stage gs - 1); fold vectors stored a stage ago visible
     TSTAMP(1);
+    // the next tile's fold vectors: loaded in its predecessor's first stage, stored in the second (published by the
+    // next barrier, read from the predecessor's last stage on); with two stages per tile, stored at once
+    if (ks == 0) {
+      load_fold(ti + 1);
+      if (nks < 3) store_fold(ti + 1);
+    } else if (ks == 1 && nks >= 3) {
+      store_fold(ti + 1);
+    }
     // the A registers of gs + 1 ready before the DMA is issued (a use here makes the compiler's wait precede it)
-    asm volatile("" ::"v"(ra0), "v"(ra1), "v"(rs0), "v"(rs1), "v"(rh0), "v"(rh1));
+    asm volatile("" ::"v"(ra0), "v"(ra1));
     issue_b(gn, so);
+    if (ks == nks - 1) {   // the tile's residual, in flight during its last stage's MFMAs
+      const int t = slot + ti * G;
+      const int b = t / ntn, nb0 = (t % ntn) * C2_BN + wn * 64;
+      const float* Rb = g.R + (int64_t)b * g.sRb;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int gm = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int gnc = min(nb0 + j * 32 + 4 * p8, N4 - 4);
+            w[ii][j][q] = *reinterpret_cast<const float4*>(Rb + (int64_t)gm * g.ldc + gnc);
+          }
+        }
+    }
     TSTAMP(2);
     const uint16_t* As = sm + (gs & 1) * C2_SLOT;
     const uint16_t* Bs = As + 3 * C2_APL;
@@ -1125,13 +1165,13 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
       if (st == 0) {
         issue_a(min(gs + 2, S - 1));
         // 12 fragment reads, then the 24 MFMAs each followed by a share of the split (VALU, its 3 LDS writes)
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // (+ the 4 fold-vector reads of the split)
 #pragma unroll
         for (int u = 0; u < 24; ++u) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
           if (u == 20) __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
-          if (u == 21) __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
+          if (u == 21) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         TSTAMP(3);
@@ -1158,19 +1198,6 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
         }
       }
       float* Cb = g.C + (int64_t)b * g.sCb;
-      const float* Rb = g.R + (int64_t)b * g.sRb;
-      float4 w[2][2][4];
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int gm = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int gn = min(nb0 + j * 32 + 4 * p8, N4 - 4);
-            w[ii][j][q] = *reinterpret_cast<const float4*>(Rb + (int64_t)gm * g.ldc + gn);
-          }
-        }
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
 #pragma unroll
@@ -1242,7 +1269,7 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
     // B(gs + 1) landed, A(gs + 2) (6 loads, younger) in flight.  After an epilogue its stores are outstanding too
     // (not ordered with the loads): drain everything.
     TSTAMP(5);
-    if (ks != nks - 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (ks != nks - 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
@@ -1258,6 +1285,7 @@ int g_oaf_conv2 = 1;   // mvr_set_oaf_conv2 (default on: 0.25 vs 0.30 ms per lau
 static bool oaf_conv2_covers(const GemmArgs& g) {
   return g.wimg && g.M == 128 && g.pro == PRO_A_K && g.bkc == 1 && g.sBb == 0 && g.bias_mode == BIAS_N &&
          g.stats_mode == ST_ROW && g.has_res && !g.no_store && !g.head_w && !g.xin && g.K % 4 == 0 &&
+         g.K > C2_BK && g.K <= C2_KMAX &&
          g.wimg_bytes >= oaf_conv2_image_bytes(g.N, g.K) && (reinterpret_cast<uintptr_t>(g.wimg) & 15) == 0 &&
          (int64_t)c2_nks(g.K) * c2_npad(g.N) * C2_BK * 2 * 3 < ((int64_t)1 << 31);
 }

@@ -109,7 +109,8 @@ int mvr_set_gemm_f16(int on);
  * statistics per 128-column tile as mvr_gemm_f32's stats_mode 1 (st_off 0), on the split-once kernel (gemm.hip
  * oaf_conv2_kernel: W split into an image once per launch, each A element folded and split once per workgroup,
  * 128 x 256 tiles).  img: >= mvr_oaf_conv2_image_bytes(N, K) bytes of 16-byte aligned device scratch, written by the
- * call.  Layout as mvr_gemm_f32 (K % 4 == 0).  MVR_EINVAL when the shape is not the kernel's. */
+ * call.  Layout as mvr_gemm_f32; K % 4 == 0 and 32 < K <= 512.  MVR_EINVAL when the shape is not the kernel's
+ * (mvr_oan_block_forward then runs the generic GEMM). */
 int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, int64_t lda, const float* W,
                       int64_t ldw, float* C, int64_t sCb, int64_t ldc, const float* R, int64_t sRb, const float* bias,
                       const float* psc, const float* psh, int64_t sPb, float* stats, int64_t st_ld, void* img,

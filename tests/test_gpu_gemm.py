@@ -358,14 +358,15 @@ def test_gemm_rejects_bad_layout(gpu):
 
 
 @pytest.mark.parametrize("N,K,batch,shared_fold", [(500, 500, 5, False), (500, 500, 300, True), (36, 36, 3, False),
-                                                   (300, 260, 4, False), (517, 128, 3, True), (256, 4, 2, False),
-                                                   (1, 32, 2, False), (640, 500, 300, False)])
+                                                   (300, 260, 4, False), (517, 128, 3, True), (256, 40, 2, False),
+                                                   (1, 68, 2, False), (640, 500, 300, False), (200, 512, 7, True)])
 def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
     """OAFilter conv2 on the split-once kernel (gemm.hip oaf_conv2_kernel: weight image split once per launch, the
     A slab folded and split once per workgroup, 128 x 256 tiles) against float64 and against the generic kernel:
-    ragged N (partial 256-column tiles, an empty second statistics half at N = 517 and 1), a K tail, K = 4, more
-    tiles than workgroups (batch 300: every workgroup runs several tiles across the stage ring), the eval-mode
-    fold shared by every pair (sPb = 0) and per-pair folds (train)."""
+    ragged N (partial 256-column tiles, an empty second statistics half at N = 517 and 1), K tails, two-stage
+    tiles (K = 36, 40: the next tile's fold vectors stored at once) and the largest K (512), more tiles than
+    workgroups (batch 300: every workgroup runs several tiles across the stage ring), the eval-mode fold shared
+    by every pair (sPb = 0) and per-pair folds (train)."""
     import torch
     from lib import _native as NV
     M = 128
@@ -427,5 +428,7 @@ def test_oaf_conv2_rejects_other_shapes(gpu):
                                     img_bytes, NV.stream())
     assert L.mvr_oaf_conv2_f32(*args(64, 64, nb)) == -1       # M != 128
     assert L.mvr_oaf_conv2_f32(*args(128, 66, nb)) == -1      # K % 4
+    assert L.mvr_oaf_conv2_f32(*args(128, 32, nb)) == -1      # one stage per tile
+    assert L.mvr_oaf_conv2_f32(*args(128, 516, 1 << 20)) == -1   # K > 512
     assert L.mvr_oaf_conv2_f32(*args(128, 64, nb - 16)) == -1  # image scratch too small
     torch.cuda.synchronize()
