@@ -964,6 +964,9 @@ constexpr int C2_APL = 128 * C2_BK;                  // bf16 per A plane and sta
 constexpr int C2_BPL = C2_BN * C2_BK;                // bf16 per B plane and stage (16 KB)
 constexpr int C2_SLOT = 3 * (C2_APL + C2_BPL);       // bf16 per stage slot (72 KB)
 constexpr int C2_KMAX = 512;                         // largest K (the per-tile fold vectors live in LDS)
+#ifndef C2_AISSUE
+#define C2_AISSUE 3   // MFMA slot of the first k16 step after which the next A loads issue (21: round-4 first version)
+#endif
 
 __host__ __device__ inline int c2_npad(int N) { return (N + C2_BN - 1) / C2_BN * C2_BN; }
 __host__ __device__ inline int c2_nks(int K) { return (K + C2_BK - 1) / C2_BK; }
@@ -1170,8 +1173,8 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
         for (int u = 0; u < 24; ++u) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+          if (u == C2_AISSUE) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);   // once the fold has read ra
           if (u == 20) __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
-          if (u == 21) __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
         TSTAMP(3);
