@@ -84,6 +84,34 @@ constexpr float W_SUM_MAX = 128.f;      // max sum_c |W[j][c] log2 e| of a weigh
 __device__ __forceinline__ bool v_row_bad(float rmax) { return !(rmax < F16_RANGE) || (rmax > 0.f && rmax < F16_FLOOR); }
 
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+#ifndef ATTN_TRACE
+#define ATTN_TRACE 0   // 1: per-phase cycle totals per wave (s_memtime) of the pool / 4-wave unpool kernels, tools only
+#endif
+#if ATTN_TRACE
+__device__ unsigned long long g_attn_trace[16];   // [0, 8) pool, [8, 16) unpool
+#define ATSTAMP(slot)                                                  \
+  do {                                                                 \
+    unsigned long long t_;                                             \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));  \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    tr_[prev_] += t_ - tlast_;                                         \
+    tlast_ = t_;                                                       \
+    prev_ = (slot);                                                    \
+  } while (0)
+#define ATSTART() unsigned long long tr_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast_ = __builtin_amdgcn_s_memtime(); int prev_ = 7
+#define ATEND(base)                                                                  \
+  do {                                                                               \
+    ATSTAMP(7);                                                                      \
+    if ((threadIdx.x & 63) == 0)                                                     \
+      for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&g_attn_trace[(base) + q_], tr_[q_]); \
+  } while (0)
+#else
+#define ATSTAMP(slot) do {} while (0)
+#define ATSTART() do {} while (0)
+#define ATEND(base) do {} while (0)
+#endif
 // one MFMA, then a share of the VALU and LDS writes placed in the same scheduling region, six times
 #define ATTN_INTERLEAVE6()                          \
   do {                                              \
@@ -283,6 +311,9 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     pair_block(a.nqb, p, jb);
   }
   if (p >= a.P) return;   // uniform over the workgroup
+  ATSTART();   // pool phases: 0 prologue, 1 S MFMAs (+ V split), 2 softmax + P split, 3 O MFMAs (+ K split),
+               // 4 stage-end wait + barrier, 5 split merge, 6 epilogue
+  ATSTAMP(0);
   const float* X = a.X + (int64_t)p * a.xps;
   const int N = a.N;
   const int nkb = (N + AKB - 1) / AKB;
@@ -423,6 +454,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kb = kb0; kb < kb1; ++kb) {
+    ATSTAMP(1);
     const int st = kb & 1;
     // tile kb + 1 (zeros past the end) -> stage st ^ 1, split between the MFMAs below
     const float4 x0 = load_x(kb + 1, 0);
@@ -452,6 +484,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
+    ATSTAMP(2);
     FragT<H> vf = v_frag(V, l32, 0);   // first V fragment, in flight during the softmax
     float v[16];
 #pragma unroll
@@ -463,6 +496,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     }
     online_softmax<H ? 7 : 0>(v, m, l, O);
     FragT<H> pf[2] = {split8t<H>(v), split8t<H>(v + 8)};
+    ATSTAMP(3);
     // O[c][j] += sum_n x[c][n] P[n][j]
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -479,9 +513,11 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       SCHED_FENCE();
       if (i < 7) vf = nxt;
     }
+    ATSTAMP(4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  ATSTAMP(5);
   if (H) {
     // rows: the 8 threads of a channel (tid & 7) saw all of this split's keys of it
     bool bad = wbad || !(kmax < F16_RANGE);
@@ -518,7 +554,10 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       flag[0] = tk % nks == nks - 1;
     }
     __syncthreads();
-    if (!flag[0]) return;   // uniform
+    if (!flag[0]) {   // uniform
+      ATEND(0);
+      return;
+    }
     // merge the splits in split order (whichever arrived last: the result does not depend on arrival order)
     const floatx16 own[4] = {O[0], O[1], O[2], O[3]};
     const float mown = m, lown = l;
@@ -546,11 +585,13 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       m = mn;
     }
   }
+  ATSTAMP(6);
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   const int ntile = (a.Kc + 127) / 128;
   tile_out(reinterpret_cast<float*>(smem), O, inv, jok, a.out + (int64_t)p * a.ops, a.old, jb * AQ, a.Kc,
            a.stats ? a.stats + ((int64_t)p * ntile + 2 * jb) * a.st_ld + a.st_off : nullptr, a.st_ld);
+  ATEND(0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -848,6 +889,9 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
   int p, nb;
   pair_block(a.nqb, p, nb);
   if (p >= a.P) return;   // uniform over the workgroup
+  ATSTART();   // unpool phases: 0 prologue, 1 S MFMAs, 2 softmax + split, 3 x_down wait + barrier, 4 O MFMAs,
+               // 5 barrier + DMA issue, 6 epilogue
+  ATSTAMP(0);
   const int N = a.N, nkb = a.nkb;
   const char* dimg = a.dimg + (int64_t)p * nkb * XIMG;
 
@@ -942,6 +986,7 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
   // stage kb: W(kb) landed (waited before the barrier that ended stage kb - 1 / the prologue);
   // x_down(kb) in flight
   for (int kb = 0; kb < nkb; ++kb) {
+    ATSTAMP(1);
     if (kb + 1 < nkb) issue_w(kb + 1);   // the other W buffer: last read by stage kb - 1
     const char* Wi = smem + (kb & 1) * WI4;
     const char* D = smem + XDO;
@@ -966,6 +1011,7 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
       SCHED_FENCE();
       if (ks < 7) cur = nxt;
     }
+    ATSTAMP(2);
     float v[16];
     if (H) {
 #pragma unroll
@@ -982,8 +1028,10 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
     }
     online_softmax<H ? 7 : 0>(v, m, l, O);
     FragT<H> pf[2] = {split8t<H>(v), split8t<H>(v + 8)};
+    ATSTAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // x_down(kb) (and W(kb + 1))
     __syncthreads();
+    ATSTAMP(4);
     FragT<H> df = d_frag(D, l32, 0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -995,11 +1043,13 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
       SCHED_FENCE();
       if (i < 7) df = nxt;
     }
+    ATSTAMP(5);
     __syncthreads();   // every wave is done with x_down(kb) and W(kb)
     if (kb + 1 < nkb) issue_xd(kb + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  ATSTAMP(6);
 
   // epilogue: O (rows c = 32 cb + (q & 3) + 8 (q >> 2) + 4h, column 32 w + l32) / l -> out[c][nb 128 + col]
   // through an LDS tile in two passes of 64 rows; a wave stores two rows per step (lane half h: row
@@ -1047,6 +1097,7 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
     }
     __syncthreads();
   }
+  ATEND(8);
 }
 
 #ifndef UNPOOL4_DEFAULT
@@ -1064,6 +1115,17 @@ using namespace mvr;
 
 static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 static int64_t round_up4(int64_t x) { return (x + 3) & ~(int64_t)3; }
+
+#if ATTN_TRACE
+extern "C" int mvr_attn_trace(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mvr::g_attn_trace), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mvr::g_attn_trace), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int clusters) {
   if (P <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return 0;

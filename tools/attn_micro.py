@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--clusters", type=int, default=K)
     ap.add_argument("--points", type=int, default=N)
     ap.add_argument("--math", type=int, default=-1, help="1 split-fp16, 0 split-bf16, -1 both (+ max difference)")
+    ap.add_argument("--trace", action="store_true", help="library built with -DATTN_TRACE=1 (MVR_LIB): phase shares")
     a = ap.parse_args()
     run(a, a.clusters, a.points)
 
@@ -65,6 +66,22 @@ def run(a, K, N):
             torch.cuda.synchronize()
             res[mth] = o.clone()
             time_it(a, name + "/h%d" % mth, fn, flops)
+            if a.trace:
+                import ctypes
+                L.mvr_attn_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                buf = (ctypes.c_ulonglong * 16)()
+                L.mvr_attn_trace(buf, 1)
+                fn()
+                torch.cuda.synchronize()
+                L.mvr_attn_trace(buf, 1)
+                base = 0 if name == "pool" else 8
+                names = (["prologue", "S mfma (+V split)", "softmax+P split", "O mfma (+K split)", "stage-end wait",
+                          "split merge", "epilogue", "tail"] if name == "pool" else
+                         ["prologue", "S mfma", "softmax+split", "x_down wait+barrier", "O mfma", "barrier+issue",
+                          "epilogue", "tail"])
+                tot = sum(buf[base + q] for q in range(8))
+                print("   phase shares: " + ", ".join("%s %.1f%%" % (names[q], 100.0 * buf[base + q] / max(tot, 1))
+                                                    for q in range(8)), flush=True)
         if len(res) == 2:
             d = (res[0] - res[1]).abs().max().item()
             print("%-7s max |h1 - h0| %.3e (max |out| %.3e)" % (name, d, res[0].abs().max().item()), flush=True)
