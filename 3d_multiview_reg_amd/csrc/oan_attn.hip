@@ -279,6 +279,7 @@ __device__ __forceinline__ void glds16b(const char* src, char* lds_base) {
 // (glds16s: the same from a wave-uniform base + 32-bit lane offset, common.hpp)
 
 constexpr int XT = AC * AKB * 4;   // raw fp32 key tile [128 c][32 n] (16 KB)
+constexpr int PRAW = 3;            // raw key tiles in the LDS-DMA ring: a tile's DMA has two stages to land
 template <int H> constexpr int pool_smem() {
   return 4 * planes<H>() * PLANE > 64 * ATL * 4 ? 4 * planes<H>() * PLANE : 64 * ATL * 4;
 }
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   constexpr int IMGT = NP * PLANE;         // one stage image (K or V)
   constexpr int STAGET = 2 * IMGT;         // one stage: K image, V image
   __shared__ __attribute__((aligned(16))) char smem[pool_smem<H>()];   // stage ring; epilogue tile
-  __shared__ __attribute__((aligned(16))) char xraw[2 * XT];           // LDS-DMA ring of raw key tiles
+  __shared__ __attribute__((aligned(16))) char xraw[PRAW * XT];        // LDS-DMA ring of raw key tiles
   __shared__ float2 ssh[AC];                                          // (sc, sh) of this pair
   if (a.guard) {
     if (*a.guard == 0) return;   // uniform: the fp16 launch before this one stayed in range
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   const uint32_t xld4 = (uint32_t)a.xld * 4u;
   auto dma_tile = [&](int kb) {
     const int n = min(kb * AKB + 4 * (lane & 7), nlast);
-    const uint32_t dst = xraw_lds + (uint32_t)((kb & 1) * XT);
+    const uint32_t dst = xraw_lds + (uint32_t)((kb % PRAW) * XT);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r0 = 16 * wu + 8 * i;
@@ -386,7 +387,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   // store_v / store_k write one of them to the V / K image of stage st
   auto load_x = [&](int kb, int i) {
     const int c = (tid >> 3) + 64 * i;
-    float4 x = *reinterpret_cast<const float4*>(xraw + (kb & 1) * XT + c * 128 + 16 * sq);
+    float4 x = *reinterpret_cast<const float4*>(xraw + (kb % PRAW) * XT + c * 128 + 16 * sq);
     if (kb * AKB + 4 * sq >= N) x = make_float4(0.f, 0.f, 0.f, 0.f);
     return x;
   };
@@ -440,10 +441,12 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     return ld_frag<H>(V + row * 64 + 16 * ((2 * s + h) ^ ((row >> 2) & 3)), PLANE);
   };
 
-  // ring: raw tile kb + 2 lands while stage kb & 1 is consumed and tile kb + 1 is split into the other
+  // ring: raw tile kb + 3 lands while stage kb & 1 is consumed and tile kb + 1 is split into the other (two DMA
+  // instructions per lane and tile, nothing else in flight: vmcnt(2) = all but the youngest tile)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   dma_tile(kb0 + 1);
+  dma_tile(kb0 + 2);
   {
     const float4 x0 = load_x(kb0, 0), x1 = load_x(kb0, 1);
     store_v(kb0 & 1, 0, x0);
@@ -451,7 +454,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     store_v(kb0 & 1, 1, x1);
     store_k(kb0 & 1, 1, x1, ssh[(tid >> 3) + 64]);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // tile kb0 + 1 landed, kb0 + 2 in flight
   __syncthreads();
   for (int kb = kb0; kb < kb1; ++kb) {
     ATSTAMP(1);
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
     // tile kb + 1 (zeros past the end) -> stage st ^ 1, split between the MFMAs below
     const float4 x0 = load_x(kb + 1, 0);
     float4 x1;
-    dma_tile(kb + 2);             // into the buffer of tile kb, split one iteration ago
+    dma_tile(kb + 3);             // into the buffer of tile kb, split one iteration ago
     const char* K = smem + st * STAGET;
     const char* V = K + IMGT;
     // S^T[n][j] = b[j] + sum_c xn[c][n] W[j][c] (log2 units; H = 1: times wsc), fragments one k-step ahead
@@ -514,9 +517,10 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
       if (i < 7) vf = nxt;
     }
     ATSTAMP(4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // tile kb + 2 landed, kb + 3 in flight
     __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // no tile DMA outlives the loop
   ATSTAMP(5);
   if (H) {
     // rows: the 8 threads of a channel (tid & 7) saw all of this split's keys of it
