@@ -26,6 +26,7 @@
 //     reduced with 3 swizzles, column statistics with 2 DPP moves and one cross-half shuffle.
 // Roofline: 2*M*N*K flops per GEMM against the 157.3 TF/s fp32 MFMA peak.
 #include <atomic>
+#include <type_traits>
 #include <utility>
 
 #include "common.hpp"
@@ -964,6 +965,9 @@ constexpr int C2_APL = 128 * C2_BK;                  // bf16 per A plane and sta
 constexpr int C2_BPL = C2_BN * C2_BK;                // bf16 per B plane and stage (16 KB)
 constexpr int C2_SLOT = 3 * (C2_APL + C2_BPL);       // bf16 per stage slot (72 KB)
 constexpr int C2_KMAX = 512;                         // largest K (the per-tile fold vectors live in LDS)
+#ifndef C2_RPRE
+#define C2_RPRE 0     // 1: a tile's residual loaded at the start of its last stage (64 VGPRs across that stage)
+#endif
 #ifndef C2_AISSUE
 #define C2_AISSUE 3   // MFMA slot of the first k16 step after which the next A loads issue (21: round-4 first version)
 #endif
@@ -1020,15 +1024,20 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   // A staging: thread -> row am, 8 k from 8 ac (32 bytes of fp32 per stage)
   const int am = tid >> 2, ac = tid & 3;
   const int apos = am * C2_BK + 8 * (ac ^ ((am >> 2) & 3));
-  f32x4 ra0, ra1;
-  auto issue_a = [&](int gs) {   // 2 loads
+  // A registers: two sets, stage s in set s & 1 (selected at compile time: the stage loop is unrolled by two), so a
+  // stage's loads are issued two stages before its split
+  f32x4 ra[2][2];
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto issue_a = [&](auto SET, int gs) {   // 2 loads
+    constexpr int s_ = decltype(SET)::value;
     const int t = slot + (gs / nks) * G, ks = gs % nks;
     const int b = t / ntn;
     const int k = ks * C2_BK + 8 * ac;
     const int k0 = min(k, K - 4), k1 = min(k + 4, K - 4);   // clamped into the row; zeroed past K at the fold
     const float* Ar = g.A + (int64_t)b * g.sAb + (int64_t)am * g.lda;
-    ra0 = *reinterpret_cast<const f32x4*>(Ar + k0);
-    ra1 = *reinterpret_cast<const f32x4*>(Ar + k1);
+    ra[s_][0] = *reinterpret_cast<const f32x4*>(Ar + k0);
+    ra[s_][1] = *reinterpret_cast<const f32x4*>(Ar + k1);
   };
   // the fold vectors (scale, shift per k) of this workgroup's tile i -> LDS parity i & 1: one float4 per thread
   // (2 K / 4 <= 256 threads), loaded a stage before it is stored
@@ -1042,7 +1051,9 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
   auto store_fold = [&](int i) {
     if (tid < 2 * q4) *reinterpret_cast<f32x4*>(&fsv[i & 1][tid < q4 ? 0 : 1][4 * (tid < q4 ? tid : tid - q4)]) = fv;
   };
-  auto store_a = [&](int gs, int sl) {   // fold + split the registers of stage gs into slot sl's A planes
+  auto store_a = [&](auto SET, int gs, int sl) {   // fold + split the registers of stage gs into slot sl's A planes
+    constexpr int s_ = decltype(SET)::value;
+    const f32x4 ra0 = ra[s_][0], ra1 = ra[s_][1];
     const int k = (gs % nks) * C2_BK + 8 * ac;
     const float* fs = fsv[(gs / nks) & 1][0] + k;
     const float* fh = fsv[(gs / nks) & 1][1] + k;
@@ -1096,14 +1107,17 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
 #endif
   load_fold(0);
   store_fold(0);
-  issue_a(0);
+  issue_a(I0{}, 0);
+  issue_a(I1{}, min(1, S - 1));
   __syncthreads();
-  store_a(0, 0);
+  store_a(I0{}, 0, 0);
   issue_b(0, 0);
-  issue_a(min(1, S - 1));
-  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // B(0) landed; A(1) in flight
+  issue_a(I0{}, min(2, S - 1));
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");   // B(0) (and A(1), older) landed; A(2) in flight
   float4 w[2][2][4];   // the residual of the tile's output, loaded at the start of its last stage
-  for (int gs = 0; gs < S; ++gs) {
+  // stage gs: splits A(gs + 1) from set (gs + 1) & 1 and reloads that set with A(gs + 3)
+  auto stage = [&](auto SET, const int gs) {
+    constexpr int s_ = decltype(SET)::value;
     const int ks = gs % nks, ti = gs / nks;
     const int gn = min(gs + 1, S - 1), so = (gs + 1) & 1;
     TSTAMP(0);
@@ -1119,9 +1133,9 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
       store_fold(ti + 1);
     }
     // the A registers of gs + 1 ready before the DMA is issued (a use here makes the compiler's wait precede it)
-    asm volatile("" ::"v"(ra0), "v"(ra1));
+    asm volatile("" ::"v"(ra[s_][0]), "v"(ra[s_][1]));
     issue_b(gn, so);
-    if (ks == nks - 1) {   // the tile's residual, in flight during its last stage's MFMAs
+    if (C2_RPRE && ks == nks - 1) {   // the tile's residual, in flight during its last stage's MFMAs
       const int t = slot + ti * G;
       const int b = t / ntn, nb0 = (t % ntn) * C2_BN + wn * 64;
       const float* Rb = g.R + (int64_t)b * g.sRb;
@@ -1160,13 +1174,13 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
         fb[j].m = *reinterpret_cast<const bf16x8*>(Bs + C2_BPL + o);
         fb[j].l = *reinterpret_cast<const bf16x8*>(Bs + 2 * C2_BPL + o);
       }
-      if (st == 0) store_a(gn, so);
+      if (st == 0) store_a(SET, gn, so);
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[ii][j] = bx::mfma6(fa[ii], fb[j], acc[ii][j]);
       if (st == 0) {
-        issue_a(min(gs + 2, S - 1));
+        issue_a(SET, min(gs + 3, S - 1));
         // 12 fragment reads, then the 24 MFMAs each followed by a share of the split (VALU, its 3 LDS writes)
         __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);   // (+ the 4 fold-vector reads of the split)
 #pragma unroll
@@ -1201,6 +1215,20 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
         }
       }
       float* Cb = g.C + (int64_t)b * g.sCb;
+      if (!C2_RPRE) {   // the residual loaded here (no prefetch during the last stage)
+        const float* Rb = g.R + (int64_t)b * g.sRb;
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int gm = wm * 64 + ii * 32 + 8 * q + 4 * kh + t4;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const int gnc = min(nb0 + j * 32 + 4 * p8, N4 - 4);
+              w[ii][j][q] = *reinterpret_cast<const float4*>(Rb + (int64_t)gm * g.ldc + gnc);
+            }
+          }
+      }
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
 #pragma unroll
@@ -1269,11 +1297,15 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;   // the next tile's accumulators
     }
-    // B(gs + 1) landed, A(gs + 2) (6 loads, younger) in flight.  After an epilogue its stores are outstanding too
-    // (not ordered with the loads): drain everything.
     TSTAMP(5);
+    // B(gs + 1) landed (and A(gs + 2), older), A(gs + 3) (2 loads, younger) in flight.  After an epilogue its stores
+    // are outstanding too (not ordered with the loads): drain everything.
     if (ks != nks - 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  for (int gs = 0; gs < S; gs += 2) {
+    stage(I1{}, gs);
+    if (gs + 1 < S) stage(I0{}, gs + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA outlives the workgroup
 #if GEMM_TRACE
