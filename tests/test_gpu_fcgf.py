@@ -250,3 +250,35 @@ def test_brick_kernel_map_edge_cases(gpu):
                 dx, dy, dz = k % 3 - 1, (k // 3) % 3 - 1, k // 9 - 1
                 ref[o, k] = idx[in_s].get((b, x + sg * dx, y + sg * dy, z + sg * dz), -1)
         np.testing.assert_array_equal(nb.cpu().numpy(), ref, err_msg=name)
+
+
+def test_fcgf_forward_independent_of_tiling_order(gpu, frags, monkeypatch):
+    """The sparse convs' row order only decides which rows share a tile: every output row sums its active offsets in
+    offset order whatever else its tile holds (inactive offsets add exact zeros), so FCGF's output is bit-identical
+    over the table path (mask-then-Morton order), the brick path (the same order from the brick kernel's keys), the
+    brick path with the spatial order for the s1 / strided maps (MVR_SPCONV_ORDER=spatial) and XCD-contiguous tiles."""
+    import torch
+    import lib.sparse
+    from lib import _native as NV
+    from lib.descriptor.fcgf import FCGFNet
+    from lib.sparse import voxelize, SparseTensor
+    net = FCGFNet()
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    st = synth_state(shapes, seed=4)
+    net.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in st.items()})
+    net = net.to(gpu).eval()
+    c, _, _, _ = voxelize(frags, 0.025, gpu)
+    F = torch.ones(c.shape[0], 1, device=gpu)
+    outs = []
+    L = NV.lib()
+    for bricks, order, xcd in ((False, "mask", 0), (True, "mask", 0), (True, "spatial", 0), (True, "spatial", 1)):
+        monkeypatch.setattr(lib.sparse, "BRICK_MAPS", bricks)
+        monkeypatch.setattr(lib.sparse, "SPCONV_ORDER", order)
+        prev = L.mvr_set_spconv_xcd(xcd)
+        try:
+            with torch.no_grad():
+                outs.append(net(SparseTensor(F, coords=c).to(gpu)).F.clone())
+        finally:
+            L.mvr_set_spconv_xcd(prev)
+    for i, o in enumerate(outs[1:], 1):
+        assert torch.equal(outs[0], o), (i, (outs[0] - o).abs().max().item())
