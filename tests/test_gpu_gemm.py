@@ -361,8 +361,9 @@ def test_gemm_rejects_bad_layout(gpu):
                                                    (300, 260, 4, False), (517, 128, 3, True), (256, 40, 2, False),
                                                    (1, 68, 2, False), (640, 500, 300, False), (200, 512, 7, True)])
 def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
-    """OAFilter conv2 on the split-once kernel (gemm.hip oaf_conv2_kernel: weight image split once per launch, the
-    A slab folded and split once per workgroup, 128 x 256 tiles) against float64 and against the generic kernel:
+    """OAFilter conv2 on the split-once kernels (gemm.hip oaf_conv2_kernel: weight image split once per launch, the
+    A slab folded and split once per workgroup, 128 x 256 tiles; oaf_conv2b_kernel: 128 x 128 tiles, two workgroups
+    per CU) against float64, against each other (bit-identical) and against the generic kernel:
     ragged N (partial 256-column tiles, an empty second statistics half at N = 517 and 1), K tails, two-stage
     tiles (K = 36, 40: the next tile's fold vectors stored at once) and the largest K (512), more tiles than
     workgroups (batch 300: every workgroup runs several tiles across the stage ring), the eval-mode fold shared
@@ -388,13 +389,15 @@ def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
     L = NV.lib()
     img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(N, K)) // 4 + 4, device=gpu)
     outs = []
-    for new in (True, False):
+    for new in (1, 2, 0):   # 128 x 256 tiles, 128 x 128 tiles at two workgroups per CU, the generic kernel
         C = torch.full((batch, M, N4), float("nan"), device=gpu)
         st = torch.zeros(batch, nT, M, 2, device=gpu)
         if new:
+            prev = L.mvr_set_oaf_conv2(new)
             rc = L.mvr_oaf_conv2_f32(M, N, K, batch, NV.ptr(tA), M * K4, K4, NV.ptr(tW), K4, NV.ptr(C), M * N4, N4,
                                      NV.ptr(tR), M * N4, NV.ptr(tb), NV.ptr(tsc), NV.ptr(tsh), 0 if shared_fold else K,
                                      NV.ptr(st), M, NV.ptr(img), img.numel() * 4, NV.stream())
+            L.mvr_set_oaf_conv2(prev)
         else:
             rc = L.mvr_gemm_f32(M, N, K, batch, NV.ptr(tA), M * K4, K4, NV.ptr(tW), 0, K4, 1, NV.ptr(C), M * N4, N4,
                                 NV.ptr(tR), M * N4, NV.ptr(tb), 2, NV.ptr(tsc), NV.ptr(tsh), 0 if shared_fold else K,
@@ -412,8 +415,10 @@ def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
             dev2 = ((blk - blk.mean(-1, keepdims=True)) ** 2).sum(-1)
             np.testing.assert_allclose(S[:, tt, :, 1], dev2, rtol=1e-4, atol=1e-3)
         outs.append(Cg)
-    # the two kernels differ only in the MFMA k order inside a 32-k stage
-    assert np.all(np.abs(outs[0] - outs[1]) <= 2e-6 * scale), np.max(np.abs(outs[0] - outs[1]) / scale)
+    # the split-once kernels run one MFMA k order: the same bits
+    assert np.array_equal(outs[0], outs[1])
+    # the generic kernel differs only in the MFMA k order inside a 32-k stage
+    assert np.all(np.abs(outs[0] - outs[2]) <= 2e-6 * scale), np.max(np.abs(outs[0] - outs[2]) / scale)
 
 
 def test_oaf_conv2_rejects_other_shapes(gpu):

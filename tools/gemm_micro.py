@@ -22,6 +22,7 @@ CASES = {
     "unpool": (C, N, K, 3, 0, 0, 1, 0),
     "oaf_conv2": (C, K, K, 1, 1, 2, 1, 1),    # OAFilter conv2 (oanet.hip oafilter): W2 shared, bias per n, residual
     "oaf_conv2_so": (C, K, K, 1, 1, 2, 1, 1),  # the same on the split-once kernel (mvr_oaf_conv2_f32)
+    "oaf_conv2_so2": (C, K, K, 1, 1, 2, 1, 1),  # split-once, 128 x 128 tiles at two workgroups per CU
     "conv_oaf1": (C, K, C, 2, 0, 1, 4, 0),    # OAFilter conv1 over the clusters: IN/BN/ReLU prologue, column stats
 }
 
@@ -56,7 +57,9 @@ def run(name, iters, math, pconv=1):
     st_ld = M if stats in (1, 2) else Nn
     L = NV.lib()
     L.mvr_set_pconv(pconv)
-    img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(Nn, Kk)) // 4 + 4, device=d) if name == "oaf_conv2_so" else None
+    so = name.startswith("oaf_conv2_so")
+    img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(Nn, Kk)) // 4 + 4, device=d) if so else None
+    L.mvr_set_oaf_conv2(2 if name == "oaf_conv2_so2" else 1)
 
     def go():
         if img is not None:
