@@ -1476,9 +1476,10 @@ static int launch_oaf_conv2(const GemmArgs& g, hipStream_t s) {
   hipLaunchKernelGGL(oaf_w_image_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, g.B, g.N, g.K, g.ldb,
                      Npad, nks, g.wimg);
   MVR_CHECK_LAUNCH();
-  if (g_oaf_conv2 == 2) {   // 128 x 128 tiles, two workgroups per CU
+  if (g_oaf_conv2 >= 2) {   // 128 x 128 tiles, two workgroups per CU; 3: one workgroup per tile (no persistent
+                            // grid: under another stream's kernels the tiles go to whichever CU frees up)
     const long long tiles = (long long)((g.N + C2B_BN - 1) / C2B_BN) * g.batch;
-    const unsigned wgs = (unsigned)(tiles < 512 ? tiles : 512);
+    const unsigned wgs = (unsigned)(g_oaf_conv2 == 3 || tiles < 512 ? tiles : 512);
     hipLaunchKernelGGL(oaf_conv2b_kernel, dim3(wgs), dim3(C2B_THREADS), 0, s, g, (const uint16_t*)g.wimg);
     MVR_CHECK_LAUNCH();
     return MVR_OK;
@@ -1644,7 +1645,7 @@ extern "C" size_t mvr_oaf_conv2_image_bytes(int N, int K) { return (size_t)mvr::
 
 extern "C" int mvr_set_oaf_conv2(int on) {
   const int prev = mvr::g_oaf_conv2;
-  mvr::g_oaf_conv2 = on == 2 ? 2 : (on ? 1 : 0);
+  mvr::g_oaf_conv2 = on >= 1 && on <= 3 ? on : 0;
   return prev;
 }
 

@@ -117,7 +117,10 @@ int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A, int64_t sA
                       int64_t img_bytes, mvr_stream_t stream);
 size_t mvr_oaf_conv2_image_bytes(int N, int K);
 /* Run the OANet block's OAFilter conv2 launches (mvr_oan_block_forward) on that kernel: 1 (default) the
- * split-once kernel, 0 the generic GEMM (A/B).  Process-wide; returns the previous setting. */
+ * split-once kernel, 0 the generic GEMM (A/B); 2 the split-once product on 128 x 128 tiles at two workgroups per CU
+ * (oaf_conv2b_kernel, a persistent grid of <= 512), 3 the same with one workgroup per tile.  1, 2 and 3 give the
+ * same bits.  Also selects the kernel mvr_oaf_conv2_f32 runs (1 for 0).  Process-wide; returns the previous
+ * setting. */
 int mvr_set_oaf_conv2(int on);
 /* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
  * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off

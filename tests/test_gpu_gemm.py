@@ -389,7 +389,7 @@ def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
     L = NV.lib()
     img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(N, K)) // 4 + 4, device=gpu)
     outs = []
-    for new in (1, 2, 0):   # 128 x 256 tiles, 128 x 128 tiles at two workgroups per CU, the generic kernel
+    for new in (1, 2, 3, 0):   # 128 x 256 tiles; 128 x 128 tiles, two per CU (persistent, per tile); generic
         C = torch.full((batch, M, N4), float("nan"), device=gpu)
         st = torch.zeros(batch, nT, M, 2, device=gpu)
         if new:
@@ -416,9 +416,9 @@ def test_oaf_conv2_split_once(gpu, N, K, batch, shared_fold):
             np.testing.assert_allclose(S[:, tt, :, 1], dev2, rtol=1e-4, atol=1e-3)
         outs.append(Cg)
     # the split-once kernels run one MFMA k order: the same bits
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
     # the generic kernel differs only in the MFMA k order inside a 32-k stage
-    assert np.all(np.abs(outs[0] - outs[2]) <= 2e-6 * scale), np.max(np.abs(outs[0] - outs[2]) / scale)
+    assert np.all(np.abs(outs[0] - outs[3]) <= 2e-6 * scale), np.max(np.abs(outs[0] - outs[3]) / scale)
 
 
 def test_oaf_conv2_rejects_other_shapes(gpu):

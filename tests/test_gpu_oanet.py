@@ -96,7 +96,8 @@ def test_oanet_small_golden(gpu, fx, train, ovr):
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["conv2_generic", "conv2_split_once", "conv2_split_once_2wg"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["conv2_generic", "conv2_split_once", "conv2_split_once_2wg",
+                                          "conv2_split_once_2wg_per_tile"])
 def conv2(request):
     """mvr_set_oaf_conv2: the OAFilter conv2 launches on the generic GEMM or a split-once kernel (128 x 256 tiles,
     or 128 x 128 tiles at two workgroups per CU)"""
