@@ -786,7 +786,10 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   const int ks = g.K / 16;
   // resident workgroups (2 / 1 per CU); g_pconv_grid > 1: that many contiguous group ranges per slot, dealt by the
   // dispatcher as slots free up (balances against another stream's kernels holding some CUs)
-  const int64_t slots = (ks == 8 ? 512 : 256) * (int64_t)g_pconv_grid;
+  // g_pconv_grid < 0: a persistent grid of 1 / |g_pconv_grid| of the resident slots (leaves register file for another
+  // stream's workgroups on every CU)
+  const int64_t res_slots = ks == 8 ? 512 : 256;
+  const int64_t slots = g_pconv_grid > 0 ? res_slots * g_pconv_grid : res_slots / -g_pconv_grid;
   const int grid = (int)(a.groups < slots ? a.groups : slots);
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
   const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
@@ -870,7 +873,7 @@ extern "C" int mvr_set_pconv_math(int h) {
 
 extern "C" int mvr_set_pconv_grid(int mul) {
   const int prev = mvr::g_pconv_grid;
-  mvr::g_pconv_grid = mul < 1 ? 1 : (mul > 64 ? 64 : mul);
+  mvr::g_pconv_grid = mul == -2 || mul == -4 ? mul : (mul < 1 ? 1 : (mul > 64 ? 64 : mul));
   return prev;
 }
 

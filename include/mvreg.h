@@ -127,7 +127,8 @@ int mvr_set_oaf_conv2(int on);
  * (A/B timing).  Returns the previous setting. */
 int mvr_set_pconv(int on);
 /* Point-conv launch grid (process-wide): mul (1..64, default 1) workgroups per resident slot, each a contiguous
- * range of 128-point statistics groups (1: one persistent round).  Results do not depend on it (each group's
+ * range of 128-point statistics groups (1: one persistent round); -2 / -4: a persistent grid of half / a quarter of
+ * the resident slots (register file left for another stream's workgroups).  Results do not depend on it (each group's
  * statistics come from one workgroup; the folds merge them in group order).  Returns the previous setting. */
 int mvr_set_pconv_grid(int mul);
 /* operand math of the point convs (not the output-head launches): 0 (default) split-bf16 (fp32-equivalent);

@@ -470,7 +470,7 @@ def test_pconv_grid_bit_identical(gpu, P, npts, train, fused):
     prev, prevf = L.mvr_set_pconv_grid(1), L.mvr_set_oan_fused(fused)
     outs = []
     try:
-        for m in (1, 3, 8):
+        for m in (1, 3, 8, -2, -4):
             L.mvr_set_pconv_grid(m)
             with torch.no_grad():
                 outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))

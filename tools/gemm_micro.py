@@ -28,6 +28,7 @@ CASES = {
 
 
 TRACE = False
+PGRID = 1
 
 
 def run(name, iters, math, pconv=1):
@@ -57,6 +58,7 @@ def run(name, iters, math, pconv=1):
     st_ld = M if stats in (1, 2) else Nn
     L = NV.lib()
     L.mvr_set_pconv(pconv)
+    L.mvr_set_pconv_grid(PGRID)
     so = name.startswith("oaf_conv2_so")
     img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(Nn, Kk)) // 4 + 4, device=d) if so else None
     L.mvr_set_oaf_conv2(2 if name == "oaf_conv2_so2" else 1)
@@ -127,8 +129,10 @@ if __name__ == "__main__":
     ap.add_argument("--math", default="01")
     ap.add_argument("--trace", action="store_true", help="library built with -DGEMM_TRACE=1 (MVR_LIB)")
     ap.add_argument("--pairs", type=int, default=P, help="pair batch (small batches stay in the Infinity Cache)")
+    ap.add_argument("--pconv-grid", type=int, default=1, help="mvr_set_pconv_grid")
     a = ap.parse_args()
     P = a.pairs
+    PGRID = a.pconv_grid
     TRACE = a.trace
     if TRACE:
         import ctypes
