@@ -38,6 +38,25 @@ struct SpArgs {
 
 constexpr int SP_KMAX = 32;
 
+#ifndef SP_TRACE
+#define SP_TRACE 0   // 1: spconv_bx per-phase cycle totals per wave (s_memtime), tools only (mvr_spconv_trace)
+#endif
+#if SP_TRACE
+__device__ unsigned long long g_sp_trace[8];
+#define SPSTAMP(slot)                                                  \
+  do {                                                                 \
+    unsigned long long t_;                                             \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));  \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    tr[prev_slot] += t_ - t_last;                                      \
+    t_last = t_;                                                       \
+    prev_slot = (slot);                                                \
+  } while (0)
+#else
+#define SPSTAMP(slot) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // The gather-GEMM on v_mfma_f32_32x32x16_bf16 with both operands as three bf16 terms (fp32-level accuracy, see
 // mfma_bf16.hpp) — 2.7x the fp32 MFMA rate.
@@ -80,12 +99,16 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   if (a.guard && *a.guard != a.epoch) return;   // uniform: the split-fp16 launch stayed in range
   __shared__ __attribute__((aligned(16))) uint16_t Bs[2][NPL * BPL];
   __shared__ int32_t nb[TM][SP_KMAX + 1];
-  __shared__ int kact[SP_KMAX];
   __shared__ int klist[SP_KMAX];
-  __shared__ int nk;
+  __shared__ int orow_s[TM];     // the tile's output rows (perm applied; -1 past Mout)
+  __shared__ unsigned wmask[4];  // per-wave OR of the rows' active-offset masks
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, h = lane >> 5;
+#if SP_TRACE   // phases: 0 tile setup, 1 weight store (+ wait), 2 A split, 3 gather issue, 4 MFMAs, 5 barrier, 6 epilogue
+  unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime();
+  int prev_slot = 0;
+#endif
   // 1-D grid of (row tile, column tile) in XCD-contiguous order: the column tiles of a row tile (same gathered
   // rows) and neighbouring row tiles (spatially close in the kernel map's row order) share an XCD's L2
   const int gy = (a.Cout + TN - 1) / TN;
@@ -94,26 +117,50 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   const int c0 = (int)(t % gy) * TN;
   const int K = a.K;
 
-  if (tid < SP_KMAX) kact[tid] = 0;
+  // tile setup in two dependent rounds of loads (the rows' perm entries, then every neighbour entry of the tile at
+  // once, coalesced along the rows of the map) instead of one round per 256 entries
+  if (tid < TM) {
+    const int64_t o = o0 + tid;
+    orow_s[tid] = o < a.Mout ? (int)(a.perm ? a.perm[o] : o) : -1;
+  }
   __syncthreads();
-  for (int e = tid; e < TM * K; e += 256) {
-    const int row = e / K, k = e - row * K;
-    const int64_t o = o0 + row;
-    int v = -1;
-    if (o < a.Mout) {
-      const int64_t orow = a.perm ? a.perm[o] : o;
-      v = a.nbr ? a.nbr[orow * K + k] : (int)orow;
+  {
+    constexpr int EMAX = (TM * SP_KMAX + 255) / 256;
+    const int dq = 256 / K, dr = 256 - dq * K;   // entry e + 256 = (row + dq, k + dr), carried
+    int row = tid / K, k = tid - row * K;
+    int vv[EMAX], ks[EMAX], rs[EMAX];
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      ks[i] = k;
+      rs[i] = row;
+      vv[i] = -1;
+      if (row < TM) {
+        const int orow = orow_s[row];
+        if (orow >= 0) vv[i] = a.nbr ? a.nbr[(int64_t)orow * K + k] : orow;
+      }
+      row += dq;
+      k += dr;
+      if (k >= K) {
+        k -= K;
+        ++row;
+      }
     }
-    nb[row][k] = v;
-    if (v >= 0) kact[k] = 1;
+    unsigned m = 0;
+#pragma unroll
+    for (int i = 0; i < EMAX; ++i) {
+      if (rs[i] < TM) {
+        nb[rs[i]][ks[i]] = vv[i];
+        if (vv[i] >= 0) m |= 1u << ks[i];
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m |= (unsigned)__shfl_xor((int)m, off, 64);
+    if (lane == 0) wmask[w] = m;
   }
   __syncthreads();
-  if (tid == 0) {
-    int n = 0;
-    for (int k = 0; k < K; ++k)
-      if (kact[k]) klist[n++] = k;
-    nk = n;
-  }
+  const unsigned kmask = wmask[0] | wmask[1] | wmask[2] | wmask[3];
+  if (tid < K && ((kmask >> tid) & 1u)) klist[__popc(kmask & ((1u << tid) - 1u))] = tid;
+  const int nk = __popc(kmask);
   __syncthreads();
 
   const int nci = (a.Cin + SB_K - 1) / SB_K;
@@ -191,15 +238,20 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     // step s: the weights of step s + 1 (loaded NS steps ago) -> the other LDS stage, the split of step s's
     // gathered rows, its set refilled with step s + NS, the MFMAs; one barrier
     ASet A[NS];
+    SPSTAMP(7);
 #pragma unroll
     for (int u = 0; u < NS; ++u) load_a(u, A[u]);
     store_b(A[0], 0);
     __syncthreads();
     auto step = [&](int s, ASet& A, const ASet& An) {
       const int cur = s & 1;
+      SPSTAMP(1);
       if (s + 1 < steps) store_b(An, cur ^ 1);
+      SPSTAMP(2);
       const FragT<H> fa0 = frag_a(A, 0), fa1 = frag_a(A, 1);
+      SPSTAMP(3);
       load_a(s + NS, A);
+      SPSTAMP(4);
       const uint16_t* Bq = Bs[cur];
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
@@ -211,6 +263,7 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
           acc[j] = mma<H>(fa, fb, acc[j]);
         }
       }
+      SPSTAMP(5);
       __syncthreads();
     };
     int s = 0;
@@ -223,6 +276,11 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
       if (s + u < steps) step(s + u, A[u], A[(u + 1) % NS]);
   }
 
+  SPSTAMP(6);
+  // epilogue: the rows from LDS, every residual of a column tile loaded before its stores (out may be res)
+  int orr[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) orr[r] = orow_s[32 * w + (r & 3) + 8 * (r >> 2) + 4 * h];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int c = c0 + j * 32 + l32;
@@ -234,19 +292,25 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     }
     const float bias = a.bias ? a.bias[c] : 0.f;
     const float is = H ? isc[c] : 1.f;
+    float rv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rv[r] = a.res && orr[r] >= 0 ? a.res[(int64_t)orr[r] * a.ldres + c] : 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t ot = o0 + 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
-      if (ot >= a.Mout) continue;
-      const int64_t o = a.perm ? a.perm[ot] : ot;
+      if (orr[r] < 0) continue;
       float v = (H ? acc[j][r] * is : acc[j][r]) + bias;
       v = fmaf(v, bsc, bsh);
-      if (a.res) v += a.res[o * a.ldres + c];
+      if (a.res) v += rv[r];
       if (a.relu) v = fmaxf(v, 0.f);
-      a.out[o * a.ldout + c] = v;
+      a.out[(int64_t)orr[r] * a.ldout + c] = v;
     }
   }
   if (H && __any(xbad || (xmx > 0.f && xmx < 0.125f)) && lane == 0) atomicExch(a.range, a.epoch);
+#if SP_TRACE
+  SPSTAMP(0);
+  if (lane == 0)
+    for (int q = 0; q < 8; ++q) atomicAdd(&g_sp_trace[q], tr[q]);
+#endif
 }
 
 // per output channel c: s_c = range_scale(max_{k, ci} |W[k][ci][c]|) -> wsc[c], isc[c] = 1 / (s_c 2^6); one wave
@@ -413,3 +477,15 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }
+
+#if SP_TRACE
+// tools only (library built with -DSP_TRACE=1): the phase totals of every spconv_bx wave since the last reset
+extern "C" int mvr_spconv_trace(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mvr::g_sp_trace), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mvr::g_sp_trace), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--order", default=None, help="run only this row order (e.g. mask+morton)")
     ap.add_argument("--xcd", type=int, default=None, help="run only this xcd setting (0/1)")
+    ap.add_argument("--trace", action="store_true", help="library built with -DSP_TRACE=1 (MVR_LIB): phase shares")
     a = ap.parse_args()
     from synth import synth_scene_fragments
     from lib.sparse import voxelize, CoordinateManager
@@ -90,6 +91,19 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res["%s/x%d" % (oname, xcd)] = e0.elapsed_time(e1) / a.iters
+                if a.trace:
+                    import ctypes
+                    buf = (ctypes.c_ulonglong * 8)()
+                    L.mvr_spconv_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+                    L.mvr_spconv_trace(buf, 1)
+                    go()
+                    torch.cuda.synchronize()
+                    L.mvr_spconv_trace(buf, 1)
+                    tot = max(sum(buf), 1)
+                    names = ["setup", "w-store(+wait)", "A split", "gather issue", "mfma", "barrier", "epilogue",
+                             "prologue"]
+                    print("   %s phase shares: %s" % (tag, ", ".join("%s %.1f%%" % (names[q], 100.0 * buf[q] / tot)
+                                                                     for q in range(8))), flush=True)
         L.mvr_set_spconv_xcd(0)
         fl = 2.0 * act * cin * cout
         print("%-16s Mout %7d active/row %.1f  %s   (useful TF/s at best %.1f)" % (
