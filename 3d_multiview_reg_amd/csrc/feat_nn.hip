@@ -63,7 +63,7 @@ struct NNArgs {
 // per target — so that a stage is two LDS-DMA copies instead of loads, splits and LDS stores in every workgroup
 // (each target fragment is staged by 40 query blocks x 29 pairs).
 constexpr int NN_IMG_PLANES = 3 * NN_STAGE * NN_ROW * 2;   // 24 KB
-constexpr int NN_IMG_STAGE = NN_IMG_PLANES + NN_STAGE * 16; // + 2 KB of (x, y, z, w)
+constexpr int NN_IMG_STAGE = NN_IMG_PLANES + NN_STAGE * 16 + NN_STAGE * 4;   // + 2 KB of (x, y, z, w hm) + 512 B of w l
 
 __device__ __forceinline__ unsigned nn_cvt_pk(f32x2 x) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf16x2));
@@ -99,6 +99,23 @@ __device__ __forceinline__ void nn_split8h(const float4& a, const float4& b, u32
     L[i] = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(hh, f32x2), f16x2));
   }
 }
+// The split-bf16 fast path folds the target term -k2 |ft|^2 of the logit into the distance MFMAs (one more MFMA per
+// 32-target chunk against a constant operand of ones, instead of one fma per (query, target)): -w as three bf16
+// terms, (h | m << 16) in the .w slot of the target's (x, y, z, .) entry and l in a second word.  Invalid targets
+// (past Mt): h = -inf, m = l = 0 (weight 0).
+__device__ __forceinline__ void nn_wsplit(float w, bool ok, unsigned& hm, unsigned& l) {
+  if (!ok) {
+    hm = 0xFF80u;   // bf16 -inf
+    l = 0u;
+    return;
+  }
+  const float v = -w;
+  const unsigned hp = nn_cvt_pk((f32x2){v, 0.f}) & 0xFFFFu;
+  const float r = v - __uint_as_float(hp << 16);
+  const unsigned mp = nn_cvt_pk((f32x2){r, 0.f}) & 0xFFFFu;
+  hm = hp | (mp << 16);
+  l = nn_cvt_pk((f32x2){r - __uint_as_float(mp << 16), 0.f}) & 0xFFFFu;
+}
 __device__ __forceinline__ float nn_max3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 // |f|^2 over a stage thread's 16 dims in one fixed fma order (the stage split and the pre-split image share it:
 // identical stages)
@@ -118,8 +135,9 @@ struct NNSmem {
   unsigned short Fp[2][3][NN_STAGE][NN_ROW];   // bf16 planes h, m, l of the target features
   union {
     float Xs[2][4][NN_STAGE];                  // online path: x, y, z, |ft|^2 k2 (SoA)
-    float4 Xf[2][NN_STAGE];                    // fast path: (x, y, z, |ft|^2 k2) per target
-  };
+    float4 Xf[2][NN_STAGE];                    // fast path: (x, y, z, |ft|^2 k2) per target (split-bf16: .w = hm
+  };                                           // bits of nn_wsplit)
+  unsigned Wl[2][NN_STAGE];                    // split-bf16 fast path: the l term of nn_wsplit
   int flag;
 };
 
@@ -416,8 +434,11 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
         nn_split8h(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], Hh, L);
         q16h[s] = __builtin_bit_cast(f16x8, Hh);
         q16l[s] = __builtin_bit_cast(f16x8, L);
-      } else {
-        nn_split8(qp[4 * s + 2 * kh], qp[4 * s + 2 * kh + 1], Hh, Mm, L);
+      } else {   // the logit's scale 2 k2 folded into the query operand
+        const float kq = 2.f * a.k2;
+        const float4 u0 = qp[4 * s + 2 * kh], u1 = qp[4 * s + 2 * kh + 1];
+        nn_split8(make_float4(u0.x * kq, u0.y * kq, u0.z * kq, u0.w * kq),
+                  make_float4(u1.x * kq, u1.y * kq, u1.z * kq, u1.w * kq), Hh, Mm, L);
         qh[s] = __builtin_bit_cast(bf16x8, Hh);
         qm[s] = __builtin_bit_cast(bf16x8, Mm);
         ql[s] = __builtin_bit_cast(bf16x8, L);
@@ -426,10 +447,15 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   }
   constexpr float ACC_UNIT = H ? 65536.f : 1.f;   // accumulator units (2^8 x 2^8 with H = 1)
   bool bad = H && !(q2 < 16384.f);                 // H = 1 range (NaN included)
-  // accumulator register r holds query row 8 (r >> 2) + 4 kh + (r & 3): its start value -|fs|^2 / 2
+  // accumulator register r holds query row 8 (r >> 2) + 4 kh + (r & 3): its start value -|fs|^2 / 2 (H = 1), or
+  // -k2 |fs|^2 (split-bf16: the accumulator is the logit itself, 2 k2 fs.ft - k2 |fs|^2 - k2 |ft|^2, the last term
+  // from the ones MFMA below)
   floatx16 init;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) init[r] = -0.5f * ACC_UNIT * __shfl(q2, 8 * (r >> 2) + 4 * kh + (r & 3), 64);
+  for (int r = 0; r < 16; ++r)
+    init[r] = (H ? -0.5f * ACC_UNIT : -a.k2) * __shfl(q2, 8 * (r >> 2) + 4 * kh + (r & 3), 64);
+  // the ones operand: k-slots 0, 1 of the low lane half and slot 8 of the high one (the target's h, m | l words)
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, (u32x4){kh ? 0x3F80u : 0x3F803F80u, 0u, 0u, 0u});
 
   const int srow = tid / NN_TPR, spart = tid % NN_TPR;
   float4 fr[NN_FPT / 4];
@@ -474,7 +500,16 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       Xf[buf][tid].z = xr2;
     }
     // invalid targets: +inf -> logit -inf -> weight 0 (their coordinates stay finite)
-    if (spart == 0) Xf[buf][srow].w = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
+    if (spart == 0) {
+      if (H) {
+        Xf[buf][srow].w = (t0 + srow < Mt) ? n2 * a.k2 : __builtin_inff();
+      } else {
+        unsigned hm, wl;
+        nn_wsplit(n2 * a.k2, t0 + srow < Mt, hm, wl);
+        Xf[buf][srow].w = __uint_as_float(hm);
+        sm.Wl[buf][srow] = wl;
+      }
+    }
   };
 
   // pre-split image: stage st -> buffer buf by LDS-DMA (each wave copies its 1 KB slices; completion awaited before
@@ -490,6 +525,9 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
       glds16s(src, (uint32_t)(i * 4096 + wu * 1024 + lane * 16), fp + (uint32_t)(i * 4096 + wu * 1024));
     if (wu < NN_STAGE * 16 / 1024)
       glds16s(src, (uint32_t)(NN_IMG_PLANES + wu * 1024 + lane * 16), xf + (uint32_t)(wu * 1024));
+    static_assert(NN_STAGE * 4 == 512 && NN_STAGE * 16 / 1024 == 2, "the w l words: half a DMA of wave 2");
+    if (wu == 2 && lane < 32)
+      glds16s(src, (uint32_t)(NN_IMG_PLANES + NN_STAGE * 16 + lane * 16), lds_addr(&sm.Wl[buf][0]));
   };
 
   float S[16], AX[16], AY[16], AZ[16];
@@ -509,6 +547,11 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
   auto mfma_chunk = [&](int i0) {
     floatx16 acc = init;
     const int row = i0 + l32;
+    if (!H) {   // -k2 |ft|^2 of target row (h + m in the low lane half, l in the high one)
+      const unsigned wv = kh ? sm.Wl[cur][row] : __float_as_uint(Xf[cur][row].w);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, __builtin_bit_cast(bf16x8, (u32x4){wv, 0u, 0u, 0u}), acc, 0,
+                                                    0, 0);
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int c = 8 * ((2 * s + kh) ^ ((row >> 2) & 3));
@@ -537,7 +580,7 @@ __device__ __forceinline__ bool feat_nn_fast(const NNArgs& a, NNSmem& sm) {
     const float4 X = Xf[cur][i0 + l32];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float pw = __builtin_amdgcn_exp2f(fmaf(acc[r], kk2, -X.w));
+      const float pw = __builtin_amdgcn_exp2f(H ? fmaf(acc[r], kk2, -X.w) : acc[r]);
       S[r] += pw;
       AX[r] = fmaf(pw, X.x, AX[r]);
       AY[r] = fmaf(pw, X.y, AY[r]);
@@ -637,12 +680,15 @@ __global__ void nn_presplit_kernel(const float* __restrict__ Ft, int64_t ft_fs, 
   float n2 = nn_norm16(fr);
   n2 += __shfl_xor(n2, 1, 64);
   if (in && spart == 0) {
-    float4 x = make_float4(0.f, 0.f, 0.f, __builtin_inff());
+    unsigned hm, wl;
+    nn_wsplit(n2 * k2, ok, hm, wl);
+    float4 x = make_float4(0.f, 0.f, 0.f, __uint_as_float(hm));
     if (ok) {
       const float* xp = Xt + f * xt_fs + (int64_t)r * 3;
-      x = make_float4(xp[0], xp[1], xp[2], n2 * k2);
+      x = make_float4(xp[0], xp[1], xp[2], __uint_as_float(hm));
     }
     *reinterpret_cast<float4*>(base + NN_IMG_PLANES + srow * 16) = x;
+    *reinterpret_cast<unsigned*>(base + NN_IMG_PLANES + NN_STAGE * 16 + srow * 4) = wl;
   }
 }
 
