@@ -1460,6 +1460,7 @@ __global__ __launch_bounds__(C2B_THREADS, 2) void oaf_conv2b_kernel(GemmArgs g, 
   }
 }
 
+int g_cu_budget = 256;   // mvr_set_cu_budget: CUs the persistent grids are sized for
 int g_oaf_conv2 = 1;   // mvr_set_oaf_conv2 (default on: 0.25 vs 0.30 ms per launch, oafilter 2.08 vs 2.38 ms per step)
 
 static bool oaf_conv2_covers(const GemmArgs& g) {
@@ -1479,13 +1480,13 @@ static int launch_oaf_conv2(const GemmArgs& g, hipStream_t s) {
   if (g_oaf_conv2 >= 2) {   // 128 x 128 tiles, two workgroups per CU; 3: one workgroup per tile (no persistent
                             // grid: under another stream's kernels the tiles go to whichever CU frees up)
     const long long tiles = (long long)((g.N + C2B_BN - 1) / C2B_BN) * g.batch;
-    const unsigned wgs = (unsigned)(g_oaf_conv2 == 3 || tiles < 512 ? tiles : 512);
+    const unsigned wgs = (unsigned)(g_oaf_conv2 == 3 || tiles < 2 * g_cu_budget ? tiles : 2 * g_cu_budget);
     hipLaunchKernelGGL(oaf_conv2b_kernel, dim3(wgs), dim3(C2B_THREADS), 0, s, g, (const uint16_t*)g.wimg);
     MVR_CHECK_LAUNCH();
     return MVR_OK;
   }
   const long long tiles = (long long)(Npad / C2_BN) * g.batch;
-  const unsigned wgs = (unsigned)(tiles < 256 ? tiles : 256);   // one 144-KB-LDS workgroup per CU
+  const unsigned wgs = (unsigned)(tiles < g_cu_budget ? tiles : g_cu_budget);   // one 144-KB-LDS workgroup per CU
   hipLaunchKernelGGL(oaf_conv2_kernel, dim3(wgs), dim3(C2_THREADS), 0, s, g, (const uint16_t*)g.wimg);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
@@ -1540,7 +1541,7 @@ static int launch_gemm_impl(const GemmArgs& g, hipStream_t s, bool conv2) {
   if (!ok) return MVR_EINVAL;
   KArgs ka{};
   ka.g = g;
-  ka.persist = 2 * 256;  // 2 workgroups per CU (LDS-bound), 256 CUs
+  ka.persist = 2 * g_cu_budget;  // 2 workgroups per CU (LDS-bound), 256 CUs unless mvr_set_cu_budget
   ka.m_fast = (g.sAb == 0 && gemm_mtiles(g.M) > 1) ? 1 : 0;
   const long long tiles = (long long)gemm_ntiles(g.N) * gemm_mtiles(g.M) * g.batch;
   if (tiles > 0x7fffffffLL) return MVR_EINVAL;
@@ -1642,6 +1643,12 @@ extern "C" int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A,
 }
 
 extern "C" size_t mvr_oaf_conv2_image_bytes(int N, int K) { return (size_t)mvr::oaf_conv2_image_bytes(N, K); }
+
+extern "C" int mvr_set_cu_budget(int n) {
+  const int prev = mvr::g_cu_budget;
+  mvr::g_cu_budget = n < 8 ? 8 : (n > 256 ? 256 : n);
+  return prev;
+}
 
 extern "C" int mvr_set_oaf_conv2(int on) {
   const int prev = mvr::g_oaf_conv2;

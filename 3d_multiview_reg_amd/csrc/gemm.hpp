@@ -100,6 +100,7 @@ int launch_pconv(const GemmArgs& g, hipStream_t stream);
 
 // bytes of the weights' split-bf16 image the OAFilter conv2 kernel reads (GemmArgs.wimg)
 int64_t oaf_conv2_image_bytes(int N, int K);
+extern int g_cu_budget;     // mvr_set_cu_budget
 extern int g_oaf_conv2;      // mvr_set_oaf_conv2
 
 inline int gemm_ntiles(int N){ return (N + GEMM_BN - 1) / GEMM_BN; }

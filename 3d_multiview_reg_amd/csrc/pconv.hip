@@ -788,7 +788,7 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   // dispatcher as slots free up (balances against another stream's kernels holding some CUs)
   // g_pconv_grid < 0: a persistent grid of 1 / |g_pconv_grid| of the resident slots (leaves register file for another
   // stream's workgroups on every CU)
-  const int64_t res_slots = ks == 8 ? 512 : 256;
+  const int64_t res_slots = (ks == 8 ? 2 : 1) * (int64_t)g_cu_budget;
   const int64_t slots = g_pconv_grid > 0 ? res_slots * g_pconv_grid : res_slots / -g_pconv_grid;
   const int grid = (int)(a.groups < slots ? a.groups : slots);
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;

@@ -131,6 +131,10 @@ int mvr_set_pconv(int on);
  * the resident slots (register file left for another stream's workgroups).  Results do not depend on it (each group's
  * statistics come from one workgroup; the folds merge them in group order).  Returns the previous setting. */
 int mvr_set_pconv_grid(int mul);
+/* CUs the persistent grids (point convs, the OAFilter conv2 kernels, the generic GEMM) are sized for: n (8..256,
+ * default 256, all of an MI355X).  For a caller that confines the launching stream to a CU mask of n CUs, so that a
+ * persistent grid stays one round.  Results do not depend on it.  Process-wide; returns the previous setting. */
+int mvr_set_cu_budget(int n);
 /* operand math of the point convs (not the output-head launches): 0 (default) split-bf16 (fp32-equivalent);
    1 split-fp16 for launches that have a range flag (see mvr_set_gemm_f16): 3 MFMAs per product, weight rows
    range-scaled, activations x 2^6 after the prologue and range-checked, with a guarded split-bf16 re-run of a
