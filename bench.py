@@ -573,8 +573,8 @@ def golden_accuracy(dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default=os.environ.get("MVR_BENCH_WORKLOAD", "scene"),
                     choices=["scene", "precomputed"])
     ap.add_argument("--pairs", type=int, default=435)
