@@ -371,6 +371,7 @@ __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin
 #endif
 int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_spconv_math
 int g_spconv_xcd = 0;                   // mvr_set_spconv_xcd (0: load-balanced round robin measured faster)
+int g_spconv_narrow = 0;                // mvr_set_spconv_narrow: below this many output rows, 64-channel column tiles
 
 }  // namespace mvr
 
@@ -387,6 +388,12 @@ static size_t sp_f16_bytes(int K, int Cin, int Cout) { return sp_bf16_bytes(K, C
 extern "C" size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout) {
   if (K <= 0 || Cin <= 0 || Cout <= 0) return 0;
   return sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout) + 2 * sp_coutp(Cout) * sizeof(float);
+}
+
+extern "C" int mvr_set_spconv_narrow(int rows) {
+  const int prev = g_spconv_narrow;
+  g_spconv_narrow = rows < 0 ? 0 : rows;
+  return prev;
 }
 
 extern "C" int mvr_set_spconv_xcd(int on) {
@@ -467,10 +474,12 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
     }                                                                                                          \
     hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc);   \
   } while (0)
+  // (a level with few row tiles, fewer than the GPU's workgroup slots: 64-channel column tiles, twice the workgroups
+  // of 128-channel ones, each regathering the tile's rows)
   if (Cout <= 32)
     MVR_SPL(32, SPBX_NS32, 1);
-  else if (Cout <= 64)
-    MVR_SPL(64, SPBX_NS64, 1);
+  else if (Cout <= 64 || Mout < g_spconv_narrow)
+    MVR_SPL(64, SPBX_NS64, (Cout + 63) / 64);
   else
     MVR_SPL(128, SPBX_NS128, (Cout + 127) / 128);
 #undef MVR_SPL

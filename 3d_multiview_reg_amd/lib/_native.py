@@ -64,6 +64,7 @@ _SIGS = {
     "mvr_set_pconv": (c_int, [c_int]),
     "mvr_set_pconv_grid": (c_int, [c_int]),
     "mvr_set_cu_budget": (c_int, [c_int]),
+    "mvr_set_spconv_narrow": (c_int, [c_int]),
     "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
     "mvr_set_oan_fused": (c_int, [c_int]),

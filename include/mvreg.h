@@ -462,6 +462,10 @@ int mvr_set_spconv_math(int h);
    transposed convs, whose mask-sorted tiles differ in cost — one XCD gets all the expensive ones; A/B timing).
    Returns the previous setting. */
 int mvr_set_spconv_xcd(int on);
+/* Sparse convs with fewer than `rows` output rows (default 0: none) and more than 64 output channels run on
+ * 64-channel column tiles (twice the workgroups of the 128-channel tiles; results do not depend on it).  Process-wide;
+ * returns the previous setting. */
+int mvr_set_spconv_narrow(int rows);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below and of mvr_kernel_map_bricks.  Workspace:
  * mvr_brick_map_bytes(M).  _stride: a set at tensor stride `stride` (a power of two, coordinates multiples of it):

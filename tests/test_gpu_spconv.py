@@ -127,3 +127,19 @@ def test_spconv_fp16_window(gpu, edit, inplace):
     finally:
         L.mvr_set_spconv_math(prev)
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 128), (128, 256), (256, 128)])
+def test_spconv_narrow_tiles_bit_identical(gpu, cin, cout, smath):
+    """mvr_set_spconv_narrow: a small level's convs with more than 64 output channels on 64-channel column tiles
+    (twice the workgroups) — each output column's reduction runs in the same order, so the bits do not change"""
+    from lib import _native as NV
+    L = NV.lib()
+    prev = L.mvr_set_spconv_narrow(0)
+    try:
+        wide = _run(gpu, cin, cout, 27, 1000, 900, perm=True, seed=cin + cout, raw=True)
+        L.mvr_set_spconv_narrow(1 << 30)
+        narrow = _run(gpu, cin, cout, 27, 1000, 900, perm=True, seed=cin + cout, raw=True)
+    finally:
+        L.mvr_set_spconv_narrow(prev)
+    assert np.array_equal(wide, narrow)

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--order", default=None, help="run only this row order (e.g. mask+morton)")
     ap.add_argument("--xcd", type=int, default=None, help="run only this xcd setting (0/1)")
+    ap.add_argument("--narrow", type=int, default=None, help="mvr_set_spconv_narrow(rows)")
     ap.add_argument("--trace", action="store_true", help="library built with -DSP_TRACE=1 (MVR_LIB): phase shares")
     a = ap.parse_args()
     from synth import synth_scene_fragments
@@ -34,6 +35,8 @@ def main():
     c, _, counts, _ = voxelize([torch.from_numpy(f).to(dev) for f in frags], 0.025, dev)
     cm = CoordinateManager(c, len(frags))
     L = NV.lib()
+    if a.narrow is not None:
+        L.mvr_set_spconv_narrow(a.narrow)
     g = torch.Generator(device=dev).manual_seed(0)
     for kind, s, cin, cout in CASES:
         tag = "%s:%d:%d:%d" % (kind, s, cin, cout)
