@@ -37,6 +37,7 @@ struct SpArgs {
 };
 
 constexpr int SP_KMAX = 32;
+__device__ __attribute__((aligned(16))) float g_sp_zero[4];   // what an absent neighbour gathers
 
 #ifndef SP_TRACE
 #define SP_TRACE 0   // 1: spconv_bx per-phase cycle totals per wave (s_memtime), tools only (mvr_spconv_trace)
@@ -172,7 +173,6 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   typedef float f32x4 __attribute__((ext_vector_type(4)));   // (a HIP float4 copy becomes a memcpy through scratch)
   struct ASet {
     float4 v[4];
-    uint32_t m;
     f32x4 bq[GPT];   // the step's weight stage granules (this thread's share)
   };
   auto load_a = [&](int s, ASet& A) {
@@ -181,14 +181,12 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     const int ci0 = (s % nci) * SB_K;
     const int src = nb[row][k];
     const float* base = a.in + (int64_t)(src >= 0 ? src : 0) * a.ldin;
-    uint32_t m = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 4; ++q) {   // an absent neighbour reads zeros (no masking at the split; Cin % 32 == 0)
       const int ci = ci0 + 16 * (q >> 1) + 8 * h + 4 * (q & 1);
-      m |= (src >= 0 && ci < a.Cin) ? (1u << q) : 0u;
-      A.v[q] = *reinterpret_cast<const float4*>(base + min(ci, a.Cin - 4));
+      const float* pq = src >= 0 ? base + ci : g_sp_zero;
+      A.v[q] = *reinterpret_cast<const float4*>(pq);
     }
-    A.m = m;
     const int cb = s % nci;
     const char* wb = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * NPL * CoutP + c0) * SB_BST * 2;
 #pragma unroll
@@ -203,9 +201,8 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   auto frag_a = [&](const ASet& A, int st) {
     float v[8];
     const float4 x0 = A.v[2 * st], x1 = A.v[2 * st + 1];
-    const bool k0 = (A.m >> (2 * st)) & 1, k1 = (A.m >> (2 * st + 1)) & 1;
-    v[0] = k0 ? x0.x : 0.f; v[1] = k0 ? x0.y : 0.f; v[2] = k0 ? x0.z : 0.f; v[3] = k0 ? x0.w : 0.f;
-    v[4] = k1 ? x1.x : 0.f; v[5] = k1 ? x1.y : 0.f; v[6] = k1 ? x1.z : 0.f; v[7] = k1 ? x1.w : 0.f;
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+    v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
     if (H) {
       float mx = 0.f;
 #pragma unroll
@@ -434,7 +431,7 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
   if (!in || !W || !out || !wimg || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
   if (reinterpret_cast<uintptr_t>(wimg) & 15) return MVR_EINVAL;
   if (!nbr && K != 1) return MVR_EINVAL;
-  if ((Cin & 3) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
+  if ((Cin % SB_K) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
       (reinterpret_cast<uintptr_t>(W) & 15))
     return MVR_EINVAL;
   if (Mout == 0) return MVR_OK;

@@ -436,8 +436,9 @@ int mvr_set_spconv_order(int mode);
  * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
  * perm (optional): order in which output rows are tiled (mvr_kernel_map_order); results are
  * written to their own rows either way.
- * wimg (optional, 16-byte aligned): the weights pre-split by mvr_spconv_wimage -> split-bf16 MFMA path
- * (fp32-level accuracy, ~2.7x the exact-fp32 MFMA rate); NULL -> exact fp32 MFMA on W.
+ * wimg (required, 16-byte aligned): the weights pre-split by mvr_spconv_wimage -> split-bf16 MFMA path
+ * (fp32-level accuracy, ~2.7x the exact-fp32 MFMA rate).  Cin a multiple of 32 (every FCGF conv), Cout and ldin
+ * multiples of 4, in and W 16-byte aligned; MVR_EINVAL otherwise.
  * range_flag (optional, device int32 owned by the stream's call sequence): enables the split-fp16 pass when
  * mvr_set_spconv_math(1) (the flag is cleared by the call, set by a split-fp16 pass whose operands left the fp16
  * window, and read by its guarded split-bf16 re-run); NULL -> split-bf16 only.  out is either disjoint from res

@@ -103,6 +103,21 @@ def test_spconv_requires_weight_image(gpu):
     assert rc == -1
 
 
+def test_spconv_rejects_channel_tail(gpu):
+    """input channels come in whole 32-channel steps (an absent neighbour gathers a zero vector instead of masking
+    each value): Cin % 32 != 0 is refused"""
+    import torch
+    from lib import _native as NV
+    L = NV.lib()
+    x = torch.zeros(8, 36, device=gpu)
+    W = torch.zeros(1, 36, 32, device=gpu)
+    nb = int(L.mvr_spconv_wimage_bytes(1, 36, 32))
+    wimg = torch.zeros(nb, dtype=torch.uint8, device=gpu)
+    rc = L.mvr_spconv(NV.ptr(x), 36, 36, None, None, 1, 8, NV.ptr(W), 32, None, NV.BnP(None, None, None, None),
+                      1e-5, None, 0, 0, NV.ptr(x), 32, NV.ptr(wimg), None, NV.stream())
+    assert rc == -1
+
+
 def _big_feat(f):
     f[17, 5] = 2.0e3      # x 2^6 past 65504
 
