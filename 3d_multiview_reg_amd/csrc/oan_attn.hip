@@ -951,8 +951,12 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
   float xmax = 0.f;
 #pragma unroll
   for (int qt = 0; qt < 4; ++qt) {
-    if (qt < 3) qdma(qt + 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the W(0) DMAs are older: waited with them)
+    if (qt < 3) {   // (the W(0) DMAs are older: waited with quarter 0)
+      qdma(qt + 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // all but quarter qt + 1 landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     const float* xt = reinterpret_cast<const float*>(smem + WI4 + (qt & 1) * U4QB) + 32 * w + l32;
 #pragma unroll
