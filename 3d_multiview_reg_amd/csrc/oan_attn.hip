@@ -1147,7 +1147,9 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
 // last one reads back (135 KB each), and the split changes a unit's summation order.
 //  * default: every unit in 2 parts at N >= 16 key blocks (3.5 rounds instead of 4 at 435 pairs), a function of N
 //    alone, so a pair's result does not depend on the batch it came in (pair-sharded runs over any number of ranks
-//    give the one-process records bit for bit, tests/test_gpu_distributed.py);
+//    give the one-process records bit for bit at the default f32eq maths, tests/test_gpu_distributed.py; under
+//    split16 a guarded launch re-runs in split-bf16 when ANY of its pairs leaves the fp16 window, so there the
+//    precision a pair gets depends on which pairs share its launch);
 //  * mvr_set_pool_tail(1): only a TAIL is split: the pair octets [0, g0) run whole, the rest in k parts,
 //    dispatched after them.  Candidates (k in {1, 2, 4} with >= 8 key blocks per part; g0 = every octet, no octet,
 //    or the most octets whose whole units fill complete rounds) are ranked by the makespan of the dispatch order

@@ -165,8 +165,10 @@ __device__ __forceinline__ int floor_div(int a, int s) { return (a >= 0) ? a / s
 // voxel keys of raw points: coords = floor(xyz / voxel) with the reference's arithmetic: the float32 PLY values
 // widened to float64 (Open3D's points), divided (correctly rounded fp64 division, not a multiply by 1 / voxel)
 // by the float64 voxel size, floored (scripts/utils.py:108-109, scripts/pairwise_demo.py:75-79); batch index from
-// the fragment offsets
-__global__ void vox_keys_kernel(const float* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
+// the fragment offsets.  T = double: the caller's float64 points as they are (scripts/utils.py extract_features
+// floors Open3D's float64 array), no float32 rounding first.
+template <typename T>
+__global__ void vox_keys_kernel(const T* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
                                 double voxel, uint64_t* keys, int4* vcoords) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -770,7 +772,22 @@ extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, in
   if (n == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   DedupWs d = dedup_ws(ws, n);
-  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
+  hipLaunchKernelGGL(vox_keys_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
+                     d.keys, d.cc);
+  return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s);
+}
+
+// mvr_voxelize over float64 points (same workspace, outputs and order)
+extern "C" int mvr_voxelize_f64(const double* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* ws,
+                                size_t ws_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
+                                hipStream_t s) {
+  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !ws || !coords_out || !counts_out)
+    return MVR_EINVAL;
+  if (ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
+  if (n == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 52.0, s);
+  DedupWs d = dedup_ws(ws, n);
+  hipLaunchKernelGGL(vox_keys_kernel<double>, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
                      d.keys, d.cc);
   return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s);
 }
@@ -795,7 +812,7 @@ extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int 
   if (n == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   DedupWs d = dedup_ws(ws, n, keys);
-  hipLaunchKernelGGL(vox_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
+  hipLaunchKernelGGL(vox_keys_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
                      d.keys, d.cc);
   return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s,
                    reinterpret_cast<int*>(counts_out + 1 + B));

@@ -113,6 +113,7 @@ _SIGS = {
     "mvr_voxelize_hint": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_i64, c_vp, c_size, c_vp, c_vp, c_vp,
                                   c_vp]),
     "mvr_voxelize": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_vp, c_size, c_vp, c_vp, c_vp, c_vp]),
+    "mvr_voxelize_f64": (c_int, [c_vp, c_vp, c_int, c_i64, ctypes.c_double, c_vp, c_size, c_vp, c_vp, c_vp, c_vp]),
     "mvr_coords_downsample_workspace_bytes": (c_size, [c_i64]),
     "mvr_coords_downsample": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_size, c_vp, c_vp, c_vp]),
     "mvr_hash_build": (c_int, [c_vp, c_i64, c_vp, c_size, c_vp]),

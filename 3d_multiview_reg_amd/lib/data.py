@@ -99,9 +99,16 @@ class PrecomputedPairwiseEvalDataset(data.Dataset):
         return len(self.files)
 
 
-def make_pairwise_eval_data_loader(args, num_workers=4):
+def make_pairwise_eval_data_loader(args, num_workers=4, world=1, rank=0):
     """scripts/utils.py:146-197: the loader (batch 1 with mutuals, else args.batch_size; no shuffling) and
-    scene_info {scene: [4 * first pair, 4 * end pair]} (row ranges of the stacked 4x4 estimates)."""
+    scene_info {scene: [4 * first pair, 4 * end pair]} (row ranges of the stacked 4x4 estimates).
+
+    world > 1: the loader covers only this rank's contiguous block of the evaluation's
+    file list, made of whole loader batches (lib.distributed.shard_pairs with group = the batch size), so every
+    batch — and with it the train-mode BatchNorm statistics and the zero-row guard of its forward — is exactly one
+    of the single-process loader's batches.  Samples keep their global index ('idx').  `loader.pair_block` =
+    [first, end) of this rank's block; scene_info always describes the whole evaluation."""
+    from lib.distributed import shard_pairs
     dset = PrecomputedPairwiseEvalDataset(args)
     batch_size = 1 if args.mutuals else args.batch_size
     scene_info, nr = {}, 0
@@ -109,6 +116,9 @@ def make_pairwise_eval_data_loader(args, num_workers=4):
         scene_info[scene] = [nr * 4, (nr + len(files)) * 4]
         nr += len(files)
     scene_info["nr_examples"] = nr
-    loader = torch.utils.data.DataLoader(dset, batch_size=batch_size, shuffle=False, num_workers=num_workers,
+    s, e = shard_pairs(len(dset), world, rank, group=batch_size)
+    part = dset if (s, e) == (0, len(dset)) else data.Subset(dset, range(s, e))
+    loader = torch.utils.data.DataLoader(part, batch_size=batch_size, shuffle=False, num_workers=num_workers,
                                          collate_fn=collate_fn, pin_memory=False, drop_last=False)
+    loader.pair_block = (s, e)
     return loader, scene_info

@@ -96,11 +96,12 @@ def all_gather_rows(buf, world, pg=None):
 
 def gather_records(rec, P, world, group=GROUP, pg=None):
     """All-gather every rank's block of records (padded to block_capacity rows) and return the
-    [P, 16] records of all pairs in pair order, on every rank."""
+    [P, width] records of all pairs in pair order, on every rank.  Any record width and dtype (the evaluation
+    harness gathers float64 rows: its estimates are written to traj.txt in full precision)."""
     if world == 1:
         return rec
     cap = block_capacity(P, world, group)
-    buf = torch.zeros(cap, REC, dtype=rec.dtype, device=rec.device)
+    buf = torch.zeros((cap,) + tuple(rec.shape[1:]), dtype=rec.dtype, device=rec.device)
     buf[:rec.shape[0]] = rec
     out = all_gather_rows(buf, world, pg)
     rows = []
@@ -108,6 +109,41 @@ def gather_records(rec, P, world, group=GROUP, pg=None):
         s, e = shard_pairs(P, world, r, group)
         rows.append(out[r * cap:r * cap + (e - s)])
     return torch.cat(rows)
+
+
+def init_from_env(backend=None):
+    """torchrun's environment (WORLD_SIZE / RANK / LOCAL_RANK / MASTER_*) -> (world, rank, device).
+    WORLD_SIZE > 1 initialises the default process group once: backend "nccl" (RCCL over xGMI) when a HIP device
+    is present, else "gloo"; under gloo several ranks may share the box's GPUs (LOCAL_RANK modulo the device
+    count).  A world of one needs no process group."""
+    import os
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    has_gpu = torch.cuda.is_available()
+    backend = backend or ("nccl" if has_gpu else "gloo")
+    dev = torch.device("cpu")
+    if has_gpu:
+        if backend != "nccl":
+            local %= max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
+    return world, rank, dev
+
+
+def collective_device(pg=None):
+    """where a collective's tensors live: the current HIP device under RCCL, the host under gloo"""
+    import torch.distributed as dist
+    if dist.get_backend(pg) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
 
 
 def unpack_records(rec):

@@ -117,13 +117,15 @@ class Sampler(torch.nn.Module):
             start += n
         return torch.from_numpy(np.stack(out).astype(np.int64))
 
-    def indices(self, pts_list, input_C=None):
-        """Global row indices [B, targeted] (int64, on the device of input_C for 'fps')."""
+    def indices(self, pts_list, input_C=None, k=None):
+        """Global row indices [B, targeted] (int64, on the device of input_C for 'fps').  `k` ('fps' only) overrides
+        the sample count min(targeted, min(pts_list)): a rank holding some of a scene's fragments passes the
+        scene-wide count, so every fragment is sampled as on one GPU."""
         pts = self._pts(pts_list)
         if self.samp_type == "rand":
             return self._rand_indices(pts)
         from lib.fps import furthest_point_sample
-        return furthest_point_sample(input_C, pts, min(self.targeted_num_points, min(pts)))
+        return furthest_point_sample(input_C, pts, min(self.targeted_num_points, min(pts)) if k is None else int(k))
 
     def forward(self, input_C, input_F, pts_list):
         N.require_hip(input_F)

@@ -168,7 +168,12 @@ class SparseTensor:
 def voxelize(points_list, voxel_size, device, distinct_hint=None):
     """Batched sparse_quantize of raw fragments (scripts/pairwise_demo.py:74-96).
     points_list: list of float arrays/tensors [n_b, 3].  Returns (coords int32 [M,4],
-    sel int64 [M] (global point index), counts list, xyz_down float32 [M,3])."""
+    sel int64 [M] (global point index), counts list, xyz_down float32 [M,3]).
+    float64 inputs (all of them) are floored as they are (mvr_voxelize_f64: the reference's np.floor on Open3D's
+    float64 points); anything else is read as float32."""
+    if points_list and all(p.dtype == torch.float64 if torch.is_tensor(p) else np.asarray(p).dtype == np.float64
+                           for p in points_list):
+        return _voxelize_f64(points_list, voxel_size, device)
     pts = [torch.as_tensor(np.asarray(p, dtype=np.float32)) if not torch.is_tensor(p) else p.float() for p in points_list]
     B = len(pts)
     n = [int(p.shape[0]) for p in pts]
@@ -204,6 +209,31 @@ def voxelize(points_list, voxel_size, device, distinct_hint=None):
     return coords, sel, [int(v) for v in c[1:1 + B]], xyz_down
 
 
+def _voxelize_f64(points_list, voxel_size, device):
+    """voxelize() of float64 fragments (mvr_voxelize_f64), same outputs; xyz_down rounded to float32 after the
+    gather (the reference's pcd0 is float32, scripts/pairwise_demo.py:92)"""
+    pts = [torch.as_tensor(np.asarray(p)) if not torch.is_tensor(p) else p for p in points_list]
+    B = len(pts)
+    n = [int(p.shape[0]) for p in pts]
+    xyz = torch.cat([p.reshape(-1, 3) for p in pts], 0).to(device).contiguous()
+    off = torch.tensor(np.concatenate([[0], np.cumsum(n)]), dtype=torch.int64).to(device)
+    total = int(sum(n))
+    L = N.lib()
+    coords = torch.empty(total, 4, dtype=torch.int32, device=device)
+    sel = torch.empty(total, dtype=torch.int64, device=device)
+    cnt = torch.empty(1 + B, dtype=torch.int64, device=device)
+    ws = N.workspace(L.mvr_voxelize_workspace_bytes(total), device)
+    N.check(L.mvr_voxelize_f64(N.ptr(xyz), N.ptr(off), B, total, float(voxel_size), N.ptr(ws), ws.numel(),
+                               N.ptr(coords), N.ptr(sel), N.ptr(cnt), N.stream()), "mvr_voxelize_f64")
+    c = cnt.cpu().numpy()
+    M = int(c[0])
+    coords, sel = coords[:M], sel[:M]
+    x32 = xyz.float()
+    xyz_down = torch.empty(M, 3, device=device)
+    N.check(L.mvr_gather_rows(N.ptr(x32), 3, N.ptr(sel), M, N.ptr(xyz_down), N.stream()), "mvr_gather_rows")
+    return coords, sel, [int(v) for v in c[1:1 + B]], xyz_down
+
+
 def fragment_views(points_list, device):
     """The fragments copied once into ONE contiguous device buffer, returned as views of it: voxelize() then
     reads them in place (no per-call concatenation of the raw points)."""
@@ -226,12 +256,18 @@ def _adjacent_views(pts, device):
     if first.device.type != dev.type or (dev.index is not None and first.device.index != dev.index):
         return None
     ptr = first.data_ptr()
+    base = first.untyped_storage().data_ptr()
     for p in pts:
+        # consecutive in memory is not enough: separately allocated tensors can sit side by side in the caching
+        # allocator, and set_() on the first one's (too small) storage would then resize it and leave the rest
+        # uninitialised — every fragment must be a view of the SAME storage
         if p.device != first.device or p.dim() != 2 or p.shape[1] != 3 or p.dtype != torch.float32 or \
-                not p.is_contiguous() or p.data_ptr() != ptr:
+                not p.is_contiguous() or p.data_ptr() != ptr or p.untyped_storage().data_ptr() != base:
             return None
         ptr += p.numel() * 4
     total = sum(int(p.shape[0]) for p in pts)
+    if (first.storage_offset() + total * 3) * 4 > first.untyped_storage().nbytes():
+        return None
     return first.new_empty(0).set_(first.untyped_storage(), first.storage_offset(), (total, 3), (3, 1))
 
 

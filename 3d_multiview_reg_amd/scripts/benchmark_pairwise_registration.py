@@ -79,48 +79,91 @@ def load_model(method, model_path, cfg_path=None):
     return model.to(torch.device("cuda"))
 
 
+# per-pair record of the estimation loop: [pair idx, T_est (4 x 4, row-major), overlap flag, fragment i, fragment j]
+REC = 20
+
+
+def _batch_records(batch, bi, method, model, refine, seed, overlap_method, overlap_threshold):
+    """benchmark:193-224 for one loader batch: the estimate of every pair (batched: OANet + Procrustes, or RANSAC,
+    on the GPU), T_est = inv(estimate), the overlap gate -> float64 records [b, REC].  `bi` is the batch's index
+    in the whole evaluation (it seeds the RANSAC draws, so a batch gets the same draws on whichever rank it runs)."""
+    xs = batch["xs"][:, 0].numpy()
+    if method == "RANSAC":
+        T = _ransac(xs, seed=seed + bi)
+    else:
+        out = model.filter_correspondences(batch)
+        R = out["rot_est"][-1].double().cpu().numpy()
+        t = out["trans_est"][-1].double().cpu().numpy().reshape(-1, 3)
+        if refine:
+            T = _ransac(xs, keep=out["scores"][-1].cpu().numpy() > 0.5, seed=seed + bi)
+        else:
+            T = np.tile(np.eye(4), (len(R), 1, 1))
+            T[:, :3, :3], T[:, :3, 3] = R, t
+    # the overlap gate of every pair of the batch in one call (benchmark:217-220 scores one pair at a time on
+    # the CPU): the batch's 2B clouds indexed once on the GPU, pair k = clouds (2k, 2k + 1)
+    T_est = np.linalg.inv(T)
+    b = T.shape[0]
+    clouds = [c for k in range(b) for c in (batch["xyz1"][k][0], batch["xyz2"][k][0])]
+    ratios = FragmentOverlap(clouds, method=overlap_method).ratios(
+        [[2 * k, 2 * k + 1] for k in range(b)], list(T_est)) if b else []
+    rec = np.zeros((b, REC), np.float64)
+    for k in range(b):
+        meta = batch["metadata"][k]
+        rec[k, 0] = int(batch["idx"][k].numpy().item())
+        rec[k, 1:17] = T_est[k].reshape(16)
+        rec[k, 17] = float(ratios[k] >= overlap_threshold)
+        rec[k, 18], rec[k, 19] = int(meta[1]), int(meta[2])
+    return rec
+
+
+def _gather_records(rec, num_pairs, batch_size, world, pg=None):
+    """every rank's records -> the records of all pairs in pair order (one all-gather over RCCL, ~160 B per pair;
+    host-staged under gloo): lib.distributed.gather_records over the loader's batch-aligned blocks"""
+    if world == 1:
+        return rec
+    from lib import distributed as D
+    dev = D.collective_device(pg)
+    out = D.gather_records(torch.from_numpy(rec).to(dev), num_pairs, world, group=batch_size, pg=pg)
+    return out.cpu().numpy()
+
+
 def estimate_trans_params(eval_data, source_path, dataset, scene_info, method, model, mutuals,
-                          overlap_method="FCGF", refine=False, seed=0):
-    """benchmark:56-133 (method RANSAC) and :137-245 (learned filters), batched: writes traj.txt per scene"""
+                          overlap_method="FCGF", refine=False, seed=0, world=1, rank=0):
+    """benchmark:56-133 (method RANSAC) and :137-245 (learned filters), batched: writes traj.txt per scene.
+    world > 1: `eval_data` is this rank's block of whole loader batches (lib.data.make_pairwise_eval_data_loader);
+    the per-pair records are all-gathered and rank 0 writes the trajectories."""
     num_pairs = scene_info["nr_examples"]
     est = np.tile(np.eye(4), reps=[num_pairs, 1])
     save_path = _save_path(source_path, method, mutuals)
-    ensure_dir(save_path)
-    reg_metadata = []
     overlap_threshold = 0.3 if dataset == "3d_match" else 0.23
-    logging.info("Starting %s based registration estimation for %d pairs (overlap threshold %.2f)!",
-                 method, num_pairs, overlap_threshold)
+    logging.info("Starting %s based registration estimation for %d pairs (overlap threshold %.2f, %d rank%s)!",
+                 method, num_pairs, overlap_threshold, world, "s" if world > 1 else "")
+    first = getattr(eval_data, "pair_block", (0, num_pairs))[0]
+    bsz = eval_data.batch_size or 1
     timer, full = Timer(), Timer()
     full.tic()
+    recs = []
     for bi, batch in enumerate(eval_data):
         timer.tic()
-        xs = batch["xs"][:, 0].numpy()
-        if method == "RANSAC":
-            T = _ransac(xs, seed=seed + bi)
-        else:
-            out = model.filter_correspondences(batch)
-            R = out["rot_est"][-1].double().cpu().numpy()
-            t = out["trans_est"][-1].double().cpu().numpy().reshape(-1, 3)
-            if refine:
-                T = _ransac(xs, keep=out["scores"][-1].cpu().numpy() > 0.5, seed=seed + bi)
-            else:
-                T = np.tile(np.eye(4), (len(R), 1, 1))
-                T[:, :3, :3], T[:, :3, 3] = R, t
+        recs.append(_batch_records(batch, first // bsz + bi, method, model, refine, seed, overlap_method,
+                                   overlap_threshold))
         timer.toc()
-        # the overlap gate of every pair of the batch in one call (benchmark:217-220 scores one pair at a time on
-        # the CPU): the batch's 2B clouds indexed once on the GPU, pair k = clouds (2k, 2k + 1)
-        T_est = np.linalg.inv(T)
-        clouds = [c for k in range(T.shape[0]) for c in (batch["xyz1"][k][0], batch["xyz2"][k][0])]
-        ratios = FragmentOverlap(clouds, method=overlap_method).ratios(
-            [[2 * k, 2 * k + 1] for k in range(T.shape[0])], list(T_est)) if T.shape[0] else []
-        for k in range(T.shape[0]):
-            pair_idx = int(batch["idx"][k].numpy().item())
-            meta = batch["metadata"][k]
-            est[4 * pair_idx:4 * pair_idx + 4, :] = T_est[k]
-            reg_metadata.append([str(int(meta[1])), str(int(meta[2])), bool(ratios[k] >= overlap_threshold)])
-    if num_pairs:
+    rec = np.concatenate(recs) if recs else np.zeros((0, REC), np.float64)
+    rec = _gather_records(rec, num_pairs, bsz, world)
+    if num_pairs and recs:
         logging.info("%d pairwise registration parameters estimated in %.3fs (%.4fs per batch of pure run time)",
                      num_pairs, full.toc(average=False), timer.avg)
+    if rank != 0:
+        return
+    order = np.argsort(rec[:, 0], kind="stable")
+    rec = rec[order]
+    assert rec.shape[0] == num_pairs and np.array_equal(rec[:, 0], np.arange(num_pairs)), "records of every pair"
+    reg_metadata = []
+    for r in rec:
+        p = int(r[0])
+        est[4 * p:4 * p + 4, :] = r[1:17].reshape(4, 4)
+        reg_metadata.append([str(int(r[18])), str(int(r[19])), bool(r[17])])
+    ensure_dir(save_path)
     for key, rng in scene_info.items():
         if key == "nr_examples":
             continue
@@ -130,10 +173,21 @@ def estimate_trans_params(eval_data, source_path, dataset, scene_info, method, m
 
 
 def evaluate_registration_performance(eval_data, source_path, dataset, scene_info, method, model, mutuals=False,
-                                      overlap_method="FCGF", refine=False, seed=0):
-    """benchmark:250-345: estimate (scenes without results), then the per-scene report; returns the summary"""
+                                      overlap_method="FCGF", refine=False, seed=0, world=1, rank=0):
+    """benchmark:250-345: estimate (scenes without results), then the per-scene report; returns the summary.
+    world > 1: rank 0 writes the trajectories and the report; every rank returns rank 0's summary."""
     estimate_trans_params(eval_data, source_path, dataset, scene_info, method, model, mutuals, overlap_method,
-                          refine, seed)
+                          refine, seed, world, rank)
+    if world > 1:
+        import torch.distributed as dist
+        box = [_report(source_path, dataset, method, mutuals) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return box[0]
+    return _report(source_path, dataset, method, mutuals)
+
+
+def _report(source_path, dataset, method, mutuals):
+    """benchmark:280-345: precision / recall / rotation and translation errors per scene against gt.log / gt.info"""
     re_medians, te_medians, precision, recall = [], [], [], []
     per_scene = {}
     logging.info("Results of %s on %s dataset!", method, dataset)
@@ -185,19 +239,27 @@ def parser():
                     "registration/eval/<method>.yaml, as the reference reads it)")
     ap.add_argument("--seed", type=int, default=0, help="RANSAC draw stream seed")
     ap.add_argument("--num_workers", type=int, default=4)
+    ap.add_argument("--dist_backend", default=None, choices=["nccl", "gloo"],
+                    help="under torchrun (WORLD_SIZE > 1): the process group's backend (default nccl = RCCL on a GPU "
+                    "box, gloo without one); the evaluation's file list is split into contiguous blocks of whole "
+                    "batches over the ranks, the per-pair records all-gathered, the results written by rank 0")
     return ap
 
 
 def main(argv=None):
+    from lib.distributed import init_from_env
     args = parser().parse_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s [%(levelname)s] %(message)s")
+    world, rank, _ = init_from_env(args.dist_backend)
+    logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING,
+                        format="%(asctime)s [%(levelname)s] %(message)s")
     assert args.source_path is not None
     args.source_path = os.path.join(args.source_path, args.dataset)
-    eval_data, scene_info = make_pairwise_eval_data_loader(args, num_workers=args.num_workers)
+    eval_data, scene_info = make_pairwise_eval_data_loader(args, num_workers=args.num_workers, world=world, rank=rank)
     model = None if args.method == "RANSAC" else load_model(args.method, args.model, args.config)
     with torch.no_grad():
         return evaluate_registration_performance(eval_data, args.source_path, args.dataset, scene_info, args.method,
-                                                 model, args.mutuals, args.overlap_method, args.refine, args.seed)
+                                                 model, args.mutuals, args.overlap_method, args.refine, args.seed,
+                                                 world, rank)
 
 
 if __name__ == "__main__":

@@ -54,7 +54,9 @@ def extract_features(model, xyz, rgb=None, normal=None, voxel_size=0.05, device=
     if device is None:
         device = torch.device("cuda:0")
     from lib.sparse import SparseTensor, voxelize
-    coords, sel, counts, _ = voxelize([np.ascontiguousarray(xyz, dtype=np.float32)], voxel_size, device)
+    # floor(xyz / voxel) on the caller's array as it is (float64 from Open3D in the reference: no float32 rounding)
+    xyz_in = np.ascontiguousarray(xyz, dtype=np.float64 if np.asarray(xyz).dtype == np.float64 else np.float32)
+    coords, sel, counts, _ = voxelize([xyz_in], voxel_size, device)
     feats = torch.ones(coords.shape[0], 1, device=device)
     out = model(SparseTensor(feats, coords=coords, batch_size=1).to(device))
     return xyz[sel.cpu().numpy()], out.F

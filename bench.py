@@ -215,11 +215,13 @@ class SceneWorkload:
         m = self.model
         allc = data["pts_all"]
         if self.samp == "rand":
+            # the reference's draws always have `targeted` columns (with replacement when a fragment is smaller)
+            n = m.sampler.targeted_num_points
             idx = m.sampler.indices(allc)                                 # [n_frag, k] rows of the whole scene
             idx = idx[self.f0:self.f1] - int(np.sum(allc[:self.f0]))      # -> rows of this rank's fragments
-        else:                                                             # fps: per fragment, no shared state
-            idx = m.sampler.indices(data["pts_list"], data["pcd0"])
-        n = min(m.sampler.targeted_num_points, min(allc))
+        else:                                                             # fps: per fragment, no shared state, but
+            n = min(m.sampler.targeted_num_points, min(allc))             # the scene-wide count, as on one GPU
+            idx = m.sampler.indices(data["pts_list"], data["pcd0"], k=n) if self.f1 > self.f0 else None
         buf = torch.zeros(self.fper, n, 35, device=self.dev)
         if self.f1 > self.f0:
             F0 = m.descriptor_module(SparseTensor(data["sinput0_F"], coords_manager=data["sinput0_coords_manager"])).F

@@ -379,6 +379,11 @@ size_t mvr_voxelize_workspace_bytes(int64_t n);
 int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* workspace,
                  size_t workspace_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                  mvr_stream_t stream);
+/* mvr_voxelize over float64 points (the caller's float64 array floored as it is: scripts/utils.py:108-109 applies
+ * np.floor to Open3D's float64 points; no float32 rounding first).  Same workspace size, outputs and order. */
+int mvr_voxelize_f64(const double* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* workspace,
+                     size_t workspace_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
+                     mvr_stream_t stream);
 /* mvr_voxelize with the dedup hash table sized for distinct_hint voxels instead of n raw points (the raw
  * cloud holds ~12 points per voxel); inserts probe at most 64 slots and a key that finds none sets
  * counts_out[B + 1] (counts_out has B + 2 entries): the caller then re-runs mvr_voxelize. */

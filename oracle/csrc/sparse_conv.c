@@ -68,6 +68,9 @@ int mvo_kernel_map(const int32_t* in_c, int64_t Mi, const int32_t* out_c, int64_
 }
 
 /* out [Mo][Cout] = sparse conv of feat [Mi][Cin] over nbr [Mo][K] with W [K][Cin][Cout] (+ bias [Cout]). */
+/* AVX2/FMA clone chosen at load time on hosts that have it (the CPU baseline's speed), the baseline-ISA one
+ * elsewhere: the library itself is built for plain x86-64 */
+__attribute__((target_clones("arch=haswell", "default")))
 int mvo_sparse_conv(const float* feat, int64_t Mi, int Cin, const int64_t* nbr, int64_t Mo, int K, const float* W,
                     int Cout, const float* bias, float* out) {
   if (!feat || !nbr || !W || !out || Mi < 0 || Mo < 0 || Cin <= 0 || Cout <= 0 || K <= 0) return -1;

@@ -5,13 +5,16 @@ matches + uniform outliers, gt.log holds the true transformations and gt.info id
 RANSAC must register every pair (precision = recall = 1, small errors); the learned filter (random weights,
 with and without --refine) must run through the same plumbing and write well-formed trajectories."""
 import os
+import sys
 
 import numpy as np
 import pytest
 
 from conftest import GOLDEN
-from synth import random_rotation
 
+HELPERS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers")
+if HELPERS not in sys.path:
+    sys.path.insert(0, HELPERS)
 DEMO = os.path.join(GOLDEN, "demo")
 # the reference's configs/pairwise_registration/demo/config.yaml, unchanged (tests/golden/configs/)
 DEMO_CFG = os.path.join(GOLDEN, "configs", "pairwise_registration", "demo", "config.yaml")
@@ -19,44 +22,9 @@ DEMO_CFG = os.path.join(GOLDEN, "configs", "pairwise_registration", "demo", "con
 pytestmark = pytest.mark.gpu
 
 
-def _write_log(path, pairs, mats, n):
-    with open(path, "w") as f:
-        for (i, j), T in zip(pairs, mats):
-            f.write("%d\t%d\t%d\n" % (i, j, n))
-            f.write("\n".join("\t".join("%.12f" % v for v in row) for row in T) + "\n")
-
-
 def _scene(root, scene="kitchen", n_frag=5, n_corr=800, seed=0):
-    rng = np.random.default_rng(seed)
-    base = rng.uniform(-1.0, 1.0, (3000, 3))
-    poses = []
-    for k in range(n_frag):
-        P = np.eye(4)
-        P[:3, :3], P[:3, 3] = random_rotation(rng), rng.normal(0, 0.5, 3)
-        poses.append(P)
-    frag = [(base - P[:3, 3]) @ P[:3, :3] for P in poses]          # inv(P) applied: fragment frame
-    for d in ("correspondences", "features", "raw_data"):
-        os.makedirs(os.path.join(root, d, scene))
-    for k in range(n_frag):
-        np.savez(os.path.join(root, "features", scene, "%s_%03d.npz" % (scene, k)), xyz=frag[k].astype(np.float32))
-    pairs, gts = [], []
-    for i in range(n_frag):
-        for j in range(i + 1, n_frag):
-            sel = rng.choice(3000, n_corr, replace=False)
-            x1, x2 = frag[i][sel].copy(), frag[j][sel].copy()
-            out = rng.random(n_corr) > 0.4
-            x2[out] = rng.uniform(-1.5, 1.5, (out.sum(), 3))
-            np.savez(os.path.join(root, "correspondences", scene, "%s_%03d_%03d.npz" % (scene, i, j)),
-                     x=np.concatenate([x1, x2], 1).astype(np.float32),
-                     mutuals=np.ones((n_corr, 1), np.float32))
-            pairs.append((i, j))
-            gts.append(np.linalg.inv(poses[i]) @ poses[j])                # fragment j -> fragment i
-    _write_log(os.path.join(root, "raw_data", scene, "gt.log"), pairs, gts, n_frag)
-    with open(os.path.join(root, "raw_data", scene, "gt.info"), "w") as f:
-        for i, j in pairs:
-            f.write("%d\t%d\t%d\n" % (i, j, n_frag) + "\n".join(" ".join("1" if r == c else "0" for c in range(6))
-                                                              for r in range(6)) + "\n")
-    return pairs
+    from eval_layout import write_scene
+    return write_scene(root, scene, n_frag, n_corr, seed)
 
 
 def test_ransac_method_registers_every_pair(gpu, tmp_path):

@@ -27,6 +27,32 @@ def test_voxelize_matches_oracle(gpu, frags):
     np.testing.assert_array_equal(xyz.cpu().numpy(), np.concatenate(frags)[osel])
 
 
+def test_voxelize_float64_points_floored_as_given(gpu):
+    """float64 clouds (Open3D's points in the reference's scripts/utils.py:108-109 extract_features) are floored
+    in float64 as they are (mvr_voxelize_f64): points just below a voxel boundary, whose float32 rounding would
+    land on or past it, keep the lower voxel — the oracle's np.floor(xyz / voxel) on the float64 array — and
+    scripts.utils.extract_features keeps the float64 points it was given"""
+    import torch
+    from lib.sparse import voxelize
+    from oracle.fcgf import voxelize as ovox
+    rng = np.random.default_rng(3)
+    k = rng.integers(-200, 200, (4000, 3))
+    x = k * 0.025 - rng.uniform(1e-12, 1e-9, (4000, 3))          # just below the boundary k * 0.025
+    x = np.concatenate([x, rng.uniform(-3, 3, (2000, 3))])
+    oc, osel, ocnt = ovox([x], 0.025)
+    c, sel, counts, xyz = voxelize([x], 0.025, gpu)
+    assert counts == list(ocnt)
+    np.testing.assert_array_equal(c.cpu().numpy(), oc)
+    np.testing.assert_array_equal(sel.cpu().numpy(), osel)
+    np.testing.assert_array_equal(xyz.cpu().numpy(), x[osel].astype(np.float32))
+    # the test has teeth: the float32-rounded cloud gives other voxels
+    c32, _, _ = ovox([x.astype(np.float32)], 0.025)
+    assert len(c32) != len(oc) or not np.array_equal(c32, oc)
+    # torch float64 on the device: the same
+    c2, sel2, _, _ = voxelize([torch.from_numpy(x).to(gpu)], 0.025, gpu)
+    np.testing.assert_array_equal(sel2.cpu().numpy(), osel)
+
+
 @pytest.mark.parametrize("hint", [None, 1000, 10 ** 6, "exact"])
 def test_voxelize_hint_sized_table_matches_oracle(gpu, frags, hint):
     """mvr_voxelize_hint: the hash table sized for the expected voxel count (lib.sparse keeps the last

@@ -22,3 +22,16 @@ def test_non_adjacent_fragments_fall_back():
     assert _adjacent_views([a[4:10], a[0:4]], "cpu") is None          # out of order
     assert _adjacent_views([a[0:4].double(), a[4:10].double()], "cpu") is None
     assert _adjacent_views([], "cpu") is None
+
+
+def test_adjacent_but_separate_storages_fall_back():
+    """two tensors that sit side by side in memory but are NOT views of one storage (as separately allocated
+    device tensors can be in the caching allocator): no in-place view (set_() on the first storage would resize it
+    and leave the later fragments uninitialised); the copy path is taken"""
+    from lib.sparse import _adjacent_views
+    ba = bytearray(4 * 3 * 7)
+    a = torch.frombuffer(ba, dtype=torch.float32, count=12, offset=0).reshape(4, 3)
+    b = torch.frombuffer(ba, dtype=torch.float32, count=9, offset=48).reshape(3, 3)
+    assert b.data_ptr() == a.data_ptr() + a.numel() * 4                     # adjacent ...
+    assert a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr()  # ... but two storages
+    assert _adjacent_views([a, b], "cpu") is None
