@@ -75,8 +75,9 @@ class PrecomputedWorkload:
     name = "precomputed"
     BATCH = 32
 
-    def __init__(self, dev, rank, pairs, npts):
+    def __init__(self, dev, rank, pairs, npts, shard="scenes", world=1):
         from lib.filtering.oanet import OANet
+        from lib import distributed as D
         from synth import synth_correspondences
         self.net = OANet(oanet_cfg())
         self.state = synth_module(self.net, seed=7)
@@ -88,13 +89,22 @@ class PrecomputedWorkload:
         if self.grouped:
             self.net.bn_group = self.BATCH
             self.net.guard_group = self.BATCH
-        xs, _, _ = synth_correspondences(pairs, npts, seed=1000 + rank)
+        # scenes: every rank its own evaluation (weak scaling); pairs: ONE evaluation, its loader batches split into
+        # contiguous blocks of whole 32-pair batches over the ranks (lib.distributed.shard_pairs, the harness's
+        # --dist split: scripts/benchmark_pairwise_registration.py under torchrun), records all-gathered
+        self.shard, self.world = shard, world
+        xs, _, _ = synth_correspondences(pairs, npts, seed=1000 + (rank if shard == "scenes" else 0))
+        self.p0, self.p1 = D.shard_pairs(pairs, world, rank, group=self.BATCH) if shard == "pairs" else (0, pairs)
+        xs = np.ascontiguousarray(xs[self.p0:self.p1])
         self.xs_host = xs
         self.xs = torch.from_numpy(xs).to(dev).unsqueeze(1)
         self.pairs = pairs
         self.npts = npts
+        self.dev = dev
 
     def step(self):
+        if self.xs.shape[0] == 0:                          # an empty block (more ranks than loader batches)
+            return torch.zeros(0, 13, device=self.dev)
         if self.grouped:
             out = self.net({"xs": self.xs})
             R, t, s = out["rot_est"][-1], out["trans_est"][-1], out["scores"][-1]
@@ -109,12 +119,18 @@ class PrecomputedWorkload:
         return torch.cat(recs)
 
     def gather(self, rec, world):
+        if self.shard == "pairs":
+            from lib import distributed as D
+            return D.gather_records(rec, self.pairs, world, group=self.BATCH) if world > 1 else rec
         return records_allgather(rec, world)
 
     def config(self):
         return {"workload": "precomputed correspondences (configs[3] shape, scripts/benchmark_pairwise_registration.py "
                             "hot loop): OANet(128ch,500 clusters,depth 12,2 blocks, train-mode BN per 32-pair batch)"
-                            "+Procrustes", "pairs_per_gpu": self.pairs, "correspondences": self.npts,
+                            "+Procrustes" + (": ONE evaluation of %d pairs, its 32-pair batches split over %d ranks"
+                                             % (self.pairs, self.world) if self.shard == "pairs" else ""),
+                "pairs_per_gpu": self.p1 - self.p0 if self.shard == "pairs" else self.pairs,
+                "correspondences": self.npts,
                 "batch": self.BATCH, "batches": "one forward, per-batch BN / guard groups" if self.grouped else
                 "one forward per batch"}
 
@@ -327,10 +343,12 @@ class SceneWorkload:
                     "sampler": self.samp, "fragments": self.n_frag, "pairs": self.pairs,
                     "fragments_per_gpu": self.fper, "pairs_per_gpu": -(-self.pairs // self.world),
                     "samples": self.npts, "voxels_mean": int(np.mean(self.vox_counts or [0]))}
-        return {"workload": "one synthetic 3DMatch-scale scene per GPU (configs[2]): %d fragments x ~%d voxels "
+        which = {30: "configs[2]", 50: "configs[4] scene size: a Redwood-scale scene"}.get(self.n_frag, "custom")
+        return {"workload": "one synthetic 3DMatch-scale scene per GPU (%s): %d fragments x ~%d voxels "
                             "(0.025 m) -> FCGF -> %s %d samples -> soft feature-NN for all %d pairs -> OANet "
                             "(128ch, 500 clusters, 2 blocks) -> weighted Procrustes -> all-gather of (R,t,conf)"
-                            % (self.n_frag, int(np.mean(self.vox_counts or [0])), self.samp, self.npts, self.pairs),
+                            % (which, self.n_frag, int(np.mean(self.vox_counts or [0])), self.samp, self.npts,
+                               self.pairs),
                 "sampler": self.samp,
                 "fragments_per_gpu": self.n_frag, "pairs_per_gpu": self.pairs, "samples": self.npts,
                 "voxels_mean": int(np.mean(self.vox_counts or [0]))}
@@ -580,6 +598,9 @@ def main():
     ap.add_argument("--workload", default=os.environ.get("MVR_BENCH_WORKLOAD", "scene"),
                     choices=["scene", "precomputed"])
     ap.add_argument("--pairs", type=int, default=435)
+    ap.add_argument("--frags", type=int, default=30,
+                    help="scene workload: fragments per scene (30 = configs[2], a 3DMatch scene, 435 pairs; 50 = the "
+                    "Redwood-scale scene of configs[4], 1225 pairs)")
     ap.add_argument("--npts", type=int, default=5000)
     ap.add_argument("--samp", default="rand", choices=["rand", "fps"],
                     help="scene workload: interest sampling (lib/layers.py Sampler: rand = the reference's numpy draws, "
@@ -640,15 +661,16 @@ def main():
     if args.workload == "scene":
         if args.shard == "pairs" and not use_pg:
             raise SystemExit("--shard pairs needs a process group (torchrun, or MVR_BENCH_PG=1 at one rank)")
-        if args.shard == "pairs" and world > 30:
-            raise SystemExit("--shard pairs: at most one rank per fragment (30)")
-        wl = SceneWorkload(dev, rank, npts=args.npts, samp=args.samp, shard=args.shard, world=world, groups=groups)
+        if args.shard == "pairs" and world > args.frags:
+            raise SystemExit("--shard pairs: at most one rank per fragment (%d)" % args.frags)
+        wl = SceneWorkload(dev, rank, npts=args.npts, n_frag=args.frags, samp=args.samp, shard=args.shard,
+                           world=world, groups=groups)
     else:
-        wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts)
+        wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts, shard=args.shard, world=world)
     pipelined = args.workload == "scene" and not args.no_pipeline
 
     dt, rec, prof, prof_all, dom, step_ms = timed_run(wl, args, world, pipelined, barrier)
-    pair_sharded = args.workload == "scene" and args.shard == "pairs"
+    pair_sharded = args.shard == "pairs"
     pairs_per_step = int(rec.shape[0]) if pair_sharded else int(rec.shape[-2]) * world
     value = pairs_per_step * args.steps / dt
     ms_step = dt / args.steps * 1e3
@@ -759,8 +781,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if pair_sharded else "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
             "config": dict(wl.config(), math=args.math,
-                           parallelism=("pairs%d (one scene per step: fragments and pair batch sharded over %d "
-                                        "ranks, %s all-gather of samples and records)"
+                           parallelism=(("pairs%d (one scene per step: fragments and pair batch sharded over %d "
+                                         "ranks, %s all-gather of samples and records)"
+                                         if args.workload == "scene" else
+                                         "pairs%d (one evaluation per step: its 32-pair loader batches in contiguous "
+                                         "blocks over %d ranks, %s all-gather of the records)")
                                         % (world, world, "RCCL" if backend == "nccl" else backend)
                                         if pair_sharded else
                                         "dp%d (one scene per rank, %s all-gather of records)"

@@ -159,7 +159,8 @@ def test_oanet_full_train_golden(gpu, conv2):
             d, d64, e = dist(got, r32), dist(got, r64), dist(r32, r64)
             spread = np.max([dist(got, o[k][i].cpu().numpy()) for o in outs[1:]], axis=0)
             # every pair within max(1e-4, 2 x the reference's own distance from exact, 3 x our rounding spread) of
-            # exact arithmetic; at least 30 of 32 within 1e-4 of the reference's fp32
+            # exact arithmetic; at least 28 of 32 within 1e-4 of the reference's fp32 (30 until round 4: see the
+            # docstring and DESIGN §3.2)
             assert (d64 <= np.maximum(1e-4, np.maximum(2 * e, 3 * spread))).all(), (i, k, d64, e, spread)
             assert (d <= 1e-4).sum() >= 28, (i, k, d)
     assert out["gradient_flag"] == bool(g["gradient_flag"])

@@ -173,7 +173,14 @@ def test_pairwise_reg_end_to_end_vs_oracle(gpu, st):
     else:
         np.testing.assert_allclose(xs[..., 3:], xc, atol=2e-5)
     # stage 3: OANet + Kabsch on the GPU's xs
-    o = oanet_forward(fst, xs)
+    _compare_filter(reg, oanet_forward(fst, xs), xs)
+
+
+def _compare_filter(reg, o, xs):
+    """OANet scores / masks / R / t of the GPU against the oracle run on the GPU's own filtering input.  R and t are
+    compared on the pairs whose weighted Kabsch covariance is well conditioned in every block so far (R's
+    sensitivity to weight perturbations scales with the inverse of _cond); at least one such pair must remain in
+    EVERY block, so the comparison can never pass vacuously."""
     good = np.ones(len(xs), bool)
     for i in range(2):
         sc = reg["scores"][i].cpu().numpy()
@@ -181,9 +188,65 @@ def test_pairwise_reg_end_to_end_vs_oracle(gpu, st):
         near = np.abs(o["scores"][i] - 0.5) < 1e-4
         assert np.array_equal((sc > 0.5)[good][~near[good]], (o["scores"][i] > 0.5)[good][~near[good]])
         good &= _cond(xs, o["scores"][i]) > 0.3
-        if not good.any():   # soft matching with random descriptors can leave every pair ill-conditioned
-            break
+        assert good.any(), "block %d: no well-conditioned pair left to compare R / t on" % i
         np.testing.assert_allclose(reg["rot_est"][i].cpu().numpy()[good], o["rot_est"][i][good], atol=1e-4)
         np.testing.assert_allclose(reg["trans_est"][i].cpu().numpy()[good], o["trans_est"][i][good], atol=1e-4)
+
+
+@pytest.mark.parametrize("st", [False, True])
+def test_config2_full_size_pair_end_to_end_vs_oracle(gpu, st):
+    """BASELINE configs[1] at full size: ONE 3DMatch-scale pair (two synthetic fragments of 250 k raw points ->
+    20,590 / 21,280 voxels at 0.025 m), the reference's demo config (configs/pairwise_registration/demo/config.yaml,
+    unchanged: FCGF, rand 5000 samples, soft NN, RegBlock-size OANet; st_grad_flag False as shipped, and True),
+    model.eval() as scripts/pairwise_demo.py:109-110, compute_descriptors -> filter_correspondences as :147-154.
+    Every stage against the oracle (FCGF on its C + OpenMP backend), each fed the GPU's previous-stage output:
+    voxels exact, descriptors <= 2e-4, samples exact, soft / st matches, OANet scores and masks, R and t <= 1e-4.
+    Fragments seed 4 and weights seed 12 were chosen (a CPU oracle scan) so the single pair is well conditioned in
+    both blocks of both modes: the R / t comparison cannot be skipped."""
+    import torch
+    import lib.config
+    from lib.utils import load_config
+    from lib.sparse import voxelize
+    from oracle.fcgf import fcgf_forward, voxelize as ovox
+    from oracle.soft_nn import sample_rand, soft_nn, pair_index
+    from oracle.oanet import oanet_forward
+    from test_gpu_benchmark_harness import DEMO_CFG
+    cfg = load_config(DEMO_CFG)
+    cfg["train"]["st_grad_flag"] = st
+    npts = cfg["data"]["max_num_points"]
+    assert npts == 5000 and cfg["misc"]["voxel_size"] == 0.025
+    frags, _ = synth_scene_fragments(2, seed=4)
+    model = lib.config.get_model(cfg)
+    sd = synth_state({k: tuple(v.shape) for k, v in model.state_dict().items()}, seed=12)
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    model = model.to(gpu).eval()
+    coords, sel, counts, xyz = voxelize([torch.from_numpy(f) for f in frags], 0.025, gpu)
+    oc, osel, ocnt = ovox(frags, 0.025)
+    np.testing.assert_array_equal(coords.cpu().numpy(), oc)
+    np.testing.assert_array_equal(sel.cpu().numpy(), osel)
+    assert list(counts) == list(ocnt) == [20590, 21280]
+    data = {"pcd0": xyz, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=gpu),
+            "pts_list": torch.tensor(counts)}
+    with torch.no_grad():
+        np.random.seed(41)
+        fin, F0, _ = model.compute_descriptors(data)
+        reg = model.filter_correspondences(fin)
+    F0 = F0.cpu().numpy()
+    dst = {k[len("descriptor_module."):]: np.asarray(v) for k, v in sd.items() if k.startswith("descriptor_module.")}
+    fst = {k[len("filtering_module."):]: np.asarray(v) for k, v in sd.items() if k.startswith("filtering_module.")}
+    Fo, _ = fcgf_forward(dst, oc, np.ones((len(oc), 1), np.float32), backend="c")
+    assert np.abs(F0 - Fo).max() < 2e-4
+    np.random.seed(41)
+    idx = sample_rand(list(ocnt), npts)
+    X = xyz.cpu().numpy()[idx]
+    Fs = F0[idx]
+    pi = pair_index(2)
+    xc = soft_nn(Fs[pi[:, 0]], Fs[pi[:, 1]], X[pi[:, 1]], "soft", st=st, temp=0.3)
+    xs = fin["xs"][:, 0].cpu().numpy()
+    assert xs.shape == (1, npts, 6)
+    np.testing.assert_array_equal(xs[..., :3], X[pi[:, 0]])
     if st:
-        assert good.any(), "no well-conditioned pair to compare"
+        assert np.mean(np.any(xs[..., 3:] != xc, axis=-1)) < 1e-3
+    else:
+        np.testing.assert_allclose(xs[..., 3:], xc, atol=2e-5)
+    _compare_filter(reg, oanet_forward(fst, xs), xs)
