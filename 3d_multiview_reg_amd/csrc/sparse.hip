@@ -15,13 +15,13 @@
 //   offset index k = (dx+r) + ks*(dy+r) + ks^2*(dz+r) (x fastest); strided output
 //   coordinates floor(c/s)*s; transposed conv: in = out - off*s_out; output rows of
 //   every dedup in first-occurrence order of the input rows.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 
 #include "common.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
+#include "radix.hpp"
 #include "sparse.hpp"
 
 namespace mvr {
@@ -669,90 +669,37 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {   // 9 bits -> every t
 // wrapped): rows of one mask class are tiled in spatial order, so the tiles an XCD runs together gather
 // neighbour rows from one compact region (L2 reuse).  Only the tiling order changes: every output row is
 // computed the same way wherever it sits.
-__global__ void offset_mask_kernel(const int32_t* __restrict__ nbr, const int4* __restrict__ coords, int step,
-                                   int64_t Mo, int K, uint64_t* keys, int32_t* rows) {
-  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= Mo) return;
-  uint32_t m = 0;
-  for (int k = 0; k < K; ++k) m |= (nbr[o * K + k] >= 0 ? 1u : 0u) << k;
-  uint32_t lo = 0;
-  if (coords) {
-    const int4 c = coords[o];
-    lo = ((uint32_t)c.x & 31u) << 27 | spread3((uint32_t)(c.y / step)) << 2 | spread3((uint32_t)(c.z / step)) << 1 |
-         spread3((uint32_t)(c.w / step));
-  }
-  keys[o] = (uint64_t)m << 32 | lo;
-  rows[o] = (int32_t)o;
-}
 
-// 3^3 kernel map over the input set's brick map (stride 2^tin): one thread per output row.  The 27 neighbours
-// c + sign * d * step lie in at most 2 bricks per axis, so the row resolves <= 8 brick ids (one hash probe each,
-// in a table of ~M / 10 bricks) and reads each neighbour's row from its brick's 64-slot array — instead of 27
-// probes of the per-voxel coordinate table.  A neighbour off the input lattice (transposed maps: c - d s not a
-// multiple of 2^tin) is absent.  Same nbr[o][k] (k = (dx+1) + 3 (dy+1) + 9 (dz+1)) as kernel_map_kernel; with
-// `keys` it also writes the row's mvr_kernel_map_order sort key (active-offset mask, fragment, Morton code of
-// c / kstep), so the order needs no second pass over the table.
-__device__ __forceinline__ int brick_id_of(const HashView& h, int b, int bx, int by, int bz) {
-  const int64_t sl = hash_slot(h, pack_key(b, bx, by, bz));
-  return sl >= 0 ? h.vals[sl] : -1;
-}
-__global__ __launch_bounds__(256) void kernel_map_brick_kernel(const int4* __restrict__ oc, int64_t Mo, BrickView bv,
-                                                               int tin, int step, int sign, int32_t* __restrict__ nbr,
-                                                               uint64_t* __restrict__ keys, int kstep) {
-  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= Mo) return;
-  const int4 c = oc[o];
-  const int tb = tin + 2, amask = (1 << tin) - 1;
-  int n[3][3];   // [axis][d + 1]: neighbour coordinate
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    n[0][d] = c.y + sign * (d - 1) * step;
-    n[1][d] = c.z + sign * (d - 1) * step;
-    n[2][d] = c.w + sign * (d - 1) * step;
-  }
-  int lo[3], two[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const int b0 = n[a][0] >> tb, b2 = n[a][2] >> tb;   // monotone in d: the extremes are d = -1 and d = +1
-    lo[a] = min(b0, b2);
-    two[a] = b0 != b2;
-  }
-  int id[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const int ix = q & 1, iy = (q >> 1) & 1, iz = q >> 2;
-    id[q] = ((ix && !two[0]) || (iy && !two[1]) || (iz && !two[2]))
-                ? -1 : brick_id_of(bv.h, c.x, lo[0] + ix, lo[1] + iy, lo[2] + iz);
-  }
-  uint32_t m = 0;
-  int32_t* dst = nbr + o * 27;
-#pragma unroll
-  for (int dz = 0; dz < 3; ++dz)
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int x = n[0][dx], y = n[1][dy], z = n[2][dz];
-        const int q = ((x >> tb) != lo[0]) | (((y >> tb) != lo[1]) << 1) | (((z >> tb) != lo[2]) << 2);
-        int bid = id[0];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) bid = q == j ? id[j] : bid;   // register select, no indexed scratch
-        const bool ok = bid >= 0 && ((x | y | z) & amask) == 0;
-        const int row = ok ? bv.rows[(int64_t)bid * 64 + brick_cell(x >> tin, y >> tin, z >> tin)] : -1;
-        const int k = dx + 3 * dy + 9 * dz;
-        dst[k] = row;
-        m |= (row >= 0 ? 1u : 0u) << k;
-      }
-  if (keys) {
-    const uint32_t l = ((uint32_t)c.x & 31u) << 27 | spread3((uint32_t)(c.y / kstep)) << 2 |
-                       spread3((uint32_t)(c.z / kstep)) << 1 | spread3((uint32_t)(c.w / kstep));
-    keys[o] = (uint64_t)m << 32 | l;
-  }
-}
-
-__global__ void iota_kernel(int32_t* v, int64_t n) {
+// the sort keys of the kernel maps of one batched order call (mvr_kernel_map_orders): thread i = row o of map j
+// (maps back to back in the combined key array); key = map index << 59 | offset mask << 32 | fragment and Morton
+// code of c / step (9 bits per axis), value = o.  Sorted stably, map j's rows form the segment [start_j, start_j +
+// M_j) of the result, in exactly mvr_kernel_map_order's order.
+constexpr int ORDER_MAX_MAPS = 16;
+struct OrderMaps {
+  const int32_t* nbr[ORDER_MAX_MAPS];
+  const int4* coords[ORDER_MAX_MAPS];
+  int step[ORDER_MAX_MAPS];
+  int64_t start[ORDER_MAX_MAPS + 1];
+  int n, K;
+};
+__global__ void order_keys_kernel(OrderMaps m, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) v[i] = (int32_t)i;
+  if (i >= m.start[m.n]) return;
+  int j = 0;
+  while (i >= m.start[j + 1]) ++j;
+  const int64_t o = i - m.start[j];
+  const int32_t* row = m.nbr[j] + o * m.K;
+  uint32_t mask = 0;
+  for (int k = 0; k < m.K; ++k) mask |= (row[k] >= 0 ? 1u : 0u) << k;
+  uint32_t lo = 0;
+  if (m.coords[j]) {
+    const int4 c = m.coords[j][o];
+    const int st = m.step[j];
+    lo = ((uint32_t)c.x & 31u) << 27 | spread3((uint32_t)(c.y / st)) << 2 | spread3((uint32_t)(c.z / st)) << 1 |
+         spread3((uint32_t)(c.w / st));
+  }
+  keys[i] = (uint64_t)j << 59 | (uint64_t)mask << 32 | lo;
+  vals[i] = (int32_t)o;
 }
 
 }  // namespace mvr
@@ -961,104 +908,45 @@ extern "C" int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, hipStream
   return MVR_OK;
 }
 
-// Order the output rows of a kernel map by their active-offset mask, then (out_coords given) fragment and
-// Morton code (LSD radix sort of 64-bit keys, stable): perm[i] = i-th row.  Workspace:
-// mvr_kernel_map_order_bytes(Mo).
-static size_t order_sort_bytes(int64_t Mo) {
-  size_t tmp = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                         (const int32_t*)nullptr, (int32_t*)nullptr, (int)(Mo > 0 ? Mo : 1), 0,
-                                         64) != hipSuccess)
-    return 0;
-  return tmp;
-}
-extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) {
-  const size_t n = (size_t)(Mo > 0 ? Mo : 1);
-  return order_sort_bytes(Mo) + n * 20 + 3 * 256;
-}
-static int g_spconv_order = 0;
-extern "C" int mvr_set_spconv_order(int mode) {
-  const int prev = g_spconv_order;
-  g_spconv_order = mode == 1 ? 1 : 0;
-  return prev;
+// Order the output rows of kernel maps by their active-offset mask, then (out_coords given) fragment and Morton
+// code: one stable LSD radix sort (radix.hip, hand-written onesweep) over the keys of ALL the maps of the call, the
+// map index in the top key bits, so n maps cost one sort (a control-block clear, a histogram and 8 digit passes)
+// instead of one each.  perm_out: int32 [sum M_j]; map j's order is perm_out[start_j : start_j + M_j) (start_j =
+// M_0 + ... + M_{j-1}), local row indices.  Workspace: mvr_kernel_map_orders_bytes(total rows).
+extern "C" size_t mvr_kernel_map_orders_bytes(int64_t total) { return radix_ws_bytes(total); }
+
+extern "C" int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, const int32_t* const* out_coords,
+                                     const int* steps, const int64_t* Mo, int K, int32_t* perm_out, void* ws,
+                                     size_t ws_bytes, hipStream_t s) {
+  if (n_maps <= 0 || n_maps > ORDER_MAX_MAPS || !nbr || !Mo || K <= 0 || K > 27 || !perm_out || !ws) return MVR_EINVAL;
+  OrderMaps m{};
+  m.n = n_maps;
+  m.K = K;
+  m.start[0] = 0;
+  for (int j = 0; j < n_maps; ++j) {
+    const int32_t* c = out_coords ? out_coords[j] : nullptr;
+    if (Mo[j] < 0 || (Mo[j] > 0 && !nbr[j]) || (c && (!steps || steps[j] <= 0))) return MVR_EINVAL;
+    m.nbr[j] = nbr[j];
+    m.coords[j] = reinterpret_cast<const int4*>(c);
+    m.step[j] = c ? steps[j] : 1;
+    m.start[j + 1] = m.start[j] + Mo[j];
+  }
+  const int64_t total = m.start[n_maps];
+  if (total > (int64_t)(1 << 30) - 1 || ws_bytes < radix_ws_bytes(total)) return MVR_EINVAL;
+  if (total == 0) return MVR_OK;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)total * (4.0 * K + 16 + 8 * 24 + 4), s);
+  RadixWs w = radix_ws(ws, total);
+  hipLaunchKernelGGL(order_keys_kernel, dim3(nblk(total)), dim3(256), 0, s, m, w.ka, w.va);
+  int bits = 32 + K;                                   // mask above bit 32, fragment + Morton below
+  if (n_maps > 1) bits = 59 + (32 - __builtin_clz((unsigned)(n_maps - 1)));   // + the map index from bit 59
+  return radix_sort(w, bits, perm_out, s);
 }
 
-// 3^3 kernel maps over brick maps (kernel_map_brick_kernel): in_bricks = mvr_brick_map_build_stride of the Min
-// input coordinates at tensor stride in_stride; neighbour of output c at offset d: c + d step (transposed:
-// c - d step).  order_keys (optional, uint64 [Mout]): the rows' sort keys for mvr_kernel_map_order_keys
-// (out_stride: the output set's tensor stride, for the Morton code).
-extern "C" int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, int out_stride, const void* in_bricks,
-                                     int64_t Min, size_t in_bricks_bytes, int in_stride, int step, int transposed,
-                                     int32_t* nbr, uint64_t* order_keys, hipStream_t s) {
-  if (!out_coords || Mout < 0 || !in_bricks || Min < 0 || in_bricks_bytes < brick_map_bytes(Min) || step <= 0 ||
-      in_stride <= 0 || (in_stride & (in_stride - 1)) || in_stride > (1 << 12) || out_stride <= 0 || !nbr)
-    return MVR_EINVAL;
-  if (Mout == 0) return MVR_OK;
-  BrickView v = brick_view(const_cast<void*>(in_bricks), Min);
-  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mout * (16 + 27 * 4 + 8 * 12 + (order_keys ? 8 : 0)), s);
-  hipLaunchKernelGGL(kernel_map_brick_kernel, dim3(nblk(Mout)), dim3(256), 0, s,
-                     reinterpret_cast<const int4*>(out_coords), Mout, v, __builtin_ctz((unsigned)in_stride), step,
-                     transposed ? -1 : 1, nbr, order_keys, out_stride);
-  MVR_CHECK_LAUNCH();
-  return MVR_OK;
-}
-
-// the row order from precomputed keys (mvr_kernel_map_bricks' order_keys): the same stable LSD radix sort as
-// mvr_kernel_map_order over the same keys.  keys is not modified.  Workspace: mvr_kernel_map_order_bytes(Mo).
-extern "C" int mvr_kernel_map_order_keys_bits(const uint64_t* keys, int64_t Mo, int begin_bit, int end_bit,
-                                              int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s);
-extern "C" int mvr_kernel_map_order_keys(const uint64_t* keys, int64_t Mo, int K, int32_t* perm, void* ws,
-                                         size_t ws_bytes, hipStream_t s) {
-  if (K <= 0 || K > 32) return MVR_EINVAL;
-  // g_spconv_order 1: the fragment + Morton bits only (spatially compact tiles, larger offset unions; A/B timing)
-  return mvr_kernel_map_order_keys_bits(keys, Mo, 0, g_spconv_order == 1 ? 32 : 32 + K, perm, ws, ws_bytes, s);
-}
-
-// the same over the key bits [begin_bit, end_bit) only (0 <= begin_bit < end_bit <= 64): e.g. [0, 32) orders by
-// fragment and Morton code alone
-extern "C" int mvr_kernel_map_order_keys_bits(const uint64_t* keys, int64_t Mo, int begin_bit, int end_bit,
-                                              int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (!keys || !perm || Mo < 0 || begin_bit < 0 || end_bit > 64 || begin_bit >= end_bit || !ws ||
-      ws_bytes < mvr_kernel_map_order_bytes(Mo) || Mo > 0x7fffffff)
-    return MVR_EINVAL;
-  if (Mo == 0) return MVR_OK;
-  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mo * 32, s);
-  char* p = reinterpret_cast<char*>(ws);
-  auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
-  take((size_t)Mo * 8);   // (mvr_kernel_map_order's key buffer: unused here)
-  uint64_t* kout = reinterpret_cast<uint64_t*>(take((size_t)Mo * 8));
-  int32_t* vin = reinterpret_cast<int32_t*>(take((size_t)Mo * 4));
-  size_t tmp = order_sort_bytes(Mo);
-  if (!tmp) return MVR_ELAUNCH;
-  void* tbuf = take(tmp);
-  hipLaunchKernelGGL(iota_kernel, dim3(nblk(Mo)), dim3(256), 0, s, vin, Mo);
-  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, keys, kout, vin, perm, (int)Mo, begin_bit, end_bit, s) !=
-      hipSuccess)
-    return MVR_ELAUNCH;
-  MVR_CHECK_LAUNCH();
-  return MVR_OK;
-}
+// one map (the same order as mvr_kernel_map_orders with n_maps = 1).  Workspace: mvr_kernel_map_order_bytes(Mo).
+extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) { return radix_ws_bytes(Mo); }
 
 extern "C" int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mo, int K,
                                     int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (!nbr || !perm || Mo < 0 || K <= 0 || K > 32 || !ws || ws_bytes < mvr_kernel_map_order_bytes(Mo) ||
-      Mo > 0x7fffffff || (out_coords && step <= 0))
-    return MVR_EINVAL;
-  if (Mo == 0) return MVR_OK;
-  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)Mo * (4.0 * K + 32), s);
-  char* p = reinterpret_cast<char*>(ws);
-  auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
-  uint64_t* kin = reinterpret_cast<uint64_t*>(take((size_t)Mo * 8));
-  uint64_t* kout = reinterpret_cast<uint64_t*>(take((size_t)Mo * 8));
-  int32_t* vin = reinterpret_cast<int32_t*>(take((size_t)Mo * 4));
-  size_t tmp = order_sort_bytes(Mo);
-  if (!tmp) return MVR_ELAUNCH;
-  void* tbuf = take(tmp);
-  hipLaunchKernelGGL(offset_mask_kernel, dim3(nblk(Mo)), dim3(256), 0, s, nbr, reinterpret_cast<const int4*>(out_coords),
-                     step, Mo, K, kin, vin);
-  if (hipcub::DeviceRadixSort::SortPairs(tbuf, tmp, kin, kout, vin, perm, (int)Mo, out_coords ? 0 : 32, 32 + K, s) !=
-      hipSuccess)
-    return MVR_ELAUNCH;
-  MVR_CHECK_LAUNCH();
-  return MVR_OK;
+  if (!nbr || !perm || Mo < 0 || K <= 0 || K > 27 || (out_coords && step <= 0)) return MVR_EINVAL;
+  return mvr_kernel_map_orders(1, &nbr, &out_coords, &step, &Mo, K, perm, ws, ws_bytes, s);
 }

@@ -121,10 +121,10 @@ _SIGS = {
     "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
     "mvr_kernel_map_order_bytes": (c_size, [c_i64]),
     "mvr_kernel_map_order": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
-    "mvr_kernel_map_bricks": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_size, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
-    "mvr_kernel_map_order_keys": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
-    "mvr_kernel_map_order_keys_bits": (c_int, [c_vp, c_i64, c_int, c_int, c_vp, c_vp, c_size, c_vp]),
-    "mvr_set_spconv_order": (c_int, [c_int]),
+    "mvr_kernel_map_orders_bytes": (c_size, [c_i64]),
+    "mvr_kernel_map_orders": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_size, c_vp]),
+    "mvr_radix_sort_pairs_bytes": (c_size, [c_i64]),
+    "mvr_radix_sort_pairs": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_set_pool_tail": (c_int, [c_int]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
                            c_int, c_vp, c_i64, c_vp, c_vp, c_vp]),

@@ -143,6 +143,7 @@ class FCGFNet(nn.Module):
         if self.training:
             raise NotImplementedError("FCGFNet on the HIP path runs in eval mode (BatchNorm running statistics)")
         cm = x.coords_man
+        cm.prepare_orders()   # all ten 3^3 maps and their row orders up front: one radix sort for the ten orders
 
         def km(kind, s):
             return cm.kernel_map(kind, s), cm.kernel_map_order(kind, s)

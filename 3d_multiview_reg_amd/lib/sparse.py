@@ -8,20 +8,17 @@ ME 0.4 itself stored the batch index last).  Every coordinate set, hash table
 and kernel map lives in HBM and is cached on the CoordinateManager shared by all
 tensors of one forward pass.
 """
-import os
+import ctypes
 
 import numpy as np
 import torch
 
 from lib import _native as N
 
-# 3^3 kernel maps over brick maps (csrc/sparse.hip kernel_map_brick_kernel) with MVR_BRICK_MAPS=1, else over the
-# per-level coordinate tables (identical maps; A/B timing)
-BRICK_MAPS = os.environ.get("MVR_BRICK_MAPS", "0") == "1"
-# tiling order of the sparse convs over brick-path keys: "mask" (default) active-offset mask, then fragment and
-# Morton code; "spatial": fragment and Morton code alone for the s1 / down maps (fewer distinct rows gathered per
-# tile, larger offset unions), the mask kept for the transposed maps (whose rows use <= 8 of 27 offsets by parity)
-SPCONV_ORDER = os.environ.get("MVR_SPCONV_ORDER", "mask")
+# the ten 3^3 kernel maps of FCGF (lib/descriptor/fcgf.py; fcgf.py:118-227 of the reference): stride-1 stencils at
+# tensor strides 1-8, the strided convs 1->2, 2->4, 4->8 and the transposed 8->4, 4->2, 2->1 (keyed by output stride)
+FCGF_MAPS = (("s1", 1), ("s1", 2), ("s1", 4), ("s1", 8), ("down", 1), ("down", 2), ("down", 4),
+             ("up", 4), ("up", 2), ("up", 1))
 
 
 class CoordinateManager:
@@ -35,7 +32,6 @@ class CoordinateManager:
         self.bricks = {}
         self.maps = {}
         self.orders = {}
-        self.order_keys = {}
 
     def coords_at(self, s):
         if s not in self.coords:
@@ -76,21 +72,9 @@ class CoordinateManager:
         return self.bricks[s]
 
     def kernel_map(self, kind, s, ks=3):
-        """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed).
-        3^3 maps are resolved over the input level's brick map (mvr_kernel_map_bricks, which also writes the
-        rows' order keys for kernel_map_order); other sizes over the level's coordinate table."""
+        """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed), resolved
+        over the input level's lattice coordinate table."""
         key = (kind, s, ks)
-        if key not in self.maps and ks == 3 and BRICK_MAPS:
-            out_s, in_s, tr = {"s1": (s, s, 0), "down": (2 * s, s, 0), "up": (s, 2 * s, 1)}[kind]
-            out_c, in_c = self.coords_at(out_s), self.coords_at(in_s)
-            bricks = self.brick_map(in_s)
-            nbr = torch.empty(out_c.shape[0], 27, dtype=torch.int32, device=self.device)
-            keys = torch.empty(out_c.shape[0], dtype=torch.int64, device=self.device)
-            N.check(N.lib().mvr_kernel_map_bricks(N.ptr(out_c), out_c.shape[0], out_s, N.ptr(bricks), in_c.shape[0],
-                                                  bricks.numel(), in_s, s, tr, N.ptr(nbr), N.ptr(keys), N.stream()),
-                    "mvr_kernel_map_bricks")
-            self.maps[key] = nbr
-            self.order_keys[key] = keys
         if key not in self.maps:
             if kind == "s1":
                 out_c, tab, tr = self.coords_at(s), self.table(s), 0
@@ -107,31 +91,50 @@ class CoordinateManager:
             self.maps[key] = nbr
         return self.maps[key]
 
+    def _order_args(self, kind, s, ks):
+        nbr = self.kernel_map(kind, s, ks)
+        step = 2 * s if kind == "down" else s
+        return nbr, self.coords_at(step), step
 
     def kernel_map_order(self, kind, s, ks=3):
         """Rows of kernel_map(kind, s) sorted by their active-offset mask, then fragment and Morton code of their
         coordinates (tiling order of mvr_spconv)."""
         key = (kind, s, ks)
         if key not in self.orders:
-            nbr = self.kernel_map(kind, s, ks)
-            out_c = self.coords_at(2 * s if kind == "down" else s)
+            nbr, out_c, step = self._order_args(kind, s, ks)
             L = N.lib()
             ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr.shape[0]), self.device)
             perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.device)
-            if key in self.order_keys and SPCONV_ORDER == "spatial" and kind != "up":
-                N.check(L.mvr_kernel_map_order_keys_bits(N.ptr(self.order_keys.pop(key)), nbr.shape[0], 0, 32,
-                                                         N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
-                        "mvr_kernel_map_order_keys_bits")
-            elif key in self.order_keys:   # keys written by the brick kernel map
-                N.check(L.mvr_kernel_map_order_keys(N.ptr(self.order_keys.pop(key)), nbr.shape[0], nbr.shape[1],
-                                                    N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
-                        "mvr_kernel_map_order_keys")
-            else:
-                N.check(L.mvr_kernel_map_order(N.ptr(nbr), N.ptr(out_c), 2 * s if kind == "down" else s,
-                                               nbr.shape[0], nbr.shape[1], N.ptr(perm), N.ptr(ws), ws.numel(),
-                                               N.stream()), "mvr_kernel_map_order")
+            N.check(L.mvr_kernel_map_order(N.ptr(nbr), N.ptr(out_c), step, nbr.shape[0], nbr.shape[1], N.ptr(perm),
+                                           N.ptr(ws), ws.numel(), N.stream()), "mvr_kernel_map_order")
             self.orders[key] = perm
         return self.orders[key]
+
+    def prepare_orders(self, specs=FCGF_MAPS, ks=3):
+        """The kernel maps of `specs` ((kind, stride) pairs) and all their row orders in ONE sort
+        (mvr_kernel_map_orders: the map index in the top key bits; the same orders as kernel_map_order one by one,
+        with one histogram and eight digit passes for all of them instead of per map)."""
+        todo = [(k, s) for k, s in specs if (k, s, ks) not in self.orders]
+        if not todo:
+            return
+        args = [self._order_args(k, s, ks) for k, s in todo]
+        n = len(args)
+        Mo = [int(a[0].shape[0]) for a in args]
+        total = sum(Mo)
+        L = N.lib()
+        ws = N.workspace(L.mvr_kernel_map_orders_bytes(total), self.device)
+        perm = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
+        vp = ctypes.c_void_p
+        nbr_a = (vp * n)(*[a[0].data_ptr() for a in args])
+        crd_a = (vp * n)(*[a[1].data_ptr() for a in args])
+        stp_a = (ctypes.c_int * n)(*[a[2] for a in args])
+        mo_a = (ctypes.c_int64 * n)(*Mo)
+        N.check(L.mvr_kernel_map_orders(n, nbr_a, crd_a, stp_a, mo_a, ks ** 3, N.ptr(perm), N.ptr(ws), ws.numel(),
+                                        N.stream()), "mvr_kernel_map_orders")
+        o = 0
+        for (k, s), m in zip(todo, Mo):
+            self.orders[(k, s, ks)] = perm[o:o + m]
+            o += m
 
 
 class SparseTensor:

@@ -406,36 +406,29 @@ int mvr_hash_build_lattice(const int32_t* coords, int64_t M, int stride, void* t
  * row of out_coords[o] + sign*off_k*step in the input table (sign -1 if transposed), or -1 */
 int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
                    int step, int transposed, int32_t* nbr, mvr_stream_t stream);
-/* Row order of a kernel map: output rows sorted by their active-offset mask (K <= 32), so that a
+/* Row order of a kernel map: output rows sorted by their active-offset mask (K <= 27), so that a
  * tile of consecutive rows shares its active offsets; with out_coords (int32 [Mout][4], the map's output
  * coordinates, multiples of step) rows of one mask are further ordered by fragment and Morton code of
- * coordinates / step (spatially compact tiles: L2 reuse of the gathered rows).  Workspace:
- * mvr_kernel_map_order_bytes(Mout). */
+ * coordinates / step (spatially compact tiles: L2 reuse of the gathered rows).  Stable: ties keep row order.
+ * A hand-written onesweep LSD radix sort (csrc/radix.hip: a control-block clear, one histogram launch, one launch
+ * per 8-bit digit).  Workspace: mvr_kernel_map_order_bytes(Mout). */
 size_t mvr_kernel_map_order_bytes(int64_t Mout);
 int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mout, int K, int32_t* perm,
                          void* workspace, size_t workspace_bytes, mvr_stream_t stream);
-/* 3^3 kernel map (the same nbr[o][k] as mvr_kernel_map with ksize 3) over the INPUT set's brick map
- * (mvr_brick_map_build_stride of its Min coordinates at tensor stride in_stride, a power of two): neighbour of
- * out_coords[o] at offset d = out + d*step (transposed: out - d*step; a neighbour off the input lattice is absent).
- * One thread per output row resolves the <= 8 bricks its 27 neighbours fall in.  order_keys (optional, uint64
- * [Mout]): each row's sort key of mvr_kernel_map_order (active-offset mask, then fragment and Morton code of
- * out_coords / out_stride), for mvr_kernel_map_order_keys.  Replaces the per-voxel table probes of the ME
- * CoordinateManager's kernel maps (fcgf.py:118-227). */
-int mvr_kernel_map_bricks(const int32_t* out_coords, int64_t Mout, int out_stride, const void* in_bricks, int64_t Min,
-                          size_t in_bricks_bytes, int in_stride, int step, int transposed, int32_t* nbr,
-                          uint64_t* order_keys, mvr_stream_t stream);
-/* mvr_kernel_map_order from mvr_kernel_map_bricks' order_keys (the same stable sort of the same keys: the same
- * perm).  Workspace: mvr_kernel_map_order_bytes(Mout). */
-int mvr_kernel_map_order_keys(const uint64_t* order_keys, int64_t Mout, int K, int32_t* perm, void* workspace,
-                              size_t workspace_bytes, mvr_stream_t stream);
-/* The same over the key bits [begin_bit, end_bit) only (0 <= begin_bit < end_bit <= 64; [0, 32): fragment and
- * Morton code alone, [0, 32 + K): the full key). */
-int mvr_kernel_map_order_keys_bits(const uint64_t* keys, int64_t Mo, int begin_bit, int end_bit, int32_t* perm,
-                                   void* ws, size_t ws_bytes, mvr_stream_t stream);
-/* row order of mvr_kernel_map_order_keys (process-wide): 0 (default) active-offset mask, then fragment and Morton
- * code; 1 fragment and Morton code only (spatially compact tiles whose offset unions are larger; A/B timing).
- * Returns the previous setting. */
-int mvr_set_spconv_order(int mode);
+/* The row orders of n_maps (<= 16) kernel maps in ONE sort (the map index in the top key bits): host arrays
+ * nbr[j] (int32 [Mo[j]][K]), out_coords[j] (or out_coords NULL: masks only) with steps[j]; perm_out int32
+ * [sum Mo]: map j's order (local row indices, exactly mvr_kernel_map_order's) at offset Mo[0] + ... + Mo[j-1].
+ * Workspace: mvr_kernel_map_orders_bytes(sum Mo).  (FCGF: all ten 3^3 maps of a scene, lib/sparse.py
+ * CoordinateManager.prepare_orders.) */
+size_t mvr_kernel_map_orders_bytes(int64_t total);
+int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, const int32_t* const* out_coords, const int* steps,
+                          const int64_t* Mo, int K, int32_t* perm_out, void* workspace, size_t workspace_bytes,
+                          mvr_stream_t stream);
+/* The same stable radix sort on its own: values int32 [n] (NULL: 0..n-1) in ascending order of the key bits
+ * [0, bits) of keys uint64 [n] -> vals_out.  Workspace: mvr_radix_sort_pairs_bytes(n). */
+size_t mvr_radix_sort_pairs_bytes(int64_t n);
+int mvr_radix_sort_pairs(const uint64_t* keys, const int32_t* vals, int64_t n, int bits, int32_t* vals_out,
+                         void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 /* MinkowskiConvolution forward, gather-GEMM over the neighbour table (nbr NULL & K==1:
  * identity map, i.e. a 1x1x1 conv); W [K][Cin][Cout]; epilogue (+bias[Cout]) ->
  * BatchNorm eval (bn.gamma NULL: none) -> (+res[o*ldres+c]) -> ReLU if relu.
@@ -473,7 +466,7 @@ int mvr_set_spconv_xcd(int on);
  * returns the previous setting. */
 int mvr_set_spconv_narrow(int rows);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
- * neighbourhood structure of the large-stencil conv below and of mvr_kernel_map_bricks.  Workspace:
+ * neighbourhood structure of the large-stencil conv below.  Workspace:
  * mvr_brick_map_bytes(M).  _stride: a set at tensor stride `stride` (a power of two, coordinates multiples of it):
  * cells are coordinates / stride; mvr_brick_map_build = stride 1. */
 size_t mvr_brick_map_bytes(int64_t M);

@@ -73,12 +73,8 @@ def test_voxelize_hint_sized_table_matches_oracle(gpu, frags, hint):
     np.testing.assert_array_equal(sel2.cpu().numpy(), osel)
 
 
-@pytest.mark.parametrize("bricks", [False, True])
-def test_strided_sets_and_kernel_maps_match_oracle(gpu, frags, bricks, monkeypatch):
-    """every level's coordinate set and the 3^3 kernel maps (over the coordinate tables, and over brick maps:
-    mvr_kernel_map_bricks) equal the oracle's"""
-    import lib.sparse
-    monkeypatch.setattr(lib.sparse, "BRICK_MAPS", bricks)
+def test_strided_sets_and_kernel_maps_match_oracle(gpu, frags):
+    """every level's coordinate set and the 3^3 kernel maps equal the oracle's"""
     from lib.sparse import voxelize, CoordinateManager
     from oracle.fcgf import Levels
     c, _, counts, _ = voxelize(frags, 0.025, gpu)
@@ -145,46 +141,40 @@ def test_lattice_table_kernel_maps_dense_and_sparse(gpu, stride):
                 dx, dy, dz = k % 3 - 1, (k // 3) % 3 - 1, k // 9 - 1
                 ref[o, k] = index.get((b, x + sg * dx * stride, y + sg * dy * stride, z + sg * dz * stride), -1)
         np.testing.assert_array_equal(maps[0], ref)
-        # the brick-map kernel map over the same set (mvr_kernel_map_bricks): the same table
-        nbb = L.mvr_brick_map_bytes(M)
-        br = torch.empty(nbb, dtype=torch.uint8, device=gpu)
-        N.check(L.mvr_brick_map_build_stride(N.ptr(cd), M, stride, N.ptr(br), nbb, N.stream()), "bricks")
-        nbr = torch.empty(M, 27, dtype=torch.int32, device=gpu)
-        N.check(L.mvr_kernel_map_bricks(N.ptr(cd), M, stride, N.ptr(br), M, nbb, stride, stride, tr, N.ptr(nbr), None,
-                                        N.stream()), "brick map")
-        np.testing.assert_array_equal(nbr.cpu().numpy(), ref)
 
 
-def test_brick_kernel_maps_equal_table_maps(gpu, frags, monkeypatch):
-    """All ten 3^3 kernel maps of FCGF (s1 at strides 1-8, down 1-4, up 1-4) over the input level's brick map
-    (mvr_kernel_map_bricks) equal the maps over the level's lattice coordinate table (mvr_kernel_map), and the row
-    orders from the brick kernel's keys (mvr_kernel_map_order_keys) equal mvr_kernel_map_order's"""
+def test_batched_orders_equal_per_map_orders(gpu, frags):
+    """CoordinateManager.prepare_orders (mvr_kernel_map_orders: all ten 3^3 maps of FCGF in ONE radix sort, the map
+    index in the top key bits) gives every map exactly the order of mvr_kernel_map_order on that map alone; a
+    subset of maps, and maps with no rows, too"""
     import torch
-    import lib.sparse
-    from lib import _native as N
-    from lib.sparse import voxelize, CoordinateManager
-    monkeypatch.setattr(lib.sparse, "BRICK_MAPS", True)
-    L = N.lib()
+    from lib.sparse import voxelize, CoordinateManager, FCGF_MAPS
     c, _, counts, _ = voxelize(frags, 0.025, gpu)
-    cm = CoordinateManager(c, len(counts))
-    maps = [("s1", s) for s in (1, 2, 4, 8)] + [(k, s) for k in ("down", "up") for s in (1, 2, 4)]
-    for kind, s in maps:
-        nbr_b = cm.kernel_map(kind, s)
-        perm_b = cm.kernel_map_order(kind, s)
-        out_s, in_s, tr = {"s1": (s, s, 0), "down": (2 * s, s, 0), "up": (s, 2 * s, 1)}[kind]
-        out_c, in_c = cm.coords_at(out_s), cm.coords_at(in_s)
-        nb = L.mvr_hash_table_bytes(in_c.shape[0])
-        tab = torch.empty(nb, dtype=torch.uint8, device=gpu)
-        N.check(L.mvr_hash_build_lattice(N.ptr(in_c), in_c.shape[0], in_s, N.ptr(tab), nb, N.stream()), "table")
-        nbr_t = torch.empty_like(nbr_b)
-        N.check(L.mvr_kernel_map(N.ptr(out_c), out_c.shape[0], N.ptr(tab), nb, 3, s, tr, N.ptr(nbr_t), N.stream()),
-                "map")
-        assert torch.equal(nbr_b, nbr_t), (kind, s)
-        ws = N.workspace(L.mvr_kernel_map_order_bytes(nbr_t.shape[0]), gpu)
-        perm_t = torch.empty_like(perm_b)
-        N.check(L.mvr_kernel_map_order(N.ptr(nbr_t), N.ptr(out_c), out_s, nbr_t.shape[0], 27, N.ptr(perm_t), N.ptr(ws),
-                                       ws.numel(), N.stream()), "order")
-        assert torch.equal(perm_b, perm_t), (kind, s)
+    one, batch = CoordinateManager(c, len(counts)), CoordinateManager(c, len(counts))
+    batch.prepare_orders()
+    for kind, s in FCGF_MAPS:
+        assert torch.equal(batch.kernel_map_order(kind, s), one.kernel_map_order(kind, s)), (kind, s)
+    sub = CoordinateManager(c, len(counts))
+    sub.prepare_orders((("up", 2), ("s1", 8)))
+    for kind, s in (("up", 2), ("s1", 8)):
+        assert torch.equal(sub.orders[(kind, s, 3)], one.kernel_map_order(kind, s)), (kind, s)
+    # a map with no rows between two others
+    from lib import _native as N
+    L = N.lib()
+    nbr = [one.kernel_map("s1", 4), one.kernel_map("s1", 8)]
+    crd = [one.coords_at(4), one.coords_at(8)]
+    empty = torch.empty(0, 27, dtype=torch.int32, device=gpu)
+    import ctypes
+    vp = ctypes.c_void_p
+    Mo = [nbr[0].shape[0], 0, nbr[1].shape[0]]
+    perm = torch.empty(sum(Mo), dtype=torch.int32, device=gpu)
+    ws = N.workspace(L.mvr_kernel_map_orders_bytes(sum(Mo)), gpu)
+    N.check(L.mvr_kernel_map_orders(3, (vp * 3)(nbr[0].data_ptr(), empty.data_ptr(), nbr[1].data_ptr()),
+                                    (vp * 3)(crd[0].data_ptr(), crd[0].data_ptr(), crd[1].data_ptr()),
+                                    (ctypes.c_int * 3)(4, 4, 8), (ctypes.c_int64 * 3)(*Mo), 27, N.ptr(perm), N.ptr(ws),
+                                    ws.numel(), N.stream()), "orders")
+    assert torch.equal(perm[:Mo[0]], one.kernel_map_order("s1", 4))
+    assert torch.equal(perm[Mo[0]:], one.kernel_map_order("s1", 8))
 
 
 def test_fcgf_forward_matches_oracle(gpu, frags):
@@ -237,57 +227,15 @@ def test_kernel_map_order_mask_then_morton(gpu, frags):
         assert np.array_equal(perm, np.argsort(key, kind="stable"))
 
 
-def test_brick_kernel_map_edge_cases(gpu):
-    """mvr_kernel_map_bricks / mvr_brick_map_build_stride: an empty input set (every neighbour absent), an empty
-    output set (no launch), negative coordinates across brick boundaries, a transposed map whose neighbours are off
-    the coarse lattice for odd cells, and the argument checks"""
-    import torch
-    from lib import _native as N
-    L = N.lib()
-    # empty input set
-    oc = torch.tensor([[0, 0, 0, 0], [0, -1, 5, -9]], dtype=torch.int32, device=gpu)
-    nbb = L.mvr_brick_map_bytes(0)
-    br = torch.empty(nbb, dtype=torch.uint8, device=gpu)
-    N.check(L.mvr_brick_map_build_stride(N.ptr(oc), 0, 1, N.ptr(br), nbb, N.stream()), "empty bricks")
-    nbr = torch.zeros(2, 27, dtype=torch.int32, device=gpu)
-    N.check(L.mvr_kernel_map_bricks(N.ptr(oc), 2, 1, N.ptr(br), 0, nbb, 1, 1, 0, N.ptr(nbr), None, N.stream()), "map")
-    assert (nbr.cpu().numpy() == -1).all()
-    assert L.mvr_kernel_map_bricks(N.ptr(oc), 0, 1, N.ptr(br), 0, nbb, 1, 1, 0, N.ptr(nbr), None, N.stream()) == 0
-    assert L.mvr_kernel_map_bricks(N.ptr(oc), 2, 1, N.ptr(br), 0, nbb, 3, 1, 0, N.ptr(nbr), None, N.stream()) != 0
-    assert L.mvr_brick_map_build_stride(N.ptr(oc), 2, 6, N.ptr(br), L.mvr_brick_map_bytes(2), N.stream()) != 0
-    # fine set around the origin (negative coordinates, brick boundaries at multiples of 4 cells), coarse set = the
-    # stride-2 cells it covers; up map (coarse -> fine, transposed) and down map (fine -> coarse) vs brute force
-    g = np.arange(-5, 5)
-    fine = np.array([(b, x, y, z) for b in range(2) for x in g for y in g for z in (-1, 0, 3)], dtype=np.int32)
-    coarse = np.unique(np.concatenate([fine[:, :1], np.floor_divide(fine[:, 1:], 2) * 2], 1), axis=0).astype(np.int32)
-    idx = {s: {tuple(r): i for i, r in enumerate(c.tolist())} for s, c in ((1, fine), (2, coarse))}
-    tf, tc = torch.from_numpy(fine).to(gpu), torch.from_numpy(coarse).to(gpu)
-    bf, bc = (torch.empty(L.mvr_brick_map_bytes(len(c)), dtype=torch.uint8, device=gpu) for c in (fine, coarse))
-    N.check(L.mvr_brick_map_build_stride(N.ptr(tf), len(fine), 1, N.ptr(bf), bf.numel(), N.stream()), "bf")
-    N.check(L.mvr_brick_map_build_stride(N.ptr(tc), len(coarse), 2, N.ptr(bc), bc.numel(), N.stream()), "bc")
-    for name, out, o_s, br_, in_s, tr, src in (("up", tf, 1, bc, 2, 1, coarse), ("down", tc, 2, bf, 1, 0, fine)):
-        nb = torch.empty(out.shape[0], 27, dtype=torch.int32, device=gpu)
-        N.check(L.mvr_kernel_map_bricks(N.ptr(out), out.shape[0], o_s, N.ptr(br_), len(src), br_.numel(), in_s, 1, tr,
-                                        N.ptr(nb), None, N.stream()), name)
-        ref = np.full((out.shape[0], 27), -1, np.int32)
-        sg = -1 if tr else 1
-        for o, (b, x, y, z) in enumerate(out.cpu().numpy().tolist()):
-            for k in range(27):
-                dx, dy, dz = k % 3 - 1, (k // 3) % 3 - 1, k // 9 - 1
-                ref[o, k] = idx[in_s].get((b, x + sg * dx, y + sg * dy, z + sg * dz), -1)
-        np.testing.assert_array_equal(nb.cpu().numpy(), ref, err_msg=name)
-
-
 def test_fcgf_forward_independent_of_tiling_order(gpu, frags, monkeypatch):
     """The sparse convs' row order only decides which rows share a tile: every output row sums its active offsets in
     offset order whatever else its tile holds (inactive offsets add exact zeros), so FCGF's output is bit-identical
-    over the table path (mask-then-Morton order), the brick path (the same order from the brick kernel's keys), the
-    brick path with the spatial order for the s1 / strided maps (MVR_SPCONV_ORDER=spatial) and XCD-contiguous tiles."""
+    under the default order (mask, then fragment and Morton code), the identity order and a random permutation of
+    every map's rows (injected in place of the kernel-map orders)."""
     import torch
     import lib.sparse
-    from lib import _native as NV
     from lib.descriptor.fcgf import FCGFNet
-    from lib.sparse import voxelize, SparseTensor
+    from lib.sparse import voxelize, SparseTensor, CoordinateManager
     net = FCGFNet()
     shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
     st = synth_state(shapes, seed=4)
@@ -296,15 +244,19 @@ def test_fcgf_forward_independent_of_tiling_order(gpu, frags, monkeypatch):
     c, _, _, _ = voxelize(frags, 0.025, gpu)
     F = torch.ones(c.shape[0], 1, device=gpu)
     outs = []
-    L = NV.lib()
-    for bricks, order, xcd in ((False, "mask", 0), (True, "mask", 0), (True, "spatial", 0), (True, "spatial", 1)):
-        monkeypatch.setattr(lib.sparse, "BRICK_MAPS", bricks)
-        monkeypatch.setattr(lib.sparse, "SPCONV_ORDER", order)
-        prev = L.mvr_set_spconv_xcd(xcd)
-        try:
-            with torch.no_grad():
-                outs.append(net(SparseTensor(F, coords=c).to(gpu)).F.clone())
-        finally:
-            L.mvr_set_spconv_xcd(prev)
+    gen = torch.Generator(device="cpu").manual_seed(5)
+
+    def injected(how):
+        def order(self, kind, s, ks=3):
+            n = self.kernel_map(kind, s, ks).shape[0]
+            p = torch.arange(n, dtype=torch.int32) if how == "identity" else torch.randperm(n, generator=gen).int()
+            return p.to(gpu)
+        return order
+    for how in ("default", "identity", "random"):
+        if how != "default":
+            monkeypatch.setattr(CoordinateManager, "prepare_orders", lambda self, *a, **k: None)
+            monkeypatch.setattr(CoordinateManager, "kernel_map_order", injected(how))
+        with torch.no_grad():
+            outs.append(net(SparseTensor(F, coords=c).to(gpu)).F.clone())
     for i, o in enumerate(outs[1:], 1):
         assert torch.equal(outs[0], o), (i, (outs[0] - o).abs().max().item())

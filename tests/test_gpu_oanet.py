@@ -163,6 +163,11 @@ def test_oanet_full_train_golden(gpu, conv2):
             # docstring and DESIGN §3.2)
             assert (d64 <= np.maximum(1e-4, np.maximum(2 * e, 3 * spread))).all(), (i, k, d64, e, spread)
             assert (d <= 1e-4).sum() >= 28, (i, k, d)
+            # and every pair beyond 1e-4 of the reference's fp32 is a rounding-sensitive one: the reference's own
+            # fp32 result or our result under another diff_pool summation order moves >= 3e-5 (round 5 diagnosis,
+            # tools/diag_stress.py: block 0 R pair 9 (spread 9.5e-5), block 1 pairs 28 (the reference 2.5e-4 from
+            # exact, ours 6.8e-5), 22 (spread 8.8e-5) and 0 (spread 4.5e-5, the reference 3.9e-5 from exact))
+            assert np.all((d <= 1e-4) | (np.maximum(e, spread) >= 3e-5)), (i, k, d, e, spread)
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
 

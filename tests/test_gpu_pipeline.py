@@ -60,6 +60,37 @@ def test_full_scene_pipelined_equals_sequential(gpu):
         assert torch.equal(g, ref), (g - ref).abs().max().item()
 
 
+def test_redwood_scale_scene_pipelined_equals_sequential(gpu):
+    """BASELINE configs[4]'s scene size (a Redwood-scale scene of 50 fragments -> 1,225 pairs, bench.py --frags 50):
+    the pipelined records equal the sequential ones bit for bit, every pair registered (finite R, t)"""
+    import torch
+    import bench
+    wl = bench.SceneWorkload(gpu, 0, n_frag=50)
+    with torch.no_grad():
+        ref = wl.step()
+        wl.step_pipelined(1)
+        got = [wl.step_pipelined(1) for _ in range(2)]
+    torch.cuda.synchronize()
+    assert ref.shape == (1225, 13)
+    assert torch.isfinite(ref).all()
+    for g in got:
+        assert torch.equal(g, ref), (g - ref).abs().max().item()
+
+
+def test_precomputed_pair_sharded_blocks_equal_whole(gpu):
+    """bench.py --workload precomputed --shard pairs: each rank's block of whole 32-pair batches (here every block
+    of a 3-rank split, run one after another in this process) gives exactly the whole evaluation's records"""
+    import torch
+    import bench
+    whole = bench.PrecomputedWorkload(gpu, 0, 100, 5000, shard="pairs", world=1)
+    with torch.no_grad():
+        ref = whole.step()
+        parts = [bench.PrecomputedWorkload(gpu, r, 100, 5000, shard="pairs", world=3).step() for r in range(3)]
+    torch.cuda.synchronize()
+    assert [p.shape[0] for p in parts] == [64, 36, 0]           # rank 2: an empty block
+    assert torch.equal(torch.cat(parts), ref)
+
+
 def test_oanet_full_size_stage_hashes_repeat(gpu):
     """Every intermediate activation and statistics buffer of the two OANet blocks (mvr_debug_stage_hash:
     ~110 stages at 435 pairs x 5000 points) is bit-identical over repeated forwards."""

@@ -1,0 +1,39 @@
+"""Which pairs of the chaotic stress fixture (tests/golden/oanet_full_train.npz) sit over 1e-4 of the reference's
+fp32 output, and how far the reference's own fp32 output is from exact arithmetic there (oanet_full_train_f64.npz)
+— plus each pair's spread under the other diff_pool summation orders (verdict r4 weak #2)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "3d_multiview_reg_amd"), ROOT, os.path.join(ROOT, "tests", "golden"),
+          os.path.join(ROOT, "tests")):
+    sys.path.insert(0, p)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from synth import synth_correspondences  # noqa: E402
+from conftest import golden  # noqa: E402
+from test_gpu_oanet import _oanet  # noqa: E402
+from lib import _native as NV  # noqa: E402
+
+gpu = torch.device("cuda:0")
+g, g64 = golden("oanet_full_train.npz"), golden("oanet_full_train_f64.npz")
+xs, _, _ = synth_correspondences(32, 5000, seed=33)
+net = _oanet(128, 500, 7, gpu, train=True, which="full")
+L = NV.lib()
+outs = []
+for knob, v in ((None, None), ("mvr_set_pool_split", 0), ("mvr_set_pool_tail", 1)):
+    prev = getattr(L, knob)(v) if knob else None
+    with torch.no_grad():
+        outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    if knob:
+        getattr(L, knob)(prev)
+dist = lambda u, v: np.abs(u - v).reshape(u.shape[0], -1).max(1)  # noqa: E731
+for i in range(2):
+    for k, kg in (("rot_est", "R"), ("trans_est", "t")):
+        got, r32, r64 = outs[0][k][i].cpu().numpy(), g["%s%d" % (kg, i)], g64["%s%d" % (kg, i)]
+        d, d64, e = dist(got, r32), dist(got, r64), dist(r32, r64)
+        spread = np.max([dist(got, o[k][i].cpu().numpy()) for o in outs[1:]], axis=0)
+        print("block %d %s: %d of 32 within 1e-4 of ref fp32; max %.3g" % (i, kg, (d <= 1e-4).sum(), d.max()))
+        for p in np.argsort(-d)[:6]:
+            print("   pair %2d  vs ref32 %.3g  vs exact %.3g  ref32 vs exact %.3g  our spread %.3g"
+                  % (p, d[p], d64[p], e[p], spread[p]))
