@@ -20,6 +20,7 @@
 // FLOPs per pair ~ 2*N*M*C (MFMA) + N*M*(exp + ~6 VALU); HBM: features/coords of the two
 // fragments (L2/MALL-resident across the pairs that share them).
 #include "common.hpp"
+#include "knobs.hpp"
 #include "prof.hpp"
 
 namespace mvr {
@@ -692,7 +693,7 @@ __global__ void nn_presplit_kernel(const float* __restrict__ Ft, int64_t ft_fs, 
   }
 }
 
-int g_nn_fast = 1;   // mvr_set_feat_nn_fast: 0 online path only, 1 fast path split-bf16 (default), 2 fast path split-fp16
+int g_feat_nn_fast = 1;   // knobs.hpp: 0 online path only, 1 fast path split-bf16 (default), 2 fast path split-fp16
 
 // MODE 0 (soft) with a.fast: the bounded-shift path, falling back to the online path for a workgroup
 // whose softmax sums underflowed; otherwise the online path (MODE 1 argmax, 2 two nearest).
@@ -777,11 +778,11 @@ extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* 
   if (mode != 0 && mode != 1) return MVR_EINVAL;
   if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt,
-                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out, mvr::g_nn_fast,
+                inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out, mvr::g_feat_nn_fast,
                 nullptr, 0};
   // the split-bf16 fast path stages its targets from a pre-split image when the caller gives the workspace (the
   // pair list's target fragments must be < n_frag)
-  if (workspace && mode == 0 && mvr::g_nn_fast == 1) {
+  if (workspace && mode == 0 && mvr::g_feat_nn_fast == 1) {
     const int nst = (Mt + mvr::NN_STAGE - 1) / mvr::NN_STAGE;
     const int64_t n = (int64_t)n_frag * nst * mvr::NN_STAGE * 2;
     hipLaunchKernelGGL(mvr::nn_presplit_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, Ft, ft_fstride,
@@ -834,8 +835,3 @@ extern "C" int mvr_gather_rows(const float* src, int C, const int64_t* idx, int 
   return MVR_OK;
 }
 
-extern "C" int mvr_set_feat_nn_fast(int on) {
-  const int prev = mvr::g_nn_fast;
-  mvr::g_nn_fast = on < 0 ? 0 : on > 2 ? 2 : on;
-  return prev;
-}

@@ -30,6 +30,7 @@
 #include <utility>
 
 #include "common.hpp"
+#include "knobs.hpp"
 #include "gemm.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
@@ -1315,153 +1316,6 @@ __global__ __launch_bounds__(C2_THREADS, 1) void oaf_conv2_kernel(GemmArgs g, co
 #endif
 }
 
-// The same product on 128 x 128 tiles at two workgroups per CU (mvr_set_oaf_conv2(2)): one 48-KB stage slot per
-// workgroup, A and B both staged through registers one stage ahead (A folded + split, B copied from the weight image),
-// two barriers per stage.  One workgroup's epilogue (its residual read and output write) and barriers then overlap
-// the other's MFMAs, which the 128 x 256 kernel above cannot (one workgroup per CU).  The epilogue is the generic
-// kernel's (tile_epilogue, the same 2 x 2 wave layout).
-constexpr int C2B_BN = 128, C2B_THREADS = 256;
-constexpr int C2B_APL = 128 * C2_BK, C2B_BPL = C2B_BN * C2_BK;   // bf16 per plane and stage (8 KB each)
-
-__global__ __launch_bounds__(C2B_THREADS, 2) void oaf_conv2b_kernel(GemmArgs g, const uint16_t* __restrict__ img) {
-  __shared__ __attribute__((aligned(16))) uint16_t sa[3 * C2B_APL];
-  __shared__ __attribute__((aligned(16))) uint16_t sb[3 * C2B_BPL];
-  __shared__ __attribute__((aligned(16))) float fsv[2][2][C2_KMAX + C2_BK];   // [tile parity][scale | shift][k]
-  __shared__ float2 red[2 * BM];
-  __shared__ float redm[2 * BM];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
-  const int l32 = lane & 31, kh = lane >> 5;
-  const int N = g.N, K = g.K;
-  const int ntn = (N + C2B_BN - 1) / C2B_BN;
-  const int Npad = c2_npad(N), nks = c2_nks(K);
-  const int ntiles = ntn * g.batch;
-  const int G = gridDim.x, slot = xcd_slot();
-  const int my_tiles = (ntiles - slot + G - 1) / G;
-  const int S = my_tiles * nks;
-  if (S <= 0) return;
-
-  // A: thread -> row t >> 1, k 16 (t & 1) .. + 15 (64 bytes of fp32); B: 6 of the stage's 1536 16-byte image chunks
-  const int am = tid >> 1, ah = tid & 1;
-  f32x4 ra[4];
-  u32x4 rb[6];
-  auto issue = [&](int gs) {
-    const int t = slot + (gs / nks) * G, ks = gs % nks;
-    const int b = t / ntn, tn = t % ntn;
-    const float* Ar = g.A + (int64_t)b * g.sAb + (int64_t)am * g.lda;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = min(ks * C2_BK + 16 * ah + 4 * q, K - 4);   // clamped into the row; zeroed past K at the fold
-      ra[q] = *reinterpret_cast<const f32x4*>(Ar + k);
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int id = tid + C2B_THREADS * q, p = id >> 9, c = id & 511;
-      rb[q] = *reinterpret_cast<const u32x4*>(img + (((int64_t)p * nks + ks) * Npad + (int64_t)tn * C2B_BN) * C2_BK +
-                                                8 * c);
-    }
-  };
-  const int q4 = K / 4;
-  f32x4 fv;
-  auto load_fold = [&](int i) {
-    const int b = (slot + min(i, my_tiles - 1) * G) / ntn;
-    if (tid < 2 * q4)
-      fv = *reinterpret_cast<const f32x4*>((tid < q4 ? g.psc : g.psh) + (int64_t)b * g.sPb + 4 * (tid < q4 ? tid : tid - q4));
-  };
-  auto store_fold = [&](int i) {
-    if (tid < 2 * q4) *reinterpret_cast<f32x4*>(&fsv[i & 1][tid < q4 ? 0 : 1][4 * (tid < q4 ? tid : tid - q4)]) = fv;
-  };
-  auto store = [&](int gs) {   // fold + split A, copy B: registers of stage gs -> the slot
-    const int ks = gs % nks, par = (gs / nks) & 1;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int k = ks * C2_BK + 16 * ah + 8 * hh;
-      const float* fs = fsv[par][0] + k;
-      const float* fh = fsv[par][1] + k;
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = k + e < K ? fmaxf(fmaf(ra[2 * hh][e], fs[e], fh[e]), 0.f) : 0.f;
-        v[4 + e] = k + 4 + e < K ? fmaxf(fmaf(ra[2 * hh + 1][e], fs[4 + e], fh[4 + e]), 0.f) : 0.f;
-      }
-      u32x4 H, Mm, L;
-      split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), H, Mm, L);
-      const int c = 2 * ah + hh;
-      const int pos = am * C2_BK + 8 * (c ^ ((am >> 2) & 3));
-      *reinterpret_cast<u32x4*>(sa + pos) = H;
-      *reinterpret_cast<u32x4*>(sa + C2B_APL + pos) = Mm;
-      *reinterpret_cast<u32x4*>(sa + 2 * C2B_APL + pos) = L;
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int id = tid + C2B_THREADS * q, p = id >> 9, c = id & 511;
-      *reinterpret_cast<u32x4*>(sb + p * C2B_BPL + 8 * c) = rb[q];
-    }
-  };
-
-  floatx16 acc[2][2];
-#pragma unroll
-  for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
-  load_fold(0);
-  store_fold(0);
-  issue(0);
-  for (int gs = 0; gs < S; ++gs) {
-    const int ks = gs % nks, ti = gs / nks;
-    if (ks == 0) {
-      load_fold(ti + 1);
-      if (nks < 3) store_fold(ti + 1);
-    } else if (ks == 1 && nks >= 3) {
-      store_fold(ti + 1);
-    }
-    lds_barrier();   // every wave has read the slot's previous stage (and the fold vectors stored are visible)
-    store(gs);
-    issue(min(gs + 1, S - 1));   // the next stage's registers, in flight during this stage's MFMAs
-    lds_barrier();   // the slot holds stage gs
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const int cc = 2 * st + kh;
-      bx::Frag fa[2], fb[2];
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        const int r = wm * 64 + ii * 32 + l32;
-        const int o = r * C2_BK + 8 * (cc ^ ((r >> 2) & 3));
-        fa[ii].h = *reinterpret_cast<const bf16x8*>(sa + o);
-        fa[ii].m = *reinterpret_cast<const bf16x8*>(sa + C2B_APL + o);
-        fa[ii].l = *reinterpret_cast<const bf16x8*>(sa + 2 * C2B_APL + o);
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int r = wn * 64 + j * 32 + l32;
-        const int o = r * C2_BK + 8 * (cc ^ ((r >> 2) & 3));
-        fb[j].h = *reinterpret_cast<const bf16x8*>(sb + o);
-        fb[j].m = *reinterpret_cast<const bf16x8*>(sb + C2B_BPL + o);
-        fb[j].l = *reinterpret_cast<const bf16x8*>(sb + 2 * C2B_BPL + o);
-      }
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[ii][j] = bx::mfma6(fa[ii], fb[j], acc[ii][j]);
-    }
-    if (ks == nks - 1) {
-      const int t = slot + ti * G;
-      tile_epilogue<BIAS_N, ST_ROW, 1>(g, acc, t / ntn, 0, t % ntn, red, redm);
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[ii][j][r] = 0.f;
-    }
-  }
-}
-
-int g_cu_budget = 256;   // mvr_set_cu_budget: CUs the persistent grids are sized for
-int g_oaf_conv2 = 1;   // mvr_set_oaf_conv2 (default on: 0.25 vs 0.30 ms per launch, oafilter 2.08 vs 2.38 ms per step)
 
 static bool oaf_conv2_covers(const GemmArgs& g) {
   return g.wimg && g.M == 128 && g.pro == PRO_A_K && g.bkc == 1 && g.sBb == 0 && g.bias_mode == BIAS_N &&
@@ -1477,16 +1331,8 @@ static int launch_oaf_conv2(const GemmArgs& g, hipStream_t s) {
   hipLaunchKernelGGL(oaf_w_image_kernel, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, s, g.B, g.N, g.K, g.ldb,
                      Npad, nks, g.wimg);
   MVR_CHECK_LAUNCH();
-  if (g_oaf_conv2 >= 2) {   // 128 x 128 tiles, two workgroups per CU; 3: one workgroup per tile (no persistent
-                            // grid: under another stream's kernels the tiles go to whichever CU frees up)
-    const long long tiles = (long long)((g.N + C2B_BN - 1) / C2B_BN) * g.batch;
-    const unsigned wgs = (unsigned)(g_oaf_conv2 == 3 || tiles < 2 * g_cu_budget ? tiles : 2 * g_cu_budget);
-    hipLaunchKernelGGL(oaf_conv2b_kernel, dim3(wgs), dim3(C2B_THREADS), 0, s, g, (const uint16_t*)g.wimg);
-    MVR_CHECK_LAUNCH();
-    return MVR_OK;
-  }
   const long long tiles = (long long)(Npad / C2_BN) * g.batch;
-  const unsigned wgs = (unsigned)(tiles < g_cu_budget ? tiles : g_cu_budget);   // one 144-KB-LDS workgroup per CU
+  const unsigned wgs = (unsigned)(tiles < GPU_CUS ? tiles : GPU_CUS);   // one 144-KB-LDS workgroup per CU
   hipLaunchKernelGGL(oaf_conv2_kernel, dim3(wgs), dim3(C2_THREADS), 0, s, g, (const uint16_t*)g.wimg);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
@@ -1495,7 +1341,7 @@ static int launch_oaf_conv2(const GemmArgs& g, hipStream_t s) {
 #ifndef GEMM_F16_DEFAULT
 #define GEMM_F16_DEFAULT 0
 #endif
-int g_gemm_h = GEMM_F16_DEFAULT;   // mvr_set_gemm_f16: MATH_BF16X3 launches run split-fp16 first
+int g_gemm_h = GEMM_F16_DEFAULT;   // mvr_set_math: MATH_BF16X3 launches run split-fp16 first
 
 template <int PRO, int BKC, int BIAS, int STATS, int RES>
 static void launch_t(const KArgs& ka0, long long tiles, hipStream_t s) {
@@ -1541,7 +1387,7 @@ static int launch_gemm_impl(const GemmArgs& g, hipStream_t s, bool conv2) {
   if (!ok) return MVR_EINVAL;
   KArgs ka{};
   ka.g = g;
-  ka.persist = 2 * g_cu_budget;  // 2 workgroups per CU (LDS-bound), 256 CUs unless mvr_set_cu_budget
+  ka.persist = 2 * GPU_CUS;  // 2 workgroups per CU (LDS-bound)
   ka.m_fast = (g.sAb == 0 && gemm_mtiles(g.M) > 1) ? 1 : 0;
   const long long tiles = (long long)gemm_ntiles(g.N) * gemm_mtiles(g.M) * g.batch;
   if (tiles > 0x7fffffffLL) return MVR_EINVAL;
@@ -1554,7 +1400,7 @@ static int launch_gemm_impl(const GemmArgs& g, hipStream_t s, bool conv2) {
   }
   ProfScope prof(g.prof_kind, fl, by, s);
   if (pconv_covers(g)) return launch_pconv(g, s);
-  if (conv2 && oaf_conv2_covers(g)) return launch_oaf_conv2(g, s);
+  if (conv2 && oaf_conv2_covers(g)) return launch_oaf_conv2(g, s);   // (not under FORCE_GENERIC_GEMM)
   if (g.head_w) return MVR_EINVAL;   // the fused head exists on the point-conv kernel only
   // Dispatch only the combinations the OANet schedule uses (oanet.hip).
 #define MVR_CASE(P, BKC_, BI, ST, RS)                                                                     \
@@ -1580,7 +1426,7 @@ static int launch_gemm_impl(const GemmArgs& g, hipStream_t s, bool conv2) {
   return MVR_EINVAL;
 }
 
-int launch_gemm(const GemmArgs& g, hipStream_t s) { return launch_gemm_impl(g, s, g_oaf_conv2 != 0); }
+int launch_gemm(const GemmArgs& g, hipStream_t s) { return launch_gemm_impl(g, s, !g_force[FORCE_GENERIC_GEMM]); }
 
 }  // namespace mvr
 
@@ -1618,7 +1464,7 @@ extern "C" int mvr_gemm_trace(unsigned long long* out, int reset) {
 }
 #endif
 
-// C-ABI: the OAFilter conv2 launch on the split-once kernel whatever mvr_set_oaf_conv2 says (tests): W [N][K]
+// C-ABI: the OAFilter conv2 launch on the split-once kernel (tests; also under FORCE_GENERIC_GEMM): W [N][K]
 // (row stride ldw) shared by every pair, A folded by (psc, psh) per k, bias per n, residual R, row statistics per
 // 128-column tile; img: img_bytes >= mvr_oaf_conv2_image_bytes(N, K) of scratch.  MVR_EINVAL when the shape is not
 // the kernel's (M != 128, K % 4 != 0, a null operand).
@@ -1644,21 +1490,4 @@ extern "C" int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A,
 
 extern "C" size_t mvr_oaf_conv2_image_bytes(int N, int K) { return (size_t)mvr::oaf_conv2_image_bytes(N, K); }
 
-extern "C" int mvr_set_cu_budget(int n) {
-  const int prev = mvr::g_cu_budget;
-  mvr::g_cu_budget = n < 8 ? 8 : (n > 256 ? 256 : n);
-  return prev;
-}
-
-extern "C" int mvr_set_oaf_conv2(int on) {
-  const int prev = mvr::g_oaf_conv2;
-  mvr::g_oaf_conv2 = on >= 1 && on <= 3 ? on : 0;
-  return prev;
-}
-
-extern "C" int mvr_set_gemm_f16(int on) {
-  const int prev = mvr::g_gemm_h;
-  mvr::g_gemm_h = on ? 1 : 0;
-  return prev;
-}
 

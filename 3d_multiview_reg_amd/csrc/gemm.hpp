@@ -2,6 +2,7 @@
 // Used for every 1x1 convolution / pooling matmul of the OANet filter
 // (lib/filtering/oanet.py) — see gemm.hip.
 #pragma once
+#include "knobs.hpp"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -34,11 +35,9 @@ enum Stats : int {
 // six products hh, hm, mh, mm, hl, lh accumulated in fp32 by v_mfma_f32_32x32x16_bf16 — fp32-level
 // accuracy (the dropped ml, lm, ll terms are <= 2^-23 relative) at 6/16 of the fp32 MFMA cycles.
 // MATH_F16X2 (internal): two-term split-fp16 (mfma_bf16.hpp) of A x 2^6 and B x 2^6, 3 MFMAs per product; what a
-// MATH_BF16X3 launch runs first when mvr_set_gemm_f16 is on, with a guarded MATH_BF16X3 re-run when an operand
+// MATH_BF16X3 launch runs first under mvr_set_math(1), with a guarded MATH_BF16X3 re-run when an operand
 // left the split-fp16 window (gemm.hip launch_t).
 enum Math : int { MATH_BF16X3 = 1, MATH_F16X2 = 2 };
-extern int g_gemm_h;         // mvr_set_gemm_f16
-extern int g_pconv_h;        // mvr_set_pconv_math
 
 constexpr int GEMM_BM = 128, GEMM_BN = 128, GEMM_BK = 32;
 
@@ -65,7 +64,7 @@ struct GemmArgs {
   // (columns >= xci zero), xb [128] (nullable)
   int xin; int xci; const float* xw; const float* xb;
   int64_t xld;   // row stride of the block input (xin = 2: R's rows; xin = 1 uses ldb)
-  // MATH_BF16X3 with mvr_set_gemm_f16 / mvr_set_pconv_math on: a zeroed int in device memory owned by this launch
+  // MATH_BF16X3 under mvr_set_math(1): a zeroed int in device memory owned by this launch
   // (stream-ordered); the split-fp16 pass sets it when an operand leaves the fp16 window and the guarded split-bf16
   // pass then recomputes every output.  Null: split-bf16 only.
   int* flag;
@@ -78,7 +77,7 @@ struct GemmArgs {
   float fin_eps2; mvr_bn_p fin_bn2; float* fin_sc2; float* fin_sh2;
   int fin_train; float2* fin_mv; int* fin_done;
   // OAFilter conv2 shape (M = 128, PRO_A_K, B = weights [N][K] shared by every pair, BIAS_N, ST_ROW, residual) with
-  // mvr_set_oaf_conv2 on: scratch for the weights' split-bf16 image (oaf_conv2_image_bytes(N, K) bytes, written
+  // the split-once OAFilter conv2 kernel: scratch for the weights' split-bf16 image (oaf_conv2_image_bytes(N, K) bytes, written
   // by the launch), which routes it to the split-once kernel (gemm.hip oaf_conv2_kernel).  Null: generic kernel.
   uint16_t* wimg; int64_t wimg_bytes;
 };
@@ -100,8 +99,6 @@ int launch_pconv(const GemmArgs& g, hipStream_t stream);
 
 // bytes of the weights' split-bf16 image the OAFilter conv2 kernel reads (GemmArgs.wimg)
 int64_t oaf_conv2_image_bytes(int N, int K);
-extern int g_cu_budget;     // mvr_set_cu_budget
-extern int g_oaf_conv2;      // mvr_set_oaf_conv2
 
 inline int gemm_ntiles(int N){ return (N + GEMM_BN - 1) / GEMM_BN; }
 inline int gemm_mtiles(int M) { return (M + GEMM_BM - 1) / GEMM_BM; }

@@ -153,6 +153,15 @@ template <int H> __device__ __forceinline__ FragT<H> ld_frag(const char* p, int 
   for (int pl = 0; pl < planes<H>(); ++pl) f.p[pl] = *reinterpret_cast<const typename FragT<H>::V*>(p + pl * ps);
   return f;
 }
+// the (h, m, l) split-bf16 planes of one value (split_pair<0>, element for element) at p, p + ld, p + 2 ld: a
+// producer's epilogue writes them beside its fp32 output for the next sparse conv (spconv.hip PS = 1)
+__device__ __forceinline__ void store_planes(uint16_t* p, int64_t ld, float v) {
+  unsigned o[3];
+  split_pair<0>(f32x2{v, 0.f}, o);
+  p[0] = (uint16_t)o[0];
+  p[ld] = (uint16_t)o[1];
+  p[2 * ld] = (uint16_t)o[2];
+}
 // power-of-two scale bringing |x| <= amax to <= 2^14 (amax = 0: 2^14)
 __device__ __forceinline__ float range_scale(float amax) {
   int e;

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "knobs.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
 #include "mvreg.h"
@@ -1108,14 +1109,10 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
   ATEND(8);
 }
 
-#ifndef UNPOOL4_DEFAULT
-#define UNPOOL4_DEFAULT 1
-#endif
-int g_unpool4 = UNPOOL4_DEFAULT;   // mvr_set_unpool4: the 4-wave diff_unpool kernel (0: the 8-wave one, A/B timing)
 #ifndef ATTN_MATH_DEFAULT
 #define ATTN_MATH_DEFAULT 0
 #endif
-int g_attn_h = ATTN_MATH_DEFAULT;  // mvr_set_attn_math: split-fp16 (1) or split-bf16 (0) pool / 4-wave unpool
+int g_attn_h = ATTN_MATH_DEFAULT;  // mvr_set_math: split-fp16 (1) or split-bf16 (0) pool / 4-wave unpool
 
 }  // namespace mvr
 
@@ -1150,13 +1147,15 @@ extern "C" size_t mvr_oan_diff_unpool_workspace_bytes(int P, int channels, int c
 //    give the one-process records bit for bit at the default f32eq maths, tests/test_gpu_distributed.py; under
 //    split16 a guarded launch re-runs in split-bf16 when ANY of its pairs leaves the fp16 window, so there the
 //    precision a pair gets depends on which pairs share its launch);
-//  * mvr_set_pool_tail(1): only a TAIL is split: the pair octets [0, g0) run whole, the rest in k parts,
+//  * POOL_TAIL builds (round 4, not kept): only a TAIL is split: the pair octets [0, g0) run whole, the rest in k parts,
 //    dispatched after them.  Candidates (k in {1, 2, 4} with >= 8 key blocks per part; g0 = every octet, no octet,
 //    or the most octets whose whole units fill complete rounds) are ranked by the makespan of the dispatch order
 //    on `cus` slots (a unit = 1, a part = 1 / k), ties to fewer slabs: fewer slabs (224 instead of 1760 at 435
 //    pairs), but the split of a pair then depends on the batch size and the device's CU count.
 struct PoolSplit { int nks, g0; };
-int g_pool_tail = 0;   // mvr_set_pool_tail
+#ifndef POOL_TAIL
+#define POOL_TAIL 0
+#endif
 static double pool_makespan(int64_t full, int64_t parts, int k, int cus) {
   // greedy in dispatch order: the whole units first, then the parts, each to the earliest free slot
   std::vector<double> slot((size_t)cus, 0.0);
@@ -1172,7 +1171,7 @@ static double pool_makespan(int64_t full, int64_t parts, int k, int cus) {
 }
 static PoolSplit pool_splits(int P, int nqb, int N) {
   const int nkb = (N + AKB - 1) / AKB;
-  if (!g_pool_tail) return nkb >= 16 ? PoolSplit{2, 0} : PoolSplit{1, (P + 7) / 8};
+  if (!POOL_TAIL) return nkb >= 16 ? PoolSplit{2, 0} : PoolSplit{1, (P + 7) / 8};
   int dev = 0, cus = 0;   // the current device's CU count (an attribute query, no process state)
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
@@ -1206,11 +1205,6 @@ static size_t pool_ws_bytes(int P, int clusters, int nks) {
   return (nks > 1 ? slots * ((size_t)nks * PSLAB * 4 + 4) : 0) + 512;
 }
 
-extern "C" int mvr_set_pool_tail(int on) {
-  const int prev = g_pool_tail;
-  g_pool_tail = on ? 1 : 0;
-  return prev;
-}
 
 extern "C" size_t mvr_oan_diff_pool_workspace_bytes(int P, int channels, int clusters) {
   if (P <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return 0;
@@ -1324,7 +1318,7 @@ extern "C" int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t
   a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
   const int64_t nx = (int64_t)P * nkb * 1024;
   const dim3 gw((nkb * 512 + 255) / 256), gx((unsigned)((nx + 255) / 256));
-  if (g_unpool4 && clusters <= 512) {
+  if (!g_force[FORCE_UNPOOL8] && clusters <= 512) {
     a.nqb = (N + U4Q - 1) / U4Q;
     const int grid = ((P + 7) / 8) * 8 * a.nqb;
     const int* guard = nullptr;
@@ -1374,14 +1368,3 @@ extern "C" int mvr_attn_reruns(int reset) {
   return v;
 }
 
-extern "C" int mvr_set_attn_math(int h) {
-  const int prev = mvr::g_attn_h;
-  mvr::g_attn_h = h ? 1 : 0;
-  return prev;
-}
-
-extern "C" int mvr_set_unpool4(int on) {
-  const int prev = mvr::g_unpool4;
-  mvr::g_unpool4 = on ? 1 : 0;
-  return prev;
-}

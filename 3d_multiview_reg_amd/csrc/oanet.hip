@@ -267,14 +267,11 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 // ----------------------------------------------------------------------------
 // Host orchestration
 // ----------------------------------------------------------------------------
-#ifndef OAN_FUSED_DEFAULT
-#define OAN_FUSED_DEFAULT 5
+// InstanceNorm folds finished inside their producing point conv by its last-arriving workgroups instead of a separate
+// finalize launch (bit-identical; measured no faster in the pipelined step): a build-time choice
+#ifndef OAN_FUSED_FIN
+#define OAN_FUSED_FIN 0
 #endif
-int g_oan_fused = OAN_FUSED_DEFAULT;   // mvr_set_oan_fused: bit 0 diff_pool/unpool, bit 2 conv1 folded into the first
-                                       // PointCN, bit 3 InstanceNorm folds finished in their producer's
-                                       // last-arriving workgroups
-                       // (point-conv XI variants); bit 1 is unused
-int g_pool_split = 1;  // mvr_set_pool_split: key-split diff_pool launches (A/B timing)
 
 namespace {
 
@@ -363,7 +360,7 @@ struct Plan {
   int* fcnt;             // FIN_SLOTS x P arrival counters of the fused finalizes (zeroed at the block's start)
   float2 *st11, *stA, *stT, *stD, *stO, *smx, *mv, *stcol;
   int* flags;            // FLAG_SLOTS range flags of the split-fp16 launches (zeroed at the block's start)
-  uint16_t* w2img;       // OAFilter conv2's weight image (mvr_set_oaf_conv2; rewritten by every conv2 launch)
+  uint16_t* w2img;       // OAFilter conv2's weight image (rewritten by every conv2 launch)
   int64_t w2img_bytes;
 };
 
@@ -392,7 +389,7 @@ Plan plan(int C, int Kc, int Cin, int P, int N, void* base) {
   Plan pl{};
   pl.P = P; pl.N = N; pl.C = C; pl.Kc = Kc; pl.Cin = Cin;
   pl.Np = round32(N); pl.Kp = round32(Kc); pl.Cinp = round4(Cin);
-  pl.fused = (g_oan_fused & 1) && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
+  pl.fused = !g_force[FORCE_UNFUSED_ATTN] && mvr_oan_diff_unpool_workspace_bytes(P, C, Kc) > 0;
   const int TS = gemm_ntiles(N);   // statistics tiles over points
   Ws w{reinterpret_cast<char*>(base), 0, 0};
   const size_t PN = (size_t)P * pl.Np, PK = (size_t)P * pl.Kp;
@@ -525,7 +522,7 @@ struct Ctx {
 
   // request the fold in a producer's launch (counter slot, target buffers); zero when out of slots
   void fuse(GemmArgs& g, const FoldReq& f, int* done) {
-    if (!(g_oan_fused & 8) || nfin >= FIN_SLOTS) return;
+    if (!OAN_FUSED_FIN || nfin >= FIN_SLOTS) return;
     g.fin_cnt = pl.fcnt + (size_t)nfin * pl.P;
     g.fin_eps = f.eps; g.fin_bn = f.bn;
     g.fin_sc = fcur ? pl.sc : pl.sc2; g.fin_sh = fcur ? pl.sh : pl.sh2; g.fin_ld = 128;
@@ -608,7 +605,7 @@ struct Ctx {
     g.stats_mode = ST_ROW; g.stats = o2.st; g.st_ld = C; g.st_off = 0;
     g.prof_kind = PK_OAFILTER;
     g.flag = flag();
-    g.wimg = pl.w2img; g.wimg_bytes = pl.w2img_bytes;   // the split-once kernel when mvr_set_oaf_conv2 is on
+    g.wimg = pl.w2img; g.wimg_bytes = pl.w2img_bytes;   // the split-once kernel (not under FORCE_GENERIC_GEMM)
     chk(launch_gemm(g, s));
     finalize_in(o2, 1e-3f, f.bn3);
     return conv(f.conv3, o2, true, xd, &xd, ST_ROW, nullptr, false, next);  // in place: out = conv3(...) + x
@@ -627,17 +624,6 @@ struct Ctx {
 
 using namespace mvr;
 
-extern "C" int mvr_set_pool_split(int on) {
-  const int prev = g_pool_split;
-  g_pool_split = on ? 1 : 0;
-  return prev;
-}
-
-extern "C" int mvr_set_oan_fused(int on) {
-  const int prev = g_oan_fused;
-  g_oan_fused = on & 13;
-  return prev;
-}
 
 extern "C" size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N) {
   return plan(channels, clusters, in_channels, P, N, nullptr).bytes;
@@ -659,7 +645,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (workspace_bytes < pl.bytes) return MVR_EINVAL;
   Ctx cx{pl, s, bn_train ? 1 : 0, bn_train > 1 ? std::min(bn_train, P) : P, g_gemm_h || g_pconv_h};
   if (cx.f16 && hipMemsetAsync(pl.flags, 0, sizeof(int) * FLAG_SLOTS, s) != hipSuccess) return MVR_ELAUNCH;
-  if ((g_oan_fused & 8) && hipMemsetAsync(pl.fcnt, 0, sizeof(int) * FIN_SLOTS * P, s) != hipSuccess)
+  if (OAN_FUSED_FIN && hipMemsetAsync(pl.fcnt, 0, sizeof(int) * FIN_SLOTS * P, s) != hipSuccess)
     return MVR_ELAUNCH;
   const int64_t Np = pl.Np, Kp = pl.Kp;
   const int64_t CN = (int64_t)C * Np;
@@ -690,7 +676,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   f3.stats_mode = ST_ROW; f3.stats = pl.stT; f3.st_ld = C; f3.st_off = 0;
   f3.xin = 1; f3.xci = Cin; f3.xw = pl.W8; f3.xb = blk->conv1.bias; f3.xld = ld;
   f3.prof_kind = PK_CONV_PTS;
-  const bool fold1 = (g_oan_fused & 4) && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
+  const bool fold1 = !g_force[FORCE_NO_CONV1_FOLD] && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
                      pconv_covers(f3);
   // folds the last l1_1 conv fuses: down1's IN(1e-3) + BN for diff_pool, and up1's into scU for diff_unpool
   FoldReq fx11{1e-3f, blk->down_bn};
@@ -758,7 +744,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (pl.fused) {
     cx.chk(mvr_oan_diff_pool_ws(pl.X11, 2 * CN, Np, cx.sc(), cx.sh(), C, blk->down_conv.weight, blk->down_conv.bias, P,
                                 C, N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD), C, 0,
-                                g_pool_split ? pl.uimg : nullptr, pl.uimg_bytes, s));
+                                !g_force[FORCE_POOL_NOSPLIT] ? pl.uimg : nullptr, pl.uimg_bytes, s));
   } else {
     Act e{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, Kc, 0};
     cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);

@@ -46,12 +46,13 @@ namespace mvr {
 #define PCONV_NTL 2   // cache-policy bits of the activation buffer loads: nt (streamed once; -3 % per step's point convs)
 #endif
 
-int g_pconv = 1;   // mvr_set_pconv: 0 routes these convs to gemm_kernel (A/B timing)
-int g_pconv_grid = 1;   // mvr_set_pconv_grid: workgroups per resident slot (1: one persistent round)
+#ifndef PCONV_GRID
+#define PCONV_GRID 1   // workgroups per resident slot (1: one persistent round; >1 / <0: the round-4 grid experiments)
+#endif
 #ifndef PCONV_MATH_DEFAULT
 #define PCONV_MATH_DEFAULT 0
 #endif
-int g_pconv_h = PCONV_MATH_DEFAULT;   // mvr_set_pconv_math: 0 split-bf16 (fp32-equivalent, default), 1 split-fp16
+int g_pconv_h = PCONV_MATH_DEFAULT;   // mvr_set_math: 0 split-bf16 (fp32-equivalent, default), 1 split-fp16
                                       // (re-run in split-bf16 when out of range)
 
 namespace {
@@ -754,7 +755,7 @@ bool pconv_covers(const GemmArgs& g) {
   if ((PCONV_OFF & 8) && g.K == 2 * PC) return false;
   if ((PCONV_OFF & 1) && !g.xin && !g.head_w && g.K == PC) return false;
   if (g.xin) {   // folded conv1: only the two shapes the OANet schedule uses
-    const bool ok = g_pconv && g.math == MATH_BF16X3 && g.M == PC && g.K == PC && !g.bkc && g.sAb == 0 &&
+    const bool ok = !g_force[FORCE_GENERIC_GEMM] && g.math == MATH_BF16X3 && g.M == PC && g.K == PC && !g.bkc && g.sAb == 0 &&
                     g.pro == PRO_B_K && g.stats_mode == ST_ROW && !g.head_w && !g.no_store && g.bias_mode != BIAS_N &&
                     g.N > CH && g.xw && g.xci >= 1 && g.xci <= 8 && (g.xin != 2 || (g.xld % 4 == 0 && g.xld >= round4(g.N)));
     return ok && ((g.xin == 1 && !g.has_res) || (g.xin == 2 && g.has_res));
@@ -763,7 +764,7 @@ bool pconv_covers(const GemmArgs& g) {
   // statistics-only passes (the fused PointCN's conv3 pass): 128 -> 128 with the prologue, no residual
   if (g.no_store && !g.head_w && !(g.stats_mode == ST_ROW && !g.has_res && g.K == PC && g.pro == PRO_B_K)) return false;
   if (g.K == 2 * PC && (g.has_res || g.head_w)) return false;   // KS = 16 runs the 256 -> 128 convs only
-  return g_pconv && g.math == MATH_BF16X3 && g.M == PC && (g.K == PC || g.K == 2 * PC) && !g.bkc && g.sAb == 0 &&
+  return !g_force[FORCE_GENERIC_GEMM] && g.math == MATH_BF16X3 && g.M == PC && (g.K == PC || g.K == 2 * PC) && !g.bkc && g.sAb == 0 &&
          (g.pro == PRO_NONE || g.pro == PRO_B_K) && (g.stats_mode == ST_NONE || g.stats_mode == ST_ROW) &&
          g.bias_mode != BIAS_N && g.N > CH;
 }
@@ -784,12 +785,10 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
   a.hw = g.head_w; a.hb = g.head_bp; a.logits = g.logits; a.scores = g.scores; a.pos = g.pos;
   a.xci = g.xci; a.xw = g.xw; a.xb = g.xb; a.rld = g.xld;
   const int ks = g.K / 16;
-  // resident workgroups (2 / 1 per CU); g_pconv_grid > 1: that many contiguous group ranges per slot, dealt by the
-  // dispatcher as slots free up (balances against another stream's kernels holding some CUs)
-  // g_pconv_grid < 0: a persistent grid of 1 / |g_pconv_grid| of the resident slots (leaves register file for another
-  // stream's workgroups on every CU)
-  const int64_t res_slots = (ks == 8 ? 2 : 1) * (int64_t)g_cu_budget;
-  const int64_t slots = g_pconv_grid > 0 ? res_slots * g_pconv_grid : res_slots / -g_pconv_grid;
+  // resident workgroups (2 / 1 per CU), one persistent round (PCONV_GRID > 1: that many contiguous group ranges per
+  // slot; < 0: 1 / |PCONV_GRID| of the slots — both measured slower in the pipeline)
+  const int64_t res_slots = (ks == 8 ? 2 : 1) * (int64_t)GPU_CUS;
+  const int64_t slots = PCONV_GRID > 0 ? res_slots * PCONV_GRID : res_slots / -PCONV_GRID;
   const int grid = (int)(a.groups < slots ? a.groups : slots);
   const int pro = g.pro == PRO_B_K, res = g.has_res != 0, st = g.stats_mode == ST_ROW;
   const int head = g.head_w ? (g.no_store ? 2 : 1) : 0;
@@ -865,20 +864,3 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace mvr
 
-extern "C" int mvr_set_pconv_math(int h) {
-  const int prev = mvr::g_pconv_h;
-  mvr::g_pconv_h = h ? 1 : 0;
-  return prev;
-}
-
-extern "C" int mvr_set_pconv_grid(int mul) {
-  const int prev = mvr::g_pconv_grid;
-  mvr::g_pconv_grid = mul == -2 || mul == -4 ? mul : (mul < 1 ? 1 : (mul > 64 ? 64 : mul));
-  return prev;
-}
-
-extern "C" int mvr_set_pconv(int on) {
-  const int prev = mvr::g_pconv;
-  mvr::g_pconv = on ? 1 : 0;
-  return prev;
-}

@@ -459,7 +459,7 @@ struct C1Smem {
 __global__ __launch_bounds__(512) void spconv_c1_brick_kernel(BrickView bv, const float* __restrict__ feat,
                                                               const float* __restrict__ W, mvr_bn_p bn,
                                                               float bn_eps, int relu, float* __restrict__ out,
-                                                              int64_t ldout) {
+                                                              int64_t ldout, uint16_t* __restrict__ outp) {
   using namespace bx;
   __shared__ __attribute__((aligned(16))) C1Smem sm;
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hh = lane >> 5;
@@ -555,6 +555,10 @@ __global__ __launch_bounds__(512) void spconv_c1_brick_kernel(BrickView bv, cons
       }
       if (r0 >= 0) out[(int64_t)r0 * ldout + l32] = v0;
       if (r1 >= 0) out[(int64_t)r1 * ldout + l32] = v1;
+      if (outp) {   // the split-bf16 planes for the next sparse conv (spconv.hip PS = 1)
+        if (r0 >= 0) store_planes(outp + (int64_t)r0 * 3 * ldout + l32, ldout, v0);
+        if (r1 >= 0) store_planes(outp + (int64_t)r1 * 3 * ldout + l32, ldout, v1);
+      }
     }
   }
 }
@@ -867,10 +871,12 @@ extern "C" int mvr_brick_map_build(const int32_t* coords, int64_t M, void* ws, s
   return mvr_brick_map_build_stride(coords, M, 1, ws, ws_bytes, s);
 }
 
-extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
-                             size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
-                             mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, hipStream_t s) {
+extern "C" int mvr_spconv_c1_x(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
+                               size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
+                               mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, uint16_t* out_planes,
+                               hipStream_t s) {
   if (Mout < 0 || !in_bricks || !feat || !W || !out || (ksize & 1) == 0 || step <= 0 || Min < 0) return MVR_EINVAL;
+  if (out_planes && (out_coords || (reinterpret_cast<uintptr_t>(out_planes) & 1))) return MVR_EINVAL;   // bricks only
   if (Cout != 32) return MVR_EINVAL;  // FCGF conv1: 1 -> CHANNELS[1] = 32 (fcgf.py:118-125)
   if (in_bricks_bytes < brick_map_bytes(Min)) return MVR_EINVAL;
   if (!out_coords) {   // the output set is the brick map's own set: output row o = input row o
@@ -880,7 +886,7 @@ extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void
     ProfScope prof(PK_SPCONV, 2.0 * Mout * C1_K * Cout, (double)Mout * (16 + Cout * 4), s);
     const int grid = (int)std::min<int64_t>(256, (Mout + 63) / 64);
     hipLaunchKernelGGL(spconv_c1_brick_kernel, dim3(grid), dim3(512), 0, s, v, feat, W, bn, bn_eps, relu, out,
-                       ldout);
+                       ldout, out_planes);
     MVR_CHECK_LAUNCH();
     return MVR_OK;
   }
@@ -895,6 +901,13 @@ extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void
                      ldout);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
+                             size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
+                             mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, hipStream_t s) {
+  return mvr_spconv_c1_x(out_coords, Mout, in_bricks, Min, in_bricks_bytes, feat, ksize, step, W, Cout, bn, bn_eps,
+                         relu, out, ldout, nullptr, s);
 }
 
 extern "C" int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, hipStream_t s) {

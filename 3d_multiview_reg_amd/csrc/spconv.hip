@@ -14,6 +14,7 @@
 // owned by exactly one workgroup (deterministic results).
 
 #include "common.hpp"
+#include "knobs.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
 #include "sparse.hpp"
@@ -33,11 +34,13 @@ struct SpArgs {
   int relu;
   float* out; int64_t ldout;
   int* range; const int* guard; int epoch;   // split-fp16 flag word (set to epoch 1) / split-bf16 re-run guard
-  int xcd;                                   // spconv_bx: XCD-contiguous tile order (mvr_set_spconv_xcd)
+  const uint16_t* inp;   // optional: the input as split-bf16 planes, row r plane p at inp + (3 r + p) ldin (bf16)
+  uint16_t* outp;        // optional: the output's planes too, row r plane p at outp + (3 r + p) ldout
 };
 
 constexpr int SP_KMAX = 32;
 __device__ __attribute__((aligned(16))) float g_sp_zero[4];   // what an absent neighbour gathers
+
 
 #ifndef SP_TRACE
 #define SP_TRACE 0   // 1: spconv_bx per-phase cycle totals per wave (s_memtime), tools only (mvr_spconv_trace)
@@ -80,12 +83,26 @@ constexpr int SB_CP = 128;   // output-channel padding of the weight image (larg
 #ifndef SPBX_NS128
 #define SPBX_NS128 3
 #endif
+// the same for the pre-split gathers (PS = 1: 24 VGPRs per set of gathered planes instead of 16 of fp32)
+#ifndef SPBX_PS_NS32
+#define SPBX_PS_NS32 3
+#endif
+#ifndef SPBX_PS_NS64
+#define SPBX_PS_NS64 3
+#endif
+#ifndef SPBX_PS_NS128
+#define SPBX_PS_NS128 2
+#endif
 
 // H = 1: split-fp16 (mfma_bf16.hpp, 3 MFMAs per product): the image's fp16 section (each output channel's
 // weights scaled by a power of two to <= 2^14), the gathered features x XS = 2^6 as they are split, both undone
 // per column in the epilogue (isc); a lane that splits a value of 1023.5 or more, or whose values are all below
 // 2^-9 without being zero, marks the launch (the caller's flag word) for its guarded split-bf16 re-run.
-template <int TN, int NS, int H>
+// PS = 1 (H = 0 only): the input arrives pre-split — its producer's epilogue wrote the (h, m, l) bf16 planes of
+// every value (a.outp below, the same RNE split as split8t) — so a step gathers the three planes of its 8 channels
+// (three 16-byte loads per half instead of two of fp32) and splits nothing: the ~5 VALU per gathered value that
+// every one of a row's ~14 uses repeated are gone.  Bit-identical to PS = 0.
+template <int TN, int NS, int H, int PS>
 __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint16_t* __restrict__ wimg, int64_t CoutP,
                                                            const float* __restrict__ isc) {
   using namespace bx;
@@ -110,10 +127,10 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   unsigned long long tr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_last = __builtin_amdgcn_s_memtime();
   int prev_slot = 0;
 #endif
-  // 1-D grid of (row tile, column tile) in XCD-contiguous order: the column tiles of a row tile (same gathered
-  // rows) and neighbouring row tiles (spatially close in the kernel map's row order) share an XCD's L2
+  // 1-D grid of (row tile, column tile) in dispatch order (round robin over the XCDs: an XCD-contiguous tile order
+  // was measured slower, DESIGN §4.1 — one XCD then gets all the expensive tiles of a mask class)
   const int gy = (a.Cout + TN - 1) / TN;
-  const int64_t t = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t t = (int64_t)blockIdx.x;
   const int64_t o0 = (t / gy) * TM;
   const int c0 = (int)(t % gy) * TN;
   const int K = a.K;
@@ -171,8 +188,10 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   // gathered A of one step: k-step st, channels ci0 + 16 st + 8h + (0..7) of the lane's row, as two
   // float4 each (clamped addresses; validity bits applied at the split)
   typedef float f32x4 __attribute__((ext_vector_type(4)));   // (a HIP float4 copy becomes a memcpy through scratch)
+  static_assert(!(PS && H), "pre-split planes are split-bf16");
   struct ASet {
-    float4 v[4];
+    float4 v[PS ? 1 : 4];                  // fp32 gathers (PS = 0)
+    bf16x8 pv[PS ? 2 : 1][PS ? 3 : 1];     // pre-split gathers (PS = 1): [k16 half][plane]
     f32x4 bq[GPT];   // the step's weight stage granules (this thread's share)
   };
   auto load_a = [&](int s, ASet& A) {
@@ -180,12 +199,24 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     const int k = klist[s / nci];
     const int ci0 = (s % nci) * SB_K;
     const int src = nb[row][k];
-    const float* base = a.in + (int64_t)(src >= 0 ? src : 0) * a.ldin;
+    if (PS) {
+      const uint16_t* base = a.inp + (int64_t)(src >= 0 ? src : 0) * 3 * a.ldin;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {   // an absent neighbour reads zeros (no masking at the split; Cin % 32 == 0)
-      const int ci = ci0 + 16 * (q >> 1) + 8 * h + 4 * (q & 1);
-      const float* pq = src >= 0 ? base + ci : g_sp_zero;
-      A.v[q] = *reinterpret_cast<const float4*>(pq);
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {   // an absent neighbour reads zero planes
+          const uint16_t* pq = base + pl * a.ldin + ci0 + 16 * st + 8 * h;
+          A.pv[st % (PS ? 2 : 1)][pl % (PS ? 3 : 1)] =
+              *reinterpret_cast<const bf16x8*>(src >= 0 ? (const void*)pq : (const void*)g_sp_zero);
+        }
+    } else {
+      const float* base = a.in + (int64_t)(src >= 0 ? src : 0) * a.ldin;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // an absent neighbour reads zeros (no masking at the split; Cin % 32 == 0)
+        const int ci = ci0 + 16 * (q >> 1) + 8 * h + 4 * (q & 1);
+        const float* pq = src >= 0 ? base + ci : g_sp_zero;
+        A.v[q % (PS ? 1 : 4)] = *reinterpret_cast<const float4*>(pq);
+      }
     }
     const int cb = s % nci;
     const char* wb = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * NPL * CoutP + c0) * SB_BST * 2;
@@ -199,8 +230,15 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
   bool xbad = false;   // H = 1: a gathered value past the fp16 window
   float xmx = 0.f;     // H = 1: max |value| x XS of this lane's splits
   auto frag_a = [&](const ASet& A, int st) {
+    if (PS) {
+      FragT<H> f;
+#pragma unroll
+      for (int pl = 0; pl < planes<H>(); ++pl)
+        f.p[pl] = __builtin_bit_cast(typename FragT<H>::V, A.pv[st % (PS ? 2 : 1)][pl % (PS ? 3 : 1)]);
+      return f;
+    }
     float v[8];
-    const float4 x0 = A.v[2 * st], x1 = A.v[2 * st + 1];
+    const float4 x0 = A.v[(2 * st) % (PS ? 1 : 4)], x1 = A.v[(2 * st + 1) % (PS ? 1 : 4)];
     v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
     v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
     if (H) {
@@ -300,6 +338,7 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
       if (a.res) v += rv[r];
       if (a.relu) v = fmaxf(v, 0.f);
       a.out[(int64_t)orr[r] * a.ldout + c] = v;
+      if (a.outp) bx::store_planes(a.outp + (int64_t)orr[r] * 3 * a.ldout + c, a.ldout, v);
     }
   }
   if (H && __any(xbad || (xmx > 0.f && xmx < 0.125f)) && lane == 0) atomicExch(a.range, a.epoch);
@@ -366,9 +405,7 @@ __global__ void spconv_wimage_kernel(const float* __restrict__ W, int K, int Cin
 #ifndef SPCONV_MATH_DEFAULT
 #define SPCONV_MATH_DEFAULT 0
 #endif
-int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_spconv_math
-int g_spconv_xcd = 0;                   // mvr_set_spconv_xcd (0: load-balanced round robin measured faster)
-int g_spconv_narrow = 0;                // mvr_set_spconv_narrow: below this many output rows, 64-channel column tiles
+int g_spconv_h = SPCONV_MATH_DEFAULT;   // mvr_set_math: split-fp16 (1) where a range flag is passed
 
 }  // namespace mvr
 
@@ -385,24 +422,6 @@ static size_t sp_f16_bytes(int K, int Cin, int Cout) { return sp_bf16_bytes(K, C
 extern "C" size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout) {
   if (K <= 0 || Cin <= 0 || Cout <= 0) return 0;
   return sp_bf16_bytes(K, Cin, Cout) + sp_f16_bytes(K, Cin, Cout) + 2 * sp_coutp(Cout) * sizeof(float);
-}
-
-extern "C" int mvr_set_spconv_narrow(int rows) {
-  const int prev = g_spconv_narrow;
-  g_spconv_narrow = rows < 0 ? 0 : rows;
-  return prev;
-}
-
-extern "C" int mvr_set_spconv_xcd(int on) {
-  const int prev = g_spconv_xcd;
-  g_spconv_xcd = on ? 1 : 0;
-  return prev;
-}
-
-extern "C" int mvr_set_spconv_math(int h) {
-  const int prev = g_spconv_h;
-  g_spconv_h = h ? 1 : 0;
-  return prev;
 }
 
 extern "C" int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, hipStream_t s) {
@@ -424,11 +443,14 @@ extern "C" int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void*
   return MVR_OK;
 }
 
-extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K,
-                          int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
-                          const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
-                          int32_t* range_flag, hipStream_t s) {
+extern "C" int mvr_spconv_x(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K,
+                            int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
+                            const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
+                            int32_t* range_flag, const uint16_t* in_planes, uint16_t* out_planes, hipStream_t s) {
   if (!in || !W || !out || !wimg || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
+  if ((in_planes && ((ldin & 7) || (reinterpret_cast<uintptr_t>(in_planes) & 15))) ||
+      (out_planes && (reinterpret_cast<uintptr_t>(out_planes) & 1)))
+    return MVR_EINVAL;
   if (reinterpret_cast<uintptr_t>(wimg) & 15) return MVR_EINVAL;
   if (!nbr && K != 1) return MVR_EINVAL;
   if ((Cin % SB_K) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
@@ -436,7 +458,7 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
     return MVR_EINVAL;
   if (Mout == 0) return MVR_OK;
   SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout,
-           nullptr, nullptr, 0, g_spconv_xcd};
+           nullptr, nullptr, 0, in_planes, out_planes};
   // the launch cannot see how many kernel-map entries are present (no host sync): FLOPs as if every offset were,
   // bytes compulsory (input rows ~ output rows, the neighbour table, the weights); bench.py replaces both class
   // totals with counts from the kernel maps
@@ -461,27 +483,36 @@ extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t*
     a.range = range_flag;
     a.epoch = 1;
   }
-#define MVR_SPL(TN_, NS_, GY)                                                                                   \
+#define MVR_SPL(TN_, NS_, PNS_, GY)                                                                             \
   do {                                                                                                         \
     if (h1) {                                                                                                  \
-      hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 1>), dim3(gx * (GY)), dim3(256), 0, s, a, wi16, CoutP, isc); \
+      hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 1, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi16, CoutP, isc); \
       MVR_CHECK_LAUNCH();                                                                                      \
       a.guard = a.range;                                                                                       \
       a.range = nullptr;                                                                                       \
     }                                                                                                          \
-    hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc);   \
+    if (in_planes)                                                                                             \
+      hipLaunchKernelGGL((spconv_bx_kernel<TN_, PNS_, 0, 1>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((spconv_bx_kernel<TN_, NS_, 0, 0>), dim3(gx * (GY)), dim3(256), 0, s, a, wi, CoutP, isc); \
   } while (0)
-  // (a level with few row tiles, fewer than the GPU's workgroup slots: 64-channel column tiles, twice the workgroups
-  // of 128-channel ones, each regathering the tile's rows)
   if (Cout <= 32)
-    MVR_SPL(32, SPBX_NS32, 1);
-  else if (Cout <= 64 || Mout < g_spconv_narrow)
-    MVR_SPL(64, SPBX_NS64, (Cout + 63) / 64);
+    MVR_SPL(32, SPBX_NS32, SPBX_PS_NS32, 1);
+  else if (Cout <= 64)
+    MVR_SPL(64, SPBX_NS64, SPBX_PS_NS64, (Cout + 63) / 64);
   else
-    MVR_SPL(128, SPBX_NS128, (Cout + 127) / 128);
+    MVR_SPL(128, SPBX_NS128, SPBX_PS_NS128, (Cout + 127) / 128);
 #undef MVR_SPL
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K,
+                          int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
+                          const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
+                          int32_t* range_flag, hipStream_t s) {
+  return mvr_spconv_x(in, ldin, Cin, nbr, perm, K, Mout, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout, wimg,
+                      range_flag, nullptr, nullptr, s);
 }
 
 #if SP_TRACE

@@ -60,21 +60,9 @@ _SIGS = {
     "mvr_oaf_conv2_f32": (c_int, [c_int, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_i64,
                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mvr_oaf_conv2_image_bytes": (c_size, [c_int, c_int]),
-    "mvr_set_oaf_conv2": (c_int, [c_int]),
-    "mvr_set_pconv": (c_int, [c_int]),
-    "mvr_set_pconv_grid": (c_int, [c_int]),
-    "mvr_set_cu_budget": (c_int, [c_int]),
-    "mvr_set_spconv_narrow": (c_int, [c_int]),
-    "mvr_set_feat_nn_fast": (c_int, [c_int]),
     "mvr_oan_block_workspace_bytes": (c_size, [c_int, c_int, c_int, c_int, c_int]),
-    "mvr_set_oan_fused": (c_int, [c_int]),
-    "mvr_set_pool_split": (c_int, [c_int]),
-    "mvr_set_unpool4": (c_int, [c_int]),
-    "mvr_set_attn_math": (c_int, [c_int]),
-    "mvr_set_pconv_math": (c_int, [c_int]),
-    "mvr_set_spconv_math": (c_int, [c_int]),
-    "mvr_set_spconv_xcd": (c_int, [c_int]),
-    "mvr_set_gemm_f16": (c_int, [c_int]),
+    "mvr_set_math": (c_int, [c_int]),
+    "mvr_debug_force": (c_int, [c_int, c_int]),
     "mvr_attn_reruns": (c_int, [c_int]),
     "mvr_debug_stage_hash": (c_int, [c_vp, c_int]),
     "mvr_debug_stage_dump": (c_int, [c_int, c_vp, c_size]),
@@ -125,9 +113,12 @@ _SIGS = {
     "mvr_kernel_map_orders": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_radix_sort_pairs_bytes": (c_size, [c_i64]),
     "mvr_radix_sort_pairs": (c_int, [c_vp, c_vp, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
-    "mvr_set_pool_tail": (c_int, [c_int]),
     "mvr_spconv": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp, c_i64,
                            c_int, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "mvr_spconv_x": (c_int, [c_vp, c_i64, c_int, c_vp, c_vp, c_int, c_i64, c_vp, c_int, c_vp, BnP, c_float, c_vp,
+                             c_i64, c_int, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mvr_spconv_c1_x": (c_int, [c_vp, c_i64, c_vp, c_i64, c_size, c_vp, c_int, c_int, c_vp, c_int, BnP, c_float,
+                                c_int, c_vp, c_i64, c_vp, c_vp]),
     "mvr_spconv_wimage_bytes": (c_size, [c_int, c_int, c_int]),
     "mvr_spconv_wimage": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_size, c_vp]),
     "mvr_brick_map_bytes": (c_size, [c_i64]),
@@ -227,38 +218,47 @@ def prof_get(kind):
     return ms.value, n.value, fl.value, by.value
 
 
-_MATH_KNOBS = ("pconv_math", "attn_math", "spconv_math", "gemm_f16")
+MATH_KERNELS = "pconv_math,attn_math,spconv_math,gemm_f16,feat_nn"   # the kernels mvr_set_math(1) switches
+# mvr_debug_force paths (include/mvreg.h, csrc/knobs.hpp ForcePath)
+FORCE = {"feat_nn_online": 0, "generic_gemm": 1, "unfused_attn": 2, "no_conv1_fold": 3, "pool_nosplit": 4,
+         "unpool8": 5}
 
 
 def math_state():
-    """The library's arithmetic knobs as they are set now: {knob: value}.  feat_nn_fast: 1 = the fast Soft_NN
-    path on split-bf16 distances, 2 = on split-fp16 distances (0: online path only, split-bf16)."""
+    """The library's arithmetic as it is set now: 0 f32eq, 1 split16 (read back: mvr_set_math returns the previous
+    mode)."""
     L = lib()
-    st = {}
-    for k in _MATH_KNOBS + ("feat_nn_fast",):
-        f = getattr(L, "mvr_set_" + k)
-        v = f(0)
-        f(v)
-        st[k] = v
-    return st
+    m = L.mvr_set_math(0)
+    L.mvr_set_math(m)
+    return m
 
 
 def set_math(mode):
-    """Select the MFMA operand arithmetic of every kernel that has a choice.
+    """Select the MFMA operand arithmetic of every kernel that has a choice (mvr_set_math).
 
     f32eq   : every fp32 product on the 3-term bf16 split (h + m + l, 6 MFMA products: fp32-equivalent operands).
     split16 : the 2-term fp16 split (h + l, 3 products, 22-bit operands) where a kernel has it, with the
               split-bf16 re-run of any launch whose operands leave the fp16 window.
-    Returns {"mode", "dtype", "knobs"}: dtype derived from the knobs as read back, never from `mode`."""
+    Returns {"mode", "dtype", "knobs"}: dtype derived from the mode as read back, never from `mode`."""
     L = lib()
-    h = {"f32eq": 0, "split16": 1}[mode]
-    for k in _MATH_KNOBS:
-        getattr(L, "mvr_set_" + k)(h)
-    L.mvr_set_feat_nn_fast(2 if h else 1)
-    st = math_state()
-    f16 = [k for k in _MATH_KNOBS if st[k]] + (["feat_nn"] if st["feat_nn_fast"] == 2 else [])
-    dtype = "f32 (bf16x3 MFMA operands)" if not f16 else "mixed: split-fp16 (22-bit) operands in " + ",".join(f16)
-    return {"mode": mode, "dtype": dtype, "knobs": st}
+    L.mvr_set_math({"f32eq": 0, "split16": 1}[mode])
+    m = math_state()
+    dtype = "f32 (bf16x3 MFMA operands)" if not m else "mixed: split-fp16 (22-bit) operands in " + MATH_KERNELS
+    return {"mode": "split16" if m else "f32eq", "dtype": dtype, "knobs": {"split16": m}}
+
+
+class force:
+    """with force("generic_gemm"): ... — a fallback path forced for the block (mvr_debug_force; tests only)"""
+
+    def __init__(self, what, value=1):
+        self.what, self.value = FORCE[what], int(value)
+
+    def __enter__(self):
+        self.prev = lib().mvr_debug_force(self.what, self.value)
+        return self
+
+    def __exit__(self, *a):
+        lib().mvr_debug_force(self.what, self.prev)
 
 
 _ws_cache = {}

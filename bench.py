@@ -450,16 +450,14 @@ def records_allgather(rec, world):
 
 
 MFMA_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter", "feat_nn", "spconv", "pointcn")
-# kernel classes with a split-fp16 form, and the knob that selects it (lib/_native.set_math)
-F16_KNOB = {"conv_pts": "pconv_math", "embed": "gemm_f16", "pool": "attn_math", "unpool": "attn_math",
-            "oafilter": "gemm_f16", "feat_nn": "feat_nn_fast", "spconv": "spconv_math"}
+# kernel classes with a split-fp16 form (switched together by lib/_native.set_math -> mvr_set_math)
+F16_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter", "feat_nn", "spconv")
 
 
 def class_peak_tflops(cls, knobs):
     """fp32-equivalent MFMA peak of a kernel class at the arithmetic it runs: split-bf16 (6 products per fp32
     product) = 16 x 157.3 / 6 TF; split-fp16 (3 products) = 16 x 157.3 / 3 TF"""
-    k = F16_KNOB.get(cls)
-    on = k is not None and (knobs.get(k) == 2 if k == "feat_nn_fast" else bool(knobs.get(k)))
+    on = cls in F16_CLASSES and bool(knobs.get("split16"))
     return PEAK_BF16_TFLOPS / (3 if on else 6)
 
 

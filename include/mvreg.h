@@ -10,12 +10,12 @@
  *     re-entrant, and thread-safe across distinct streams/devices;
  *   - strides are in ELEMENTS.
  *
- * Process-wide settings: every mvr_set_* entry point (operand maths, kernel variants, A/B switches) writes ONE
- * process-global value of the library, read by the host side of each later call when it builds its launches.
- * They are not per stream, per thread or per call.  Set them once, before any thread issues work, and leave
- * them: two threads selecting different settings race (a call sees whichever value was last written), and a
- * change never affects launches already enqueued.  The defaults are the fp32-equivalent paths the parity tests
- * pin; the Python mirror sets them only through lib._native.set_math, before the first forward.
+ * Process-wide settings: exactly two entry points, mvr_set_math (operand arithmetic) and mvr_debug_force (tests:
+ * fallback paths), write process-global values of the library, read by the host side of each later call when it
+ * builds its launches.  They are not per stream, per thread or per call.  Set them once, before any thread issues
+ * work: two threads selecting different settings race, and a change never affects launches already enqueued.  The
+ * defaults are the fp32-equivalent paths the parity tests pin; the Python mirror sets the arithmetic only through
+ * lib._native.set_math, before the first forward.
  *
  * Each entry point names the reference interface it replaces
  * (paths relative to the reference repo).
@@ -78,6 +78,24 @@ int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride, const int3
                int32_t* best_iter, double* hyp_out, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 
 /* ------------------------------------------------------------------------
+ * Process-wide selections (the only two; every other choice a launch makes is a function of its arguments).
+ * mvr_set_math: the operand arithmetic of every kernel that has a choice.  0 (default) f32eq: every fp32 product on
+ *   the three-term bf16 split (h + m + l, 6 MFMAs: fp32-equivalent operands).  1 split16: the two-term fp16 split
+ *   (h + l, 3 MFMAs per product, 22-bit operands) in the generic GEMM, the point convs, diff_pool / the 4-wave
+ *   diff_unpool, the sparse convs with > 64 output channels and the feature-NN distances, wherever the launch has a
+ *   range flag: weight rows range-scaled, activations range-checked, and a guarded split-bf16 re-run of any launch
+ *   whose operands left the fp16 window; split-bf16 directly where the output overwrites an input.  Returns the
+ *   previous mode.
+ * mvr_debug_force (tests): force one of the fallback paths the library keeps for shapes its fast kernels do not
+ *   cover — 0 the feature NN's online softmax only, 1 point convs and OAFilter conv2 on the generic GEMM, 2 diff_pool
+ *   / diff_unpool unfused (embedding GEMM + softmax + pooling GEMM), 3 the block's conv1 stored instead of folded
+ *   into the first PointCN, 4 diff_pool without key splits, 5 the 8-wave diff_unpool at <= 512 clusters.  value 0
+ *   restores the default.  Returns the previous value (MVR_EINVAL for an unknown path).
+ * ---------------------------------------------------------------------- */
+int mvr_set_math(int mode);
+int mvr_debug_force(int what, int value);
+
+/* ------------------------------------------------------------------------
  * One fused MFMA batched GEMM of the OANet schedule (exposed for tests):
  *   C[b](m,n) = sum_k pro_A(A(m,k)) pro_B(B(k,n)) + bias + R[b](m,n)
  * pro: 0 none, 1 relu(A*sc[k]+sh[k]), 2 relu(B*sc[k]+sh[k]) (sc/sh at [b*sPb + k]),
@@ -97,13 +115,6 @@ int mvr_gemm_f32(int M, int N, int K, int batch, const float* A, int64_t sAb, in
                  int64_t sRb, const float* bias, int bias_mode, const float* psc, const float* psh, int64_t sPb,
                  int64_t pld, int pro, float* stats, int64_t st_ld, int st_off, int stats_mode, int math,
                  int32_t* range_flag, mvr_stream_t stream);
-/* With the split math (1), run each generic GEMM launch that has a range flag (mvr_gemm_f32's range_flag: a device
-   int32 the call clears; mvr_oan_block_forward: words of its workspace) as two-term split-fp16 first (A and B x 2^6,
-   3 MFMAs per product, 22-bit operands) with a guarded split-bf16 re-run when an operand left the window
-   (|x| >= 1023.5, or a lane's values nonzero but all below 2^-9); split-bf16 directly when the output is an input
-   (in place).  0 (default) off, 1 on.  Returns the previous setting.  The choice never depends on process state
-   (launch counts, buffer addresses). */
-int mvr_set_gemm_f16(int on);
 /* OAFilter conv2 (oanet.py:72-81: the 1x1 conv over the clusters on the transpose, W2 [K][K] shared by every pair):
  * C[b](m, n) = sum_k relu(A[b](m, k) psc[b*sPb + k] + psh[b*sPb + k]) W(n, k) + bias[n] + R[b](m, n), M = 128, row
  * statistics per 128-column tile as mvr_gemm_f32's stats_mode 1 (st_off 0), on the split-once kernel (gemm.hip
@@ -116,30 +127,6 @@ int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A, int64_t sA
                       const float* psc, const float* psh, int64_t sPb, float* stats, int64_t st_ld, void* img,
                       int64_t img_bytes, mvr_stream_t stream);
 size_t mvr_oaf_conv2_image_bytes(int N, int K);
-/* Run the OANet block's OAFilter conv2 launches (mvr_oan_block_forward) on that kernel: 1 (default) the
- * split-once kernel, 0 the generic GEMM (A/B); 2 the split-once product on 128 x 128 tiles at two workgroups per CU
- * (oaf_conv2b_kernel, a persistent grid of <= 512), 3 the same with one workgroup per tile.  1, 2 and 3 give the
- * same bits.  Also selects the kernel mvr_oaf_conv2_f32 runs (1 for 0).  Process-wide; returns the previous
- * setting. */
-int mvr_set_oaf_conv2(int on);
-/* 128 -> 128 channel point convolutions (PointCN / OAFilter conv3, oanet.py:18-43,86-92) with the split
- * arithmetic run on a dedicated kernel (pconv.hip) instead of the generic GEMM: 1 (default) on, 0 off
- * (A/B timing).  Returns the previous setting. */
-int mvr_set_pconv(int on);
-/* Point-conv launch grid (process-wide): mul (1..64, default 1) workgroups per resident slot, each a contiguous
- * range of 128-point statistics groups (1: one persistent round); -2 / -4: a persistent grid of half / a quarter of
- * the resident slots (register file left for another stream's workgroups).  Results do not depend on it (each group's
- * statistics come from one workgroup; the folds merge them in group order).  Returns the previous setting. */
-int mvr_set_pconv_grid(int mul);
-/* CUs the persistent grids (point convs, the OAFilter conv2 kernels, the generic GEMM) are sized for: n (8..256,
- * default 256, all of an MI355X).  For a caller that confines the launching stream to a CU mask of n CUs, so that a
- * persistent grid stays one round.  Results do not depend on it.  Process-wide; returns the previous setting. */
-int mvr_set_cu_budget(int n);
-/* operand math of the point convs (not the output-head launches): 0 (default) split-bf16 (fp32-equivalent);
-   1 split-fp16 for launches that have a range flag (see mvr_set_gemm_f16): 3 MFMAs per product, weight rows
-   range-scaled, activations x 2^6 after the prologue and range-checked, with a guarded split-bf16 re-run of a
-   launch that saw one past the fp16 range.  Returns the previous setting. */
-int mvr_set_pconv_math(int h);
 
 /* ------------------------------------------------------------------------
  * OANet block (lib/filtering/oanet.py:132-185 OANBlock.forward) — parameters
@@ -171,25 +158,6 @@ typedef struct {
 } mvr_oan_block_p;
 
 size_t mvr_oan_block_workspace_bytes(int channels, int clusters, int in_channels, int P, int N);
-/* Fused paths inside mvr_oan_block_forward (process-wide; query workspace bytes after setting):
- *   bit 0: diff_pool / diff_unpool as the fused attention kernels (mvr_oan_diff_pool / _unpool) when
- *          channels == 128 and clusters <= 1024 (else embedding GEMM + softmax factors + pooling GEMM);
- *   bit 2: the block's conv1 (in_channels <= 8 -> 128) folded into the first PointCN's point convs;
- *   bit 3: InstanceNorm folds (the next conv's IN + BN scale / shift) finished inside the producing point conv
- *          by the workgroup whose arrival completes a pair's statistics, instead of a separate finalize launch
- *          (bit-identical results: the same merge order);
- *   bit 1 is unused (ignored).  Default 5 (bit 3 until validated on the device; 13 with it).
- * Returns the previous value. */
-int mvr_set_oan_fused(int on);
-/* Key-split diff_pool launches inside mvr_oan_block_forward (mvr_oan_diff_pool_ws): 1 (default) on, 0 off
- * (A/B timing).  Returns the previous setting. */
-int mvr_set_pool_split(int on);
-/* How mvr_oan_diff_pool_ws splits (process-wide): 0 (default) every (pair, cluster block) in 2 parts when N >= 512
- * (none below), a function of N alone: a pair's result does not depend on the batch (or rank shard) it came in;
- * 1 only the launch's tail past its complete rounds, chosen by the batch's makespan on the device's CUs (fewer
- * partial slabs, the same makespan, but a pair's summation order then depends on the batch size).  Returns the
- * previous setting. */
-int mvr_set_pool_tail(int on);
 
 /* input(p,c,n) = input[p*in_pstride + c*ld + n]  (Cin = blk->in_channels); ld >= round_up(N, 4),
  * a multiple of 4, input 16-byte aligned, padding columns [N, ld) finite (zero).
@@ -206,14 +174,6 @@ int mvr_set_pool_tail(int on);
  * (module.train(): the reference's forward batch); G > 1 batch statistics per group of G consecutive pairs (the
  * last group may be smaller) — G forwards of the reference's loader batches in one call (pair it with
  * guard_group = G). */
-/* diff_unpool kernel choice (process-wide): 1 (default) the 4-wave, two-per-CU kernel when clusters <= 512,
- * 0 the 8-wave kernel (A/B timing).  Returns the previous setting. */
-int mvr_set_unpool4(int on);
-/* operand math of diff_pool and the 4-wave diff_unpool: 0 (default) split-bf16 (6 MFMAs, fp32-equivalent);
-   1 split-fp16 (3 MFMAs per product, 22-bit operands, weight rows range-scaled, activations range-checked with a
-   split-bf16 re-run when one exceeds the fp16 range; the flag word lives in the caller's workspace: diff_pool
-   without a workspace runs split-bf16).  Returns the previous setting. */
-int mvr_set_attn_math(int h);
 /* Diagnostics: how many split-bf16 re-runs of split-fp16 attention launches ran on the current device since
    the last reset (synchronises the device); -1 on error. */
 int mvr_attn_reruns(int reset);
@@ -343,13 +303,6 @@ int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t
                    int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P, int Nq,
                    int Mt, int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
                    int32_t* idx_out, int n_frag, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
-/* Soft mode runs a bounded-shift softmax first (shift k2 |fs|^2 per query instead of a running maximum:
- * no max tracking or rescaling) and falls back to the online softmax per 128-query workgroup where a
- * softmax sum underflows (< 2^-60).  1 (default) on with three-term split-bf16 distances (6 MFMAs,
- * fp32-equivalent), 2 on with two-term split-fp16 of the features scaled by 2^8 (3 MFMAs per k-step, 22-bit
- * operands; a workgroup with a descriptor norm^2 >= 2^14 falls back too), 0 online only.  Returns the previous
- * setting. */
-int mvr_set_feat_nn_fast(int on);
 
 /* Two nearest neighbours in feature space (scripts/extract_data.py:178-184, sklearn NearestNeighbors
  * kneighbors(n_neighbors=2), Euclidean): for pair p and query j of fragment pairs[2p] (Fq rows, fragment stride
@@ -438,33 +391,28 @@ int mvr_radix_sort_pairs(const uint64_t* keys, const int32_t* vals, int64_t n, i
  * (fp32-level accuracy, ~2.7x the exact-fp32 MFMA rate).  Cin a multiple of 32 (every FCGF conv), Cout and ldin
  * multiples of 4, in and W 16-byte aligned; MVR_EINVAL otherwise.
  * range_flag (optional, device int32 owned by the stream's call sequence): enables the split-fp16 pass when
- * mvr_set_spconv_math(1) (the flag is cleared by the call, set by a split-fp16 pass whose operands left the fp16
+ * mvr_set_math(1) (the flag is cleared by the call, set by a split-fp16 pass whose operands left the fp16
  * window, and read by its guarded split-bf16 re-run); NULL -> split-bf16 only.  out is either disjoint from res
  * or equal to it (in place). */
 int mvr_spconv(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K, int64_t Mout,
                const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
                int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg, int32_t* range_flag,
                mvr_stream_t stream);
+/* mvr_spconv with split-bf16 planes beside the fp32 buffers (FCGF: every conv's output feeds the next conv's
+ * gathers).  in_planes (optional, 16-byte aligned, ldin % 8 == 0): the input's (h, m, l) bf16 planes, row r plane p
+ * at in_planes + (3 r + p) ldin — the split the kernel would otherwise repeat for each of a row's ~14 gathers; the
+ * split-bf16 pass gathers them instead of `in` (bit-identical results; a split-fp16 pass still reads `in`).
+ * out_planes (optional): also write the output's planes, row r plane p at out_planes + (3 r + p) ldout. */
+int mvr_spconv_x(const float* in, int64_t ldin, int Cin, const int32_t* nbr, const int32_t* perm, int K, int64_t Mout,
+                 const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps, const float* res,
+                 int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg, int32_t* range_flag,
+                 const uint16_t* in_planes, uint16_t* out_planes, mvr_stream_t stream);
 /* Weight image of mvr_spconv's split paths: W [K][Cin][Cout] fp32 -> three bf16 planes in
  * [K][ceil(Cin/32)][plane][round_up(Cout,128)][40] rows (80-byte rows, zero padded), then the same rows as two
  * fp16 planes of W[.][.][c] s_c (s_c: a power of two bringing output channel c's weights to <= 2^14), then
  * s_c and 1 / (s_c 2^6) per channel. */
 size_t mvr_spconv_wimage_bytes(int K, int Cin, int Cout);
 int mvr_spconv_wimage(const float* W, int K, int Cin, int Cout, void* img, size_t bytes, mvr_stream_t stream);
-/* operand math of mvr_spconv with a weight image: 0 (default) split-bf16 (fp32-equivalent); 1 split-fp16 where a
-   range_flag is passed (3 MFMAs per product, 22-bit operands; gathered features x 2^6 and window-checked, a guarded
-   split-bf16 re-run of a launch that saw one outside it; split-bf16 directly when the output is the residual).
-   Returns the previous setting. */
-int mvr_set_spconv_math(int h);
-/* tile order of mvr_spconv's split kernels: 0 (default) round-robin dispatch order, 1 XCD-contiguous (the
-   workgroups one XCD runs together take neighbouring tiles of the row order: measured slower, up to 1.5x on the
-   transposed convs, whose mask-sorted tiles differ in cost — one XCD gets all the expensive ones; A/B timing).
-   Returns the previous setting. */
-int mvr_set_spconv_xcd(int on);
-/* Sparse convs with fewer than `rows` output rows (default 0: none) and more than 64 output channels run on
- * 64-channel column tiles (twice the workgroups of the 128-channel tiles; results do not depend on it).  Process-wide;
- * returns the previous setting. */
-int mvr_set_spconv_narrow(int rows);
 /* Brick map of a coordinate set (4x4x4 bricks: hash of brick coordinates -> 64 row slots), the
  * neighbourhood structure of the large-stencil conv below.  Workspace:
  * mvr_brick_map_bytes(M).  _stride: a set at tensor stride `stride` (a power of two, coordinates multiples of it):
@@ -481,6 +429,11 @@ int mvr_brick_map_build_stride(const int32_t* coords, int64_t M, int stride, voi
 int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min, size_t in_bricks_bytes,
                   const float* feat, int ksize, int step, const float* W, int Cout, mvr_bn_p bn, float bn_eps,
                   int relu, float* out, int64_t ldout, mvr_stream_t stream);
+/* mvr_spconv_c1 (brick path, out_coords NULL) also writing the output's split-bf16 planes (mvr_spconv_x's layout) */
+int mvr_spconv_c1_x(const int32_t* out_coords, int64_t Mout, const void* in_bricks, int64_t Min,
+                    size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
+                    mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, uint16_t* out_planes,
+                    mvr_stream_t stream);
 /* x[o][:C] /= ||x[o][:C]||  (fcgf.py:274-278) */
 int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, mvr_stream_t stream);
 

@@ -29,17 +29,12 @@ def _case(gpu):
     return net, torch.from_numpy(xs).unsqueeze(1)
 
 
-def _forward(net, xs, fused):
+def _forward(net, xs, unfused):
     import torch
     from lib import _native as NV
-    L = NV.lib()
-    prev = L.mvr_set_oan_fused(fused)
-    try:
-        with torch.no_grad():
-            out = net({"xs": xs})
-        torch.cuda.synchronize()
-    finally:
-        L.mvr_set_oan_fused(prev)
+    with NV.force("unfused_attn", unfused), torch.no_grad():
+        out = net({"xs": xs})
+    torch.cuda.synchronize()
     return [t.detach().cpu().numpy().copy() for k in ("logits", "rot_est", "trans_est") for t in out[k]]
 
 
@@ -78,14 +73,13 @@ def test_forward_independent_of_process_history(gpu, tmp_path, math):
     NV.set_math(math)
     try:
         net, xs = _case(gpu)
-        before = {f: _forward(net, xs, f) for f in (5, 1)}
+        before = {f: _forward(net, xs, f) for f in (0, 1)}
         keep = _disturb(gpu, tmp_path)
         NV.set_math(math)                  # (the harness may have changed nothing; make sure)
-        after = {f: _forward(net, xs, f) for f in (5, 1)}
+        after = {f: _forward(net, xs, f) for f in (0, 1)}
         del keep
     finally:
-        for k, v in prev.items():
-            getattr(NV.lib(), "mvr_set_" + k)(v)
+        NV.lib().mvr_set_math(prev)
     for f in before:
         for a, b in zip(before[f], after[f]):
             assert np.array_equal(a, b), (math, f, np.abs(a - b).max())
@@ -94,5 +88,9 @@ def test_forward_independent_of_process_history(gpu, tmp_path, math):
 def test_math_knobs_default_f32eq():
     """the library's defaults are the fp32-equivalent operand maths (split-fp16 is opt-in)"""
     from lib import _native as NV
-    st = NV.math_state()
-    assert st == {"pconv_math": 0, "attn_math": 0, "spconv_math": 0, "gemm_f16": 0, "feat_nn_fast": 1}, st
+    assert NV.math_state() == 0
+    # and no fallback path is forced
+    L = NV.lib()
+    for what in NV.FORCE.values():
+        assert L.mvr_debug_force(what, 0) == 0
+    assert L.mvr_debug_force(6, 0) == -1

@@ -70,14 +70,19 @@ def test_feat_nn_fast_path_matches_online(gpu, scale, offset):
     tf, tx, tp = (torch.from_numpy(a).to(gpu) for a in (f, x, pairs))
     L = NV.lib()
     outs = []
-    for fast in (2, 1, 0):
-        prev = L.mvr_set_feat_nn_fast(fast)
-        out = torch.empty(len(pairs), n, 6, device=gpu)
-        rc = L.mvr_feat_nn(NV.ptr(tf), n * 32, NV.ptr(tf), n * 32, NV.ptr(tx), n * 3, NV.ptr(tx), n * 3, NV.ptr(tp),
-                           len(pairs), n, n, 32, 1.0 / 0.09, 0, NV.ptr(out), n * 6, 6, None, NV.stream())
-        L.mvr_set_feat_nn_fast(prev)
-        assert rc == 0
-        outs.append(out.cpu().numpy())
+    prev = L.mvr_set_math(0)
+    try:
+        for math, online in ((1, 0), (0, 0), (0, 1)):   # fast path split-fp16, split-bf16; the online path
+            L.mvr_set_math(math)
+            with NV.force("feat_nn_online", online):
+                out = torch.empty(len(pairs), n, 6, device=gpu)
+                rc = L.mvr_feat_nn(NV.ptr(tf), n * 32, NV.ptr(tf), n * 32, NV.ptr(tx), n * 3, NV.ptr(tx), n * 3,
+                                   NV.ptr(tp), len(pairs), n, n, 32, 1.0 / 0.09, 0, NV.ptr(out), n * 6, 6, None,
+                                   NV.stream())
+            assert rc == 0
+            outs.append(out.cpu().numpy())
+    finally:
+        L.mvr_set_math(prev)
     for o in outs:
         assert np.all(np.isfinite(o))
     if offset:   # (|f|^2 ~ 2^14: fp32 distances themselves are off by ~1e-3 here, no oracle comparison)

@@ -5,7 +5,7 @@ partials, and the whole OANet block with the fused path on vs off.
 
 Tolerance: the kernels compute in fp32 with split MFMA products — the default split-bf16 (three bf16 terms,
 6 MFMAs: fp32-equivalent operands) or the opt-in split-fp16 (two fp16 terms, 22 significant bits, 3 MFMAs;
-mvr_set_attn_math(1)) — so outputs are compared to fp64 at 2e-5 relative to the output scale.  Operands outside the fp16 range send a split-fp16 launch to its
+mvr_set_math(1)) — so outputs are compared to fp64 at 2e-5 relative to the output scale.  Operands outside the fp16 range send a split-fp16 launch to its
 split-bf16 re-run: the outputs are then bit-identical to a split-bf16 launch."""
 import os
 
@@ -50,25 +50,20 @@ def _tile_stats(y, L):
 @pytest.fixture(params=[1, 0], ids=["fp16x2", "bf16x3"])
 def math(request):
     from lib import _native as NV
-    prev = NV.lib().mvr_set_attn_math(request.param)
+    prev = NV.lib().mvr_set_math(request.param)
     yield request.param
-    NV.lib().mvr_set_attn_math(prev)
+    NV.lib().mvr_set_math(prev)
 
 
-@pytest.mark.parametrize("split", [False, True, "tail"])
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (41, 700, 300),
                                     (300, 600, 500)])
 def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
     """split: mvr_oan_diff_pool_ws with a workspace (points split over 2-4 workgroups per (pair, cluster
-    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  "tail"
-    (mvr_set_pool_tail(1)): at 300 pairs x 500 clusters (608 whole workgroups on 256 CUs) only the tail past the
-    two complete rounds is split (pair octets 32-37), the rest runs whole.  The split-fp16 math needs the
-    workspace's flag word: without one the launch is split-bf16."""
+    block) and merged by the last one; N >= 256 here always splits on a 256-CU part).  The split-fp16 math needs
+    the workspace's flag word: without one the launch is split-bf16."""
     import torch
     from lib import _native as NV
-    if split == "tail" and P < 300:
-        pytest.skip("the tail split differs from the uniform one only past a complete round of workgroups")
-    prev_tail = NV.lib().mvr_set_pool_tail(1 if split == "tail" else 0)
     x, sc, sh, W, b, ld = _inputs(P, N, Kc, seed=P * 1000 + N)
     xd, e = _embed(x, sc, sh, W, b, N)
     ref = (xd @ torch.softmax(e, dim=2).transpose(1, 2)).numpy()          # oanet.py:106-110
@@ -91,7 +86,6 @@ def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
         assert L.mvr_oan_diff_pool(NV.ptr(gx), C * ld, ld, NV.ptr(gsc), NV.ptr(gsh), C, NV.ptr(gW), NV.ptr(gb),
                                    P, C, N, Kc, NV.ptr(out), C * Kp, Kp, NV.ptr(st), C, 0, NV.stream()) == 0
     torch.cuda.synchronize()
-    NV.lib().mvr_set_pool_tail(prev_tail)
     o = out.cpu().numpy()
     scale = np.abs(ref).max()
     np.testing.assert_allclose(o[:, :, :Kc], ref, atol=2e-5 * scale, rtol=0)
@@ -101,15 +95,12 @@ def test_diff_pool_matches_fp64(gpu, P, N, Kc, split, math):
     np.testing.assert_allclose(st.cpu().numpy()[..., 1], sref[..., 1], rtol=1e-4, atol=1e-6 * scale ** 2 * 128)
 
 
-@pytest.mark.parametrize("kern", [1, 0])   # mvr_set_unpool4: 4-wave two-per-CU kernel / 8-wave kernel (bf16x3)
+@pytest.mark.parametrize("unpool8", [0, 1])   # the 4-wave two-per-CU kernel / the 8-wave one (forced; > 512 clusters)
 @pytest.mark.parametrize("P,N,Kc", [(3, 1234, 500), (9, 37, 77), (1, 5000, 500), (2, 5, 33), (2, 300, 700)])
-def test_diff_unpool_matches_fp64(gpu, P, N, Kc, kern, math):
+def test_diff_unpool_matches_fp64(gpu, P, N, Kc, unpool8, math):
     from lib import _native as NV
-    prev = NV.lib().mvr_set_unpool4(kern)
-    try:
+    with NV.force("unpool8", unpool8):
         _unpool_case(gpu, P, N, Kc)
-    finally:
-        NV.lib().mvr_set_unpool4(prev)
 
 
 def _unpool_case(gpu, P, N, Kc, edit=None, check=True):
@@ -212,14 +203,14 @@ def test_diff_pool_fp16_range(gpu, edit):
     bit-identical to it)"""
     from lib import _native as NV
     L = NV.lib()
-    prev = L.mvr_set_attn_math(0)
+    prev = L.mvr_set_math(0)
     try:
         o0, s0, ref = _pool_run(gpu, 3, 1234, 500, edit)
-        L.mvr_set_attn_math(1)
+        L.mvr_set_math(1)
         L.mvr_attn_reruns(1)
         o1, s1, _ = _pool_run(gpu, 3, 1234, 500, edit)
     finally:
-        L.mvr_set_attn_math(prev)
+        L.mvr_set_math(prev)
     assert (L.mvr_attn_reruns(1) > 0) == (edit.__name__ in POOL_RERUN)
     if edit.__name__ in POOL_RERUN:   # re-run (fp64 agreement is then the split-bf16 kernel's, at logits ~1e4)
         assert np.array_equal(o0, o1) and np.array_equal(s0, s1)
@@ -245,17 +236,17 @@ UNPOOL_RERUN = ("_big_xd", "_small_xd", "_big_xn", "_big_w", "_mid_w")
 def test_diff_unpool_fp16_range(gpu, edit):
     from lib import _native as NV
     L = NV.lib()
-    prev = L.mvr_set_attn_math(0)
+    prev = L.mvr_set_math(0)
     try:
         o0, s0 = _unpool_case(gpu, 3, 1234, 500, edit, check=False)
-        L.mvr_set_attn_math(1)
+        L.mvr_set_math(1)
         L.mvr_attn_reruns(1)
         o1, s1 = _unpool_case(gpu, 3, 1234, 500, edit, check=False)
         assert (L.mvr_attn_reruns(1) > 0) == (edit.__name__ in UNPOOL_RERUN)
         if edit.__name__ not in UNPOOL_RERUN:
             _unpool_case(gpu, 3, 1234, 500, edit)   # vs fp64
     finally:
-        L.mvr_set_attn_math(prev)
+        L.mvr_set_math(prev)
     if edit.__name__ in UNPOOL_RERUN:
         assert np.array_equal(o0, o1, equal_nan=True) and np.array_equal(s0, s1)
     elif edit is _tiny_w:
@@ -277,16 +268,16 @@ def test_oanet_default_init_runs_fp16_attention(gpu):
     xs, _, _ = synth_correspondences(8, 3000, seed=4)
     L = NV.lib()
     outs = []
-    prev = L.mvr_set_attn_math(1)
+    prev = L.mvr_set_math(1)
     try:
         for mth in (1, 0):
-            L.mvr_set_attn_math(mth)
+            L.mvr_set_math(mth)
             L.mvr_attn_reruns(1)
             with torch.no_grad():
                 outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1).to(gpu)}))
             assert L.mvr_attn_reruns(1) == 0
     finally:
-        L.mvr_set_attn_math(prev)
+        L.mvr_set_math(prev)
     a, b = outs
     for i in range(2):
         la, lb = a["logits"][i].cpu().numpy(), b["logits"][i].cpu().numpy()
@@ -315,10 +306,11 @@ def test_diff_pool_rejects_bad_layout(gpu):
     assert L.mvr_oan_diff_unpool_workspace_bytes(1, 64, 16) == 0
 
 
-@pytest.mark.parametrize("fused", [1, 4, 5])
-def test_oanet_fused_vs_gemm_path(gpu, fused):
-    """Whole filter with the fused kernels (bit 0: diff_pool/diff_unpool, bit 2: conv1 folded into the first
-    PointCN) vs the plain GEMM path: same R, t (1e-4) and inlier masks."""
+@pytest.mark.parametrize("paths", [("no_conv1_fold",), ("unfused_attn",), ()])
+def test_oanet_fused_vs_gemm_path(gpu, paths):
+    """Whole filter with the fused kernels (diff_pool / diff_unpool fused attention, conv1 folded into the first
+    PointCN; each alone by forcing the other's fallback, and both) vs the plain GEMM path (both forced off):
+    same R, t (1e-4) and inlier masks."""
     import torch
     from lib import _native as NV
     from test_gpu_oanet import _oanet
@@ -326,15 +318,10 @@ def test_oanet_fused_vs_gemm_path(gpu, fused):
     xs, _, _ = synth_correspondences(6, 2000, seed=11)
     net = _oanet(128, 500, 7, gpu, which="full")
     outs = []
-    L = NV.lib()
-    prev = L.mvr_set_oan_fused(fused)
-    try:
-        for f in (fused, 0):
-            L.mvr_set_oan_fused(f)
-            with torch.no_grad():
-                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-    finally:
-        L.mvr_set_oan_fused(prev)
+    for forced in (paths, ("no_conv1_fold", "unfused_attn")):
+        with NV.force("no_conv1_fold", "no_conv1_fold" in forced), NV.force("unfused_attn", "unfused_attn" in forced), \
+                torch.no_grad():
+            outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
     a, b = outs
     for i in range(2):
         np.testing.assert_allclose(a["logits"][i].cpu().numpy(), b["logits"][i].cpu().numpy(), atol=2e-3, rtol=1e-4)
@@ -368,23 +355,11 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
     net = _oanet(128, 500, 9, gpu, train=train, which="full")
     outs = []
     L = NV.lib()
-    if os.environ.get("MVR_TEST_DEBUG"):   # the library knobs as this test finds them
-        knobs = {}
-        for k in ("pconv", "feat_nn_fast", "oan_fused", "pool_split", "unpool4", "attn_math",
-                  "pconv_math", "spconv_math", "gemm_f16"):
-            f = getattr(L, "mvr_set_" + k)
-            v = f(0)
-            f(v)
-            knobs[k] = v
-        print("\nDEBUG knobs %s reruns before %d" % (knobs, L.mvr_attn_reruns(1)), flush=True)
-    prev = L.mvr_set_oan_fused(5)
-    try:
-        for f in (5, 1):
-            L.mvr_set_oan_fused(f)
-            with torch.no_grad():
-                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-    finally:
-        L.mvr_set_oan_fused(prev)
+    if os.environ.get("MVR_TEST_DEBUG"):   # the library's settings as this test finds them
+        print("\nDEBUG math %d reruns before %d" % (NV.math_state(), L.mvr_attn_reruns(1)), flush=True)
+    for no_fold in (0, 1):
+        with NV.force("no_conv1_fold", no_fold), torch.no_grad():
+            outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
     a, b = outs
     np.testing.assert_allclose(a["logits"][0].cpu().numpy(), b["logits"][0].cpu().numpy(), atol=5e-4, rtol=1e-4)
     if npts < 100:
@@ -420,64 +395,3 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
             r32, r64 = o32[k][i], o64[k][i]
             bound = np.maximum(1e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
             assert (dist(f, r64) <= bound).all(), (i, k, dist(f, r64), dist(m, r64), dist(r32, r64))
-
-
-@pytest.mark.parametrize("P,npts,train", [(37, 1234, False), (70, 1500, True), (600, 100, False), (3, 5000, False)])
-def test_oanet_fused_finalize_bit_identical(gpu, P, npts, train):
-    """InstanceNorm folds finished inside their producing point conv (the workgroup whose arrival completes a
-    pair's statistics merges them, mvr_set_oan_fused bit 3) vs the separate in_finalize launches: the same
-    merge order in both, so every output is bit-identical — eval and train-mode BatchNorm (32-pair groups), a
-    ragged point count, one statistics tile per pair with more pairs than resident workgroups (a workgroup then
-    completes several pairs), and few pairs (a pair's tiles spread over many workgroups)."""
-    import torch
-    from lib import _native as NV
-    from test_gpu_oanet import _oanet
-    from synth import synth_correspondences
-    xs, _, _ = synth_correspondences(P, npts, seed=5)
-    net = _oanet(128, 500, 7, gpu, train=train, which="full")
-    if train:
-        net.bn_group = net.guard_group = 32
-    L = NV.lib()
-    prev = L.mvr_set_oan_fused(13)
-    outs = []
-    try:
-        for f in (13, 5):
-            L.mvr_set_oan_fused(f)
-            with torch.no_grad():
-                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-    finally:
-        L.mvr_set_oan_fused(prev)
-    a, b = outs
-    for k in ("logits", "scores", "rot_est", "trans_est"):
-        for i in range(2):
-            assert torch.equal(a[k][i], b[k][i]), (k, i, (a[k][i] - b[k][i]).abs().max().item())
-
-
-@pytest.mark.parametrize("P,npts,train,fused", [(37, 1234, False, 13), (70, 1500, True, 13), (37, 1234, False, 5)])
-def test_pconv_grid_bit_identical(gpu, P, npts, train, fused):
-    """The point-conv launch grid (mvr_set_pconv_grid: several contiguous group ranges per resident slot, dealt by
-    the dispatcher) changes which workgroup computes a 128-point group, never what it computes: every output is
-    bit-identical, with and without the fused InstanceNorm folds (whose last arriver merges in group order)."""
-    import torch
-    from lib import _native as NV
-    from test_gpu_oanet import _oanet
-    from synth import synth_correspondences
-    xs, _, _ = synth_correspondences(P, npts, seed=6)
-    net = _oanet(128, 500, 7, gpu, train=train, which="full")
-    if train:
-        net.bn_group = net.guard_group = 32
-    L = NV.lib()
-    prev, prevf = L.mvr_set_pconv_grid(1), L.mvr_set_oan_fused(fused)
-    outs = []
-    try:
-        for m in (1, 3, 8, -2, -4):
-            L.mvr_set_pconv_grid(m)
-            with torch.no_grad():
-                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-    finally:
-        L.mvr_set_pconv_grid(prev)
-        L.mvr_set_oan_fused(prevf)
-    for o in outs[1:]:
-        for k in ("logits", "scores", "rot_est", "trans_est"):
-            for i in range(2):
-                assert torch.equal(outs[0][k][i], o[k][i]), (k, i, (outs[0][k][i] - o[k][i]).abs().max().item())

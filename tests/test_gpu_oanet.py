@@ -96,15 +96,13 @@ def test_oanet_small_golden(gpu, fx, train, ovr):
     assert out["gradient_flag"] == bool(g["gradient_flag"])
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["conv2_generic", "conv2_split_once", "conv2_split_once_2wg",
-                                          "conv2_split_once_2wg_per_tile"])
+@pytest.fixture(params=[0, 1], ids=["fast_kernels", "generic_gemm"])
 def conv2(request):
-    """mvr_set_oaf_conv2: the OAFilter conv2 launches on the generic GEMM or a split-once kernel (128 x 256 tiles,
-    or 128 x 128 tiles at two workgroups per CU)"""
+    """the point convs and OAFilter conv2 on their dedicated kernels (default) or forced onto the generic GEMM
+    (mvr_debug_force 1: the fallback those kernels keep for other shapes)"""
     from lib import _native as NV
-    prev = NV.lib().mvr_set_oaf_conv2(request.param)
-    yield request.param
-    NV.lib().mvr_set_oaf_conv2(prev)
+    with NV.force("generic_gemm", request.param):
+        yield request.param
 
 
 def test_oanet_full_golden(gpu, conv2):
@@ -135,18 +133,12 @@ def test_oanet_full_train_golden(gpu, conv2):
     assert hashlib.sha1(xs.tobytes()).hexdigest() == str(g["xs_sha1"])
     from lib import _native as NV
     net = _oanet(128, 500, 7, gpu, train=True, which="full")
-    L = NV.lib()
     outs = []
-    # the default run, then two runs that differ from it only in diff_pool's summation order (key splits off / the
-    # batch-dependent tail split): their spread measures each pair's own fp32 rounding sensitivity
-    for knob, v in ((None, None), ("mvr_set_pool_split", 0), ("mvr_set_pool_tail", 1)):
-        prev = getattr(L, knob)(v) if knob else None
-        try:
-            with torch.no_grad():
-                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-        finally:
-            if knob:
-                getattr(L, knob)(prev)
+    # the default run, then runs that differ from it only in fp32 summation order (diff_pool without key splits; the
+    # unfused attention GEMMs): their spread measures each pair's own fp32 rounding sensitivity
+    for path in (None, "pool_nosplit", "unfused_attn"):
+        with NV.force(path or "pool_nosplit", 1 if path else 0), torch.no_grad():
+            outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
     out = outs[0]
     dist = lambda u, v: np.abs(u - v).reshape(u.shape[0], -1).max(1)   # noqa: E731
     for i in range(2):
@@ -249,7 +241,7 @@ def test_procrustes_guard_group(gpu):
 def test_oanet_fused_head_guard_and_pconv_off(gpu):
     """128 channels: the output head fused into the last point conv (pconv.hip) — with the zero-row guard
     triggered for every pair (output bias -1e4) against the oracle, and the default path against the
-    generic-GEMM path (mvr_set_pconv(0), separate head kernel)."""
+    generic-GEMM path (mvr_debug_force generic_gemm, separate head kernel)."""
     import torch
     from lib import _native as NV
     from oracle.oanet import oanet_forward
@@ -267,13 +259,10 @@ def test_oanet_fused_head_guard_and_pconv_off(gpu):
     assert np.all(out["logits"][0].cpu().numpy() < 0)     # every weight zero: the guard's branch ran
     net2 = _oanet(128, 500, 7, gpu, which="full")
     xs2, _, _ = synth_correspondences(4, 1000, seed=79)
-    L = NV.lib()
     res = []
-    for on in (1, 0):
-        prev = L.mvr_set_pconv(on)
-        with torch.no_grad():
+    for generic in (0, 1):
+        with NV.force("generic_gemm", generic), torch.no_grad():
             res.append(net2({"xs": torch.from_numpy(xs2).unsqueeze(1)}))
-        L.mvr_set_pconv(prev)
     for i in range(2):
         np.testing.assert_allclose(res[0]["logits"][i].cpu().numpy(), res[1]["logits"][i].cpu().numpy(), atol=2e-3,
                                    rtol=1e-4)

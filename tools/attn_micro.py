@@ -61,7 +61,7 @@ def run(a, K, N):
             continue
         res = {}
         for mth in maths:
-            L.mvr_set_attn_math(mth)
+            L.mvr_set_math(mth)
             fn()
             torch.cuda.synchronize()
             res[mth] = o.clone()
@@ -85,7 +85,7 @@ def run(a, K, N):
         if len(res) == 2:
             d = (res[0] - res[1]).abs().max().item()
             print("%-7s max |h1 - h0| %.3e (max |out| %.3e)" % (name, d, res[0].abs().max().item()), flush=True)
-        L.mvr_set_attn_math(1)
+        L.mvr_set_math(1)
 
 
 def time_it(a, name, fn, flops):

@@ -19,14 +19,10 @@ gpu = torch.device("cuda:0")
 g, g64 = golden("oanet_full_train.npz"), golden("oanet_full_train_f64.npz")
 xs, _, _ = synth_correspondences(32, 5000, seed=33)
 net = _oanet(128, 500, 7, gpu, train=True, which="full")
-L = NV.lib()
 outs = []
-for knob, v in ((None, None), ("mvr_set_pool_split", 0), ("mvr_set_pool_tail", 1)):
-    prev = getattr(L, knob)(v) if knob else None
-    with torch.no_grad():
+for path in (None, "pool_nosplit", "unfused_attn"):   # the default, then other fp32 summation orders
+    with NV.force(path or "pool_nosplit", 1 if path else 0), torch.no_grad():
         outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-    if knob:
-        getattr(L, knob)(prev)
 dist = lambda u, v: np.abs(u - v).reshape(u.shape[0], -1).max(1)  # noqa: E731
 for i in range(2):
     for k, kg in (("rot_est", "R"), ("trans_est", "t")):

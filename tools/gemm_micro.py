@@ -57,11 +57,9 @@ def run(name, iters, math, pconv=1):
     st = torch.empty(P, max(nt, mt), max(M, Nn), 2, device=d) if stats else None
     st_ld = M if stats in (1, 2) else Nn
     L = NV.lib()
-    L.mvr_set_pconv(pconv)
-    L.mvr_set_pconv_grid(PGRID)
+    L.mvr_debug_force(1, 0 if pconv else 1)   # generic_gemm
     so = name.startswith("oaf_conv2_so")
     img = torch.empty(int(L.mvr_oaf_conv2_image_bytes(Nn, Kk)) // 4 + 4, device=d) if so else None
-    L.mvr_set_oaf_conv2(2 if name == "oaf_conv2_so2" else 1)
 
     def go():
         if img is not None:

@@ -29,7 +29,8 @@ if __name__ == "__main__":
     P = pairs.shape[0]
     out = torch.empty(P, N, 6, device=d)
     L = NV.lib()
-    L.mvr_set_feat_nn_fast(a.fast)
+    L.mvr_set_math(1 if a.fast == 2 else 0)
+    L.mvr_debug_force(0, 1 if a.fast == 0 else 0)   # feat_nn_online
 
     nb = L.mvr_feat_nn_workspace_bytes(B, N)
     ws = torch.empty(nb, dtype=torch.uint8, device=d)

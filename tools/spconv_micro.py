@@ -24,8 +24,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default=None)
     ap.add_argument("--order", default=None, help="run only this row order (e.g. mask+morton)")
-    ap.add_argument("--xcd", type=int, default=None, help="run only this xcd setting (0/1)")
-    ap.add_argument("--narrow", type=int, default=None, help="mvr_set_spconv_narrow(rows)")
+    ap.add_argument("--xcd", type=int, default=0, help="(tile order selector removed in round 5: 0 only)")
     ap.add_argument("--trace", action="store_true", help="library built with -DSP_TRACE=1 (MVR_LIB): phase shares")
     a = ap.parse_args()
     from synth import synth_scene_fragments
@@ -35,8 +34,6 @@ def main():
     c, _, counts, _ = voxelize([torch.from_numpy(f).to(dev) for f in frags], 0.025, dev)
     cm = CoordinateManager(c, len(frags))
     L = NV.lib()
-    if a.narrow is not None:
-        L.mvr_set_spconv_narrow(a.narrow)
     g = torch.Generator(device=dev).manual_seed(0)
     for kind, s, cin, cout in CASES:
         tag = "%s:%d:%d:%d" % (kind, s, cin, cout)
@@ -78,7 +75,6 @@ def main():
             for xcd in (0, 1):
                 if a.xcd is not None and xcd != a.xcd:
                     continue
-                L.mvr_set_spconv_xcd(xcd)
 
                 def go():
                     NV.check(L.mvr_spconv(NV.ptr(x), cin, cin, NV.ptr(nbr), NV.ptr(pm), 27, Mout, NV.ptr(W), cout, None,
@@ -107,7 +103,6 @@ def main():
                              "prologue"]
                     print("   %s phase shares: %s" % (tag, ", ".join("%s %.1f%%" % (names[q], 100.0 * buf[q] / tot)
                                                                      for q in range(8))), flush=True)
-        L.mvr_set_spconv_xcd(0)
         fl = 2.0 * act * cin * cout
         print("%-16s Mout %7d active/row %.1f  %s   (useful TF/s at best %.1f)" % (
             tag, Mout, act / Mout, "  ".join("%s %.3f" % kv for kv in res.items()), fl / min(res.values()) / 1e9),
