@@ -22,7 +22,6 @@ CASES = {
     "unpool": (C, N, K, 3, 0, 0, 1, 0),
     "oaf_conv2": (C, K, K, 1, 1, 2, 1, 1),    # OAFilter conv2 (oanet.hip oafilter): W2 shared, bias per n, residual
     "oaf_conv2_so": (C, K, K, 1, 1, 2, 1, 1),  # the same on the split-once kernel (mvr_oaf_conv2_f32)
-    "oaf_conv2_so2": (C, K, K, 1, 1, 2, 1, 1),  # split-once, 128 x 128 tiles at two workgroups per CU
     "conv_oaf1": (C, K, C, 2, 0, 1, 4, 0),    # OAFilter conv1 over the clusters: IN/BN/ReLU prologue, column stats
 }
 
