@@ -291,13 +291,18 @@ __global__ void build_table_kernel(const int4* __restrict__ c, int64_t M, HashVi
 
 // ------------------------------------------------------------------ kernel maps
 // nbr[o][k] = row of (coords[o] + sign*off_k*step) in the input table, or -1
+// row_order (optional): thread block i / K handles output row row_order[i / K] — a spatial (fragment, Morton) order
+// of the output set (mvr_kernel_map_orders without neighbour tables), so the workgroups that run together probe
+// neighbouring lattice cells (L2 reuse) instead of the set's first-occurrence order (random in space)
 __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h, int ks, int step, int sign,
-                                  int32_t* __restrict__ nbr) {
+                                  int32_t* __restrict__ nbr, const int32_t* __restrict__ row_order) {
   const int K = ks * ks * ks;
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= Mo * K) return;
-  const int64_t o = e / K;
-  const int k = (int)(e - o * K);
+  const int64_t e0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e0 >= Mo * K) return;
+  const int64_t i = e0 / K;
+  const int k = (int)(e0 - i * K);
+  const int64_t o = row_order ? (int64_t)row_order[i] : i;
+  const int64_t e = o * K + k;
   const int r = ks / 2;
   const int dx = k % ks - r, dy = (k / ks) % ks - r, dz = k / (ks * ks) - r;
   const int4 c = oc[o];
@@ -685,6 +690,7 @@ struct OrderMaps {
   int step[ORDER_MAX_MAPS];
   int64_t start[ORDER_MAX_MAPS + 1];
   int n, K;
+  int jshift;   // key bit of the map index: 59 above the masks, 32 without neighbour tables (coordinate orders)
 };
 __global__ void order_keys_kernel(OrderMaps m, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -692,9 +698,11 @@ __global__ void order_keys_kernel(OrderMaps m, uint64_t* __restrict__ keys, int3
   int j = 0;
   while (i >= m.start[j + 1]) ++j;
   const int64_t o = i - m.start[j];
-  const int32_t* row = m.nbr[j] + o * m.K;
   uint32_t mask = 0;
-  for (int k = 0; k < m.K; ++k) mask |= (row[k] >= 0 ? 1u : 0u) << k;
+  if (m.nbr[j]) {
+    const int32_t* row = m.nbr[j] + o * m.K;
+    for (int k = 0; k < m.K; ++k) mask |= (row[k] >= 0 ? 1u : 0u) << k;
+  }
   uint32_t lo = 0;
   if (m.coords[j]) {
     const int4 c = m.coords[j][o];
@@ -702,7 +710,7 @@ __global__ void order_keys_kernel(OrderMaps m, uint64_t* __restrict__ keys, int3
     lo = ((uint32_t)c.x & 31u) << 27 | spread3((uint32_t)(c.y / st)) << 2 | spread3((uint32_t)(c.z / st)) << 1 |
          spread3((uint32_t)(c.w / st));
   }
-  keys[i] = (uint64_t)j << 59 | (uint64_t)mask << 32 | lo;
+  keys[i] = (uint64_t)j << m.jshift | (uint64_t)mask << 32 | lo;
   vals[i] = (int32_t)o;
 }
 
@@ -807,8 +815,9 @@ extern "C" int mvr_hash_build_lattice(const int32_t* coords, int64_t M, int stri
   return hash_build(coords, M, __builtin_ctz((unsigned)stride), table, table_bytes, s);
 }
 
-extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
-                              int ksize, int step, int transposed, int32_t* nbr, hipStream_t s) {
+extern "C" int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
+                                int ksize, int step, int transposed, int32_t* nbr, const int32_t* row_order,
+                                hipStream_t s) {
   if (!out_coords || Mout < 0 || !in_table || ksize <= 0 || (ksize & 1) == 0 || step <= 0 || !nbr) return MVR_EINVAL;
   HashView h = hash_view(const_cast<void*>(in_table), in_table_bytes);
   if (!h.cap) return MVR_EINVAL;
@@ -816,9 +825,14 @@ extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const voi
   if (tot == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)tot * 4.0, s);
   hipLaunchKernelGGL(kernel_map_kernel, dim3(nblk(tot)), dim3(256), 0, s, reinterpret_cast<const int4*>(out_coords),
-                     Mout, h, ksize, step, transposed ? -1 : 1, nbr);
+                     Mout, h, ksize, step, transposed ? -1 : 1, nbr, row_order);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
+}
+
+extern "C" int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
+                              int ksize, int step, int transposed, int32_t* nbr, hipStream_t s) {
+  return mvr_kernel_map_x(out_coords, Mout, in_table, in_table_bytes, ksize, step, transposed, nbr, nullptr, s);
 }
 
 static size_t brick_slot_of_bytes(int64_t M) { return ((size_t)(M > 0 ? M : 1) * 4 + 15) & ~(size_t)15; }
@@ -931,15 +945,18 @@ extern "C" size_t mvr_kernel_map_orders_bytes(int64_t total) { return radix_ws_b
 extern "C" int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, const int32_t* const* out_coords,
                                      const int* steps, const int64_t* Mo, int K, int32_t* perm_out, void* ws,
                                      size_t ws_bytes, hipStream_t s) {
-  if (n_maps <= 0 || n_maps > ORDER_MAX_MAPS || !nbr || !Mo || K <= 0 || K > 27 || !perm_out || !ws) return MVR_EINVAL;
+  if (n_maps <= 0 || n_maps > ORDER_MAX_MAPS || !Mo || K < 0 || K > 27 || !perm_out || !ws) return MVR_EINVAL;
+  if ((!nbr) != (K == 0) || (!nbr && !out_coords)) return MVR_EINVAL;   // K = 0, nbr NULL: coordinate orders
   OrderMaps m{};
   m.n = n_maps;
   m.K = K;
+  m.jshift = nbr ? 59 : 32;
   m.start[0] = 0;
   for (int j = 0; j < n_maps; ++j) {
     const int32_t* c = out_coords ? out_coords[j] : nullptr;
-    if (Mo[j] < 0 || (Mo[j] > 0 && !nbr[j]) || (c && (!steps || steps[j] <= 0))) return MVR_EINVAL;
-    m.nbr[j] = nbr[j];
+    if (Mo[j] < 0 || (Mo[j] > 0 && nbr && !nbr[j]) || (c && (!steps || steps[j] <= 0)) || (!nbr && Mo[j] > 0 && !c))
+      return MVR_EINVAL;
+    m.nbr[j] = nbr ? nbr[j] : nullptr;
     m.coords[j] = reinterpret_cast<const int4*>(c);
     m.step[j] = c ? steps[j] : 1;
     m.start[j + 1] = m.start[j] + Mo[j];
@@ -951,7 +968,7 @@ extern "C" int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, cons
   RadixWs w = radix_ws(ws, total);
   hipLaunchKernelGGL(order_keys_kernel, dim3(nblk(total)), dim3(256), 0, s, m, w.ka, w.va);
   int bits = 32 + K;                                   // mask above bit 32, fragment + Morton below
-  if (n_maps > 1) bits = 59 + (32 - __builtin_clz((unsigned)(n_maps - 1)));   // + the map index from bit 59
+  if (n_maps > 1) bits = m.jshift + (32 - __builtin_clz((unsigned)(n_maps - 1)));   // + the map index
   return radix_sort(w, bits, perm_out, s);
 }
 

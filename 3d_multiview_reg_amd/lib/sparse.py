@@ -9,6 +9,7 @@ and kernel map lives in HBM and is cached on the CoordinateManager shared by all
 tensors of one forward pass.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -19,6 +20,9 @@ from lib import _native as N
 # tensor strides 1-8, the strided convs 1->2, 2->4, 4->8 and the transposed 8->4, 4->2, 2->1 (keyed by output stride)
 FCGF_MAPS = (("s1", 1), ("s1", 2), ("s1", 4), ("s1", 8), ("down", 1), ("down", 2), ("down", 4),
              ("up", 4), ("up", 2), ("up", 1))
+# 3^3 kernel maps visit their output rows in (fragment, Morton) order instead of the sets' first-occurrence order
+# (identical maps; MVR_SPATIAL_MAPS=0 for A/B timing)
+SPATIAL_MAPS = os.environ.get("MVR_SPATIAL_MAPS", "1") == "1"
 
 
 class CoordinateManager:
@@ -32,6 +36,7 @@ class CoordinateManager:
         self.bricks = {}
         self.maps = {}
         self.orders = {}
+        self.spatial = {}
 
     def coords_at(self, s):
         if s not in self.coords:
@@ -71,23 +76,49 @@ class CoordinateManager:
             self.bricks[s] = t
         return self.bricks[s]
 
+    def spatial_orders(self, strides=(1, 2, 4, 8)):
+        """(fragment, Morton code of coordinates / stride) order of each level's rows, all levels in ONE radix sort
+        (mvr_kernel_map_orders without neighbour tables): the order the kernel maps visit their output rows in"""
+        todo = [s for s in strides if s not in self.spatial]
+        if not todo:
+            return
+        cs = [self.coords_at(s) for s in todo]
+        Mo = [int(c.shape[0]) for c in cs]
+        total, n = sum(Mo), len(todo)
+        L = N.lib()
+        ws = N.workspace(L.mvr_kernel_map_orders_bytes(total), self.device)
+        perm = torch.empty(max(total, 1), dtype=torch.int32, device=self.device)
+        vp = ctypes.c_void_p
+        N.check(L.mvr_kernel_map_orders(n, None, (vp * n)(*[c.data_ptr() for c in cs]), (ctypes.c_int * n)(*todo),
+                                        (ctypes.c_int64 * n)(*Mo), 0, N.ptr(perm), N.ptr(ws), ws.numel(), N.stream()),
+                "mvr_kernel_map_orders (coordinates)")
+        o = 0
+        for s, m in zip(todo, Mo):
+            self.spatial[s] = perm[o:o + m]
+            o += m
+
     def kernel_map(self, kind, s, ks=3):
         """kind 's1': ks^3 stencil within stride s; 'down': stride s -> 2s; 'up': 2s -> s (transposed), resolved
-        over the input level's lattice coordinate table."""
+        over the input level's lattice coordinate table (3^3 maps: output rows visited in spatial order)."""
         key = (kind, s, ks)
         if key not in self.maps:
             if kind == "s1":
-                out_c, tab, tr = self.coords_at(s), self.table(s), 0
+                out_s, tab, tr = s, self.table(s), 0
             elif kind == "down":
-                out_c, tab, tr = self.coords_at(2 * s), self.table(s), 0
+                out_s, tab, tr = 2 * s, self.table(s), 0
             elif kind == "up":
-                out_c, tab, tr = self.coords_at(s), self.table(2 * s), 1
+                out_s, tab, tr = s, self.table(2 * s), 1
             else:
                 raise ValueError(kind)
+            out_c = self.coords_at(out_s)
+            order = None
+            if ks == 3 and SPATIAL_MAPS:
+                self.spatial_orders()
+                order = self.spatial[out_s]
             K = ks ** 3
             nbr = torch.empty(out_c.shape[0], K, dtype=torch.int32, device=self.device)
-            N.check(N.lib().mvr_kernel_map(N.ptr(out_c), out_c.shape[0], N.ptr(tab), tab.numel(), ks, s, tr,
-                                           N.ptr(nbr), N.stream()), "mvr_kernel_map")
+            N.check(N.lib().mvr_kernel_map_x(N.ptr(out_c), out_c.shape[0], N.ptr(tab), tab.numel(), ks, s, tr,
+                                             N.ptr(nbr), N.ptr(order), N.stream()), "mvr_kernel_map_x")
             self.maps[key] = nbr
         return self.maps[key]
 

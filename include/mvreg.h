@@ -359,6 +359,11 @@ int mvr_hash_build_lattice(const int32_t* coords, int64_t M, int stride, void* t
  * row of out_coords[o] + sign*off_k*step in the input table (sign -1 if transposed), or -1 */
 int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
                    int step, int transposed, int32_t* nbr, mvr_stream_t stream);
+/* mvr_kernel_map visiting the output rows in row_order (int32 [Mout], a permutation; NULL: row order) — the same
+ * table; a spatial order (mvr_kernel_map_orders with nbr NULL) makes the workgroups that run together probe
+ * neighbouring cells of the input table */
+int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
+                     int step, int transposed, int32_t* nbr, const int32_t* row_order, mvr_stream_t stream);
 /* Row order of a kernel map: output rows sorted by their active-offset mask (K <= 27), so that a
  * tile of consecutive rows shares its active offsets; with out_coords (int32 [Mout][4], the map's output
  * coordinates, multiples of step) rows of one mask are further ordered by fragment and Morton code of
@@ -372,7 +377,8 @@ int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step
  * nbr[j] (int32 [Mo[j]][K]), out_coords[j] (or out_coords NULL: masks only) with steps[j]; perm_out int32
  * [sum Mo]: map j's order (local row indices, exactly mvr_kernel_map_order's) at offset Mo[0] + ... + Mo[j-1].
  * Workspace: mvr_kernel_map_orders_bytes(sum Mo).  (FCGF: all ten 3^3 maps of a scene, lib/sparse.py
- * CoordinateManager.prepare_orders.) */
+ * CoordinateManager.prepare_orders.)  nbr NULL with K = 0: coordinate sets only (out_coords required) — each
+ * set's rows in (fragment, Morton code of coordinates / step) order, stable (the kernel maps' visiting order). */
 size_t mvr_kernel_map_orders_bytes(int64_t total);
 int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, const int32_t* const* out_coords, const int* steps,
                           const int64_t* Mo, int K, int32_t* perm_out, void* workspace, size_t workspace_bytes,

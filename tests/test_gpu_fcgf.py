@@ -143,6 +143,37 @@ def test_lattice_table_kernel_maps_dense_and_sparse(gpu, stride):
         np.testing.assert_array_equal(maps[0], ref)
 
 
+def test_spatial_map_visit_order(gpu, frags, monkeypatch):
+    """the 3^3 kernel maps visiting their output rows in (fragment, Morton) order (mvr_kernel_map_x + the
+    coordinate-only mvr_kernel_map_orders) equal the maps built in row order, and each level's spatial order is the
+    stable sort of those keys"""
+    import torch
+    import lib.sparse
+    from lib.sparse import voxelize, CoordinateManager, FCGF_MAPS
+    c, _, counts, _ = voxelize(frags, 0.025, gpu)
+    monkeypatch.setattr(lib.sparse, "SPATIAL_MAPS", True)
+    a = CoordinateManager(c, len(counts))
+    monkeypatch.setattr(lib.sparse, "SPATIAL_MAPS", False)
+    b = CoordinateManager(c, len(counts))
+    for kind, s in FCGF_MAPS:
+        monkeypatch.setattr(lib.sparse, "SPATIAL_MAPS", True)
+        ma = a.kernel_map(kind, s)
+        monkeypatch.setattr(lib.sparse, "SPATIAL_MAPS", False)
+        assert torch.equal(ma, b.kernel_map(kind, s)), (kind, s)
+
+    def spread(v):
+        v = v & 511
+        out = np.zeros_like(v)
+        for bit in range(9):
+            out |= ((v >> bit) & 1) << (3 * bit)
+        return out
+    for s in (1, 2, 4, 8):
+        cs = a.coords_at(s).cpu().numpy().astype(np.int64)
+        q = cs[:, 1:] // s
+        lo = ((cs[:, 0] & 31) << 27) | (spread(q[:, 0]) << 2) | (spread(q[:, 1]) << 1) | spread(q[:, 2])
+        np.testing.assert_array_equal(a.spatial[s].cpu().numpy(), np.argsort(lo, kind="stable"))
+
+
 def test_batched_orders_equal_per_map_orders(gpu, frags):
     """CoordinateManager.prepare_orders (mvr_kernel_map_orders: all ten 3^3 maps of FCGF in ONE radix sort, the map
     index in the top key bits) gives every map exactly the order of mvr_kernel_map_order on that map alone; a
