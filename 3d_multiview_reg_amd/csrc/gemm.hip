@@ -1377,10 +1377,20 @@ static int launch_gemm_impl(const GemmArgs& g, hipStream_t s, bool conv2) {
   if (g.math != MATH_BF16X3) return MVR_EINVAL;
   // layout contract (gemm.hpp)
   const int64_t K4 = round4(g.K), N4 = round4(g.N);
+  // a chunk-major operand: rows 32 floats apart inside each chunk, the chunks past all its rows
+  const bool cm = g.bcs || g.ccs || (g.has_res && (g.rcs || (g.ldr && g.ldr != g.ldc)));
+  const int64_t ldr = g.ldr ? g.ldr : g.ldc;
   bool ok = al16(g.A) && al16(g.B) && al16(g.C) && g.lda % 4 == 0 && g.ldb % 4 == 0 && g.ldc % 4 == 0 &&
-            g.sAb % 4 == 0 && g.sBb % 4 == 0 && g.sCb % 4 == 0 && g.lda >= K4 && g.ldc >= N4 &&
-            g.ldb >= (g.bkc ? K4 : N4);
-  if (g.has_res) ok = ok && al16(g.R) && g.sRb % 4 == 0;
+            g.sAb % 4 == 0 && g.sBb % 4 == 0 && g.sCb % 4 == 0 && g.lda >= K4 && g.ldc >= (g.ccs ? 32 : N4) &&
+            g.ldb >= (g.bkc ? K4 : (g.bcs ? 32 : N4));
+  if (g.bcs) ok = ok && !g.bkc && g.ldb == 32 && g.bcs % 4 == 0 && g.bcs >= 32LL * g.K;
+  if (g.ccs) ok = ok && g.ldc == 32 && g.ccs % 4 == 0 && g.ccs >= 32LL * g.M;
+  if (g.has_res) {
+    ok = ok && al16(g.R) && g.sRb % 4 == 0;
+    if (g.xin != 2)   // (xin = 2: R is the block input, rows xld apart: pconv_covers)
+      ok = ok && ldr % 4 == 0 && (g.rcs ? ldr == 32 && g.rcs % 4 == 0 && g.rcs >= 32LL * g.M : ldr >= N4);
+  }
+  if (cm && !pconv_covers(g)) return MVR_EINVAL;   // only the point-conv kernel addresses chunk-major operands
   if (g.pro == PRO_A_K || g.pro == PRO_B_K)
     ok = ok && al16(g.psc) && al16(g.psh) && g.sPb % 4 == 0 && g.K % 4 == 0 && g.K <= KV_MAX;
   if (g.pro == PRO_B_SMX) ok = ok && al16(g.psc) && g.sPb % 4 == 0 && g.pld % 4 == 0 && g.pld >= N4;

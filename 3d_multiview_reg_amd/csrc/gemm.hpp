@@ -80,6 +80,10 @@ struct GemmArgs {
   // the split-once OAFilter conv2 kernel: scratch for the weights' split-bf16 image (oaf_conv2_image_bytes(N, K) bytes, written
   // by the launch), which routes it to the split-once kernel (gemm.hip oaf_conv2_kernel).  Null: generic kernel.
   uint16_t* wimg; int64_t wimg_bytes;
+  // chunk-major point activations (point-conv kernel only, bkc = 0): element (row, n) of B / C / R at
+  // row ld + (n >> 5) cs + (n & 31) with the operand's chunk stride cs (0: row-major, row ld + n); ldr: the
+  // residual's row stride (0: ldc)
+  int64_t bcs, ccs, rcs, ldr;
 };
 
 // Layout contract — operands are staged by 16-byte LDS-DMA with every address clamped into the
@@ -96,6 +100,18 @@ int launch_gemm(const GemmArgs& g, hipStream_t stream);
 // 128 -> 128 point convolutions (pconv.hip): launch_gemm routes the shapes pconv_covers() accepts there
 bool pconv_covers(const GemmArgs& g);   // head fields set: only pconv can run it
 int launch_pconv(const GemmArgs& g, hipStream_t stream);
+
+// diff_pool / diff_unpool (oan_attn.hip) over point activations in either layout (chunk stride cs, GemmArgs
+// bcs): the C-ABI mvr_oan_diff_pool_ws / mvr_oan_diff_unpool with cs = 32 (row-major)
+int oan_diff_pool_cm(const float* x, int64_t x_pstride, int64_t x_ld, int64_t x_cs, const float* sc, const float* sh,
+                     int64_t s_pstride, const float* weight, const float* bias, int P, int channels, int N, int clusters,
+                     float* out, int64_t out_pstride, int64_t out_ld, float* stats, int64_t st_ld, int st_off,
+                     void* workspace, size_t workspace_bytes, hipStream_t stream);
+int oan_diff_unpool_cm(const float* x_up, int64_t x_pstride, int64_t x_ld, int64_t x_cs, const float* sc,
+                       const float* sh, int64_t s_pstride, const float* weight, const float* bias, const float* x_down,
+                       int64_t xd_pstride, int64_t xd_ld, int P, int channels, int N, int clusters, float* out,
+                       int64_t out_pstride, int64_t out_ld, int64_t out_cs, float* stats, int64_t st_ld, int st_off,
+                       void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 // bytes of the weights' split-bf16 image the OAFilter conv2 kernel reads (GemmArgs.wimg)
 int64_t oaf_conv2_image_bytes(int N, int K);

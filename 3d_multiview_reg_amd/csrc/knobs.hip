@@ -5,7 +5,7 @@
 #include "mvreg.h"
 
 namespace mvr {
-int g_force[FORCE_COUNT] = {0, 0, 0, 0, 0, 0};
+int g_force[FORCE_COUNT] = {};
 }
 
 extern "C" int mvr_set_math(int mode) {

@@ -22,7 +22,8 @@ enum ForcePath : int {
   FORCE_NO_CONV1_FOLD = 3,    // the OANet block's conv1 stored instead of recomputed inside the first PointCN
   FORCE_POOL_NOSPLIT = 4,     // diff_pool without key splits (another fp32 summation order)
   FORCE_UNPOOL8 = 5,          // the 8-wave diff_unpool (clusters > 512) at <= 512 clusters too
-  FORCE_COUNT = 6
+  FORCE_ROW_LAYOUT = 6,       // the OANet block's point activations row-major instead of chunk-major
+  FORCE_COUNT = 7
 };
 extern int g_force[FORCE_COUNT];
 

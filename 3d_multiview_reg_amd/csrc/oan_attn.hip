@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "gemm.hpp"
 #include "knobs.hpp"
 #include "mfma_bf16.hpp"
 #include "prof.hpp"
@@ -203,12 +204,16 @@ __device__ __forceinline__ void online_softmax(float (&v)[16], float& m, float& 
   l += ps;
 }
 
+// column n of a row in the point activations' layout (oanet.hip): row-major (cs = 32: the row's element n) or
+// chunk-major (rows 32 floats apart inside each 32-point chunk, chunks cs apart)
+__device__ __forceinline__ int64_t cm_off(int n, int64_t cs) { return (int64_t)(n >> 5) * cs + (n & 31); }
+
 // O (rows c = 32 cb + (q & 3) + 8 (q >> 2) + 4h, column = 32 w + lane row) * inv -> out[c][col0 + col]
 // for columns < L (zeros in [L, round4(L))), and, per 128-column tile t of the 256 (tile index
 // col0 / 128 + t), st[t * st_tile + c] = (sum, squared deviations) over the tile's valid columns.
 // T: LDS scratch of 64 x ATL floats (two passes of 64 rows); the caller has synchronised.
 __device__ __forceinline__ void tile_out(float* T, const floatx16 (&O)[4], float inv, bool colok, float* out,
-                                         int64_t ld, int col0, int L, float2* st, int64_t st_tile) {
+                                         int64_t ld, int64_t cs, int col0, int L, float2* st, int64_t st_tile) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int col = 32 * w + l32;
   const int Lp = (L + 3) & ~3;
@@ -243,7 +248,7 @@ __device__ __forceinline__ void tile_out(float* T, const floatx16 (&O)[4], float
         const float m2 = half_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
         if (l32 == 0 && nv > 0) st[h * st_tile + c] = make_float2(sm, m2);
       }
-      if (sok) *reinterpret_cast<float4*>(out + (int64_t)c * ld + col0 + 4 * lane) = x;
+      if (sok) *reinterpret_cast<float4*>(out + (int64_t)c * ld + cm_off(col0 + 4 * lane, cs)) = x;
     }
     __syncthreads();
   }
@@ -253,7 +258,7 @@ __device__ __forceinline__ void tile_out(float* T, const floatx16 (&O)[4], float
 // diff_pool
 // ---------------------------------------------------------------------------------------------
 struct PoolArgs {
-  const float* X; int64_t xps, xld;                // x [P][128][xld] (raw)
+  const float* X; int64_t xps, xld, xcs;           // x [P][128][xld] (raw; xcs: chunk stride, cm_off)
   const float* sc; const float* sh; int64_t sps;   // folded IN+BN: xn = relu(x * sc[c] + sh[c])
   const float* W; const float* bias;               // embedding conv [Kc][128], [Kc]
   int P, N, Kc, nqb;                               // nqb = ceil(Kc / 256) query blocks
@@ -336,7 +341,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r0 = 16 * wu + 8 * i;
-      glds16s(X, (uint32_t)(r0 + (lane >> 3)) * xld4 + 4u * (uint32_t)n, dst + (uint32_t)(r0 * 128));
+      glds16s(X, (uint32_t)(r0 + (lane >> 3)) * xld4 + 4u * (uint32_t)cm_off(n, a.xcs), dst + (uint32_t)(r0 * 128));
     }
   };
   dma_tile(kb0);
@@ -594,7 +599,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_pool_kernel(PoolArgs a) {
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   const int ntile = (a.Kc + 127) / 128;
-  tile_out(reinterpret_cast<float*>(smem), O, inv, jok, a.out + (int64_t)p * a.ops, a.old, jb * AQ, a.Kc,
+  tile_out(reinterpret_cast<float*>(smem), O, inv, jok, a.out + (int64_t)p * a.ops, a.old, 32, jb * AQ, a.Kc,
            a.stats ? a.stats + ((int64_t)p * ntile + 2 * jb) * a.st_ld + a.st_off : nullptr, a.st_ld);
   ATEND(0);
 }
@@ -700,14 +705,14 @@ __global__ void split_xd16_kernel(const float* __restrict__ XD, int64_t ps, int6
 }
 
 struct UnpoolArgs {
-  const float* X; int64_t xps, xld;                // x_up [P][128][xld] (raw)
+  const float* X; int64_t xps, xld, xcs;           // x_up [P][128][xld] (raw; xcs: chunk stride, cm_off)
   const float* sc; const float* sh; int64_t sps;   // folded IN+BN of the embedding input
   const char* wimg;                                // split_w_kernel image [nkb][wimg_stride]
   const float* bias;                               // [Kc], nullable (the 8-wave kernel)
   const float2* bs;                                // split_w_kernel (bias, 1 / row scale) [nkb * 32]
   const char* dimg;                                // split_xd_kernel image [P][nkb][ximg_bytes]
   int P, N, Kc, nkb, nqb;                          // nqb = ceil(N / queries per workgroup)
-  float* out; int64_t ops, old;                    // [P][128][old]
+  float* out; int64_t ops, old, ocs;               // [P][128][old] (ocs: chunk stride, cm_off)
   float2* stats; int64_t st_ld; int st_off;        // [P][ceil(N/128)][st_ld] (+ st_off + c), nullable
   int* range;                                      // H = 1: set when an operand is outside the fp16 range
   const int* guard;                                // H = 0 re-run: return unless *guard is set
@@ -747,7 +752,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
   const int n = nb * AQ + 32 * w + l32;
   const bool nok = n < N;
   const int nlast = ((N + 3) & ~3) - 4;
-  const float* xb = a.X + (int64_t)p * a.xps + min(nb * AQ + 4 * lane, nlast);
+  const float* xb = a.X + (int64_t)p * a.xps + cm_off(min(nb * AQ + 4 * lane, nlast), a.xcs);
   auto qdma = [&](int qt) {
     char* dst = smem + USTAGE + (qt & 1) * 32768;
 #pragma unroll
@@ -854,7 +859,7 @@ __global__ __launch_bounds__(ATHREADS) void oan_unpool_kernel(UnpoolArgs a) {
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   const int ntile = (N + 127) / 128;
-  tile_out(reinterpret_cast<float*>(smem), O, inv, nok, a.out + (int64_t)p * a.ops, a.old, nb * AQ, N,
+  tile_out(reinterpret_cast<float*>(smem), O, inv, nok, a.out + (int64_t)p * a.ops, a.old, a.ocs, nb * AQ, N,
            a.stats ? a.stats + ((int64_t)p * ntile + 2 * nb) * a.st_ld + a.st_off : nullptr, a.st_ld);
 }
 
@@ -938,7 +943,7 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
   const int n = nb * U4Q + 32 * w + l32;
   const bool nok = n < N;
   const int nlast = ((N + 3) & ~3) - 4;
-  const float* xb = a.X + (int64_t)p * a.xps + min(nb * U4Q + 4 * l32, nlast);
+  const float* xb = a.X + (int64_t)p * a.xps + cm_off(min(nb * U4Q + 4 * l32, nlast), a.xcs);
   auto qdma = [&](int qt) {
     char* dst = smem + WI4 + (qt & 1) * U4QB;
 #pragma unroll
@@ -1102,7 +1107,7 @@ __global__ __launch_bounds__(U4T, 2) void oan_unpool4_kernel(UnpoolArgs a) {
         const float m2 = half_sum((d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3));
         if (l32 == 0 && nv > 0) st[c] = make_float2(sm, m2);
       }
-      if (sok) *reinterpret_cast<float4*>(out + (int64_t)c * a.old + col0 + 4 * l32) = x;
+      if (sok) *reinterpret_cast<float4*>(out + (int64_t)c * a.old + cm_off(col0 + 4 * l32, a.ocs)) = x;
     }
     __syncthreads();
   }
@@ -1230,16 +1235,30 @@ extern "C" int mvr_oan_diff_pool_ws(const float* x, int64_t x_pstride, int64_t x
                                     int channels, int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld,
                                     float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
                                     hipStream_t stream) {
+  return mvr::oan_diff_pool_cm(x, x_pstride, x_ld, 32, sc, sh, s_pstride, weight, bias, P, channels, N, clusters, out,
+                               out_pstride, out_ld, stats, st_ld, st_off, workspace, workspace_bytes, stream);
+}
+
+// x row-major (x_cs = 32) or chunk-major (x_ld = 32, chunks x_cs >= 32 x 128 floats apart: oanet.hip's point
+// activations)
+int mvr::oan_diff_pool_cm(const float* x, int64_t x_pstride, int64_t x_ld, int64_t x_cs, const float* sc,
+                          const float* sh, int64_t s_pstride, const float* weight, const float* bias, int P,
+                          int channels, int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld,
+                          float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
+                          hipStream_t stream) {
   if (!x || !sc || !sh || !weight || !out || P < 0 || N <= 0 || channels != AC || clusters <= 0 ||
       clusters > MAX_CLUSTERS)
     return MVR_EINVAL;
-  if (x_ld < round_up4(N) || (x_ld & 3) || (x_pstride & 3) || !al16(x) || !al16(weight) || !al16(out) ||
-      out_ld < round_up4(clusters) || (out_ld & 3) || (out_pstride & 3) || (stats && (st_ld < channels + st_off)))
+  const bool xcm = x_cs != 32;
+  if ((xcm ? (x_ld != 32 || (x_cs & 3) || x_cs < 32 * AC) : x_ld < round_up4(N)) || (x_ld & 3) || (x_pstride & 3) ||
+      !al16(x) || !al16(weight) || !al16(out) || out_ld < round_up4(clusters) || (out_ld & 3) || (out_pstride & 3) ||
+      (stats && (st_ld < channels + st_off)))
     return MVR_EINVAL;
-  if ((int64_t)AC * x_ld * 4 >= ((int64_t)1 << 31)) return MVR_EINVAL;   // 32-bit lane offsets of the tile DMAs
+  // 32-bit lane offsets of the tile DMAs
+  if ((xcm ? (int64_t)((N + 31) / 32) * x_cs : (int64_t)AC * x_ld) * 4 >= ((int64_t)1 << 31)) return MVR_EINVAL;
   if (P == 0) return MVR_OK;
   PoolArgs a{};
-  a.X = x; a.xps = x_pstride; a.xld = x_ld;
+  a.X = x; a.xps = x_pstride; a.xld = x_ld; a.xcs = x_cs;
   a.sc = sc; a.sh = sh; a.sps = s_pstride;
   a.W = weight; a.bias = bias;
   a.P = P; a.N = N; a.Kc = clusters; a.nqb = (clusters + AQ - 1) / AQ;
@@ -1293,10 +1312,25 @@ extern "C" int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t
                                    int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld, float* stats,
                                    int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
                                    hipStream_t stream) {
+  return mvr::oan_diff_unpool_cm(x_up, x_pstride, x_ld, 32, sc, sh, s_pstride, weight, bias, x_down, xd_pstride,
+                                 xd_ld, P, channels, N, clusters, out, out_pstride, out_ld, 32, stats, st_ld, st_off,
+                                 workspace, workspace_bytes, stream);
+}
+
+// x_up and out row-major (cs = 32) or chunk-major (ld = 32, chunks cs >= 32 x 128 floats apart)
+int mvr::oan_diff_unpool_cm(const float* x_up, int64_t x_pstride, int64_t x_ld, int64_t x_cs, const float* sc,
+                            const float* sh, int64_t s_pstride, const float* weight, const float* bias,
+                            const float* x_down, int64_t xd_pstride, int64_t xd_ld, int P, int channels, int N,
+                            int clusters, float* out, int64_t out_pstride, int64_t out_ld, int64_t out_cs,
+                            float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
+                            hipStream_t stream) {
   if (!x_up || !sc || !sh || !weight || !x_down || !out || !workspace || P < 0 || N <= 0 || channels != AC ||
       clusters <= 0 || clusters > MAX_CLUSTERS)
     return MVR_EINVAL;
-  if ((x_ld < round_up4(N)) || (x_ld & 3) || (x_pstride & 3) || xd_ld < clusters || out_ld < round_up4(N) ||
+  auto bad_layout = [&](int64_t ld, int64_t cs) {
+    return cs != 32 ? (ld != 32 || (cs & 3) || cs < 32 * AC) : ld < round_up4(N);
+  };
+  if (bad_layout(x_ld, x_cs) || (x_ld & 3) || (x_pstride & 3) || xd_ld < clusters || bad_layout(out_ld, out_cs) ||
       (out_ld & 3) || (out_pstride & 3) || !al16(out) || !al16(workspace) || (stats && (st_ld < channels + st_off)))
     return MVR_EINVAL;
   if (P == 0) return MVR_OK;
@@ -1310,11 +1344,11 @@ extern "C" int mvr_oan_diff_unpool(const float* x_up, int64_t x_pstride, int64_t
   const double by = 4.0 * AC * (2.0 * N + clusters) * P;
   ProfScope prof(PK_UNPOOL, fl, by, stream);
   UnpoolArgs a{};
-  a.X = x_up; a.xps = x_pstride; a.xld = x_ld;
+  a.X = x_up; a.xps = x_pstride; a.xld = x_ld; a.xcs = x_cs;
   a.sc = sc; a.sh = sh; a.sps = s_pstride;
   a.wimg = wimg; a.bias = bias; a.bs = bs; a.dimg = dimg;
   a.P = P; a.N = N; a.Kc = clusters; a.nkb = nkb; a.nqb = (N + AQ - 1) / AQ;
-  a.out = out; a.ops = out_pstride; a.old = out_ld;
+  a.out = out; a.ops = out_pstride; a.old = out_ld; a.ocs = out_cs;
   a.stats = reinterpret_cast<float2*>(stats); a.st_ld = st_ld; a.st_off = st_off;
   const int64_t nx = (int64_t)P * nkb * 1024;
   const dim3 gw((nkb * 512 + 255) / 256), gx((unsigned)((nx + 255) / 256));

@@ -243,15 +243,16 @@ __global__ void pad_cols_kernel(const float* __restrict__ w, int rows, int cols,
 
 // Output head (oanet.py:163,174-175): logits = w.x + b; weights = relu(tanh(logits));
 // guard_pos[p] += #positive weights (the batch-coupled zero-row guard reads it).
-__global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld, int C, int N, const float* __restrict__ w,
-                            const float* __restrict__ bias, float* logits, float* scores, int32_t* pos) {
+__global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld, int64_t cs, int C, int N,
+                            const float* __restrict__ w, const float* __restrict__ bias, float* logits, float* scores,
+                            int32_t* pos) {
   __shared__ int cnt;
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
   if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
   if (n < N) {
-    const float* x = X + (int64_t)p * ps + n;
+    const float* x = X + (int64_t)p * ps + (int64_t)(n >> 5) * cs + (n & 31);   // (Act layouts)
     float acc = 0.f;
     for (int c = 0; c < C; ++c) acc = fmaf(w[c], x[(int64_t)c * ld], acc);
     const float lg = acc + bias[0];
@@ -281,21 +282,23 @@ namespace {
 static unsigned long long* g_dbg = nullptr;
 static int g_dbg_cap = 0, g_dbg_n = 0;
 
-__global__ void dbg_hash_kernel(const float* __restrict__ p, int rows, int L, int64_t ps, int64_t ld, int64_t total,
-                                unsigned long long* out) {
+__global__ void dbg_hash_kernel(const float* __restrict__ p, int rows, int L, int64_t ps, int64_t ld, int64_t cs,
+                                int64_t total, unsigned long long* out) {
   unsigned long long acc = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t n = i % L, r = (i / L) % rows, b = i / ((int64_t)L * rows);
-    acc += (unsigned long long)__float_as_uint(p[b * ps + r * ld + n]) * (unsigned long long)(2 * i + 1);
+    acc += (unsigned long long)__float_as_uint(p[b * ps + r * ld + (n >> 5) * cs + (n & 31)]) *
+           (unsigned long long)(2 * i + 1);
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) atomicAdd(out, acc);
 }
 
-static void dbg_hash(const float* p, int P, int rows, int L, int64_t ps, int64_t ld, hipStream_t s) {
+// (cs: the chunk stride of a chunk-major activation, Act; 0: row-major — the hash does not depend on the layout)
+static void dbg_hash(const float* p, int P, int rows, int L, int64_t ps, int64_t ld, hipStream_t s, int64_t cs = 0) {
   if (!g_dbg || g_dbg_n >= g_dbg_cap) return;
-  hipLaunchKernelGGL(dbg_hash_kernel, dim3(1024), dim3(256), 0, s, p, rows, L, ps, ld, (int64_t)P * rows * L,
-                     g_dbg + g_dbg_n++);
+  hipLaunchKernelGGL(dbg_hash_kernel, dim3(1024), dim3(256), 0, s, p, rows, L, ps, ld, cs ? cs : 32,
+                     (int64_t)P * rows * L, g_dbg + g_dbg_n++);
 }
 
 // and a copy of one chosen stage's statistics partials (mvr_debug_stage_dump)
@@ -332,6 +335,8 @@ struct Act {
   int tw0 = 128;              // tile width of the partials of channels [0, csplit) (set by the writer)
   int csplit = 1 << 30;
   int tw1 = 128;              // ... and of channels [csplit, C)
+  int64_t cs = 0;             // chunk-major (point activations, Plan::cm): rows ld = 32 floats apart inside each
+                              // 32-point chunk, chunks cs apart; 0: row-major (rows ld apart)
 };
 
 struct Ws {
@@ -350,6 +355,8 @@ struct Plan {
   int P, N, C, Kc, Cin;
   int64_t Np, Kp, Cinp;  // padded row lengths (points, clusters, conv1 input channels)
   bool fused;            // diff_pool / diff_unpool as fused attention kernels (oan_attn.hip)
+  bool cm = false;       // the point activations XA, T1, X11 chunk-major (set by the block forward when every
+                         // kernel that touches them addresses that layout: point convs, fused attention)
   char* uimg;            // their split-bf16 operand images
   size_t uimg_bytes;
   size_t bytes;
@@ -459,6 +466,13 @@ struct Ctx {
     if (hipGetLastError() != hipSuccess && !err) err = MVR_ELAUNCH;
   }
 
+  // a point activation of C rows at p inside a buffer of `rows` rows per pair (X11: 2C), in the plan's layout
+  Act pts(float* p, int C, int rows, float2* st, int64_t st_ld, int st_off = 0) const {
+    Act a{p, (int64_t)rows * pl.Np, pl.cm ? 32 : pl.Np, C, pl.N, st, st_ld, st_off};
+    a.cs = pl.cm ? 32LL * rows : 0;
+    return a;
+  }
+
   // IN(eps)+BN fold of activation `a` -> sc / sh ([P][a.C], default pl.sc / pl.sh)
   void finalize_in(const Act& a, float eps, const mvr_bn_p& bn, float* sc = nullptr, float* sh = nullptr) {
     if (!sc) { sc = this->sc(); sh = this->sh(); }
@@ -507,9 +521,9 @@ struct Ctx {
     g.math = MATH_BF16X3;
     g.M = out.C; g.N = in.L; g.K = in.C; g.batch = pl.P;
     g.A = w_padded ? w_padded : cv.weight; g.sAb = 0; g.lda = w_padded ? round4(in.C) : in.C;
-    g.B = in.p; g.sBb = in.ps; g.ldb = in.ld; g.bkc = 0;
-    g.C = out.p; g.sCb = out.ps; g.ldc = out.ld;
-    if (res) { g.R = res->p; g.sRb = res->ps; g.has_res = 1; }
+    g.B = in.p; g.sBb = in.ps; g.ldb = in.ld; g.bkc = 0; g.bcs = in.cs;
+    g.C = out.p; g.sCb = out.ps; g.ldc = out.ld; g.ccs = out.cs;
+    if (res) { g.R = res->p; g.sRb = res->ps; g.has_res = 1; g.ldr = res->ld; g.rcs = res->cs; }
     g.bias = cv.bias; g.bias_mode = cv.bias ? BIAS_M : BIAS_NONE;
     if (pro) { g.pro = PRO_B_K; g.psc = pro_sc ? pro_sc : sc(); g.psh = pro_sh ? pro_sh : sh(); g.sPb = in.C; }
     g.stats_mode = stats_mode;
@@ -548,7 +562,7 @@ struct Ctx {
   // next consumer's); returns whether it did
   bool pointcn(const mvr_pointcn_p& pc, const Act& x, Act& y, const FoldReq* next = nullptr, bool x_folded = false) {
     if (!x_folded) finalize_in(x, 1e-5f, pc.bn1);
-    Act t{pl.T1, (int64_t)y.C * pl.Np, pl.Np, y.C, pl.N, pl.stT, y.C, 0};
+    Act t = pts(pl.T1, y.C, y.C, pl.stT, y.C);
     const bool sc = pc.shortcut.weight != nullptr;
     y.tw0 = 128;
     y.csplit = 1 << 30;
@@ -569,7 +583,7 @@ struct Ctx {
                          hd ? nullptr : next);
     head = nullptr;
     if (!hd) {
-      dbg_hash(y.p, pl.P, y.C, pl.N, y.ps, y.ld, s);
+      dbg_hash(y.p, pl.P, y.C, pl.N, y.ps, y.ld, s, y.cs);
       // rows [st_off, st_off + C) of each tile's partials (the rest of st_ld may belong to another producer)
       dbg_hash(reinterpret_cast<const float*>(y.st + y.st_off), pl.P * TNn, 1, 2 * y.C, y.st_ld * 2, 0, s);
       dbg_dump(y.st, (size_t)pl.P * TNn * y.st_ld * sizeof(float2), s);
@@ -641,7 +655,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (C % 4 || ld < round4(N) || ld % 4 || in_pstride % 4 || (reinterpret_cast<uintptr_t>(input) & 15))
     return MVR_EINVAL;
   if (!blk->l1_2[0].shortcut.weight) return MVR_EINVAL;
-  const Plan pl = plan(C, Kc, Cin, P, N, workspace);
+  Plan pl = plan(C, Kc, Cin, P, N, workspace);
   if (workspace_bytes < pl.bytes) return MVR_EINVAL;
   Ctx cx{pl, s, bn_train ? 1 : 0, bn_train > 1 ? std::min(bn_train, P) : P, g_gemm_h || g_pconv_h};
   if (cx.f16 && hipMemsetAsync(pl.flags, 0, sizeof(int) * FLAG_SLOTS, s) != hipSuccess) return MVR_ELAUNCH;
@@ -661,8 +675,6 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     w1 = pl.W1;
   }
   Act in{const_cast<float*>(input), in_pstride, ld, Cin, N, nullptr, 0, 0};
-  Act xa{pl.XA, CN, Np, C, N, pl.stA, C, 0};
-  Act x11top{pl.X11, 2 * CN, Np, C, N, pl.st11, 2 * C, 0};
   // conv1 folded into the first l1_1 PointCN when the point-conv kernel takes it: x = conv1(input) is
   // recomputed by that PointCN's conv3 (B operand) and conv7 (residual) from the input's <= 8 rows, and
   // for its InstanceNorm statistics (xin_stats_kernel)
@@ -678,6 +690,20 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   f3.prof_kind = PK_CONV_PTS;
   const bool fold1 = !g_force[FORCE_NO_CONV1_FOLD] && Cin <= 8 && C == 128 && !blk->l1_1[0].shortcut.weight &&
                      pconv_covers(f3);
+  // the point activations chunk-major when every launch that touches them can address it: the point-conv kernel
+  // for every point conv (conv1 folded, so no generic GEMM writes one) and the fused diff_pool / diff_unpool
+  auto pconv_takes = [&](int K, int pro, int res, int st) {
+    GemmArgs q{};
+    q.math = MATH_BF16X3; q.M = C; q.N = N; q.K = K; q.batch = P; q.bias_mode = BIAS_M;
+    q.pro = pro ? PRO_B_K : PRO_NONE; q.has_res = res; q.stats_mode = st ? ST_ROW : ST_NONE;
+    return pconv_covers(q);
+  };
+  pl.cm = fold1 && pl.fused && !g_force[FORCE_ROW_LAYOUT] && pconv_takes(C, 1, 1, 1) && pconv_takes(C, 1, 0, 1) &&
+          pconv_takes(2 * C, 1, 0, 1) && pconv_takes(2 * C, 0, 0, 0);
+  Act xa = cx.pts(pl.XA, C, C, pl.stA, C);
+  Act x11top = cx.pts(pl.X11, C, 2 * C, pl.st11, 2 * C);
+  const int64_t x11cs = x11top.cs ? x11top.cs : 32;   // (oan_attn.hip's convention: 32 = row-major)
+  f3.ldc = xa.ld; f3.ccs = xa.cs;                     // T1: XA's layout
   // folds the last l1_1 conv fuses: down1's IN(1e-3) + BN for diff_pool, and up1's into scU for diff_unpool
   FoldReq fx11{1e-3f, blk->down_bn};
   fx11.eps2 = 1e-3f; fx11.bn2 = blk->up_bn; fx11.sc2 = pl.scU; fx11.sh2 = pl.shU;
@@ -699,7 +725,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     int f3done = 0;
     cx.fuse(f3, f5, &f3done);
     cx.chk(launch_gemm(f3, s));   // conv3 of l1_1[0], B = relu(IN/BN(conv1(input)))
-    Act t{pl.T1, CN, Np, C, N, pl.stT, C, 0};
+    Act t = cx.pts(pl.T1, C, C, pl.stT, C);
     dbg_hash(reinterpret_cast<const float*>(pl.stT), P, 1, TN * C * 2, (int64_t)TN * C * 2, 0, s);
     if (!cx.fused(f3, &f5, f3done, C)) cx.finalize_in(t, 1e-5f, blk->l1_1[0].bn5);
     dbg_hash(cx.sc(), P, 1, C, C, 0, s);
@@ -708,8 +734,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     GemmArgs f7{};
     f7.math = MATH_BF16X3; f7.M = C; f7.N = N; f7.K = C; f7.batch = P;
     f7.A = blk->l1_1[0].conv7.weight; f7.lda = C;
-    f7.B = pl.T1; f7.sBb = CN; f7.ldb = Np;
-    f7.C = y.p; f7.sCb = y.ps; f7.ldc = y.ld;
+    f7.B = pl.T1; f7.sBb = CN; f7.ldb = t.ld; f7.bcs = t.cs;
+    f7.C = y.p; f7.sCb = y.ps; f7.ldc = y.ld; f7.ccs = y.cs;
     f7.R = input; f7.sRb = in_pstride; f7.has_res = 1;
     f7.bias = blk->l1_1[0].conv7.bias; f7.bias_mode = f7.bias ? BIAS_M : BIAS_NONE;
     f7.pro = PRO_B_K; f7.psc = cx.sc(); f7.psh = cx.sh(); f7.sPb = C;
@@ -722,8 +748,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     cx.fuse(f7, *n7, &f7done);
     cx.chk(launch_gemm(f7, s));   // conv7 of l1_1[0] + x (recomputed)
     yfold = cx.fused(f7, n7, f7done, C);
-    dbg_hash(pl.T1, P, C, N, CN, Np, s);
-    dbg_hash(y.p, P, C, N, y.ps, y.ld, s);
+    dbg_hash(pl.T1, P, C, N, CN, t.ld, s, t.cs);
+    dbg_hash(y.p, P, C, N, y.ps, y.ld, s, y.cs);
   } else {
     cx.conv(blk->conv1, in, false, xa, nullptr, ST_ROW, w1);
   }
@@ -733,8 +759,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     Act& yo = (i == H - 1) ? x11top : xa;
     const FoldReq fn{1e-5f, i + 1 < H ? blk->l1_1[i + 1].bn1 : mvr_bn_p{}};
     yfold = cx.pointcn(blk->l1_1[i], xa, yo, i == H - 1 ? &fx11 : &fn, yfold);
-    dbg_hash(pl.T1, P, C, N, CN, Np, s);
-    dbg_hash(yo.p, P, C, N, yo.ps, yo.ld, s);
+    dbg_hash(pl.T1, P, C, N, CN, xa.ld, s, xa.cs);
+    dbg_hash(yo.p, P, C, N, yo.ps, yo.ld, s, yo.cs);
   }
   const bool up_folded = yfold;   // scU holds up1's fold of x1_1 too
 
@@ -742,9 +768,9 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   if (!yfold) cx.finalize_in(x11top, 1e-3f, blk->down_bn);
   Act xd{pl.XD, (int64_t)C * Kp, Kp, C, Kc, pl.stD, C, 0};
   if (pl.fused) {
-    cx.chk(mvr_oan_diff_pool_ws(pl.X11, 2 * CN, Np, cx.sc(), cx.sh(), C, blk->down_conv.weight, blk->down_conv.bias, P,
-                                C, N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD), C, 0,
-                                !g_force[FORCE_POOL_NOSPLIT] ? pl.uimg : nullptr, pl.uimg_bytes, s));
+    cx.chk(oan_diff_pool_cm(pl.X11, 2 * CN, x11top.ld, x11cs, cx.sc(), cx.sh(), C, blk->down_conv.weight,
+                            blk->down_conv.bias, P, C, N, Kc, pl.XD, (int64_t)C * Kp, Kp, reinterpret_cast<float*>(pl.stD),
+                            C, 0, !g_force[FORCE_POOL_NOSPLIT] ? pl.uimg : nullptr, pl.uimg_bytes, s));
   } else {
     Act e{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, Kc, 0};
     cx.conv(blk->down_conv, x11top, true, e, nullptr, ST_ROWSMX);
@@ -773,9 +799,9 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   // diff_unpool (oanet.py:113-129) -> X11 rows [C, 2C): softmax over clusters
   if (!up_folded) cx.finalize_in(x11top, 1e-3f, blk->up_bn, pl.scU, pl.shU);
   if (pl.fused) {
-    cx.chk(mvr_oan_diff_unpool(pl.X11, 2 * CN, Np, pl.scU, pl.shU, C, blk->up_conv.weight, blk->up_conv.bias, pl.XD,
-                               (int64_t)C * Kp, Kp, P, C, N, Kc, pl.X11 + CN, 2 * CN, Np,
-                               reinterpret_cast<float*>(pl.st11), 2 * C, C, pl.uimg, pl.uimg_bytes, s));
+    cx.chk(oan_diff_unpool_cm(pl.X11, 2 * CN, x11top.ld, x11cs, pl.scU, pl.shU, C, blk->up_conv.weight,
+                              blk->up_conv.bias, pl.XD, (int64_t)C * Kp, Kp, P, C, N, Kc, pl.X11 + C * x11top.ld, 2 * CN,
+                              x11top.ld, x11cs, reinterpret_cast<float*>(pl.st11), 2 * C, C, pl.uimg, pl.uimg_bytes, s));
   } else {
     Act e2{pl.E, (int64_t)Kc * Np, Np, Kc, N, pl.smx, N, 0};
     cx.conv(blk->up_conv, x11top, true, e2, nullptr, ST_COLSMX, nullptr, false, nullptr, pl.scU, pl.shU);
@@ -793,13 +819,15 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     g.flag = cx.flag();
     cx.chk(launch_gemm(g, s));
   }
-  dbg_hash(pl.X11 + CN, P, C, N, 2 * CN, Np, s);
+  dbg_hash(pl.X11 + C * x11top.ld, P, C, N, 2 * CN, x11top.ld, s, x11top.cs);
   // l1_2: PointCN(2C -> C, shortcut) + (H-1) PointCN(C)
-  Act x11{pl.X11, 2 * CN, Np, 2 * C, N, pl.st11, 2 * C, 0};
+  Act x11 = cx.pts(pl.X11, 2 * C, 2 * C, pl.st11, 2 * C);
   x11.tw0 = x11top.tw0;   // rows [0, C): the last l1_1 PointCN; rows [C, 2C): diff_unpool (128)
   x11.csplit = C;
   x11.tw1 = 128;
-  Act out{latent ? latent : pl.XA, latent ? (int64_t)C * ld : CN, latent ? ld : Np, C, N, pl.stA, C, 0};
+  // in XA; the last PointCN writes the returned activation (latent, row-major [P][C][ld]) when there is one
+  Act outI = cx.pts(pl.XA, C, C, pl.stA, C);
+  Act outL{latent, (int64_t)C * ld, ld, C, N, pl.stA, C, 0};
   // the output head (oanet.py:163,174-178) runs in the epilogue of the last PointCN conv when the
   // point-conv kernel takes it; the guard counts start at zero either way
   if (hipMemsetAsync(guard_pos, 0, sizeof(int32_t) * P, s) != hipSuccess) return MVR_ELAUNCH;
@@ -816,13 +844,16 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
       cx.h_logits = logits; cx.h_scores = scores; cx.h_pos = guard_pos;
     }
     const FoldReq fn{1e-5f, i + 1 < H ? blk->l1_2[i + 1].bn1 : mvr_bn_p{}};
-    ofold = cx.pointcn(blk->l1_2[i], i == 0 ? x11 : out, out, i + 1 < H ? &fn : nullptr, i > 0 && ofold);
-    dbg_hash(pl.T1, P, C, N, CN, Np, s);
-    if (latent || i < H - 1) dbg_hash(out.p, P, C, N, out.ps, out.ld, s);
+    Act& yo = (latent && i == H - 1) ? outL : outI;
+    ofold = cx.pointcn(blk->l1_2[i], i == 0 ? x11 : outI, yo, i + 1 < H ? &fn : nullptr, i > 0 && ofold);
+    dbg_hash(pl.T1, P, C, N, CN, outI.ld, s, outI.cs);
+    if (latent || i < H - 1) dbg_hash(yo.p, P, C, N, yo.ps, yo.ld, s, yo.cs);
   }
+  const Act& out = latent ? outL : outI;
   dbg_hash(logits, P, 1, N, N, N, s);
   if (!fuse_head) {
-    hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, out.ps, out.ld, C, N,
+    hipLaunchKernelGGL(head_kernel, dim3((N + 255) / 256, P), dim3(256), 0, s, out.p, out.ps, out.ld,
+                       out.cs ? out.cs : (int64_t)32, C, N,
                        blk->output.weight, blk->output.bias, logits, scores, guard_pos);
     cx.chk_launch();
   }

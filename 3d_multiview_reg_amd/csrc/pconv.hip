@@ -64,10 +64,14 @@ constexpr int CH = 32;               // points per chunk (one MFMA column block)
 constexpr int GRP = 4;               // chunks per statistics group (128 points, gemm.hpp GEMM_BN)
 constexpr int YLD = 32;              // row stride (floats) of the per-wave transpose scratch
 
+// Activation layouts (per operand): element (row k, point n) at k ld + (n >> 5) cs + (n & 31) — row-major
+// [rows][ld] with cs = 32, or chunk-major [N / 32][rows][32] with ld = 32, cs = 32 rows (oanet.hip: every 32-point
+// chunk of a pair one contiguous block, so a chunk's loads and stores are whole 16 KB blocks instead of 128 row
+// segments 128 bytes long)
 struct PcArgs {
-  const float* X; int64_t xps, xld;     // input [P][128][xld]
-  float* Y; int64_t yps, yld;           // output [P][128][yld]
-  const float* R; int64_t rps;          // residual [P][128][yld] (RES)
+  const float* X; int64_t xps, xld, xcs;   // input [P][128][xld]
+  float* Y; int64_t yps, yld, ycs;         // output [P][128][yld]
+  const float* R; int64_t rps, rrs, rcs;   // residual (RES): rows rrs apart
   const float* W; int64_t wld;          // weight [128][wld]
   const float* bias;                    // [128] or null
   const float* sc; const float* sh; int64_t sPb;   // prologue fold [P][sPb] (PRO)
@@ -352,7 +356,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
         r[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ri, 4 * n, min(i, a.xci - 1) * xld4, 0));
       return;
     }
-    const int vo = 8 * h * xld4 + 4 * n;
+    const int vo = 8 * h * xld4 + 4 * ((n >> 5) * (int)a.xcs + (n & 31));
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -428,15 +432,15 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       rxi = *reinterpret_cast<const float4*>(a.R + (int64_t)c.p * a.rps + (int64_t)min(lane >> 3, a.xci - 1) * a.rld + n);
       return;
     }
-    const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + erow) * a.yld + n;
+    const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + erow) * a.rrs + (int64_t)(n >> 5) * a.rcs + (n & 31);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (PCONV_NTR) {
-        const u32x4 u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + (int64_t)(8 * q) * a.yld));
+        const u32x4 u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + (int64_t)(8 * q) * a.rrs));
         rres[(RES && !(XI & 2)) ? q : 0] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
                                                        __uint_as_float(u.w));
       } else {
-        rres[(RES && !(XI & 2)) ? q : 0] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.yld);
+        rres[(RES && !(XI & 2)) ? q : 0] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.rrs);
       }
     }
   };
@@ -512,7 +516,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
         PC_FENCE();
       }
     }
-    float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + n0 + ec0;
+    float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + (int64_t)c.kc * a.ycs + ec0;
     const bool full = n0 + CH <= N;   // uniform: every column of the chunk is valid
     if (HEAD != 2 && a.Y) {   // (a.Y null: a statistics-only pass)
 #pragma unroll
@@ -771,9 +775,9 @@ bool pconv_covers(const GemmArgs& g) {
 
 int launch_pconv(const GemmArgs& g, hipStream_t s) {
   PcArgs a{};
-  a.X = g.B; a.xps = g.sBb; a.xld = g.ldb;
-  a.Y = g.C; a.yps = g.sCb; a.yld = g.ldc;
-  a.R = g.R; a.rps = g.sRb;
+  a.X = g.B; a.xps = g.sBb; a.xld = g.ldb; a.xcs = g.bcs ? g.bcs : CH;
+  a.Y = g.C; a.yps = g.sCb; a.yld = g.ldc; a.ycs = g.ccs ? g.ccs : CH;
+  a.R = g.R; a.rps = g.sRb; a.rrs = g.ldr ? g.ldr : g.ldc; a.rcs = g.rcs ? g.rcs : CH;
   a.W = g.A; a.wld = g.lda;
   a.bias = g.bias_mode == BIAS_M ? g.bias : nullptr;
   a.sc = g.psc; a.sh = g.psh; a.sPb = g.sPb;

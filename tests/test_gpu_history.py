@@ -93,4 +93,4 @@ def test_math_knobs_default_f32eq():
     L = NV.lib()
     for what in NV.FORCE.values():
         assert L.mvr_debug_force(what, 0) == 0
-    assert L.mvr_debug_force(6, 0) == -1
+    assert L.mvr_debug_force(len(NV.FORCE), 0) == -1

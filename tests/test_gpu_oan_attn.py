@@ -395,3 +395,35 @@ def test_oanet_conv1_folded_vs_stored(gpu, npts, train):
             r32, r64 = o32[k][i], o64[k][i]
             bound = np.maximum(1e-4, 3 * np.maximum(dist(m, r64), dist(r32, r64)))
             assert (dist(f, r64) <= bound).all(), (i, k, dist(f, r64), dist(m, r64), dist(r32, r64))
+
+
+@pytest.mark.parametrize("npts,train,math", [(2000, False, "f32eq"), (517, False, "f32eq"), (33, False, "f32eq"),
+                                             (1200, True, "f32eq"), (2000, False, "split16")])
+def test_oanet_chunk_major_activations_bit_identical(gpu, npts, train, math):
+    """The block's point activations chunk-major (default: every 32-point chunk of a pair one contiguous block of
+    its rows) vs row-major (forced): the same kernels with other addresses, so every output — logits, scores, R, t
+    and the returned latent activation (row-major either way) — is bit-identical; ragged point counts (a partial
+    last chunk; 33 points: two chunks, one of them a single point), train-mode BatchNorm, and the split-fp16 maths
+    (its guarded re-runs read the same operands)."""
+    import torch
+    from lib import _native as NV
+    from test_gpu_oanet import _oanet
+    from synth import synth_correspondences
+    xs, _, _ = synth_correspondences(5, npts, seed=31)
+    net = _oanet(128, 500, 13, gpu, train=train, which="full")
+    prev = NV.math_state()
+    NV.set_math(math)
+    try:
+        outs = []
+        for row in (0, 1):
+            with NV.force("row_layout", row), torch.no_grad():
+                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
+    finally:
+        NV.lib().mvr_set_math(prev)
+    a, b = outs
+    for k in ("logits", "scores", "rot_est", "trans_est"):
+        for i in range(2):
+            u, v = a[k][i].cpu().numpy(), b[k][i].cpu().numpy()
+            assert np.array_equal(u, v), (k, i, np.abs(u - v).max())
+    u, v = a["latent features"].cpu().numpy(), b["latent features"].cpu().numpy()
+    assert np.array_equal(u, v), np.abs(u - v).max()

@@ -12,7 +12,7 @@ template <> struct Vec<1> { typedef float T; };
 template <> struct Vec<2> { typedef float2 T; };
 template <> struct Vec<4> { typedef float4 T; };
 
-template <int V, int STORE>
+template <int V, int STORE, int TILED = 0>
 __global__ __launch_bounds__(256, 2) void stream_kernel(const float* X, float* Y, int P, int N, int ld, float* sink) {
   typedef typename Vec<V>::T T;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l32 = lane & 31, h = lane >> 5;
@@ -24,6 +24,8 @@ __global__ __launch_bounds__(256, 2) void stream_kernel(const float* X, float* Y
   auto addr = [&](long s, int t, int i) -> long {
     const long p = s / nst;
     const int n = min((int)(s - p * nst) * PTS + V * l32, N - V);
+    if (TILED)   // chunk-major [P][N / 32][128][32]: a step's 128 rows x 128 B are one contiguous 16 KB block
+      return p * 128L * ld + (long)(n >> 5) * 4096 + (long)(32 * w + 8 * h + 16 * t + i) * 32 + (n & 31);
     return p * 128L * ld + (long)(32 * w + 8 * h + 16 * t + i) * ld + n;
   };
   T xa[16], xb[16];
@@ -45,7 +47,9 @@ __global__ __launch_bounds__(256, 2) void stream_kernel(const float* X, float* Y
     if (STORE == 2) {   // pconv's epilogue pattern: lane -> row (lane >> 1) of the wave's 32, 16 columns
       const long p = s / nst;
       const int n0 = (int)(s - p * nst) * PTS;
-      float* dst = Y + p * 128L * ld + (long)(32 * w + (lane >> 1)) * ld + min(n0 + 16 * (lane & 1), N - 16);
+      const int nn = min(n0 + 16 * (lane & 1), N - 16);
+      float* dst = TILED ? Y + p * 128L * ld + (long)(nn >> 5) * 4096 + (long)(32 * w + (lane >> 1)) * 32 + (nn & 31)
+                         : Y + p * 128L * ld + (long)(32 * w + (lane >> 1)) * ld + nn;
       const float* f = reinterpret_cast<const float*>(&r[0]);
 #pragma unroll
       for (int i4 = 0; i4 < 4; ++i4) reinterpret_cast<float4*>(dst)[i4] = make_float4(f[0], f[1], acc, f[0]);
@@ -98,16 +102,16 @@ static float run_copy(const float* X, float* Y, long n4, int grid) {
   return ms / 10;
 }
 
-template <int V, int STORE>
+template <int V, int STORE, int TILED = 0>
 static float run(const float* X, float* Y, int P, int N, int ld, float* sink, int grid) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int it = 0; it < 2; ++it) hipLaunchKernelGGL((stream_kernel<V, STORE>), dim3(grid), dim3(256), 0, 0, X, Y, P, N, ld, sink);
+  for (int it = 0; it < 2; ++it) hipLaunchKernelGGL((stream_kernel<V, STORE, TILED>), dim3(grid), dim3(256), 0, 0, X, Y, P, N, ld, sink);
   hipEventRecord(e0);
   const int iters = 10;
   for (int it = 0; it < iters; ++it)
-    hipLaunchKernelGGL((stream_kernel<V, STORE>), dim3(grid), dim3(256), 0, 0, X, Y, P, N, ld, sink);
+    hipLaunchKernelGGL((stream_kernel<V, STORE, TILED>), dim3(grid), dim3(256), 0, 0, X, Y, P, N, ld, sink);
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms;
@@ -144,6 +148,19 @@ int main() {
       printf("ld %d grid %4d  read+write: V1 %.3f ms (%.0f GB/s)  V2 %.3f (%.0f)  V4 %.3f (%.0f) | pconv-store V1 %.3f (%.0f) | read only: V1 %.3f (%.0f) V4 %.3f (%.0f)\n",
              ld, grid, t1, gb / t1 * 1e3, t2, gb / t2 * 1e3, t4, gb / t4 * 1e3, e1, gb / e1 * 1e3, r1, gb / 2 / r1 * 1e3, r4,
              gb / 2 / r4 * 1e3);
+    }
+  }
+  {   // chunk-major layout (N a multiple of 32 per pair, ld = N): pconv's loads and epilogue stores
+    const int N = 4992, ld = 4992;
+    const double gb = 2.0 * P * 128.0 * N * 4 / 1e9;
+    for (int grid : {512, 1024}) {
+      const float rw = run<1, 1>(X, Y, P, N, ld, sink, grid), rwt = run<1, 1, 1>(X, Y, P, N, ld, sink, grid);
+      const float e = run<1, 2>(X, Y, P, N, ld, sink, grid), et = run<1, 2, 1>(X, Y, P, N, ld, sink, grid);
+      const float r = run<1, 0>(X, Y, P, N, ld, sink, grid), rt = run<1, 0, 1>(X, Y, P, N, ld, sink, grid);
+      printf("N %d grid %4d  rows vs chunk-major: read+write %.3f (%.0f GB/s) / %.3f (%.0f) | pconv-store %.3f (%.0f) / "
+             "%.3f (%.0f) | read only %.3f (%.0f) / %.3f (%.0f)\n",
+             N, grid, rw, gb / rw * 1e3, rwt, gb / rwt * 1e3, e, gb / e * 1e3, et, gb / et * 1e3, r, gb / 2 / r * 1e3,
+             rt, gb / 2 / rt * 1e3);
     }
   }
   return 0;
