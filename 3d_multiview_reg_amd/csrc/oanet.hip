@@ -274,6 +274,11 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 #define OAN_FUSED_FIN 0
 #endif
 
+// Point activations chunk-major where every kernel touching them takes it (Plan::cm; 0: row-major, the A/B build)
+#ifndef OAN_CHUNK_MAJOR
+#define OAN_CHUNK_MAJOR 1
+#endif
+
 namespace {
 
 // Debugging aid (mvr_debug_stage_hash): a position-weighted 64-bit sum of the bit patterns of each stage's
@@ -698,7 +703,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
     q.pro = pro ? PRO_B_K : PRO_NONE; q.has_res = res; q.stats_mode = st ? ST_ROW : ST_NONE;
     return pconv_covers(q);
   };
-  pl.cm = fold1 && pl.fused && !g_force[FORCE_ROW_LAYOUT] && pconv_takes(C, 1, 1, 1) && pconv_takes(C, 1, 0, 1) &&
+  pl.cm = OAN_CHUNK_MAJOR && fold1 && pl.fused && !g_force[FORCE_ROW_LAYOUT] && pconv_takes(C, 1, 1, 1) && pconv_takes(C, 1, 0, 1) &&
           pconv_takes(2 * C, 1, 0, 1) && pconv_takes(2 * C, 0, 0, 0);
   Act xa = cx.pts(pl.XA, C, C, pl.stA, C);
   Act x11top = cx.pts(pl.X11, C, 2 * C, pl.st11, 2 * C);
