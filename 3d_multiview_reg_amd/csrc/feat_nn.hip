@@ -767,7 +767,9 @@ extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* 
                               const int64_t* pairs, int P, int Nq, int Mt, int C, float inv_tau2, int mode, float* out,
                               int64_t out_pstride, int64_t out_nstride, int32_t* idx_out, int n_frag, void* workspace,
                               size_t workspace_bytes, hipStream_t stream) {
-  if (!Fq || !Ft || !Xt || !pairs || !out || P < 0 || Nq < 0 || Mt <= 0) return MVR_EINVAL;
+  if (P < 0 || Nq < 0 || Mt <= 0 || C != 32 || (mode != 0 && mode != 1)) return MVR_EINVAL;
+  if (P == 0 || Nq == 0) return MVR_OK;   // empty batch: NULL pointers allowed (mvreg.h conventions)
+  if (!Fq || !Ft || !Xt || !pairs || !out) return MVR_EINVAL;
   if (workspace && (n_frag <= 0 || workspace_bytes < mvr_feat_nn_workspace_bytes(n_frag, Mt) ||
                     (reinterpret_cast<uintptr_t>(workspace) & 15)))
     return MVR_EINVAL;
@@ -775,8 +777,6 @@ extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* 
   if ((reinterpret_cast<uintptr_t>(Fq) & 15) || (reinterpret_cast<uintptr_t>(Ft) & 15) || (fq_fstride & 3) ||
       (ft_fstride & 3))
     return MVR_EINVAL;
-  if (mode != 0 && mode != 1) return MVR_EINVAL;
-  if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt,
                 inv_tau2 * 1.4426950408889634f, mode, out, out_pstride, out_nstride, idx_out, mvr::g_feat_nn_fast,
                 nullptr, 0};
@@ -805,11 +805,12 @@ extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* 
 extern "C" int mvr_feat_knn2(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride,
                              const int64_t* pairs, int P, int Nq, int Mt, int C, int32_t* idx2_out, double* dist2_out,
                              hipStream_t stream) {
-  if (!Fq || !Ft || !pairs || !idx2_out || P < 0 || Nq < 0 || Mt < 2 || C != 32) return MVR_EINVAL;
+  if (P < 0 || Nq < 0 || Mt < 2 || C != 32) return MVR_EINVAL;
+  if (P == 0 || Nq == 0) return MVR_OK;
+  if (!Fq || !Ft || !pairs || !idx2_out) return MVR_EINVAL;
   if ((reinterpret_cast<uintptr_t>(Fq) & 15) || (reinterpret_cast<uintptr_t>(Ft) & 15) || (fq_fstride & 3) ||
       (ft_fstride & 3))
     return MVR_EINVAL;
-  if (P == 0 || Nq == 0) return MVR_OK;
   mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, nullptr, 0, Ft, 0, pairs, P, Nq, Mt, 1.4426950408889634f, 2,
                 nullptr, 0, 0, idx2_out, 0, nullptr, 0};
   mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * C * 4 + P * Nq * 8.0,
@@ -826,8 +827,9 @@ extern "C" int mvr_feat_knn2(const float* Fq, int64_t fq_fstride, const float* F
 }
 
 extern "C" int mvr_gather_rows(const float* src, int C, const int64_t* idx, int n, float* dst, hipStream_t stream) {
-  if (!src || !idx || !dst || C <= 0 || n < 0) return MVR_EINVAL;
+  if (C <= 0 || n < 0) return MVR_EINVAL;
   if (n == 0) return MVR_OK;
+  if (!src || !idx || !dst) return MVR_EINVAL;
   const int64_t tot = (int64_t)n * C;
   hipLaunchKernelGGL(mvr::gather_rows_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, src, C, idx, n,
                      dst);

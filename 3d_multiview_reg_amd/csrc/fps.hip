@@ -210,7 +210,9 @@ __global__ __launch_bounds__(T) void fps_reg_kernel(const float* __restrict__ xy
 // xyz [sum n, 3] fp32 (fragments back to back, offsets off[B+1]); idx_out [B][m] int64 global rows
 extern "C" int mvr_fps(const float* xyz, const int64_t* offsets, const int64_t* offsets_host, int B, int m,
                        int64_t* idx_out, hipStream_t stream) {
-  if (!xyz || !offsets || !offsets_host || !idx_out || B < 0 || m <= 0) return MVR_EINVAL;
+  if (B < 0 || m <= 0) return MVR_EINVAL;
+  if (B == 0) return MVR_OK;
+  if (!xyz || !offsets || !offsets_host || !idx_out) return MVR_EINVAL;
   int64_t nmax = 0;
   for (int b = 0; b < B; ++b) {
     const int64_t n = offsets_host[b + 1] - offsets_host[b];

@@ -1493,7 +1493,9 @@ extern "C" int mvr_oaf_conv2_f32(int M, int N, int K, int batch, const float* A,
   g.psc = psc; g.psh = psh; g.sPb = sPb; g.pro = mvr::PRO_A_K;
   g.stats = reinterpret_cast<float2*>(stats); g.st_ld = st_ld; g.stats_mode = mvr::ST_ROW;
   g.wimg = static_cast<uint16_t*>(img); g.wimg_bytes = img_bytes;
-  if (!R || !bias || !psc || !psh || !stats || !img || M != 128 || K % 4) return MVR_EINVAL;
+  if (M != 128 || K % 4 || N < 0 || batch < 0) return MVR_EINVAL;
+  if (N == 0 || batch == 0) return MVR_OK;   // empty: NULL pointers allowed
+  if (!R || !bias || !psc || !psh || !stats || !img) return MVR_EINVAL;
   if (!mvr::oaf_conv2_covers(g)) return MVR_EINVAL;
   return mvr::launch_gemm_impl(g, stream, true);
 }

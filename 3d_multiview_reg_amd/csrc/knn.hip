@@ -136,8 +136,9 @@ int launch(const KnnArgs& a, int B, hipStream_t s) {
 extern "C" int mvr_knn1(const float* pos1, int64_t p1_bstride, int64_t p1_rstride, const float* pos2,
                         int64_t p2_bstride, int64_t p2_rstride, int B, int N, int M, float* dist_out, int64_t* idx_out,
                         mvr_stream_t stream) {
-  if (B < 0 || N <= 0 || M < 0 || !pts_ok(pos1, p1_bstride, p1_rstride) || !pts_ok(pos2, p2_bstride, p2_rstride) ||
-      (!dist_out && !idx_out) || N > (1 << 30))
+  if (B < 0 || N <= 0 || M < 0 || N > (1 << 30)) return MVR_EINVAL;
+  if (B == 0 || M == 0) return MVR_OK;   // no queries: NULL pointers allowed
+  if (!pts_ok(pos1, p1_bstride, p1_rstride) || !pts_ok(pos2, p2_bstride, p2_rstride) || (!dist_out && !idx_out))
     return MVR_EINVAL;
   KnnArgs a{};
   a.tgt = Pts{pos1, p1_bstride, p1_rstride};
@@ -153,7 +154,9 @@ extern "C" int mvr_mutuals(const float* x1, int64_t x1_bstride, int64_t x1_rstri
                            int64_t x2_bstride, int64_t x2_rstride, const float* x1m, int64_t x1m_bstride,
                            int64_t x1m_rstride, const float* x2m, int64_t x2m_bstride, int64_t x2m_rstride, int B, int N,
                            float thr2, float* flag_out, int64_t* idx_out, mvr_stream_t stream) {
-  if (B < 0 || N <= 0 || N > (1 << 30) || !flag_out || !pts_ok(x1, x1_bstride, x1_rstride) ||
+  if (B < 0 || N <= 0 || N > (1 << 30)) return MVR_EINVAL;
+  if (B == 0) return MVR_OK;
+  if (!flag_out || !pts_ok(x1, x1_bstride, x1_rstride) ||
       !pts_ok(x2, x2_bstride, x2_rstride) || !pts_ok(x1m, x1m_bstride, x1m_rstride) ||
       !pts_ok(x2m, x2m_bstride, x2m_rstride))
     return MVR_EINVAL;

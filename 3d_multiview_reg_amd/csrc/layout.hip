@@ -17,8 +17,9 @@ __global__ void xs_to_channels_kernel(const float* __restrict__ xs, int64_t ps, 
 
 extern "C" int mvr_xs_to_channels(const float* xs, int64_t xs_pstride, int64_t xs_nstride, int C, int P, int N,
                                   float* out, int64_t out_pstride, int64_t out_ld, hipStream_t stream) {
-  if (!xs || !out || C < 0 || P < 0 || N < 0 || out_ld < N) return MVR_EINVAL;
-  if (P == 0 || N == 0) return MVR_OK;
+  if (C < 0 || P < 0 || N < 0 || out_ld < N) return MVR_EINVAL;
+  if (P == 0 || N == 0 || C == 0) return MVR_OK;
+  if (!xs || !out) return MVR_EINVAL;
   hipLaunchKernelGGL(mvr::xs_to_channels_kernel, dim3((N + 255) / 256, P), dim3(256), 0, stream, xs, xs_pstride,
                      xs_nstride, C, N, out, out_pstride, out_ld);
   MVR_CHECK_LAUNCH();

@@ -1246,9 +1246,9 @@ int mvr::oan_diff_pool_cm(const float* x, int64_t x_pstride, int64_t x_ld, int64
                           int channels, int N, int clusters, float* out, int64_t out_pstride, int64_t out_ld,
                           float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
                           hipStream_t stream) {
-  if (!x || !sc || !sh || !weight || !out || P < 0 || N <= 0 || channels != AC || clusters <= 0 ||
-      clusters > MAX_CLUSTERS)
-    return MVR_EINVAL;
+  if (P < 0 || N <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return MVR_EINVAL;
+  if (P == 0) return MVR_OK;   // no pairs: NULL pointers allowed
+  if (!x || !sc || !sh || !weight || !out) return MVR_EINVAL;
   const bool xcm = x_cs != 32;
   if ((xcm ? (x_ld != 32 || (x_cs & 3) || x_cs < 32 * AC) : x_ld < round_up4(N)) || (x_ld & 3) || (x_pstride & 3) ||
       !al16(x) || !al16(weight) || !al16(out) || out_ld < round_up4(clusters) || (out_ld & 3) || (out_pstride & 3) ||
@@ -1324,9 +1324,9 @@ int mvr::oan_diff_unpool_cm(const float* x_up, int64_t x_pstride, int64_t x_ld, 
                             int clusters, float* out, int64_t out_pstride, int64_t out_ld, int64_t out_cs,
                             float* stats, int64_t st_ld, int st_off, void* workspace, size_t workspace_bytes,
                             hipStream_t stream) {
-  if (!x_up || !sc || !sh || !weight || !x_down || !out || !workspace || P < 0 || N <= 0 || channels != AC ||
-      clusters <= 0 || clusters > MAX_CLUSTERS)
-    return MVR_EINVAL;
+  if (P < 0 || N <= 0 || channels != AC || clusters <= 0 || clusters > MAX_CLUSTERS) return MVR_EINVAL;
+  if (P == 0) return MVR_OK;   // no pairs: NULL pointers allowed
+  if (!x_up || !sc || !sh || !weight || !x_down || !out || !workspace) return MVR_EINVAL;
   auto bad_layout = [&](int64_t ld, int64_t cs) {
     return cs != 32 ? (ld != 32 || (cs & 3) || cs < 32 * AC) : ld < round_up4(N);
   };

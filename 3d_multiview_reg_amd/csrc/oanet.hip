@@ -654,6 +654,8 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
                                      float* latent, float* res_row, float* score_row, int64_t row_pstride,
                                      int32_t* guard_pos, int32_t* status, int guard_group, void* workspace,
                                      size_t workspace_bytes, hipStream_t s) {
+  if (P < 0 || N < 0) return MVR_EINVAL;
+  if (P == 0) return MVR_OK;   // no pairs: NULL pointers allowed (mvreg.h conventions)
   if (!blk || !input || !xs || !logits || !scores || !R || !t || !res || !guard_pos || !workspace) return MVR_EINVAL;
   const int C = blk->channels, Kc = blk->clusters, H = blk->half_layers, Cin = blk->in_channels;
   if (P <= 0 || N <= 0 || C <= 0 || Kc <= 0 || H <= 0 || H > MVR_OAN_MAX_HALF || Cin <= 0) return MVR_EINVAL;

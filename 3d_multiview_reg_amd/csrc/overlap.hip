@@ -8,11 +8,11 @@
 //     counts as matched when some point of the other fragment lies at distance < r (the
 //     reference's 1-NN distance test, sklearn NearestNeighbors in fp64) — a 27-cell probe with
 //     early exit instead of a KD-tree.
-// All geometry is fp64 (the reference works on float64 arrays).  Latency / hash-probe bound.
-#include <hipcub/hipcub.hpp>
-
+// All geometry is fp64 (the reference works on float64 arrays).  Latency / hash-probe bound.  The sorts are the
+// in-tree onesweep radix sort and the scan its reduce-then-scan sibling (radix.hip): no library kernels.
 #include "common.hpp"
 #include "prof.hpp"
+#include "radix.hpp"
 #include "mvreg.h"
 
 namespace mvr {
@@ -63,14 +63,24 @@ __global__ void frag_min_kernel(const float* __restrict__ xyz, const int64_t* __
 
 // Open3D: ref = (p - (min_bound - v/2)) / v; index = floor(ref)   (fp64)
 __global__ void voxel_key_kernel(const float* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
-                                 const double* __restrict__ minb, double v, uint64_t* keys, int32_t* idx) {
+                                 const double* __restrict__ minb, double v, uint64_t* keys, uint64_t* keys2,
+                                 int32_t* idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int b = frag_of(off, B, i);
   int64_t c[3];
   for (int d = 0; d < 3; ++d) c[d] = (int64_t)floor(((double)xyz[3 * i + d] - (minb[3 * b + d] - v * 0.5)) / v);
-  keys[i] = pack_key(b, c[0], c[1], c[2]);
+  const uint64_t k = pack_key(b, c[0], c[1], c[2]);
+  keys[i] = k;
+  keys2[i] = k;
   idx[i] = (int32_t)i;
+}
+
+// sorted keys from the sort's permutation (the sort itself returns the values only)
+__global__ void gather_keys_kernel(const uint64_t* __restrict__ k, const int32_t* __restrict__ perm, int64_t n,
+                                   uint64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = k[perm[i]];
 }
 
 __global__ void head_flag_kernel(const uint64_t* __restrict__ k, int64_t n, int32_t* head) {
@@ -120,13 +130,15 @@ struct RIndex {
 };
 
 __global__ void cell_key_kernel(const double* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t M,
-                                double r, uint64_t* keys, int32_t* idx) {
+                                double r, uint64_t* keys, uint64_t* keys2, int32_t* idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   const int b = frag_of(off, B, i);
   int64_t c[3];
   for (int d = 0; d < 3; ++d) c[d] = (int64_t)floor(xyz[3 * i + d] / r) + OV_BIAS;
-  keys[i] = pack_key(b, c[0], c[1], c[2]);
+  const uint64_t k = pack_key(b, c[0], c[1], c[2]);
+  keys[i] = k;
+  keys2[i] = k;
   idx[i] = (int32_t)i;
 }
 
@@ -203,18 +215,10 @@ inline char* take(char*& p, size_t b) {
   p += b;
   return r;
 }
-size_t sort_bytes(int64_t n) {
-  size_t t = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)(n > 0 ? n : 1), 0, 64);
-  return t;
-}
-size_t scan_bytes(int64_t n) {
-  size_t t = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                         (int)(n > 0 ? n : 1));
-  return t;
-}
+size_t sort_bytes(int64_t n) { return radix_ws_bytes(n > 0 ? n : 1); }
+size_t scan_bytes(int64_t n) { return scan_ws_bytes(n > 0 ? n : 1); }
+// key bits of pack_key for fragments [0, B): 48 coordinate bits + the fragment index
+int key_bits(int B) { return 3 * OV_BITS + (B > 1 ? 32 - __builtin_clz((unsigned)(B - 1)) : 1); }
 uint64_t cap_for(int64_t M) {
   uint64_t c = 1024;
   while (c < (uint64_t)(2 * (M > 0 ? M : 1))) c <<= 1;
@@ -237,7 +241,7 @@ size_t index_bytes(int64_t M) {
 // scratch of the index build (after the index itself)
 size_t build_scratch_bytes(int64_t M) {
   const size_t m = (size_t)(M > 0 ? M : 1);
-  return m * 12 + sort_bytes(M) + 3 * 256;
+  return m * 8 + sort_bytes(M) + 3 * 256;
 }
 
 }  // namespace
@@ -247,19 +251,22 @@ using namespace mvr;
 
 extern "C" size_t mvr_voxel_centroids_workspace_bytes(int64_t n) {
   const size_t m = (size_t)(n > 0 ? n : 1);
-  return m * (8 + 4 + 8 + 4 + 4 + 4) + sort_bytes(n) + scan_bytes(n) + 4096 * 24 + 10 * 256;
+  return m * (8 + 8 + 4 + 4 + 4) + sort_bytes(n) + scan_bytes(n) + 4096 * 24 + 10 * 256;
 }
 
 extern "C" int mvr_voxel_centroids(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel,
                                    void* ws, size_t ws_bytes, double* out_xyz, int64_t* out_off, hipStream_t s) {
-  if (!xyz || !frag_off || !ws || !out_xyz || !out_off || B <= 0 || B > 4096 || n < 0 || n > 0x7fffffff ||
-      !(voxel > 0.0) || ws_bytes < mvr_voxel_centroids_workspace_bytes(n))
-    return MVR_EINVAL;
+  if (!frag_off || !out_off || B <= 0 || B > 4096 || n < 0 || n > 0x7fffffff || !(voxel > 0.0)) return MVR_EINVAL;
+  if (n > 0 && (!xyz || !ws || !out_xyz || ws_bytes < mvr_voxel_centroids_workspace_bytes(n))) return MVR_EINVAL;
+  if (n == 0) {   // every fragment empty: offsets all 0 (NULL point / workspace pointers allowed)
+    hipLaunchKernelGGL(fill_i64_kernel, dim3(nb(B + 1)), dim3(256), 0, s, out_off, (int64_t)B + 1, (int64_t)0);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   char* p = reinterpret_cast<char*>(ws);
   const size_t m = (size_t)(n > 0 ? n : 1);
   uint64_t* kin = reinterpret_cast<uint64_t*>(take(p, m * 8));
-  int32_t* vin = reinterpret_cast<int32_t*>(take(p, m * 4));
   uint64_t* kout = reinterpret_cast<uint64_t*>(take(p, m * 8));
   int32_t* vout = reinterpret_cast<int32_t*>(take(p, m * 4));
   int32_t* head = reinterpret_cast<int32_t*>(take(p, m * 4));
@@ -268,18 +275,16 @@ extern "C" int mvr_voxel_centroids(const float* xyz, const int64_t* frag_off, in
   size_t st = sort_bytes(n), sc = scan_bytes(n);
   void* tsort = take(p, st);
   void* tscan = take(p, sc);
+  RadixWs rw = radix_ws(tsort, n);
   hipLaunchKernelGGL(fill_i64_kernel, dim3(nb(B + 1)), dim3(256), 0, s, out_off, (int64_t)B + 1, (int64_t)-1);
-  if (n == 0) {
-    hipLaunchKernelGGL(fix_offsets_kernel, dim3(1), dim3(1), 0, s, out_off, B, head, pos, n);
-    MVR_CHECK_LAUNCH();
-    return MVR_OK;
-  }
   hipLaunchKernelGGL(frag_min_kernel, dim3(B), dim3(256), 0, s, xyz, frag_off, minb);
-  hipLaunchKernelGGL(voxel_key_kernel, dim3(nb(n)), dim3(256), 0, s, xyz, frag_off, B, n, minb, voxel, kin, vin);
-  if (hipcub::DeviceRadixSort::SortPairs(tsort, st, kin, kout, vin, vout, (int)n, 0, 64, s) != hipSuccess)
-    return MVR_ELAUNCH;
+  hipLaunchKernelGGL(voxel_key_kernel, dim3(nb(n)), dim3(256), 0, s, xyz, frag_off, B, n, minb, voxel, rw.ka, kin,
+                     rw.va);
+  int rc = radix_sort(rw, key_bits(B), vout, s);   // stable: a voxel's points stay in input order
+  if (rc != MVR_OK) return rc;
+  hipLaunchKernelGGL(gather_keys_kernel, dim3(nb(n)), dim3(256), 0, s, kin, vout, n, kout);
   hipLaunchKernelGGL(head_flag_kernel, dim3(nb(n)), dim3(256), 0, s, kout, n, head);
-  if (hipcub::DeviceScan::ExclusiveSum(tscan, sc, head, pos, (int)n, s) != hipSuccess) return MVR_ELAUNCH;
+  if ((rc = excl_scan_i32(head, pos, n, tscan, sc, s)) != MVR_OK) return rc;
   hipLaunchKernelGGL(centroid_kernel, dim3(nb(n)), dim3(256), 0, s, xyz, kout, vout, head, pos, n, B, out_xyz,
                      out_off);
   hipLaunchKernelGGL(fix_offsets_kernel, dim3(1), dim3(1), 0, s, out_off, B, head, pos, n);
@@ -291,15 +296,14 @@ extern "C" size_t mvr_radius_index_bytes(int64_t M) { return index_bytes(M) + bu
 
 extern "C" int mvr_radius_index_build(const double* xyz, const int64_t* off, int B, int64_t M, double r, void* index,
                                       size_t bytes, hipStream_t s) {
-  if (!xyz || !off || !index || B <= 0 || B >= (1 << 15) || M < 0 || M > 0x7fffffff || !(r > 0.0) ||
-      bytes < mvr_radius_index_bytes(M))
+  if (!off || !index || B <= 0 || B >= (1 << 15) || M < 0 || M > 0x7fffffff || !(r > 0.0) ||
+      bytes < mvr_radius_index_bytes(M) || (M > 0 && !xyz))
     return MVR_EINVAL;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)M * 60.0, s);
   RIndex ix = index_view(index, M);
   char* p = reinterpret_cast<char*>(index) + index_bytes(M);
   const size_t m = (size_t)(M > 0 ? M : 1);
   uint64_t* kin = reinterpret_cast<uint64_t*>(take(p, m * 8));
-  int32_t* vin = reinterpret_cast<int32_t*>(take(p, m * 4));
   size_t st = sort_bytes(M);
   void* tsort = take(p, st);
   hipLaunchKernelGGL(hash_clear64_kernel, dim3(nb((int64_t)ix.cap)), dim3(256), 0, s, ix.hkeys, ix.cap);
@@ -307,9 +311,11 @@ extern "C" int mvr_radius_index_build(const double* xyz, const int64_t* off, int
     MVR_CHECK_LAUNCH();
     return MVR_OK;
   }
-  hipLaunchKernelGGL(cell_key_kernel, dim3(nb(M)), dim3(256), 0, s, xyz, off, B, M, r, kin, vin);
-  if (hipcub::DeviceRadixSort::SortPairs(tsort, st, kin, ix.skey, vin, ix.sidx, (int)M, 0, 64, s) != hipSuccess)
-    return MVR_ELAUNCH;
+  RadixWs rw = radix_ws(tsort, M);
+  hipLaunchKernelGGL(cell_key_kernel, dim3(nb(M)), dim3(256), 0, s, xyz, off, B, M, r, rw.ka, kin, rw.va);
+  const int rc = radix_sort(rw, key_bits(B), ix.sidx, s);
+  if (rc != MVR_OK) return rc;
+  hipLaunchKernelGGL(gather_keys_kernel, dim3(nb(M)), dim3(256), 0, s, kin, ix.sidx, M, ix.skey);
   hipLaunchKernelGGL(cell_insert_kernel, dim3(nb(M)), dim3(256), 0, s, ix, M);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
@@ -318,11 +324,13 @@ extern "C" int mvr_radius_index_build(const double* xyz, const int64_t* off, int
 extern "C" int mvr_radius_overlap_count(const void* index, size_t bytes, const double* xyz, const int64_t* off, int B,
                                         int64_t M, const int64_t* pairs, const double* T, int P, int64_t max_points,
                                         double r, int32_t* counts, hipStream_t s) {
-  if (!index || !xyz || !off || !pairs || !T || !counts || B <= 0 || M < 0 || P < 0 || max_points < 0 ||
-      !(r > 0.0) || bytes < mvr_radius_index_bytes(M) || P > 32767)
+  if (B <= 0 || M < 0 || P < 0 || max_points < 0 || !(r > 0.0) || P > 32767) return MVR_EINVAL;
+  if (P == 0) return MVR_OK;   // no pairs: NULL pointers allowed
+  if (!counts) return MVR_EINVAL;
+  if (max_points > 0 && (!index || !xyz || !off || !pairs || !T || bytes < mvr_radius_index_bytes(M)))
     return MVR_EINVAL;
   if (hipMemsetAsync(counts, 0, sizeof(int32_t) * 2 * (size_t)P, s) != hipSuccess) return MVR_ELAUNCH;
-  if (P == 0 || max_points == 0) return hipGetLastError() == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  if (max_points == 0) return hipGetLastError() == hipSuccess ? MVR_OK : MVR_ELAUNCH;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)P * 2.0 * (double)max_points * 200.0, s);
   RIndex ix = index_view(const_cast<void*>(index), M);
   hipLaunchKernelGGL(overlap_count_kernel, dim3(nb(max_points), 2 * P), dim3(256), 0, s, ix, xyz, off, pairs, T, r,

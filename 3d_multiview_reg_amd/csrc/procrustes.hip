@@ -387,9 +387,10 @@ static int procrustes_launch(const T* x1, const T* x2, int64_t x_pstride, int64_
                              const int32_t* guard_pos, T* w_copy, int64_t wc_pstride, int P, int N, int normalize,
                              T eps, T* R, T* t, T* res, int64_t res_pstride, T* res_copy, int64_t rc_pstride,
                              int32_t* status, int guard_group, hipStream_t stream) {
-  if (P < 0 || N < 0 || !x1 || !x2 || !R || !t || guard_group < 0) return MVR_EINVAL;
-  if (guard_pos && !w) return MVR_EINVAL;
+  if (P < 0 || N < 0 || guard_group < 0) return MVR_EINVAL;
   if (P == 0) return MVR_OK;
+  if ((N > 0 && (!x1 || !x2)) || !R || !t) return MVR_EINVAL;
+  if (guard_pos && N > 0 && !w) return MVR_EINVAL;
   mvr::ProcrustesArgs<T> a{x1, x2, x_pstride, x_nstride, w, w_pstride, guard_pos, w_copy, wc_pstride,
                            P, N, normalize, eps, guard_group, R, t, res, res_pstride, res_copy, rc_pstride, status};
   mvr::ProfScope prof(mvr::PK_PROCRUSTES, 40.0 * P * N, (double)P * N * sizeof(T) * 8, stream);
@@ -427,10 +428,11 @@ extern "C" int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride,
                           int iters, double max_dist, uint64_t seed, double* T, double* fitness, double* rmse,
                           int32_t* best_iter, double* hyp_out, void* workspace, size_t workspace_bytes,
                           hipStream_t stream) {
-  if (P < 0 || !x1 || !x2 || !n || !T || !fitness || !rmse || !best_iter || ransac_n < 3 || ransac_n > 8 ||
-      iters <= 0 || iters >= (1 << 30) || P >= (1 << 23) || !(max_dist > 0.0))
+  if (P < 0 || ransac_n < 3 || ransac_n > 8 || iters <= 0 || iters >= (1 << 30) || P >= (1 << 23) ||
+      !(max_dist > 0.0))
     return MVR_EINVAL;
   if (P == 0) return MVR_OK;
+  if (!x1 || !x2 || !n || !T || !fitness || !rmse || !best_iter) return MVR_EINVAL;
   const size_t need = mvr_ransac_workspace_bytes(P, iters) - (hyp_out ? (size_t)P * iters * 12 * sizeof(double) : 0);
   if (!workspace || workspace_bytes < need) return MVR_EINVAL;
   mvr::RansacArgs a{};

@@ -49,14 +49,22 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh) {
 }
 }  // namespace
 
+// digit mask of pass p of a `bits`-bit sort: the last pass of a bit count that is not a digit multiple keeps only the
+// key bits below `bits` (key bits at or above it never decide the order)
+__device__ __host__ __forceinline__ uint32_t radix_dmask(int bits, int p) {
+  const int rem = bits - RADIX_BITS * p;
+  return rem >= RADIX_BITS ? (uint32_t)(RADIX_BINS - 1) : ((1u << rem) - 1u);
+}
+
 __global__ __launch_bounds__(RADIX_THREADS) void radix_hist_kernel(const uint64_t* __restrict__ keys, int64_t n,
-                                                                   int npass, uint32_t* __restrict__ hist) {
+                                                                   int bits, uint32_t* __restrict__ hist) {
+  const int npass = (bits + RADIX_BITS - 1) / RADIX_BITS;
   __shared__ uint32_t h[RADIX_MAX_PASSES * RADIX_BINS];
   for (int i = threadIdx.x; i < RADIX_MAX_PASSES * RADIX_BINS; i += RADIX_THREADS) h[i] = 0;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * RADIX_THREADS + threadIdx.x; i < n; i += (int64_t)gridDim.x * RADIX_THREADS) {
     const uint64_t k = keys[i];
-    for (int p = 0; p < npass; ++p) atomicAdd(&h[p * RADIX_BINS + (int)((k >> (RADIX_BITS * p)) & (RADIX_BINS - 1))], 1u);
+    for (int p = 0; p < npass; ++p) atomicAdd(&h[p * RADIX_BINS + (int)((k >> (RADIX_BITS * p)) & radix_dmask(bits, p))], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < npass * RADIX_BINS; i += RADIX_THREADS)
@@ -68,7 +76,7 @@ __global__ __launch_bounds__(RADIX_THREADS) void radix_pass_kernel(const uint64_
                                                                    const int32_t* __restrict__ vin,
                                                                    uint64_t* __restrict__ kout,
                                                                    int32_t* __restrict__ vout, int64_t n, int shift,
-                                                                   const uint32_t* __restrict__ hist,
+                                                                   uint32_t dmask, const uint32_t* __restrict__ hist,
                                                                    uint32_t* ticket, uint32_t* look) {
   __shared__ uint32_t wcnt[RADIX_THREADS / 64][RADIX_BINS];   // per wave: running digit counts, then offsets
   __shared__ uint32_t dbase[RADIX_BINS];                      // global offset of the tile's first key per digit
@@ -95,7 +103,7 @@ __global__ __launch_bounds__(RADIX_THREADS) void radix_pass_kernel(const uint64_
 #pragma unroll
   for (int r = 0; r < RADIX_KPT; ++r) {
     const bool valid = base + r * 64 < n;
-    const uint32_t d = (uint32_t)(key[r] >> shift) & (RADIX_BINS - 1);
+    const uint32_t d = (uint32_t)(key[r] >> shift) & dmask;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int b = 0; b < RADIX_BITS; ++b) {
@@ -143,12 +151,92 @@ __global__ __launch_bounds__(RADIX_THREADS) void radix_pass_kernel(const uint64_
 #pragma unroll
   for (int r = 0; r < RADIX_KPT; ++r) {
     if (base + r * 64 < n) {
-      const uint32_t dg = (uint32_t)(key[r] >> shift) & (RADIX_BINS - 1);
+      const uint32_t dg = (uint32_t)(key[r] >> shift) & dmask;
       const uint32_t pos = dbase[dg] + wcnt[w][dg] + rank[r];
       if (!LAST) kout[pos] = key[r];
       vout[pos] = val[r];
     }
   }
+}
+
+// ---------------------------------------------------------------------------- exclusive scan (overlap gate)
+namespace {
+__global__ __launch_bounds__(RADIX_THREADS) void scan_tile_sum_kernel(const int32_t* __restrict__ in, int64_t n,
+                                                                      int32_t* __restrict__ tsum) {
+  __shared__ uint32_t sh[4];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+  uint32_t v = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {   // coalesced: round r reads 256 consecutive values
+    const int64_t i = base + r * RADIX_THREADS + threadIdx.x;
+    if (i < n) v += (uint32_t)in[i];
+  }
+  const uint32_t ex = block_excl_scan(v, sh);
+  if (threadIdx.x == RADIX_THREADS - 1) tsum[blockIdx.x] = (int32_t)(ex + v);
+}
+
+// one workgroup: tile sums -> their exclusive prefix, in place
+__global__ __launch_bounds__(RADIX_THREADS) void scan_tile_prefix_kernel(int32_t* tsum, int64_t ntiles) {
+  __shared__ uint32_t sh[4];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t b = 0; b < ntiles; b += RADIX_THREADS) {
+    const int64_t i = b + threadIdx.x;
+    const uint32_t v = i < ntiles ? (uint32_t)tsum[i] : 0u;
+    const uint32_t c = carry;
+    const uint32_t ex = block_excl_scan(v, sh);
+    if (i < ntiles) tsum[i] = (int32_t)(c + ex);
+    __syncthreads();
+    if (threadIdx.x == RADIX_THREADS - 1) carry = c + ex + v;
+    __syncthreads();
+  }
+}
+
+// each thread scans 16 consecutive values of the tile (staged through LDS so the global reads stay coalesced)
+__global__ __launch_bounds__(RADIX_THREADS) void scan_tile_kernel(const int32_t* in, int32_t* out, int64_t n,
+                                                                  const int32_t* __restrict__ tpre) {
+  __shared__ int32_t tile[SCAN_TILE + SCAN_TILE / 32];   // +1 word per 32: conflict-free column reads
+  __shared__ uint32_t sh[4];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+  auto at = [](int j) { return j + (j >> 5); };
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int j = r * RADIX_THREADS + threadIdx.x;
+    tile[at(j)] = base + j < n ? in[base + j] : 0;
+  }
+  __syncthreads();
+  uint32_t loc[16], s = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    loc[r] = s;
+    s += (uint32_t)tile[at(threadIdx.x * 16 + r)];
+  }
+  const uint32_t off = (uint32_t)tpre[blockIdx.x] + block_excl_scan(s, sh);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tile[at(threadIdx.x * 16 + r)] = (int32_t)(off + loc[r]);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int j = r * RADIX_THREADS + threadIdx.x;
+    if (base + j < n) out[base + j] = tile[at(j)];
+  }
+}
+}  // namespace
+
+size_t scan_ws_bytes(int64_t n) { return ((size_t)((n + SCAN_TILE - 1) / SCAN_TILE + 1) * 4 + 255) & ~(size_t)255; }
+
+int excl_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (n < 0) return MVR_EINVAL;
+  if (n == 0) return MVR_OK;
+  if (!in || !out || !ws || ws_bytes < scan_ws_bytes(n)) return MVR_EINVAL;
+  const int64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  int32_t* tsum = reinterpret_cast<int32_t*>(ws);
+  hipLaunchKernelGGL(scan_tile_sum_kernel, dim3((unsigned)nt), dim3(RADIX_THREADS), 0, s, in, n, tsum);
+  hipLaunchKernelGGL(scan_tile_prefix_kernel, dim3(1), dim3(RADIX_THREADS), 0, s, tsum, nt);
+  hipLaunchKernelGGL(scan_tile_kernel, dim3((unsigned)nt), dim3(RADIX_THREADS), 0, s, in, out, n, tsum);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -178,13 +266,14 @@ RadixWs radix_ws(void* ws, int64_t n) {
 }
 
 int radix_sort(const RadixWs& w, int bits, int32_t* vals_out, hipStream_t s) {
-  if (w.n < 0 || w.n > (int64_t)LB_VAL || bits <= 0 || bits > 64 || !vals_out) return MVR_EINVAL;
+  if (w.n < 0 || w.n > (int64_t)LB_VAL || bits <= 0 || bits > 64) return MVR_EINVAL;
   if (w.n == 0) return MVR_OK;
+  if (!vals_out) return MVR_EINVAL;
   const int npass = (bits + RADIX_BITS - 1) / RADIX_BITS;
   const size_t clear = ((size_t)CTRL_LOOK + (size_t)npass * w.tiles * RADIX_BINS) * 4;
   if (hipMemsetAsync(w.ctrl, 0, clear, s) != hipSuccess) return MVR_ELAUNCH;
   const int hgrid = (int)std::min<int64_t>(w.tiles, 512);
-  hipLaunchKernelGGL(radix_hist_kernel, dim3(hgrid), dim3(RADIX_THREADS), 0, s, w.ka, w.n, npass, w.ctrl + CTRL_HIST);
+  hipLaunchKernelGGL(radix_hist_kernel, dim3(hgrid), dim3(RADIX_THREADS), 0, s, w.ka, w.n, bits, w.ctrl + CTRL_HIST);
   const uint64_t* kin = w.ka;
   const int32_t* vin = w.va;
   for (int p = 0; p < npass; ++p) {
@@ -193,11 +282,11 @@ int radix_sort(const RadixWs& w, int bits, int32_t* vals_out, hipStream_t s) {
     uint32_t* look = w.ctrl + CTRL_LOOK + (size_t)p * w.tiles * RADIX_BINS;
     if (p + 1 == npass)
       hipLaunchKernelGGL(radix_pass_kernel<true>, dim3((unsigned)w.tiles), dim3(RADIX_THREADS), 0, s, kin, vin,
-                         nullptr, vals_out, w.n, RADIX_BITS * p, w.ctrl + CTRL_HIST + p * RADIX_BINS,
+                         nullptr, vals_out, w.n, RADIX_BITS * p, radix_dmask(bits, p), w.ctrl + CTRL_HIST + p * RADIX_BINS,
                          w.ctrl + CTRL_TICKET + p, look);
     else
       hipLaunchKernelGGL(radix_pass_kernel<false>, dim3((unsigned)w.tiles), dim3(RADIX_THREADS), 0, s, kin, vin,
-                         kout, vout, w.n, RADIX_BITS * p, w.ctrl + CTRL_HIST + p * RADIX_BINS,
+                         kout, vout, w.n, RADIX_BITS * p, radix_dmask(bits, p), w.ctrl + CTRL_HIST + p * RADIX_BINS,
                          w.ctrl + CTRL_TICKET + p, look);
     kin = kout;
     vin = vout;
@@ -225,8 +314,9 @@ extern "C" size_t mvr_radix_sort_pairs_bytes(int64_t n) { return mvr::radix_ws_b
 
 extern "C" int mvr_radix_sort_pairs(const uint64_t* keys, const int32_t* vals, int64_t n, int bits,
                                     int32_t* vals_out, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (!keys || !vals_out || n < 0 || !ws || ws_bytes < mvr::radix_ws_bytes(n)) return MVR_EINVAL;
-  if (n == 0) return MVR_OK;
+  if (n < 0 || bits <= 0 || bits > 64) return MVR_EINVAL;
+  if (n == 0) return MVR_OK;   // pointers may be NULL with a zero count (mvreg.h conventions)
+  if (!keys || !vals_out || !ws || ws_bytes < mvr::radix_ws_bytes(n)) return MVR_EINVAL;
   mvr::RadixWs w = mvr::radix_ws(ws, n);
   hipLaunchKernelGGL(radix_load_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, keys, vals, n, w.ka, w.va);
   return mvr::radix_sort(w, bits, vals_out, s);

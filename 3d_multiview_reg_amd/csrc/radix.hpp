@@ -32,4 +32,11 @@ RadixWs radix_ws(void* ws, int64_t n);
 // (which may not alias the workspace).  Launches: one control-block clear, one histogram, ceil(bits / 8) passes.
 int radix_sort(const RadixWs& w, int bits, int32_t* vals_out, hipStream_t s);
 
+// Exclusive prefix sum of n int32 values (the total must fit in int32): reduce-then-scan over 4096-value tiles, three
+// launches (tile sums, one workgroup scanning them, the tiles' scans with their offsets).  in and out may alias.
+// Workspace: scan_ws_bytes(n).
+constexpr int SCAN_TILE = RADIX_THREADS * 16;
+size_t scan_ws_bytes(int64_t n);
+int excl_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t ws_bytes, hipStream_t s);
+
 }  // namespace mvr

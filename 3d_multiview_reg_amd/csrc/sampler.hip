@@ -57,7 +57,9 @@ struct Mt {
 // indices; ws: int64 scratch of max(counts) elements.  Requires tgt <= counts[b] (replace=False).
 extern "C" int mvr_sample_rand_mt19937(uint32_t* key, int32_t* pos, const int64_t* counts, int B, int tgt,
                                        int64_t* out, int64_t* ws) {
-  if (!key || !pos || !counts || B < 0 || tgt < 0 || !out || !ws || *pos < 0 || *pos > MT_N) return MVR_EINVAL;
+  if (B < 0 || tgt < 0) return MVR_EINVAL;
+  if (B == 0) return MVR_OK;   // no fragments: no draws (NULL pointers allowed)
+  if (!key || !pos || !counts || !out || !ws || *pos < 0 || *pos > MT_N) return MVR_EINVAL;
   for (int b = 0; b < B; ++b)
     if (counts[b] < tgt || counts[b] > 0xffffffffLL) return MVR_EINVAL;
   Mt mt{key, *pos};

@@ -725,10 +725,9 @@ extern "C" size_t mvr_voxelize_workspace_bytes(int64_t n) { return dedup_ws_byte
 extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* ws,
                             size_t ws_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                             hipStream_t s) {
-  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !ws || !coords_out || !counts_out)
-    return MVR_EINVAL;
-  if (ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
+  if (!frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !counts_out) return MVR_EINVAL;
   if (n == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  if (!xyz || !ws || !coords_out || ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   DedupWs d = dedup_ws(ws, n);
   hipLaunchKernelGGL(vox_keys_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
@@ -740,10 +739,9 @@ extern "C" int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, in
 extern "C" int mvr_voxelize_f64(const double* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* ws,
                                 size_t ws_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                                 hipStream_t s) {
-  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !ws || !coords_out || !counts_out)
-    return MVR_EINVAL;
-  if (ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
+  if (!frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !counts_out) return MVR_EINVAL;
   if (n == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  if (!xyz || !ws || !coords_out || ws_bytes < dedup_ws_bytes(n)) return MVR_EINVAL;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 52.0, s);
   DedupWs d = dedup_ws(ws, n);
   hipLaunchKernelGGL(vox_keys_kernel<double>, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
@@ -762,11 +760,10 @@ extern "C" size_t mvr_voxelize_hint_workspace_bytes(int64_t n, int64_t distinct_
 extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel,
                                  int64_t distinct_hint, void* ws, size_t ws_bytes, int32_t* coords_out,
                                  int64_t* sel_out, int64_t* counts_out, hipStream_t s) {
-  if (!xyz || !frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !ws || !coords_out || !counts_out ||
-      distinct_hint <= 0)
+  if (!frag_off || B <= 0 || B > MAX_BATCH || n < 0 || !(voxel > 0.0) || !counts_out || distinct_hint <= 0)
     return MVR_EINVAL;
   const int64_t keys = distinct_hint < n ? distinct_hint : n;
-  if (ws_bytes < dedup_ws_bytes(n, keys)) return MVR_EINVAL;
+  if (n > 0 && (!xyz || !ws || !coords_out || ws_bytes < dedup_ws_bytes(n, keys))) return MVR_EINVAL;
   if (hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (2 + B), s) != hipSuccess) return MVR_ELAUNCH;
   if (n == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
@@ -781,10 +778,9 @@ extern "C" size_t mvr_coords_downsample_workspace_bytes(int64_t M) { return dedu
 
 extern "C" int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, int stride_out, void* ws,
                                      size_t ws_bytes, int32_t* coords_out, int64_t* counts_out, hipStream_t s) {
-  if (!coords || M < 0 || B <= 0 || B > MAX_BATCH || stride_out <= 0 || !ws || !coords_out || !counts_out)
-    return MVR_EINVAL;
-  if (ws_bytes < dedup_ws_bytes(M)) return MVR_EINVAL;
+  if (M < 0 || B <= 0 || B > MAX_BATCH || stride_out <= 0 || !counts_out) return MVR_EINVAL;
   if (M == 0) return hipMemsetAsync(counts_out, 0, sizeof(int64_t) * (1 + B), s) == hipSuccess ? MVR_OK : MVR_ELAUNCH;
+  if (!coords || !ws || !coords_out || ws_bytes < dedup_ws_bytes(M)) return MVR_EINVAL;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)M * 40.0, s);
   DedupWs d = dedup_ws(ws, M);
   hipLaunchKernelGGL(coarse_keys_kernel, dim3(nblk(M)), dim3(256), 0, s, reinterpret_cast<const int4*>(coords), M,
@@ -793,7 +789,7 @@ extern "C" int mvr_coords_downsample(const int32_t* coords, int64_t M, int B, in
 }
 
 static int hash_build(const int32_t* coords, int64_t M, int t, void* table, size_t table_bytes, hipStream_t s) {
-  if (!coords || M < 0 || !table) return MVR_EINVAL;
+  if (M < 0 || !table || (M > 0 && !coords)) return MVR_EINVAL;   // an empty set still clears its table
   if (table_bytes < hash_table_bytes(M)) return MVR_EINVAL;
   HashView h = hash_view(table, table_bytes);
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)h.cap * 12 + M * 28.0, s);
@@ -818,11 +814,12 @@ extern "C" int mvr_hash_build_lattice(const int32_t* coords, int64_t M, int stri
 extern "C" int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes,
                                 int ksize, int step, int transposed, int32_t* nbr, const int32_t* row_order,
                                 hipStream_t s) {
-  if (!out_coords || Mout < 0 || !in_table || ksize <= 0 || (ksize & 1) == 0 || step <= 0 || !nbr) return MVR_EINVAL;
+  if (Mout < 0 || ksize <= 0 || (ksize & 1) == 0 || step <= 0) return MVR_EINVAL;
+  if (Mout == 0) return MVR_OK;
+  if (!out_coords || !in_table || !nbr) return MVR_EINVAL;
   HashView h = hash_view(const_cast<void*>(in_table), in_table_bytes);
   if (!h.cap) return MVR_EINVAL;
   const int64_t tot = Mout * (int64_t)ksize * ksize * ksize;
-  if (tot == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)tot * 4.0, s);
   hipLaunchKernelGGL(kernel_map_kernel, dim3(nblk(tot)), dim3(256), 0, s, reinterpret_cast<const int4*>(out_coords),
                      Mout, h, ksize, step, transposed ? -1 : 1, nbr, row_order);
@@ -860,8 +857,8 @@ extern "C" size_t mvr_brick_map_bytes(int64_t M) { return brick_map_bytes(M); }
 
 extern "C" int mvr_brick_map_build_stride(const int32_t* coords, int64_t M, int stride, void* ws, size_t ws_bytes,
                                           hipStream_t s) {
-  if (!coords || M < 0 || !ws || ws_bytes < brick_map_bytes(M) || stride <= 0 || (stride & (stride - 1)) ||
-      stride > (1 << 12))
+  if (M < 0 || !ws || ws_bytes < brick_map_bytes(M) || stride <= 0 || (stride & (stride - 1)) || stride > (1 << 12) ||
+      (M > 0 && !coords))
     return MVR_EINVAL;
   const int t = __builtin_ctz((unsigned)stride);
   BrickView v = brick_view(ws, M);
@@ -889,7 +886,9 @@ extern "C" int mvr_spconv_c1_x(const int32_t* out_coords, int64_t Mout, const vo
                                size_t in_bricks_bytes, const float* feat, int ksize, int step, const float* W, int Cout,
                                mvr_bn_p bn, float bn_eps, int relu, float* out, int64_t ldout, uint16_t* out_planes,
                                hipStream_t s) {
-  if (Mout < 0 || !in_bricks || !feat || !W || !out || (ksize & 1) == 0 || step <= 0 || Min < 0) return MVR_EINVAL;
+  if (Mout < 0 || (ksize & 1) == 0 || step <= 0 || Min < 0) return MVR_EINVAL;
+  if (Mout == 0 && (out_coords || Min == 0)) return MVR_OK;   // no output rows: NULL pointers allowed
+  if (!in_bricks || !feat || !W || !out) return MVR_EINVAL;
   if (out_planes && (out_coords || (reinterpret_cast<uintptr_t>(out_planes) & 1))) return MVR_EINVAL;   // bricks only
   if (Cout != 32) return MVR_EINVAL;  // FCGF conv1: 1 -> CHANNELS[1] = 32 (fcgf.py:118-125)
   if (in_bricks_bytes < brick_map_bytes(Min)) return MVR_EINVAL;
@@ -925,8 +924,9 @@ extern "C" int mvr_spconv_c1(const int32_t* out_coords, int64_t Mout, const void
 }
 
 extern "C" int mvr_l2norm_rows(float* x, int64_t M, int C, int64_t ld, hipStream_t s) {
-  if (!x || M < 0 || C <= 0 || ld < C) return MVR_EINVAL;
+  if (M < 0 || C <= 0 || ld < C) return MVR_EINVAL;
   if (M == 0) return MVR_OK;
+  if (!x) return MVR_EINVAL;
   if (C == 32 && ld % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0)
     hipLaunchKernelGGL(l2norm_rows32_kernel, dim3((unsigned)((M * 8 + 255) / 256)), dim3(256), 0, s, x, M, ld);
   else
@@ -945,7 +945,7 @@ extern "C" size_t mvr_kernel_map_orders_bytes(int64_t total) { return radix_ws_b
 extern "C" int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, const int32_t* const* out_coords,
                                      const int* steps, const int64_t* Mo, int K, int32_t* perm_out, void* ws,
                                      size_t ws_bytes, hipStream_t s) {
-  if (n_maps <= 0 || n_maps > ORDER_MAX_MAPS || !Mo || K < 0 || K > 27 || !perm_out || !ws) return MVR_EINVAL;
+  if (n_maps <= 0 || n_maps > ORDER_MAX_MAPS || !Mo || K < 0 || K > 27) return MVR_EINVAL;
   if ((!nbr) != (K == 0) || (!nbr && !out_coords)) return MVR_EINVAL;   // K = 0, nbr NULL: coordinate orders
   OrderMaps m{};
   m.n = n_maps;
@@ -962,8 +962,9 @@ extern "C" int mvr_kernel_map_orders(int n_maps, const int32_t* const* nbr, cons
     m.start[j + 1] = m.start[j] + Mo[j];
   }
   const int64_t total = m.start[n_maps];
-  if (total > (int64_t)(1 << 30) - 1 || ws_bytes < radix_ws_bytes(total)) return MVR_EINVAL;
-  if (total == 0) return MVR_OK;
+  if (total > (int64_t)(1 << 30) - 1) return MVR_EINVAL;
+  if (total == 0) return MVR_OK;   // every map empty: perm_out and ws may be NULL
+  if (!perm_out || !ws || ws_bytes < radix_ws_bytes(total)) return MVR_EINVAL;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)total * (4.0 * K + 16 + 8 * 24 + 4), s);
   RadixWs w = radix_ws(ws, total);
   hipLaunchKernelGGL(order_keys_kernel, dim3(nblk(total)), dim3(256), 0, s, m, w.ka, w.va);
@@ -977,6 +978,8 @@ extern "C" size_t mvr_kernel_map_order_bytes(int64_t Mo) { return radix_ws_bytes
 
 extern "C" int mvr_kernel_map_order(const int32_t* nbr, const int32_t* out_coords, int step, int64_t Mo, int K,
                                     int32_t* perm, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (!nbr || !perm || Mo < 0 || K <= 0 || K > 27 || (out_coords && step <= 0)) return MVR_EINVAL;
+  if (Mo < 0 || K <= 0 || K > 27 || (out_coords && step <= 0)) return MVR_EINVAL;
+  if (Mo == 0) return MVR_OK;
+  if (!nbr || !perm) return MVR_EINVAL;
   return mvr_kernel_map_orders(1, &nbr, &out_coords, &step, &Mo, K, perm, ws, ws_bytes, s);
 }

@@ -447,7 +447,9 @@ extern "C" int mvr_spconv_x(const float* in, int64_t ldin, int Cin, const int32_
                             int64_t Mout, const float* W, int Cout, const float* bias, mvr_bn_p bn, float bn_eps,
                             const float* res, int64_t ldres, int relu, float* out, int64_t ldout, const void* wimg,
                             int32_t* range_flag, const uint16_t* in_planes, uint16_t* out_planes, hipStream_t s) {
-  if (!in || !W || !out || !wimg || Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
+  if (Cin <= 0 || Cout <= 0 || K <= 0 || K > SP_KMAX || Mout < 0) return MVR_EINVAL;
+  if (Mout == 0) return MVR_OK;   // no output rows: NULL pointers allowed (mvreg.h conventions)
+  if (!in || !W || !out || !wimg) return MVR_EINVAL;
   if ((in_planes && ((ldin & 7) || (reinterpret_cast<uintptr_t>(in_planes) & 15))) ||
       (out_planes && (reinterpret_cast<uintptr_t>(out_planes) & 1)))
     return MVR_EINVAL;
@@ -456,7 +458,6 @@ extern "C" int mvr_spconv_x(const float* in, int64_t ldin, int Cin, const int32_
   if ((Cin % SB_K) || (Cout & 3) || (ldin & 3) || (reinterpret_cast<uintptr_t>(in) & 15) ||
       (reinterpret_cast<uintptr_t>(W) & 15))
     return MVR_EINVAL;
-  if (Mout == 0) return MVR_OK;
   SpArgs a{in, ldin, Cin, nbr, K, Mout, perm, W, Cout, bias, bn, bn_eps, res, ldres, relu, out, ldout,
            nullptr, nullptr, 0, in_planes, out_planes};
   // the launch cannot see how many kernel-map entries are present (no host sync): FLOPs as if every offset were,

@@ -8,7 +8,12 @@
  *     allocation); workspaces are sized by the paired *_workspace_bytes() query;
  *   - calls are stream-ordered on `stream` (a hipStream_t; 0 = legacy default),
  *     re-entrant, and thread-safe across distinct streams/devices;
- *   - strides are in ELEMENTS.
+ *   - strides are in ELEMENTS;
+ *   - empty work: when the count that sizes an array is 0 (no rows, pairs, points or fragments), the entry point
+ *     returns MVR_OK after validating its scalar arguments and never reads the pointers of the empty arrays, which
+ *     may be NULL (a zero-element torch tensor's data_ptr() is 0).  Outputs whose size does not depend on that
+ *     count (per-fragment counts, offsets, hash tables that are cleared) are still written, so their pointers stay
+ *     required.
  *
  * Process-wide settings: exactly two entry points, mvr_set_math (operand arithmetic) and mvr_debug_force (tests:
  * fallback paths), write process-global values of the library, read by the host side of each later call when it

@@ -291,3 +291,31 @@ def test_fcgf_forward_independent_of_tiling_order(gpu, frags, monkeypatch):
             outs.append(net(SparseTensor(F, coords=c).to(gpu)).F.clone())
     for i, o in enumerate(outs[1:], 1):
         assert torch.equal(outs[0], o), (i, (outs[0] - o).abs().max().item())
+
+
+def test_empty_fragment_through_voxelize_and_orders(gpu, frags):
+    """An empty fragment inside a batch, and a batch with no points at all, go through voxelize ->
+    CoordinateManager (strided sets, lattice tables, kernel maps, prepare_orders): zero-element tensors hand the C ABI
+    NULL pointers with zero counts, which every entry point accepts (include/mvreg.h conventions; round 5's
+    mvr_radix_sort_pairs rejected them)."""
+    import torch
+    from lib.sparse import voxelize, CoordinateManager, FCGF_MAPS
+    empty = np.zeros((0, 3), np.float32)
+    c3, _, counts3, _ = voxelize([frags[0], empty, frags[2]], 0.025, gpu)
+    c2, _, counts2, _ = voxelize([frags[0], frags[2]], 0.025, gpu)
+    assert counts3 == [counts2[0], 0, counts2[1]]
+    want = c2.cpu().numpy().copy()
+    want[want[:, 0] == 1, 0] = 2                       # the third fragment keeps its batch index
+    np.testing.assert_array_equal(c3.cpu().numpy(), want)
+    a, b = CoordinateManager(c3, 3), CoordinateManager(c3, 3)
+    a.prepare_orders()
+    for kind, s in FCGF_MAPS:
+        assert torch.equal(a.kernel_map_order(kind, s), b.kernel_map_order(kind, s)), (kind, s)
+    # no points at all: every level, map and order is empty
+    c0, sel0, counts0, xyz0 = voxelize([empty], 0.025, gpu)
+    assert counts0 == [0] and c0.shape[0] == 0 and sel0.numel() == 0 and xyz0.shape[0] == 0
+    z = CoordinateManager(c0, 1)
+    z.prepare_orders()
+    for kind, s in FCGF_MAPS:
+        assert z.kernel_map(kind, s).shape[0] == 0 and z.orders[(kind, s, 3)].numel() == 0
+    torch.cuda.synchronize()
