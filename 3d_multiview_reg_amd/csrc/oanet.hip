@@ -315,6 +315,9 @@ static void dbg_dump(const void* p, size_t bytes, hipStream_t s) {
     (void)hipMemcpyAsync(g_dump, p, bytes < g_dump_bytes ? bytes : g_dump_bytes, hipMemcpyDeviceToDevice, s);
 }
 
+static int g_last_layout = -1;   // the point-activation layout of the latest mvr_oan_block_forward (diagnostics)
+extern "C" int mvr_oan_last_layout(void) { return g_last_layout; }
+
 extern "C" int mvr_debug_stage_dump(int stage, void* dst, size_t bytes) {
   g_dump = dst;
   g_dump_bytes = bytes;
@@ -707,6 +710,7 @@ extern "C" int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* in
   };
   pl.cm = OAN_CHUNK_MAJOR && fold1 && pl.fused && !g_force[FORCE_ROW_LAYOUT] && pconv_takes(C, 1, 1, 1) && pconv_takes(C, 1, 0, 1) &&
           pconv_takes(2 * C, 1, 0, 1) && pconv_takes(2 * C, 0, 0, 0);
+  g_last_layout = pl.cm ? 1 : 0;
   Act xa = cx.pts(pl.XA, C, C, pl.stA, C);
   Act x11top = cx.pts(pl.X11, C, 2 * C, pl.st11, 2 * C);
   const int64_t x11cs = x11top.cs ? x11top.cs : 32;   // (oan_attn.hip's convention: 32 = row-major)

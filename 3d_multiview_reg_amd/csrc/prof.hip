@@ -73,6 +73,21 @@ void prof_end(int kind, hipStream_t s) {
 
 using namespace mvr;
 
+#ifndef MVR_SRC_HASH
+#define MVR_SRC_HASH "unknown"
+#endif
+// The build's source identity (csrc/Makefile: sha256 of csrc/*.hip, *.hpp, mvreg.h and the variant flags): recorded
+// by tools/pmc_traffic.py with the counters it measured, so bench.py never prices this library with the counters of
+// another build.
+extern "C" int mvr_source_hash(char* buf, size_t cap) {
+  const char* h = MVR_SRC_HASH;
+  size_t n = 0;
+  while (h[n]) ++n;
+  if (!buf || cap <= n) return (int)n + 1;
+  for (size_t i = 0; i <= n; ++i) buf[i] = h[i];
+  return MVR_OK;
+}
+
 extern "C" int mvr_prof_set(int on) {
   std::lock_guard<std::mutex> g(mu);
   drain();

@@ -133,6 +133,8 @@ _SIGS = {
     "mvr_prof_seq": (c_int, [c_vp, c_vp, c_int]),
     "mvr_prof_get": (c_int, [c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
+    "mvr_oan_last_layout": (c_int, []),
+    "mvr_source_hash": (c_int, [ctypes.c_char_p, c_size]),
     "mvr_xs_to_channels": (c_int, [c_vp, c_i64, c_i64, c_int, c_int, c_int, c_vp, c_i64, c_i64, c_vp]),
 }
 
@@ -182,6 +184,13 @@ def ptr(t):
 def check(rc, name):
     if rc != 0:
         raise RuntimeError("%s failed with code %d" % (name, rc))
+
+
+def source_hash():
+    """The loaded library's source identity (csrc/Makefile SRC_HASH; variant builds append their flags)."""
+    buf = ctypes.create_string_buffer(128)
+    check(lib().mvr_source_hash(buf, len(buf)), "mvr_source_hash")
+    return buf.value.decode()
 
 
 PROF_KINDS = {"conv_pts": 0, "embed": 1, "pool": 2, "unpool": 3, "oafilter": 4, "small": 5, "procrustes": 6,

@@ -22,9 +22,11 @@ from lib.sparse import SparseTensor
 # conv1 (7^3) as brick-tiled dense windows on split-bf16 MFMA (csrc/sparse.hip spconv_c1_brick_kernel);
 # MVR_CONV1_BRICKS=0 selects the per-row gather kernel (A/B timing)
 CONV1_BRICKS = os.environ.get("MVR_CONV1_BRICKS", "1") == "1"
-# every conv's output also written as split-bf16 planes that the next conv gathers instead of re-splitting fp32 rows
-# in its inner loop (csrc/spconv.hip PS = 1; bit-identical); MVR_SPCONV_PRESPLIT=0 keeps fp32 gathers (A/B timing)
-PRESPLIT = os.environ.get("MVR_SPCONV_PRESPLIT", "1") == "1"
+# MVR_SPCONV_PRESPLIT=1: every conv's output also written as split-bf16 planes that the next conv gathers instead of
+# re-splitting fp32 rows in its inner loop (csrc/spconv.hip PS = 1; bit-identical).  Off by default: measured slower
+# on the same box (round 6, profiles/r06/ab_r6s1.txt: the sparse convs 6.63 ms per step with fp32 gathers vs 8.40 with
+# the planes — 6 instead of 4 bytes per gathered value, and the level-1 planes no longer fit the Infinity Cache)
+PRESPLIT = os.environ.get("MVR_SPCONV_PRESPLIT", "0") == "1"
 
 
 def _planes(M, ld, dev):

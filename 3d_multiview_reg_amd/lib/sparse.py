@@ -20,9 +20,10 @@ from lib import _native as N
 # tensor strides 1-8, the strided convs 1->2, 2->4, 4->8 and the transposed 8->4, 4->2, 2->1 (keyed by output stride)
 FCGF_MAPS = (("s1", 1), ("s1", 2), ("s1", 4), ("s1", 8), ("down", 1), ("down", 2), ("down", 4),
              ("up", 4), ("up", 2), ("up", 1))
-# 3^3 kernel maps visit their output rows in (fragment, Morton) order instead of the sets' first-occurrence order
-# (identical maps; MVR_SPATIAL_MAPS=0 for A/B timing)
-SPATIAL_MAPS = os.environ.get("MVR_SPATIAL_MAPS", "1") == "1"
+# MVR_SPATIAL_MAPS=1: 3^3 kernel maps visit their output rows in (fragment, Morton) order instead of the sets'
+# first-occurrence order (identical maps).  Off by default: no gain on the same box (round 6, profiles/r06/
+# ab_r6s1.txt: the coordinate work 2.58 ms per step in first-occurrence order vs 2.68 with the extra sort)
+SPATIAL_MAPS = os.environ.get("MVR_SPATIAL_MAPS", "0") == "1"
 
 
 class CoordinateManager:

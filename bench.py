@@ -454,6 +454,16 @@ MFMA_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter", "feat_nn", "s
 F16_CLASSES = ("conv_pts", "embed", "pool", "unpool", "oafilter", "feat_nn", "spconv")
 
 
+def _fcgf_mod():
+    import lib.descriptor.fcgf as m
+    return m
+
+
+def _sparse_mod():
+    import lib.sparse as m
+    return m
+
+
 def class_peak_tflops(cls, knobs):
     """fp32-equivalent MFMA peak of a kernel class at the arithmetic it runs: split-bf16 (6 products per fp32
     product) = 16 x 157.3 / 6 TF; split-fp16 (3 products) = 16 x 157.3 / 3 TF"""
@@ -701,12 +711,21 @@ def main():
         achieved, peak, unit = by / max(nl, 1) / avg_s / 1e9, PEAK_HBM_GBS, "GB/s"
     traffic, tsrc = None, None
     tfile = os.environ.get("MVR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    tnote = "no PMC file"
     if os.path.exists(tfile):
         with open(tfile) as f:
             tr = json.load(f)
-        if dom in tr.get("classes", {}) and tr.get("math", "split16") == args.math:
+        have = _native.source_hash()
+        if tr.get("lib_hash") != have:
+            # counters of another build (e.g. a previous round's kernels) never price this one
+            tnote = "PMC file is of library %s, this run loads %s: traffic not measured for this build" % (
+                tr.get("lib_hash"), have)
+        elif tr.get("math", "split16") != args.math:
+            tnote = "PMC file measured --math %s" % tr.get("math")
+        elif dom in tr.get("classes", {}):
             traffic = tr["classes"][dom]["pmc_bytes_per_launch"]
             tsrc = tr.get("source")
+            tnote = "PMC of this library (%s)" % have
     # the same kernel class alone on the GPU (the untimed profiled step runs the stages back to back):
     # in the pipelined timed region its launches share the chip with the other stream's kernels
     iso = prof_all.get(dom, (0.0, 0, 0.0, 0.0))
@@ -733,7 +752,7 @@ def main():
             "algorithmic_bytes_per_launch": by / max(nl, 1),
             "peak_note": ("fp32-equivalent MFMA peak of the class's operand split (split-bf16 16*157.3/6 TF, "
                           "split-fp16 16*157.3/3 TF); HBM 8 TB/s (MI355X_MICROARCH.md)"),
-            "traffic_source": tsrc,
+            "traffic_source": tsrc, "traffic_note": tnote,
             # per kernel class, from the profiled untimed step (events on every launch):
             # [ms per step, algorithmic TFLOP/s, algorithmic GB/s]
             "classes": {k: [round(v[0], 3), round(v[2] / (v[0] * 1e9), 1), round(v[3] / (v[0] * 1e6))]
@@ -771,6 +790,9 @@ def main():
         v8, _, _ = wl.cpu_baseline(8, args.cpu_budget)
         cpu = dict({"value": round(v, 4), "unit": "pairs/s", "cores": cores, "kind": "port", "sample": sample,
                     "value_8_threads": round(v8, 4)}, **extra)
+        if args.workload == "scene":   # the instruction set of the C sparse conv on this host (oracle/csrc clone)
+            from oracle.fcgf import isa
+            cpu["fcgf_isa"] = isa()
     line = {"metric": METRIC if args.workload == "scene" else METRIC + " [filter+SVD only: precomputed corr.]",
             "value": round(value, 3), "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
@@ -779,6 +801,10 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if pair_sharded else "weak", "vs_baseline": None, "dtype": math_info["dtype"], "data": "synthetic",
             "config": dict(wl.config(), math=args.math,
+                           oanet_point_layout={1: "chunk-major", 0: "row-major"}.get(
+                               _native.lib().mvr_oan_last_layout(), "none"),
+                           spconv_presplit_planes=bool(_fcgf_mod().PRESPLIT), spatial_map_order=bool(
+                               _sparse_mod().SPATIAL_MAPS), library=_native.source_hash(),
                            parallelism=(("pairs%d (one scene per step: fragments and pair batch sharded over %d "
                                          "ranks, %s all-gather of samples and records)"
                                          if args.workload == "scene" else

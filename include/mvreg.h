@@ -189,6 +189,9 @@ int mvr_attn_reruns(int reset);
 int mvr_debug_stage_hash(unsigned long long* buf, int cap);
 /* Debugging: copy the statistics partials hashed as stage `stage` into dst (bytes); NULL disables. */
 int mvr_debug_stage_dump(int stage, void* dst, size_t bytes);
+/* Diagnostics: the point-activation layout the latest mvr_oan_block_forward chose — 1 chunk-major (every 32-point
+ * chunk of a pair one contiguous block), 0 row-major, -1 no forward yet (bench.py records it in its config). */
+int mvr_oan_last_layout(void);
 int mvr_oan_block_forward(const mvr_oan_block_p* blk, const float* input, int64_t in_pstride, int64_t ld,
                           const float* xs, int64_t xs_pstride, int64_t xs_nstride, int P, int N, int bn_train,
                           float* logits,
@@ -467,6 +470,9 @@ int mvr_prof_get(int kind, double* ms, long long* launches, double* flops, doubl
 /* launch order since mvr_prof_set(1): kind and algorithmic bytes per profiled launch (<= cap);
  * returns the count (joins rocprofv3 PMC dispatch rows to kernel classes) */
 int mvr_prof_seq(int* kinds, double* bytes, int cap);
+/* the library's source identity (sha256 prefix of its sources + variant flags) as a NUL-terminated string: MVR_OK,
+ * or the buffer size needed when cap is too small (bench.py uses the PMC counters only of this same build) */
+int mvr_source_hash(char* buf, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -67,10 +67,30 @@ int mvo_kernel_map(const int32_t* in_c, int64_t Mi, const int32_t* out_c, int64_
   return 0;
 }
 
-/* out [Mo][Cout] = sparse conv of feat [Mi][Cin] over nbr [Mo][K] with W [K][Cin][Cout] (+ bias [Cout]). */
-/* AVX2/FMA clone chosen at load time on hosts that have it (the CPU baseline's speed), the baseline-ISA one
- * elsewhere: the library itself is built for plain x86-64 */
+/* One output row of the sparse conv: acc [Cout] scratch.  The AVX2/FMA clone is chosen at load time on hosts that
+ * have it (the CPU baseline's speed), the baseline-ISA one elsewhere (the library itself is built for plain x86-64,
+ * so it loads on any host).  The clone is this plain function, called from the OpenMP loop body: a target_clones
+ * attribute on the function holding the `omp parallel` region would not reach GCC's outlined loop body. */
 __attribute__((target_clones("arch=haswell", "default")))
+static void conv_row(const float* feat, int64_t Mi, int Cin, const int64_t* nrow, int K, const float* W, int Cout,
+                     const float* bias, float* acc, float* dst) {
+  for (int c = 0; c < Cout; ++c) acc[c] = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const int64_t i = nrow[k];
+    if (i < 0 || i >= Mi) continue;
+    const float* f = feat + i * Cin;
+    const float* w = W + (int64_t)k * Cin * Cout;
+    for (int ci = 0; ci < Cin; ++ci) {
+      const float x = f[ci];
+      const float* wr = w + (int64_t)ci * Cout;
+#pragma omp simd
+      for (int c = 0; c < Cout; ++c) acc[c] += x * wr[c];
+    }
+  }
+  for (int c = 0; c < Cout; ++c) dst[c] = acc[c] + (bias ? bias[c] : 0.f);
+}
+
+/* out [Mo][Cout] = sparse conv of feat [Mi][Cin] over nbr [Mo][K] with W [K][Cin][Cout] (+ bias [Cout]). */
 int mvo_sparse_conv(const float* feat, int64_t Mi, int Cin, const int64_t* nbr, int64_t Mo, int K, const float* W,
                     int Cout, const float* bias, float* out) {
   if (!feat || !nbr || !W || !out || Mi < 0 || Mo < 0 || Cin <= 0 || Cout <= 0 || K <= 0) return -1;
@@ -78,26 +98,17 @@ int mvo_sparse_conv(const float* feat, int64_t Mi, int Cin, const int64_t* nbr, 
   {
     float* acc = (float*)malloc(sizeof(float) * (size_t)Cout);
 #pragma omp for schedule(dynamic, 256)
-    for (int64_t o = 0; o < Mo; ++o) {
-      for (int c = 0; c < Cout; ++c) acc[c] = 0.f;
-      for (int k = 0; k < K; ++k) {
-        const int64_t i = nbr[o * K + k];
-        if (i < 0 || i >= Mi) continue;
-        const float* f = feat + i * Cin;
-        const float* w = W + (int64_t)k * Cin * Cout;
-        for (int ci = 0; ci < Cin; ++ci) {
-          const float x = f[ci];
-          const float* wr = w + (int64_t)ci * Cout;
-#pragma omp simd
-          for (int c = 0; c < Cout; ++c) acc[c] += x * wr[c];
-        }
-      }
-      float* dst = out + o * Cout;
-      for (int c = 0; c < Cout; ++c) dst[c] = acc[c] + (bias ? bias[c] : 0.f);
-    }
+    for (int64_t o = 0; o < Mo; ++o) conv_row(feat, Mi, Cin, nbr + o * K, K, W, Cout, bias, acc, out + o * Cout);
     free(acc);
   }
   return 0;
+}
+
+/* The instruction set the sparse conv's clone runs at on this host: 1 AVX2 + FMA (haswell clone), 0 baseline x86-64
+ * (recorded with the CPU baseline's numbers) */
+int mvo_isa(void) {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
 }
 
 /* OpenMP threads of the calls above (the CPU baseline's thread count); returns the previous maximum */

@@ -27,12 +27,15 @@ def _clib():
     `make -C oracle`): the kernel map and sparse conv of this module for the host-core CPU baseline"""
     global _C
     if _C is None:
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libmvoracle.so")
+        # MVO_LIB: another build of the same source (tests/test_oracle_sanitize.py: the ASan + UBSan build)
+        path = os.environ.get("MVO_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "build",
+                                                         "libmvoracle.so")
         L = ctypes.CDLL(path)
         vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.mvo_kernel_map.argtypes = [vp, i64, vp, i64, ci, ci, ci, vp]
         L.mvo_sparse_conv.argtypes = [vp, i64, ci, vp, i64, ci, vp, ci, vp, vp]
         L.mvo_set_threads.argtypes = [ci]
+        L.mvo_isa.argtypes = []
         _C = L
     return _C
 
@@ -40,6 +43,12 @@ def _clib():
 def set_threads(n):
     """OpenMP threads of the C backend; returns the previous maximum"""
     return _clib().mvo_set_threads(int(n))
+
+
+def isa():
+    """'avx2+fma' when the C sparse conv runs its haswell clone on this host, else 'x86-64' (recorded with the CPU
+    baseline)"""
+    return "avx2+fma" if _clib().mvo_isa() else "x86-64"
 
 
 def kernel_map_c(out_coords, in_coords, ks, step, transposed=False):

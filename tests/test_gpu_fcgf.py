@@ -170,7 +170,7 @@ def test_spatial_map_visit_order(gpu, frags, monkeypatch):
     for s in (1, 2, 4, 8):
         cs = a.coords_at(s).cpu().numpy().astype(np.int64)
         q = cs[:, 1:] // s
-        lo = ((cs[:, 0] & 31) << 27) | (spread(q[:, 0]) << 2) | (spread(q[:, 1]) << 1) | spread(q[:, 2])
+        lo = ((cs[:, 0] & 127) << 25) | (spread(q[:, 0] & 255) << 2) | (spread(q[:, 1] & 255) << 1) | spread(q[:, 2] & 255)
         np.testing.assert_array_equal(a.spatial[s].cpu().numpy(), np.argsort(lo, kind="stable"))
 
 
@@ -253,7 +253,7 @@ def test_kernel_map_order_mask_then_morton(gpu, frags):
                 out |= ((v >> b) & 1) << (3 * b)
             return out
         q = out_c[:, 1:] // step
-        lo = ((out_c[:, 0] & 31) << 27) | (spread(q[:, 0] & 511) << 2) | (spread(q[:, 1] & 511) << 1) | spread(q[:, 2] & 511)
+        lo = ((out_c[:, 0] & 127) << 25) | (spread(q[:, 0] & 255) << 2) | (spread(q[:, 1] & 255) << 1) | spread(q[:, 2] & 255)
         key = (mask << 32) | lo
         assert np.array_equal(perm, np.argsort(key, kind="stable"))
 

@@ -59,6 +59,15 @@ def attribute(disp, seq):
     return out, names
 
 
+def lib_hash():
+    """source identity of the library the passes ran (the same MVR_LIB the bench loads): bench.py prices a run with
+    these counters only when its own library reports the same hash"""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "3d_multiview_reg_amd"))
+    from lib import _native
+    return _native.source_hash()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("outdir")
@@ -86,7 +95,7 @@ def main():
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of `bench.py --steps 1 --warmup 1` with "
                      "MVR_PROF_MARK=1 (tools/pmc_bench.sh): dispatches joined to the timed step's launch sequence "
                      "by region markers; FETCH x2 (gfx950 16 B/lane correction), KB -> B",
-           "math": a.math, "classes": res}
+           "math": a.math, "lib_hash": lib_hash(), "classes": res}
     txt = json.dumps(doc, indent=1)
     print(txt)
     if a.out:
