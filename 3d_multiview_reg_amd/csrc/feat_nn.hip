@@ -57,7 +57,35 @@ struct NNArgs {
   int32_t* idx;                      // optional argmax index [P][Nq]
   int fast;                          // soft mode: try the bounded-shift path first (feat_nn_fast)
   const char* timg; int64_t timg_fs; // optional: targets pre-split per stage (nn_presplit_kernel), bytes per fragment
+  unsigned seed_lo, seed_hi;         // MODE 3 / 4 (soft_gumbel): the noise's seed
+  float itau;                        // MODE 3 / 4: 1 / tau (the noise's scale in the logit)
 };
+
+// soft_gumbel (lib/layers.py:72-78, F.gumbel_softmax(-dist, tau, hard)): y = softmax((-dist + g) / tau) with
+// g = -log(e), e ~ Exp(1) per (query, target).  The noise is counter-based — a 32-bit hash of (seed, query fragment,
+// target fragment, query, target), so it does not depend on the batch a pair runs in and oracle/soft_nn.py
+// reproduces it — instead of torch's Philox stream (the reference's draws cannot be replayed: SURVEY §8a6, parity by
+// restatement).  u = (hash >> 8 + 1/2) 2^-24 in (0, 1), e = -ln u.
+__device__ __host__ __forceinline__ unsigned nn_mix32(unsigned x) {   // lowbias32 finalizer
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ unsigned nn_gumbel_query(const NNArgs& a, int64_t src, int64_t tgt, int j) {
+  const unsigned k = nn_mix32(a.seed_lo ^ nn_mix32(a.seed_hi + 0x9E3779B9u * (unsigned)tgt) ^
+                              (0x85EBCA77u * (unsigned)src));
+  return nn_mix32(k ^ (unsigned)j);
+}
+// the noise's contribution to a logit in log2 units (z = log2(e) (2 fs.ft - |ft|^2) / tau): log2(e) g / tau
+__device__ __forceinline__ float nn_gumbel_z(unsigned hq, int i, float itau) {
+  const unsigned x = nn_mix32(hq + 0x9E3779B9u * (unsigned)i);
+  const float u = ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f;           // (0, 1)
+  const float e = -0.69314718055994531f * __builtin_amdgcn_logf(u);            // -ln u > 0
+  return -itau * __builtin_amdgcn_logf(e);                                     // log2(e) g / tau, g = -ln e
+}
 
 // Pre-split target image (mvr_feat_nn_ws): per target fragment and 128-target stage, the bytes the fast path's LDS
 // stage holds — the three bf16 planes of the features in the swizzled [row][32] layout, then (x, y, z, k2 |ft|^2)
@@ -228,6 +256,8 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
   float best = NN_NEG, second = NN_NEG;
   int besti = 0x7fffffff, secondi = 0x7fffffff;
   const float kk2 = 2.f * a.k2;
+  constexpr bool GUM = MODE == 3 || MODE == 4;   // soft_gumbel: soft / hard (straight-through)
+  const unsigned hq = GUM ? nn_gumbel_query(a, src, tgt, j) : 0u;
 
   const int nst = (Mt + NN_STAGE - 1) / NN_STAGE;
   load_regs(0);
@@ -270,7 +300,12 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
         z[2 * g] = a0 * kk2 - t0v;
         z[2 * g + 1] = a1 * kk2 - t1v;
       }
-      if (MODE == 1) {
+      if (GUM) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          z[r >> 1][r & 1] += nn_gumbel_z(hq, t0 + i0 + 8 * (r >> 2) + 4 * kh + (r & 3), a.itau);
+      }
+      if (MODE == 1 || MODE == 4) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {   // increasing r = increasing target index: '>' keeps the first
           const float v = z[r >> 1][r & 1];
@@ -359,7 +394,7 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
   }
   (void)Fp;
   float ox, oy, oz;
-  if (MODE == 0) {
+  if (MODE == 0 || MODE == 3) {
     const float run_s = s2.x + s2.y, ax = ax2.x + ax2.y, ay = ay2.x + ay2.y, az = az2.x + az2.y;
     const float s = run_s + __shfl_xor(run_s, 32, 64);
     ox = (ax + __shfl_xor(ax, 32, 64)) / s;
@@ -380,7 +415,7 @@ __device__ __forceinline__ void feat_nn_online(const NNArgs& a, NNSmem& sm) {
       o += 3;
     }
     o[0] = ox; o[1] = oy; o[2] = oz;
-    if (a.idx && MODE == 1) a.idx[(int64_t)p * a.Nq + j] = besti;
+    if (a.idx && (MODE == 1 || MODE == 4)) a.idx[(int64_t)p * a.Nq + j] = besti;
   }
 }
 
@@ -798,6 +833,33 @@ extern "C" int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* 
     hipLaunchKernelGGL(mvr::feat_nn_kernel<0>, grid, dim3(256), 0, stream, a);
   else
     hipLaunchKernelGGL(mvr::feat_nn_kernel<1>, grid, dim3(256), 0, stream, a);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+// soft_gumbel (lib/layers.py:72-78): the online path with counter-based Gumbel noise (nn_gumbel_z), hard = 0 the
+// soft weights, 1 the straight-through forward value (the one-hot of the noisy argmax).  Same layouts as mvr_feat_nn.
+extern "C" int mvr_feat_nn_gumbel(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride,
+                                  const float* Xq, int64_t xq_fstride, const float* Xt, int64_t xt_fstride,
+                                  const int64_t* pairs, int P, int Nq, int Mt, int C, float inv_tau, int hard,
+                                  uint64_t seed, float* out, int64_t out_pstride, int64_t out_nstride, int32_t* idx_out,
+                                  hipStream_t stream) {
+  if (P < 0 || Nq < 0 || Mt <= 0 || C != 32 || (hard != 0 && hard != 1) || !(inv_tau > 0.f)) return MVR_EINVAL;
+  if (P == 0 || Nq == 0) return MVR_OK;
+  if (!Fq || !Ft || !Xt || !pairs || !out) return MVR_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(Fq) & 15) || (reinterpret_cast<uintptr_t>(Ft) & 15) || (fq_fstride & 3) ||
+      (ft_fstride & 3))
+    return MVR_EINVAL;
+  mvr::NNArgs a{Fq, fq_fstride, Ft, ft_fstride, Xq, xq_fstride, Xt, xt_fstride, pairs, P, Nq, Mt,
+                inv_tau * 1.4426950408889634f, hard ? 4 : 3, out, out_pstride, out_nstride, idx_out, 0, nullptr, 0,
+                (unsigned)seed, (unsigned)(seed >> 32), inv_tau};
+  mvr::ProfScope prof(mvr::PK_FEAT_NN, 2.0 * P * (double)Nq * Mt * C, (double)P * (Nq + Mt) * (C + 3) * 4 + P * Nq * 24.0,
+                      stream);
+  const dim3 grid((Nq + 127) / 128, P);
+  if (hard)
+    hipLaunchKernelGGL(mvr::feat_nn_kernel<4>, grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(mvr::feat_nn_kernel<3>, grid, dim3(256), 0, stream, a);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }

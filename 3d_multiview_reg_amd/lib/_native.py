@@ -79,6 +79,8 @@ _SIGS = {
                                       c_size, c_vp]),
     "mvr_feat_nn": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                             c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "mvr_feat_nn_gumbel": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int,
+                                   c_int, c_float, c_int, ctypes.c_uint64, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mvr_feat_nn_workspace_bytes": (c_size, [c_int, c_int]),
     "mvr_feat_nn_ws": (c_int, [c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp, c_int, c_int, c_int, c_int,
                                c_float, c_int, c_vp, c_i64, c_i64, c_vp, c_int, c_vp, c_size, c_vp]),

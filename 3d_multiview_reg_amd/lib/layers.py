@@ -47,13 +47,29 @@ class Soft_NN(torch.nn.Module):
             return 1 if self.st else 0
         if self.corr_type == "hard":
             return 1
-        raise NotImplementedError("soft_gumbel is stochastic (torch RNG); not implemented on the HIP path")
+        return 3 if self.st else 2   # soft_gumbel: hard (straight-through forward value) / soft
+
+    def _gumbel_seed(self):
+        """soft_gumbel's noise seed: one draw from torch's default (CPU) generator per call, so torch.manual_seed
+        makes runs repeatable as in the reference (whose noise comes from F.gumbel_softmax's own draws)"""
+        return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+    def _gumbel(self, Fq, fq_fs, Ft, ft_fs, Xq, xq_fs, Xt, xt_fs, pairs, P, n, m, out, o_ps, o_ns):
+        """lib/layers.py:72-78 (F.gumbel_softmax(-dist, tau=get_temp(), hard=st)) on the feature-NN kernel's online
+        path with counter-based noise (csrc/feat_nn.hip nn_gumbel_z; oracle/soft_nn.py restates it)"""
+        N.check(N.lib().mvr_feat_nn_gumbel(Fq, fq_fs, Ft, ft_fs, Xq, xq_fs, Xt, xt_fs, N.ptr(pairs), P, n, m, 32,
+                                           self._inv_tau2(), int(self.st), self._gumbel_seed(), N.ptr(out), o_ps,
+                                           o_ns, None, N.stream()), "mvr_feat_nn_gumbel")
+        return out
 
     def match_pairs(self, f_frag, xyz_frag, pairs, out, out_pstride, out_nstride, with_query_xyz=True):
         """Fused pairwise matching over fragments: f_frag [B,n,32], xyz_frag [B,n,3],
         pairs int64 [P,2] (query frag, target frag) -> out(p, i, :) = [xyz_q | x_corr]."""
         P = pairs.shape[0]
         B, n, C = f_frag.shape
+        if self.corr_type == "soft_gumbel":
+            return self._gumbel(N.ptr(f_frag), n * C, N.ptr(f_frag), n * C, N.ptr(xyz_frag) if with_query_xyz else None,
+                                n * 3, N.ptr(xyz_frag), n * 3, pairs, P, n, n, out, out_pstride, out_nstride)
         L = N.lib()
         ws = N.workspace(L.mvr_feat_nn_workspace_bytes(B, n), f_frag.device)   # pre-split target stages
         N.check(L.mvr_feat_nn_ws(N.ptr(f_frag), n * C, N.ptr(f_frag), n * C,
@@ -73,6 +89,9 @@ class Soft_NN(torch.nn.Module):
         y_c = y_c.float().contiguous()
         pairs = torch.arange(b, device=x_f.device, dtype=torch.int64).repeat_interleave(2).view(b, 2)
         out = torch.empty(b, n, 3, device=x_f.device, dtype=torch.float32)
+        if self.corr_type == "soft_gumbel":
+            return self._gumbel(N.ptr(x_f), n * c, N.ptr(y_f), m * c, None, 0, N.ptr(y_c), m * 3, pairs, b, n, m, out,
+                                n * 3, 3)
         N.check(N.lib().mvr_feat_nn(N.ptr(x_f), n * c, N.ptr(y_f), m * c, None, 0, N.ptr(y_c), m * 3, N.ptr(pairs),
                                     b, n, m, c, self._inv_tau2(), self.mode(), N.ptr(out), n * 3, 3, None,
                                     N.stream()), "mvr_feat_nn")

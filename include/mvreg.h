@@ -313,6 +313,16 @@ int mvr_feat_nn_ws(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t
                    int Mt, int C, float inv_tau2, int mode, float* out, int64_t out_pstride, int64_t out_nstride,
                    int32_t* idx_out, int n_frag, void* workspace, size_t workspace_bytes, mvr_stream_t stream);
 
+/* soft_gumbel correspondences (lib/layers.py:72-78: F.gumbel_softmax(-dist, tau, hard) . y_c): mvr_feat_nn's pairs
+ * and layouts, x_corr = softmax((2 fq.ft - |ft|^2 + g) * inv_tau) . Xt (hard = 0) or Xt[argmax of the same noisy
+ * logits] (hard = 1: the straight-through forward value; idx_out receives the index), with g = -ln(-ln u) per (query,
+ * target) and u a counter-based hash of (seed, pairs[2p], pairs[2p+1], query, target) — reproducible across batch
+ * shapes (oracle/soft_nn.py restates it); not torch's Philox stream. */
+int mvr_feat_nn_gumbel(const float* Fq, int64_t fq_fstride, const float* Ft, int64_t ft_fstride, const float* Xq,
+                       int64_t xq_fstride, const float* Xt, int64_t xt_fstride, const int64_t* pairs, int P, int Nq,
+                       int Mt, int C, float inv_tau, int hard, uint64_t seed, float* out, int64_t out_pstride,
+                       int64_t out_nstride, int32_t* idx_out, mvr_stream_t stream);
+
 /* Two nearest neighbours in feature space (scripts/extract_data.py:178-184, sklearn NearestNeighbors
  * kneighbors(n_neighbors=2), Euclidean): for pair p and query j of fragment pairs[2p] (Fq rows, fragment stride
  * fq_fstride), idx2_out[(p*Nq + j)*2 + k] = k-th nearest row of fragment pairs[2p+1] (Ft, Mt >= 2 rows),

@@ -39,7 +39,52 @@ def soft_nn(x_f, y_f, y_c, corr_type="soft", st=False, temp=0.3, min_temp=1e-4):
     if corr_type == "hard":
         idx = d.argmin(axis=2)
         return np.take_along_axis(y_c, idx[..., None], axis=1)
-    raise ValueError("soft_gumbel is stochastic and has no oracle")
+    raise ValueError("soft_gumbel: use soft_nn_gumbel (its noise needs a seed and the fragment ids)")
+
+
+def _mix32(x):
+    """lowbias32 finalizer (csrc/feat_nn.hip nn_mix32), uint32 arithmetic"""
+    x = np.asarray(x, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7feb352d)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846ca68b)
+        x = x ^ (x >> np.uint32(16))
+    return x
+
+
+def gumbel_noise(seed, src, tgt, Nq, Mt):
+    """The counter-based Gumbel noise of mvr_feat_nn_gumbel (csrc/feat_nn.hip nn_gumbel_query / nn_gumbel_z) for the
+    pair (query fragment src, target fragment tgt): g [Nq, Mt] = -ln(-ln u), u = ((hash >> 8) + 1/2) 2^-24 in
+    float64.  The reference draws g from torch's RNG (F.gumbel_softmax, lib/layers.py:72-78); this restates the
+    distribution, not the stream."""
+    u32 = np.uint32
+    lo, hi = u32(seed & 0xFFFFFFFF), u32((seed >> 32) & 0xFFFFFFFF)
+    with np.errstate(over="ignore"):
+        k = _mix32(lo ^ _mix32(hi + u32(0x9E3779B9) * u32(tgt & 0xFFFFFFFF)) ^ (u32(0x85EBCA77) * u32(src & 0xFFFFFFFF)))
+        hq = _mix32(k ^ np.arange(Nq, dtype=np.uint32))
+        x = _mix32(hq[:, None] + u32(0x9E3779B9) * np.arange(Mt, dtype=np.uint32)[None, :])
+    u = ((x >> u32(8)).astype(np.float64) + 0.5) * 2.0 ** -24
+    return -np.log(-np.log(u))
+
+
+def soft_nn_gumbel(x_f, y_f, y_c, src, tgt, seed, st=False, temp=0.3, min_temp=1e-4):
+    """lib/layers.py:72-78 with gumbel_noise: F.gumbel_softmax(-d, tau=max(temp^2, min_temp), hard=st) . y_c per
+    batch row b (query fragment src[b], target fragment tgt[b]); st: the forward value of the straight-through
+    one-hot (y_c at the noisy argmax).  float64."""
+    d = pairwise_distance(x_f.astype(np.float64), y_f.astype(np.float64))
+    tau = float(max(np.float32(temp) ** 2, np.float32(min_temp)))
+    out = []
+    for b in range(d.shape[0]):
+        z = (-d[b] + gumbel_noise(seed, int(src[b]), int(tgt[b]), d.shape[1], d.shape[2])) / tau
+        if st:
+            out.append(y_c[b][z.argmax(axis=1)])
+            continue
+        z = z - z.max(axis=1, keepdims=True)
+        e = np.exp(z)
+        out.append((e / e.sum(axis=1, keepdims=True)) @ y_c[b].astype(np.float64))
+    return np.stack(out)
 
 
 def sample_rand(pts_list, targeted_num_points, rng=np.random):

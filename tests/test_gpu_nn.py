@@ -142,3 +142,68 @@ def test_feat_nn_presplit_image_identical(gpu, n, m, scale):
             outs.append(out.cpu().numpy())
         assert np.array_equal(outs[0], outs[1]), np.nanmax(np.abs(outs[0] - outs[1]))
     assert L.mvr_feat_nn_ws(*args, B, NV.ptr(ws), nb - 16, NV.stream()) == -1   # workspace too small
+
+
+@pytest.mark.parametrize("n,m", [(1000, 1500), (33, 4097)])
+def test_soft_gumbel_vs_oracle(gpu, n, m, monkeypatch):
+    """soft_gumbel (lib/layers.py:72-78, F.gumbel_softmax(-dist, tau, hard=st)): the HIP path's counter-based noise
+    restated in oracle/soft_nn.py (float64), soft weights and the straight-through forward value, through Soft_NN and
+    the pair-indexed matcher; the noise depends on the fragment pair, not on the batch position.  (The reference's
+    own noise comes from torch's RNG and cannot be replayed: parity by restatement)"""
+    import torch
+    from lib.layers import Soft_NN
+    from oracle.soft_nn import soft_nn_gumbel
+    B = 3
+    L = max(n, m)
+    f = unit_features(B, L, 32, seed=7 + n)
+    x = np.random.RandomState(9).uniform(-2, 2, (B, L, 3)).astype(np.float32)
+    tf, tx = torch.from_numpy(f).to(gpu), torch.from_numpy(x).to(gpu)
+    seed = 0x1234_5678_9ABC
+    for st in (False, True):
+        nn = Soft_NN(corr_type="soft_gumbel", st=st).to(gpu)
+        monkeypatch.setattr(nn, "_gumbel_seed", lambda: seed)
+        got = nn(tf[:, :n].contiguous(), tf[:, :m].contiguous(), tx[:, :m].contiguous()).cpu().numpy()
+        ref = soft_nn_gumbel(f[:, :n], f[:, :m], x[:, :m], np.arange(B), np.arange(B), seed, st=st)
+        if not st:
+            np.testing.assert_allclose(got, ref, atol=2e-4)
+        else:   # the noisy argmax: exact up to fp32 near-ties of the noisy logits
+            bad = np.any(np.abs(got - ref) > 1e-6, axis=-1)
+            assert bad.mean() < 2e-3, bad.mean()
+    # the pair-indexed form (the pipeline's match_pairs): pair (s, t) gets the noise of fragments (s, t)
+    pairs = torch.tensor([[0, 1], [2, 0], [1, 1]], dtype=torch.int64, device=gpu)
+    out = torch.empty(3, n, 6, device=gpu)
+    nn = Soft_NN(corr_type="soft_gumbel", st=False).to(gpu)
+    monkeypatch.setattr(nn, "_gumbel_seed", lambda: seed)
+    if n == m:
+        nn.match_pairs(tf[:, :n].contiguous(), tx[:, :n].contiguous(), pairs, out, n * 6, 6)
+        p = pairs.cpu().numpy()
+        ref = soft_nn_gumbel(f[p[:, 0], :n], f[p[:, 1], :n], x[p[:, 1], :n], p[:, 0], p[:, 1], seed)
+        np.testing.assert_allclose(out[..., 3:].cpu().numpy(), ref, atol=2e-4)
+
+
+def test_soft_gumbel_hard_picks_follow_softmax(gpu):
+    """The Gumbel-max property the mode rests on: the straight-through pick of target j has probability
+    softmax(-d / tau)_j.  One query against 8 targets, 20000 independent draws (fragment pairs of one batch call)."""
+    import torch
+    from lib import _native as NV
+    P, M = 20000, 8
+    fq = unit_features(1, 1, 32, seed=1)[0, 0]
+    ft = unit_features(1, M, 32, seed=2)[0]
+    F = np.zeros((P + 1, M, 32), np.float32)
+    F[0, 0] = fq
+    F[1:] = ft                                    # fragment 0: the query; fragments 1..P: the same targets
+    X = np.zeros((P + 1, M, 3), np.float32)
+    X[:, :, 0] = np.arange(M, dtype=np.float32)   # x coordinate = target index
+    pairs = np.stack([np.zeros(P, np.int64), np.arange(1, P + 1)], 1)
+    tF, tX, tp = (torch.from_numpy(a).to(gpu) for a in (F, X, pairs))
+    out = torch.empty(P, 1, 3, device=gpu)
+    tau = 0.5
+    rc = NV.lib().mvr_feat_nn_gumbel(NV.ptr(tF), M * 32, NV.ptr(tF), M * 32, None, 0, NV.ptr(tX), M * 3, NV.ptr(tp), P,
+                                     1, M, 32, 1.0 / tau, 1, 99, NV.ptr(out), 3, 3, None, NV.stream())
+    assert rc == 0
+    picks = out[:, 0, 0].cpu().numpy().astype(int)
+    d = ((fq[None] - ft) ** 2).sum(-1).astype(np.float64)
+    pz = np.exp(-(d - d.min()) / tau)
+    pz /= pz.sum()
+    freq = np.bincount(picks, minlength=M) / P
+    assert np.all(np.abs(freq - pz) < 5 * np.sqrt(pz * (1 - pz) / P) + 1e-3), (freq, pz)

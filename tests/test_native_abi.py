@@ -71,6 +71,8 @@ _EMPTY_CALLS = {
                                            _Z),
     "mvr_feat_nn_ws": lambda L: L.mvr_feat_nn_ws(_Z, 0, _Z, 0, _Z, 0, _Z, 0, _Z, 3, 0, 5000, 32, 1.0, 0, _Z, 0, 0,
                                                  _Z, 0, _Z, 0, _Z),
+    "mvr_feat_nn_gumbel": lambda L: L.mvr_feat_nn_gumbel(_Z, 0, _Z, 0, _Z, 0, _Z, 0, _Z, 0, 5000, 5000, 32, 1.0, 1, 7,
+                                                         _Z, 0, 0, _Z, _Z),
     "mvr_feat_knn2": lambda L: L.mvr_feat_knn2(_Z, 0, _Z, 0, _Z, 0, 100, 100, 32, _Z, _Z, _Z),
     "mvr_gather_rows": lambda L: L.mvr_gather_rows(_Z, 32, _Z, 0, _Z, _Z),
     "mvr_fps": lambda L: L.mvr_fps(_Z, _Z, _Z, 0, 5000, _Z, _Z),
