@@ -65,7 +65,8 @@ struct NNArgs {
 // g = -log(e), e ~ Exp(1) per (query, target).  The noise is counter-based — a 32-bit hash of (seed, query fragment,
 // target fragment, query, target), so it does not depend on the batch a pair runs in and oracle/soft_nn.py
 // reproduces it — instead of torch's Philox stream (the reference's draws cannot be replayed: SURVEY §8a6, parity by
-// restatement).  u = (hash >> 8 + 1/2) 2^-24 in (0, 1), e = -ln u.
+// restatement).  u = (hash >> 9 + 1/2) 2^-23 in (0, 1) — 24 significant bits, exact in fp32, so u never rounds to
+// 1 (g = inf) and the oracle's float64 u is the same number — e = -ln u.
 __device__ __host__ __forceinline__ unsigned nn_mix32(unsigned x) {   // lowbias32 finalizer
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -82,8 +83,12 @@ __device__ __forceinline__ unsigned nn_gumbel_query(const NNArgs& a, int64_t src
 // the noise's contribution to a logit in log2 units (z = log2(e) (2 fs.ft - |ft|^2) / tau): log2(e) g / tau
 __device__ __forceinline__ float nn_gumbel_z(unsigned hq, int i, float itau) {
   const unsigned x = nn_mix32(hq + 0x9E3779B9u * (unsigned)i);
-  const float u = ((float)(x >> 8) + 0.5f) * 5.9604644775390625e-8f;           // (0, 1)
-  const float e = -0.69314718055994531f * __builtin_amdgcn_logf(u);            // -ln u > 0
+  const float u = ((float)(x >> 9) + 0.5f) * 1.1920928955078125e-7f;          // (0, 1), exact in fp32
+  const float w = ((float)(0x7FFFFFu - (x >> 9)) + 0.5f) * 1.1920928955078125e-7f;   // 1 - u, exact
+  // -ln u > 0; near u = 1 (w < 2^-6) the series of -ln(1 - w), so e keeps its relative precision where the noise
+  // is largest (g = -ln e) and that element dominates the softmax
+  const float e = w < 0.015625f ? w * fmaf(w, fmaf(w, fmaf(w, 0.25f, 0.33333334f), 0.5f), 1.f)
+                                : -0.69314718055994531f * __builtin_amdgcn_logf(u);
   return -itau * __builtin_amdgcn_logf(e);                                     // log2(e) g / tau, g = -ln e
 }
 

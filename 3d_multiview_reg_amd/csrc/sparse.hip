@@ -204,60 +204,19 @@ __global__ void insert_min_bounded_kernel(const uint64_t* __restrict__ keys, int
   if (i < n) hash_insert_min_bounded(h, keys[i], (int32_t)i, 64, overflow);
 }
 
-__global__ void first_flag_kernel(const uint64_t* __restrict__ keys, int64_t n, HashView h, int32_t* flags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int64_t s = hash_slot(h, keys[i]);
-  flags[i] = (s >= 0 && h.vals[s] == (int32_t)i) ? 1 : 0;
-}
-
-// ------------------------------------------------------------------ exclusive scan (int32 flags)
-constexpr int SCAN_B = 1024;
-
-__global__ void scan_block_kernel(const int32_t* __restrict__ in, int64_t n, int32_t* out, int32_t* bsum) {
-  __shared__ int32_t s[SCAN_B];
-  const int64_t i = (int64_t)blockIdx.x * SCAN_B + threadIdx.x;
-  const int v = (i < n) ? in[i] : 0;
-  s[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = 1; o < SCAN_B; o <<= 1) {  // Hillis-Steele inclusive
-    const int t = (threadIdx.x >= o) ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += t;
-    __syncthreads();
-  }
-  if (i < n) out[i] = s[threadIdx.x] - v;  // exclusive
-  if (threadIdx.x == SCAN_B - 1) bsum[blockIdx.x] = s[SCAN_B - 1];
-}
-
-__global__ void scan_sums_kernel(int32_t* bsum, int nb, int64_t* total) {
-  // single block: exclusive scan of nb block sums (serial chunks per thread)
-  __shared__ int32_t part[SCAN_B];
-  const int per = (nb + SCAN_B - 1) / SCAN_B;
-  const int b0 = threadIdx.x * per;
-  int acc = 0;
-  for (int k = 0; k < per && b0 + k < nb; ++k) acc += bsum[b0 + k];
-  part[threadIdx.x] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int t = 0; t < SCAN_B; ++t) { const int v = part[t]; part[t] = run; run += v; }
-    *total = run;
-  }
-  __syncthreads();
-  int run = part[threadIdx.x];
-  for (int k = 0; k < per && b0 + k < nb; ++k) { const int v = bsum[b0 + k]; bsum[b0 + k] = run; run += v; }
-}
-
-__global__ void scan_add_kernel(int32_t* out, int64_t n, const int32_t* __restrict__ bsum) {
-  const int64_t i = (int64_t)blockIdx.x * SCAN_B + threadIdx.x;
-  if (i < n) out[i] += bsum[blockIdx.x];
+// first occurrences from the table instead of a lookup per key: every occupied slot holds its key's smallest source
+// row (insert_min), so flag that row (flags zeroed before).  One pass over the table's slots (~2 per distinct key)
+// with a scattered 4-byte store per distinct key, instead of a probe per source row (raw points: ~12 per voxel).
+__global__ void slot_flag_kernel(HashView h, int32_t* flags) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < h.cap && h.keys[s] != EMPTY_KEY) flags[h.vals[s]] = 1;
 }
 
 // compact selected rows (first occurrences) in source order
 __global__ void compact_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ pos, int64_t n,
-                               const int4* __restrict__ cc, int4* coords_out, int64_t* sel_out) {
+                               const int4* __restrict__ cc, int4* coords_out, int64_t* sel_out, int64_t* total) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (total && i == n - 1) *total = (int64_t)pos[i] + flags[i];   // the count (exclusive scan + last flag)
   if (i < n && flags[i]) {
     const int p = pos[i];
     coords_out[p] = cc[i];
@@ -314,6 +273,107 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
   const int64_t v =
       hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step, c.w + sign * dz * step), t);
   nbr[e] = (int32_t)v;
+}
+
+// 3^3 kernel map over a lattice table (t >= 0), one thread per output row (row_order: as kernel_map_kernel).  The
+// 27 neighbours of a row fall in at most 2 lattice cells per axis (step <= 2^t), i.e. <= 8 of the table's 8-slot
+// cell buckets: each bucket is loaded once (keys 64 B + values 32 B) and resolves every neighbour in its cell, where
+// the thread-per-(row, offset) kernel loads a bucket per neighbour (27 per row).  Neighbours off the table's lattice
+// (coordinates not multiples of 2^t: most offsets of a transposed map) are absent without a probe.  A bucket that is
+// full without the key and without an empty slot proving its absence continues on hash_find_bucket's probe path, so
+// the map equals kernel_map_kernel's.  The rows' 27 entries leave through LDS as contiguous 108-byte rows.
+#ifndef KMAP_ROWS
+#define KMAP_ROWS 1
+#endif
+constexpr int KMR_THREADS = 256;
+__global__ __launch_bounds__(KMR_THREADS) void kernel_map_rows_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h,
+                                                                      int step, int sign, int32_t* __restrict__ nbr,
+                                                                      const int32_t* __restrict__ row_order) {
+  __shared__ int32_t sout[KMR_THREADS * 27];
+  const int64_t i0 = (int64_t)blockIdx.x * KMR_THREADS;
+  const int64_t i = i0 + threadIdx.x;
+  const int t = h.hdr[0];   // uniform: the table's home mode (-1 hashed, 0..15 lattice of stride 2^t)
+  int32_t* row = sout + threadIdx.x * 27;   // stride 27 words: conflict-free
+#pragma unroll
+  for (int k = 0; k < 27; ++k) row[k] = -1;
+  const int64_t o = i < Mo ? (row_order ? (int64_t)row_order[i] : i) : -1;
+  if (o >= 0 && t >= -1 && t <= 15) {
+    const int4 c = oc[o];
+    if (t < 0 || step > (1 << t)) {   // not a lattice case: per-offset lookups
+      for (int k = 0; k < 27; ++k) {
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        row[k] = (int32_t)hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step,
+                                                c.w + sign * dz * step), t);
+      }
+    } else {
+      const int lm = (1 << t) - 1, cs = t + 1;
+      const int cc[3] = {c.y, c.z, c.w};
+      int v[3][3];              // [axis][d]: candidate coordinate c + sign (d - 1) step
+      unsigned on[3], up[3];    // per axis, bit d: v on the table's lattice / in the upper of the axis' two cells
+      int cb[3];                // the lower cell's base coordinate per axis
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int lo = (cc[a] - step) >> cs;
+        cb[a] = lo << cs;
+        on[a] = up[a] = 0;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          const int x = cc[a] + sign * (d - 1) * step;
+          v[a][d] = x;
+          on[a] |= ((x & lm) == 0 ? 1u : 0u) << d;
+          up[a] |= ((x >> cs) != lo ? 1u : 0u) << d;
+        }
+      }
+      for (int cell = 0; cell < 8; ++cell) {
+        const unsigned sx = on[0] & ((cell & 1) ? up[0] : ~up[0]) & 7u;
+        const unsigned sy = on[1] & ((cell & 2) ? up[1] : ~up[1]) & 7u;
+        const unsigned sz = on[2] & ((cell & 4) ? up[2] : ~up[2]) & 7u;
+        if (!sx || !sy || !sz) continue;
+        const uint64_t b = hash_home(h, pack_key(c.x, cb[0] + ((cell & 1) << cs), cb[1] + (((cell >> 1) & 1) << cs),
+                                                 cb[2] + (((cell >> 2) & 1) << cs)), t);
+        const uint4* kp = reinterpret_cast<const uint4*>(h.keys + b);
+        uint64_t kk[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 u = kp[q];
+          kk[2 * q] = ((uint64_t)u.y << 32) | u.x;
+          kk[2 * q + 1] = ((uint64_t)u.w << 32) | u.z;
+        }
+        const int4 va = reinterpret_cast<const int4*>(h.vals + b)[0], vb = reinterpret_cast<const int4*>(h.vals + b)[1];
+        for (unsigned mz = sz; mz; mz &= mz - 1) {
+          const int dz = __builtin_ctz(mz);
+          for (unsigned my = sy; my; my &= my - 1) {
+            const int dy = __builtin_ctz(my);
+            for (unsigned mx = sx; mx; mx &= mx - 1) {
+              const int dx = __builtin_ctz(mx);
+              const uint64_t key = pack_key(c.x, v[0][dx], v[1][dy], v[2][dz]);
+              const int from = lattice_sub(key, t);
+              int r = -1;
+              bool empty = false;
+#pragma unroll
+              for (int j = 7; j >= 0; --j) {
+                const int vj = j < 4 ? (&va.x)[j] : (&vb.x)[j - 4];
+                if (kk[j] == key) r = vj;
+                empty |= j >= from && kk[j] == EMPTY_KEY;
+              }
+              // a full home bucket without the key proves nothing: probe on as hash_find_bucket does (rare)
+              if (r < 0 && !empty) r = (int32_t)hash_find_bucket(h, key, t);
+              row[dx + 3 * dy + 9 * dz] = r;
+            }
+          }
+        }
+      }
+    }
+  }
+  if (row_order) {   // rows visited out of order: each row written in place
+    if (o >= 0)
+      for (int k = 0; k < 27; ++k) nbr[o * 27 + k] = row[k];
+    return;
+  }
+  __syncthreads();
+  const int64_t nrow = Mo - i0 < KMR_THREADS ? Mo - i0 : KMR_THREADS;
+  int32_t* dst = nbr + i0 * 27;
+  for (int e = threadIdx.x; e < nrow * 27; e += KMR_THREADS) dst[e] = sout[e];
 }
 
 // ------------------------------------------------------------------ brick map
@@ -623,21 +683,20 @@ struct DedupWs {
 };
 
 // table sized for `keys` distinct keys (<= n)
+static size_t dedup_scan_bytes(int64_t n) { return scan_ws_bytes(n > 0 ? n : 1); }
 static size_t dedup_ws_bytes(int64_t n, int64_t keys = -1) {
-  const int64_t nb = (n + SCAN_B - 1) / SCAN_B;
-  return (size_t)n * (8 + 16 + 4 + 4) + (size_t)nb * 4 + hash_table_bytes(keys < 0 ? n : keys) + 8 * 256;
+  return (size_t)n * (8 + 16 + 4 + 4) + dedup_scan_bytes(n) + hash_table_bytes(keys < 0 ? n : keys) + 8 * 256;
 }
 
 static DedupWs dedup_ws(void* ws, int64_t n, int64_t keys = -1) {
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t b) { p = reinterpret_cast<char*>(((uintptr_t)p + 255) & ~(uintptr_t)255); char* r = p; p += b; return r; };
   DedupWs d{};
-  const int64_t nb = (n + SCAN_B - 1) / SCAN_B;
   d.keys = reinterpret_cast<uint64_t*>(take((size_t)n * 8));
   d.cc = reinterpret_cast<int4*>(take((size_t)n * 16));
   d.flags = reinterpret_cast<int32_t*>(take((size_t)n * 4));
   d.pos = reinterpret_cast<int32_t*>(take((size_t)n * 4));
-  d.bsum = reinterpret_cast<int32_t*>(take((size_t)nb * 4 + 4));
+  d.bsum = reinterpret_cast<int32_t*>(take(dedup_scan_bytes(n)));
   d.table_bytes = hash_table_bytes(keys < 0 ? n : keys);
   d.table = take(d.table_bytes);
   return d;
@@ -651,13 +710,13 @@ static int dedup_run(const DedupWs& d, int64_t n, int4* coords_out, int64_t* sel
     hipLaunchKernelGGL(insert_min_bounded_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h, overflow);
   else
     hipLaunchKernelGGL(insert_min_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h);
-  hipLaunchKernelGGL(first_flag_kernel, dim3(nblk(n)), dim3(256), 0, s, d.keys, n, h, d.flags);
-  const int nb = (int)((n + SCAN_B - 1) / SCAN_B);
+  if (hipMemsetAsync(d.flags, 0, sizeof(int32_t) * (size_t)n, s) != hipSuccess) return MVR_ELAUNCH;
+  hipLaunchKernelGGL(slot_flag_kernel, dim3(nblk((int64_t)h.cap)), dim3(256), 0, s, h, d.flags);
   if (hipMemsetAsync(counts, 0, sizeof(int64_t) * (1 + B), s) != hipSuccess) return MVR_ELAUNCH;
-  hipLaunchKernelGGL(scan_block_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.flags, n, d.pos, d.bsum);
-  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(SCAN_B), 0, s, d.bsum, nb, counts);
-  hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(SCAN_B), 0, s, d.pos, n, d.bsum);
-  hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, d.flags, d.pos, n, d.cc, coords_out, sel_out);
+  const int rc = excl_scan_i32(d.flags, d.pos, n, d.bsum, dedup_scan_bytes(n), s);   // radix.hip
+  if (rc != MVR_OK) return rc;
+  hipLaunchKernelGGL(compact_kernel, dim3(nblk(n)), dim3(256), 0, s, d.flags, d.pos, n, d.cc, coords_out, sel_out,
+                     counts);
   const int cb = (int)std::min<int64_t>(nblk(n), 512);
   hipLaunchKernelGGL(batch_count_kernel, dim3(cb), dim3(256), sizeof(int) * B, s, coords_out, B, counts);
   MVR_CHECK_LAUNCH();
@@ -692,15 +751,31 @@ struct OrderMaps {
   int n, K;
   int jshift;   // key bit of the map index: 59 above the masks, 32 without neighbour tables (coordinate orders)
 };
-__global__ void order_keys_kernel(OrderMaps m, uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+// A wave whose 64 rows lie in one map loads their neighbour rows (64 x K contiguous words) coalesced into LDS and
+// each lane builds its mask there; a wave straddling two maps (at most n_maps - 1 of them) reads its rows directly.
+__global__ __launch_bounds__(256) void order_keys_kernel(OrderMaps m, uint64_t* __restrict__ keys,
+                                                         int32_t* __restrict__ vals) {
+  __shared__ int32_t snb[4][64 * 27];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m.start[m.n]) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t total = m.start[m.n];
+  const int64_t iw = i - lane;   // the wave's first row
   int j = 0;
-  while (i >= m.start[j + 1]) ++j;
+  const int64_t ic = i < total ? i : total - 1;
+  while (ic >= m.start[j + 1]) ++j;
+  const int jf = __shfl(j, 0, 64), jl = __shfl(j, (int)min<int64_t>(63, total - 1 - iw), 64);
+  const bool staged = iw < total && jf == jl && m.nbr[jf] != nullptr;   // wave-uniform
+  if (staged) {
+    const int64_t nrow = min<int64_t>(64, total - iw);
+    const int32_t* src = m.nbr[jf] + (iw - m.start[jf]) * m.K;
+    for (int e = lane; e < nrow * m.K; e += 64) snb[w][e] = src[e];
+  }
+  __syncthreads();
+  if (i >= total) return;
   const int64_t o = i - m.start[j];
   uint32_t mask = 0;
   if (m.nbr[j]) {
-    const int32_t* row = m.nbr[j] + o * m.K;
+    const int32_t* row = staged ? &snb[w][lane * m.K] : m.nbr[j] + o * m.K;
     for (int k = 0; k < m.K; ++k) mask |= (row[k] >= 0 ? 1u : 0u) << k;
   }
   uint32_t lo = 0;
@@ -823,6 +898,15 @@ extern "C" int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const v
   if (!h.cap) return MVR_EINVAL;
   const int64_t tot = Mout * (int64_t)ksize * ksize * ksize;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)tot * 4.0, s);
+  // 3^3 stencils: one thread per row (lattice tables, the FCGF levels: <= 8 cell buckets per row; the kernel reads
+  // the table's mode from its header and takes per-offset lookups for hashed tables).  KMAP_ROWS=0 builds the
+  // thread-per-(row, offset) kernel for A/B.
+  if (ksize == 3 && KMAP_ROWS) {
+    hipLaunchKernelGGL(kernel_map_rows_kernel, dim3(nblk(Mout, KMR_THREADS)), dim3(KMR_THREADS), 0, s,
+                       reinterpret_cast<const int4*>(out_coords), Mout, h, step, transposed ? -1 : 1, nbr, row_order);
+    MVR_CHECK_LAUNCH();
+    return MVR_OK;
+  }
   hipLaunchKernelGGL(kernel_map_kernel, dim3(nblk(tot)), dim3(256), 0, s, reinterpret_cast<const int4*>(out_coords),
                      Mout, h, ksize, step, transposed ? -1 : 1, nbr, row_order);
   MVR_CHECK_LAUNCH();

@@ -56,7 +56,7 @@ def _mix32(x):
 
 def gumbel_noise(seed, src, tgt, Nq, Mt):
     """The counter-based Gumbel noise of mvr_feat_nn_gumbel (csrc/feat_nn.hip nn_gumbel_query / nn_gumbel_z) for the
-    pair (query fragment src, target fragment tgt): g [Nq, Mt] = -ln(-ln u), u = ((hash >> 8) + 1/2) 2^-24 in
+    pair (query fragment src, target fragment tgt): g [Nq, Mt] = -ln(-ln u), u = ((hash >> 9) + 1/2) 2^-23 in
     float64.  The reference draws g from torch's RNG (F.gumbel_softmax, lib/layers.py:72-78); this restates the
     distribution, not the stream."""
     u32 = np.uint32
@@ -65,7 +65,7 @@ def gumbel_noise(seed, src, tgt, Nq, Mt):
         k = _mix32(lo ^ _mix32(hi + u32(0x9E3779B9) * u32(tgt & 0xFFFFFFFF)) ^ (u32(0x85EBCA77) * u32(src & 0xFFFFFFFF)))
         hq = _mix32(k ^ np.arange(Nq, dtype=np.uint32))
         x = _mix32(hq[:, None] + u32(0x9E3779B9) * np.arange(Mt, dtype=np.uint32)[None, :])
-    u = ((x >> u32(8)).astype(np.float64) + 0.5) * 2.0 ** -24
+    u = ((x >> u32(9)).astype(np.float64) + 0.5) * 2.0 ** -23
     return -np.log(-np.log(u))
 
 

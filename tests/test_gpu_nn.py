@@ -183,7 +183,7 @@ def test_soft_gumbel_vs_oracle(gpu, n, m, monkeypatch):
 
 def test_soft_gumbel_hard_picks_follow_softmax(gpu):
     """The Gumbel-max property the mode rests on: the straight-through pick of target j has probability
-    softmax(-d / tau)_j.  One query against 8 targets, 20000 independent draws (fragment pairs of one batch call)."""
+    softmax(-d)_j (F.gumbel_softmax adds the noise to the logits -d before dividing by tau).  One query against 8 targets, 20000 independent draws (fragment pairs of one batch call)."""
     import torch
     from lib import _native as NV
     P, M = 20000, 8
@@ -203,7 +203,7 @@ def test_soft_gumbel_hard_picks_follow_softmax(gpu):
     assert rc == 0
     picks = out[:, 0, 0].cpu().numpy().astype(int)
     d = ((fq[None] - ft) ** 2).sum(-1).astype(np.float64)
-    pz = np.exp(-(d - d.min()) / tau)
+    pz = np.exp(-(d - d.min()))   # argmax((-d + g) / tau) = argmax(-d + g): tau does not enter the picks
     pz /= pz.sum()
     freq = np.bincount(picks, minlength=M) / P
     assert np.all(np.abs(freq - pz) < 5 * np.sqrt(pz * (1 - pz) / P) + 1e-3), (freq, pz)
