@@ -270,110 +270,14 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
     nbr[e] = -1;
     return;
   }
-  const int64_t v =
-      hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step, c.w + sign * dz * step), t);
-  nbr[e] = (int32_t)v;
-}
-
-// 3^3 kernel map over a lattice table (t >= 0), one thread per output row (row_order: as kernel_map_kernel).  The
-// 27 neighbours of a row fall in at most 2 lattice cells per axis (step <= 2^t), i.e. <= 8 of the table's 8-slot
-// cell buckets: each bucket is loaded once (keys 64 B + values 32 B) and resolves every neighbour in its cell, where
-// the thread-per-(row, offset) kernel loads a bucket per neighbour (27 per row).  Neighbours off the table's lattice
-// (coordinates not multiples of 2^t: most offsets of a transposed map) are absent without a probe.  A bucket that is
-// full without the key and without an empty slot proving its absence continues on hash_find_bucket's probe path, so
-// the map equals kernel_map_kernel's.  The rows' 27 entries leave through LDS as contiguous 108-byte rows.
-#ifndef KMAP_ROWS
-#define KMAP_ROWS 1
-#endif
-constexpr int KMR_THREADS = 256;
-__global__ __launch_bounds__(KMR_THREADS) void kernel_map_rows_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h,
-                                                                      int step, int sign, int32_t* __restrict__ nbr,
-                                                                      const int32_t* __restrict__ row_order) {
-  __shared__ int32_t sout[KMR_THREADS * 27];
-  const int64_t i0 = (int64_t)blockIdx.x * KMR_THREADS;
-  const int64_t i = i0 + threadIdx.x;
-  const int t = h.hdr[0];   // uniform: the table's home mode (-1 hashed, 0..15 lattice of stride 2^t)
-  int32_t* row = sout + threadIdx.x * 27;   // stride 27 words: conflict-free
-#pragma unroll
-  for (int k = 0; k < 27; ++k) row[k] = -1;
-  const int64_t o = i < Mo ? (row_order ? (int64_t)row_order[i] : i) : -1;
-  if (o >= 0 && t >= -1 && t <= 15) {
-    const int4 c = oc[o];
-    if (t < 0 || step > (1 << t)) {   // not a lattice case: per-offset lookups
-      for (int k = 0; k < 27; ++k) {
-        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
-        row[k] = (int32_t)hash_find(h, pack_key(c.x, c.y + sign * dx * step, c.z + sign * dy * step,
-                                                c.w + sign * dz * step), t);
-      }
-    } else {
-      const int lm = (1 << t) - 1, cs = t + 1;
-      const int cc[3] = {c.y, c.z, c.w};
-      int v[3][3];              // [axis][d]: candidate coordinate c + sign (d - 1) step
-      unsigned on[3], up[3];    // per axis, bit d: v on the table's lattice / in the upper of the axis' two cells
-      int cb[3];                // the lower cell's base coordinate per axis
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int lo = (cc[a] - step) >> cs;
-        cb[a] = lo << cs;
-        on[a] = up[a] = 0;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-          const int x = cc[a] + sign * (d - 1) * step;
-          v[a][d] = x;
-          on[a] |= ((x & lm) == 0 ? 1u : 0u) << d;
-          up[a] |= ((x >> cs) != lo ? 1u : 0u) << d;
-        }
-      }
-      for (int cell = 0; cell < 8; ++cell) {
-        const unsigned sx = on[0] & ((cell & 1) ? up[0] : ~up[0]) & 7u;
-        const unsigned sy = on[1] & ((cell & 2) ? up[1] : ~up[1]) & 7u;
-        const unsigned sz = on[2] & ((cell & 4) ? up[2] : ~up[2]) & 7u;
-        if (!sx || !sy || !sz) continue;
-        const uint64_t b = hash_home(h, pack_key(c.x, cb[0] + ((cell & 1) << cs), cb[1] + (((cell >> 1) & 1) << cs),
-                                                 cb[2] + (((cell >> 2) & 1) << cs)), t);
-        const uint4* kp = reinterpret_cast<const uint4*>(h.keys + b);
-        uint64_t kk[8];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint4 u = kp[q];
-          kk[2 * q] = ((uint64_t)u.y << 32) | u.x;
-          kk[2 * q + 1] = ((uint64_t)u.w << 32) | u.z;
-        }
-        const int4 va = reinterpret_cast<const int4*>(h.vals + b)[0], vb = reinterpret_cast<const int4*>(h.vals + b)[1];
-        for (unsigned mz = sz; mz; mz &= mz - 1) {
-          const int dz = __builtin_ctz(mz);
-          for (unsigned my = sy; my; my &= my - 1) {
-            const int dy = __builtin_ctz(my);
-            for (unsigned mx = sx; mx; mx &= mx - 1) {
-              const int dx = __builtin_ctz(mx);
-              const uint64_t key = pack_key(c.x, v[0][dx], v[1][dy], v[2][dz]);
-              const int from = lattice_sub(key, t);
-              int r = -1;
-              bool empty = false;
-#pragma unroll
-              for (int j = 7; j >= 0; --j) {
-                const int vj = j < 4 ? (&va.x)[j] : (&vb.x)[j - 4];
-                if (kk[j] == key) r = vj;
-                empty |= j >= from && kk[j] == EMPTY_KEY;
-              }
-              // a full home bucket without the key proves nothing: probe on as hash_find_bucket does (rare)
-              if (r < 0 && !empty) r = (int32_t)hash_find_bucket(h, key, t);
-              row[dx + 3 * dy + 9 * dz] = r;
-            }
-          }
-        }
-      }
-    }
-  }
-  if (row_order) {   // rows visited out of order: each row written in place
-    if (o >= 0)
-      for (int k = 0; k < 27; ++k) nbr[o * 27 + k] = row[k];
+  const int qx = c.y + sign * dx * step, qy = c.z + sign * dy * step, qz = c.w + sign * dz * step;
+  // a lattice table (stride 2^t) holds only multiples of 2^t: a neighbour off the lattice (most offsets of a
+  // transposed map, whose output stride is half the table's) is absent without a probe
+  if (t >= 0 && ((qx | qy | qz) & ((1 << t) - 1)) != 0) {
+    nbr[e] = -1;
     return;
   }
-  __syncthreads();
-  const int64_t nrow = Mo - i0 < KMR_THREADS ? Mo - i0 : KMR_THREADS;
-  int32_t* dst = nbr + i0 * 27;
-  for (int e = threadIdx.x; e < nrow * 27; e += KMR_THREADS) dst[e] = sout[e];
+  nbr[e] = (int32_t)hash_find(h, pack_key(c.x, qx, qy, qz), t);
 }
 
 // ------------------------------------------------------------------ brick map
@@ -898,15 +802,6 @@ extern "C" int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const v
   if (!h.cap) return MVR_EINVAL;
   const int64_t tot = Mout * (int64_t)ksize * ksize * ksize;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)tot * 4.0, s);
-  // 3^3 stencils: one thread per row (lattice tables, the FCGF levels: <= 8 cell buckets per row; the kernel reads
-  // the table's mode from its header and takes per-offset lookups for hashed tables).  KMAP_ROWS=0 builds the
-  // thread-per-(row, offset) kernel for A/B.
-  if (ksize == 3 && KMAP_ROWS) {
-    hipLaunchKernelGGL(kernel_map_rows_kernel, dim3(nblk(Mout, KMR_THREADS)), dim3(KMR_THREADS), 0, s,
-                       reinterpret_cast<const int4*>(out_coords), Mout, h, step, transposed ? -1 : 1, nbr, row_order);
-    MVR_CHECK_LAUNCH();
-    return MVR_OK;
-  }
   hipLaunchKernelGGL(kernel_map_kernel, dim3(nblk(tot)), dim3(256), 0, s, reinterpret_cast<const int4*>(out_coords),
                      Mout, h, ksize, step, transposed ? -1 : 1, nbr, row_order);
   MVR_CHECK_LAUNCH();
