@@ -961,17 +961,19 @@ __global__ __launch_bounds__(512, 1) void pcn_chain_kernel(ChArgs a) {
     // ---------------------------------------------------------------- group B: conv7 + pconv's epilogue
     const int erow = lane >> 3, ec0 = 4 * (lane & 7);
     float* yb = ys[w];
-    float4 rres[4];
-    auto load_r = [&](const Cur& c) {
+    // the residual of a chunk in registers, two sets used alternately by an unrolled loop (a loop-carried copy of
+    // registers with loads in flight would make every step wait for them, and for the stores issued before them)
+    float4 ra[4], rb[4];
+    auto load_r = [&](const Cur& c, float4 (&r)[4]) {
       const int n = min(c.kc * CH + ec0, N4 - 4);
       const float* src = a.X + (int64_t)c.p * a.xps + (int64_t)(32 * w + erow) * a.xld + (int64_t)(n >> 5) * a.xcs +
                          (n & 31);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rres[q] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.xld);
+      for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.xld);
     };
     int rn = 0;
     float ls[4], lss[4];
-    auto epilogue = [&](const Cur& c, const floatx16& acc) {
+    auto epilogue = [&](const Cur& c, const floatx16& acc, const float4 (&rres)[4]) {
       const int n0 = c.kc * CH;
       float4 ev[4];
 #pragma unroll
@@ -1071,22 +1073,28 @@ __global__ __launch_bounds__(512, 1) void pcn_chain_kernel(ChArgs a) {
       if (lane == 0 && np) atomicAdd(a.pos + c.p, np);
     };
     Cur cc = cstart, cr = cstart, ch = cstart;
-    load_r(cr);
+    load_r(cr, ra);
     adv(cr);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // step 0: group A's first chunk
-    for (int j = 1; j <= nloc; ++j) {
+    // step j: the next chunk's residual loads first (ahead of this step's stores), the MFMAs of chunk j - 1, its
+    // epilogue with the residual loaded one step ago
+    auto stepB = [&](int j, const float4 (&cur)[4], float4 (&nxt)[4]) {
+      load_r(cr, nxt);
+      adv(cr);
       if (HEAD && j > 1) {
         head_finish(ch);
         adv(ch);
       }
       const floatx16 acc = mfma(ti[(j - 1) & 1], [&](int) {});
-      epilogue(cc, acc);
+      epilogue(cc, acc, cur);
       adv(cc);
-      load_r(cr);
-      adv(cr);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    for (int j = 1; j <= nloc; j += 2) {
+      stepB(j, ra, rb);
+      if (j + 1 <= nloc) stepB(j + 1, rb, ra);
     }
     if (HEAD) head_finish(ch);
   }
