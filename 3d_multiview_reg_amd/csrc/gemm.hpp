@@ -101,22 +101,6 @@ int launch_gemm(const GemmArgs& g, hipStream_t stream);
 bool pconv_covers(const GemmArgs& g);   // head fields set: only pconv can run it
 int launch_pconv(const GemmArgs& g, hipStream_t stream);
 
-// A PointCN without shortcut (oanet.py:18-43, C = 128) chained in one launch (pconv.hip pcn_chain_kernel):
-// y = W7 . relu(x5 * sc5 + sh5) + b7 + x with x5 = W3 . relu(x * sc1 + sh1) + b3 never stored; sc5 / sh5 are the fold
-// of x5's statistics from a statistics-only conv3 pass.  Point operands in either layout (ld, chunk stride cs; cs 0:
-// row-major), y may be x (in place).  stats: y's ST_ROW partials (no head); head_w: the block's output head as
-// GemmArgs' (head_only: y not stored).  Bit-identical to the conv3 -> conv7 pair of launches.
-struct PcnChain {
-  int P, N;
-  const float* X; int64_t xps, xld, xcs;
-  float* Y; int64_t yps, yld, ycs;
-  const float* W3; const float* b3; const float* W7; const float* b7;
-  const float* sc1; const float* sh1; const float* sc5; const float* sh5; int64_t sPb;
-  float2* stats; int64_t st_ld; int st_off;
-  const float* head_w; const float* head_bp; float* logits; float* scores; int32_t* pos; int head_only;
-};
-int launch_pcn_chain(const PcnChain& c, hipStream_t stream);
-
 // diff_pool / diff_unpool (oan_attn.hip) over point activations in either layout (chunk stride cs, GemmArgs
 // bcs): the C-ABI mvr_oan_diff_pool_ws / mvr_oan_diff_unpool with cs = 32 (row-major)
 int oan_diff_pool_cm(const float* x, int64_t x_pstride, int64_t x_ld, int64_t x_cs, const float* sc, const float* sh,

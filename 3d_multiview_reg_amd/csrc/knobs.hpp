@@ -23,8 +23,7 @@ enum ForcePath : int {
   FORCE_POOL_NOSPLIT = 4,     // diff_pool without key splits (another fp32 summation order)
   FORCE_UNPOOL8 = 5,          // the 8-wave diff_unpool (clusters > 512) at <= 512 clusters too
   FORCE_ROW_LAYOUT = 6,       // the OANet block's point activations row-major instead of chunk-major
-  FORCE_NO_CHAIN = 7,         // PointCNs as conv3 + conv7 launches instead of the statistics pass + chained kernel
-  FORCE_COUNT = 8
+  FORCE_COUNT = 7
 };
 extern int g_force[FORCE_COUNT];
 

@@ -275,9 +275,6 @@ __global__ void head_kernel(const float* __restrict__ X, int64_t ps, int64_t ld,
 #endif
 
 // Point activations chunk-major where every kernel touching them takes it (Plan::cm; 0: row-major, the A/B build)
-#ifndef OAN_CHAIN
-#define OAN_CHAIN 1   // PointCNs without a shortcut as a statistics pass + the chained kernel (pointcn_chain)
-#endif
 #ifndef OAN_CHUNK_MAJOR
 #define OAN_CHUNK_MAJOR 1
 #endif
@@ -573,7 +570,6 @@ struct Ctx {
   // next consumer's); returns whether it did
   bool pointcn(const mvr_pointcn_p& pc, const Act& x, Act& y, const FoldReq* next = nullptr, bool x_folded = false) {
     if (!x_folded) finalize_in(x, 1e-5f, pc.bn1);
-    if (chain_ok(pc, x, y, next)) return pointcn_chain(pc, x, y);
     Act t = pts(pl.T1, y.C, y.C, pl.stT, y.C);
     const bool sc = pc.shortcut.weight != nullptr;
     y.tw0 = 128;
@@ -601,54 +597,6 @@ struct Ctx {
       dbg_dump(y.st, (size_t)pl.P * TNn * y.st_ld * sizeof(float2), s);
     }
     return yf;
-  }
-
-  // The chained form (pconv.hip pcn_chain_kernel): a statistics-only conv3 pass, the fold of its statistics, then
-  // ONE launch computing conv3 again, its fold + ReLU and conv7 (+ residual, statistics or head) without storing
-  // conv3's output — 48 instead of 80 KB per 32-point chunk.  128 -> 128 PointCNs without a shortcut, split-bf16
-  // arithmetic (the split-fp16 passes and fused finalizes stay on the two-launch form).
-  bool chain_ok(const mvr_pointcn_p& pc, const Act& x, const Act& y, const FoldReq* next) const {
-    return OAN_CHAIN && !g_force[FORCE_NO_CHAIN] && !g_force[FORCE_GENERIC_GEMM] && !f16 && !pc.shortcut.weight &&
-           x.C == 128 && y.C == 128 && pl.N > 32 && !(OAN_FUSED_FIN && next);
-  }
-  bool pointcn_chain(const mvr_pointcn_p& pc, const Act& x, Act& y) {
-    y.tw0 = 128;
-    y.csplit = 1 << 30;
-    const mvr_conv_p* hd = head;
-    head = nullptr;
-    float* sc1 = sc();
-    float* sh1 = sh();
-    dbg_hash(sc1, pl.P, 1, x.C, x.C, 0, s);   // the two-launch form's stage hashes, in its order
-    dbg_hash(sh1, pl.P, 1, x.C, x.C, 0, s);
-    float* sc5 = fcur ? pl.sc : pl.sc2;   // the other fold buffer: fold1 stays readable
-    float* sh5 = fcur ? pl.sh : pl.sh2;
-    Act t = pts(nullptr, y.C, y.C, pl.stT, y.C);
-    conv(pc.conv3, x, true, t, nullptr, ST_ROW, nullptr, true);   // statistics only (no store)
-    const int TNn = (pl.N + 127) / 128;
-    dbg_hash(reinterpret_cast<const float*>(pl.stT), pl.P, 1, TNn * y.C * 2, (int64_t)TNn * y.C * 2, 0, s);
-    t.tw0 = 128;
-    t.csplit = 1 << 30;
-    finalize_in(t, 1e-5f, pc.bn5, sc5, sh5);
-    dbg_hash(sc5, pl.P, 1, y.C, y.C, 0, s);
-    dbg_hash(sh5, pl.P, 1, y.C, y.C, 0, s);
-    PcnChain c{};
-    c.P = pl.P; c.N = pl.N;
-    c.X = x.p; c.xps = x.ps; c.xld = x.ld; c.xcs = x.cs;
-    c.Y = (hd && head_only) ? nullptr : y.p; c.yps = y.ps; c.yld = y.ld; c.ycs = y.cs;
-    c.W3 = pc.conv3.weight; c.b3 = pc.conv3.bias; c.W7 = pc.conv7.weight; c.b7 = pc.conv7.bias;
-    c.sc1 = sc1; c.sh1 = sh1; c.sc5 = sc5; c.sh5 = sh5; c.sPb = 128;
-    c.stats = y.st; c.st_ld = y.st_ld; c.st_off = y.st_off;
-    if (hd) {
-      c.head_w = hd->weight; c.head_bp = hd->bias; c.logits = h_logits; c.scores = h_scores; c.pos = h_pos;
-      c.head_only = head_only ? 1 : 0;
-    }
-    chk(launch_pcn_chain(c, s));
-    if (!hd) {
-      dbg_hash(y.p, pl.P, y.C, pl.N, y.ps, y.ld, s, y.cs);
-      dbg_hash(reinterpret_cast<const float*>(y.st + y.st_off), pl.P * TNn, 1, 2 * y.C, y.st_ld * 2, 0, s);
-      dbg_dump(y.st, (size_t)pl.P * TNn * y.st_ld * sizeof(float2), s);
-    }
-    return false;
   }
 
   // OAFilter (oanet.py:56-93), in place on xd; x_folded / next as for pointcn (conv3 fuses next's fold)

@@ -743,363 +743,6 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   }
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// PointCN chained (oanet.py:18-43 without the shortcut): the second of two passes over a PointCN's input x,
-//   y = W7 . relu(fold5(t)) + b7 + x,   t = W3 . relu(fold1(x)) + b3,
-// where fold5 (t's InstanceNorm + BatchNorm) comes from the statistics of a first, statistics-only pass of conv3
-// (pconv_kernel with a null output).  t never reaches HBM: per 32-point chunk 16 KB read + 16 KB written (+ the
-// residual, an L2 re-read of the chunk just loaded) instead of conv3's 16 + 16 and conv7's 16 + 16 + 16 KB.
-// One 512-thread workgroup per CU, two wave groups in a two-stage pipeline:
-//   * group A (waves 0-3, W3 rows 32w .. 32w + 31 as split A fragments): loads and splits chunk j + 1's x into the
-//     x image (as pconv_kernel), multiplies chunk j, adds b3, applies fold5 + ReLU to its accumulator, moves the
-//     values into B-fragment order with v_permlane32_swap (accumulator rows (q & 3) + 8 (q >> 2) + 4h -> k-step rows
-//     16 s + 8 h + i) and writes them, split, as k-steps 2w, 2w + 1 of the t image;
-//   * group B (waves 4-7, W7 rows): multiplies chunk j - 1 from the t image, then pconv_kernel's epilogue (bias,
-//     residual, statistics of y or the output head, stores).
-// One barrier per step.  t is the very fp32 value conv3's epilogue would have stored, split the same way, so y is
-// bit-identical to the unfused conv3 -> conv7 pair (tests/test_gpu_oanet.py).
-struct ChArgs {
-  const float* X; int64_t xps, xld, xcs;   // x (input and residual) [P][128][.]
-  float* Y; int64_t yps, yld, ycs;         // y (may equal x: in place)
-  const float* W3; const float* b3; const float* W7; const float* b7;   // [128][128]; biases nullable
-  const float* sc1; const float* sh1; const float* sc5; const float* sh5; int64_t sPb;   // folds [P][sPb]
-  float2* stats; int64_t st_ld; int st_off;   // y's statistics partials (HEAD = 0)
-  int N, nch, ngrp;
-  int64_t groups;
-  const float* hw; const float* hb; float* logits; float* scores; int32_t* pos;   // HEAD (oanet.py:163,174-178)
-};
-
-template <int HEAD>
-__global__ __launch_bounds__(512, 1) void pcn_chain_kernel(ChArgs a) {
-  constexpr int FRBT = 3 * 1024;   // one k-step's fragment set: 3 planes x 64 lanes x 16 B
-  constexpr int STATS = HEAD ? 0 : 1;
-  __shared__ __attribute__((aligned(16))) char xi[2][8 * FRBT];   // conv3 B images (group A)
-  __shared__ __attribute__((aligned(16))) char ti[2][8 * FRBT];   // conv7 B images: relu(fold5(t)), split
-  __shared__ __attribute__((aligned(16))) float ys[4][32 * YLD];  // group B: per-wave transpose scratch
-  __shared__ __attribute__((aligned(16))) float fold[2][4][PC];   // (sc1, sh1, sc5, sh5) by pair parity
-  __shared__ float sb3[PC], sb7[PC];
-  __shared__ float shw[HEAD ? PC : 1];
-  __shared__ __attribute__((aligned(16))) float hpart[HEAD ? 2 : 1][4][CH];
-
-  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = wv >> 2, w = wv & 3;
-  const int N = a.N, N4 = (N + 3) & ~3, nch = a.nch;
-  const int64_t G = a.groups;
-  const int64_t g0 = G * blockIdx.x / gridDim.x, g1 = G * (blockIdx.x + 1) / gridDim.x;
-  if (g0 >= g1) return;   // uniform
-  const int p0 = (int)(g0 / a.ngrp), p1 = (int)(g1 / a.ngrp);
-  const int64_t c0 = (int64_t)p0 * nch + GRP * (int)(g0 - (int64_t)p0 * a.ngrp);
-  const int64_t c1 = (int64_t)p1 * nch + min(GRP * (int)(g1 - (int64_t)p1 * a.ngrp), nch);
-  const int nloc = (int)(c1 - c0);
-
-  // weights -> split A fragments: row 32w + l32, k = 16q + 8h + 0..7 (group A: W3, group B: W7)
-  FragT<0> wf[8];
-  {
-    const float* wr = (grp ? a.W7 : a.W3) + (int64_t)(32 * w + l32) * PC + 8 * h;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4 u0 = *reinterpret_cast<const float4*>(wr + 16 * q);
-      const float4 u1 = *reinterpret_cast<const float4*>(wr + 16 * q + 4);
-      const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-      wf[q] = split8t<0>(v);
-    }
-  }
-  if (tid < PC) {
-    sb3[tid] = a.b3 ? a.b3[tid] : 0.f;
-    sb7[tid] = a.b7 ? a.b7[tid] : 0.f;
-    if (HEAD) shw[tid] = a.hw[tid];
-  }
-  struct Cur {
-    int p, kc, j;
-  };
-  auto adv = [&](Cur& c) {
-    if (c.j + 1 >= nloc) return;
-    ++c.j;
-    if (++c.kc == nch) { c.kc = 0; ++c.p; }
-  };
-  const Cur cstart{p0, (int)(c0 - (int64_t)p0 * nch), 0};
-  auto mfma = [&](const char* img, auto&& hook) {
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const char* im = img + lane * 16;
-    FragT<0> cur = ld_frag<0>(im, 1024);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      FragT<0> nxt;
-      if (ks < 7) nxt = ld_frag<0>(im + (ks + 1) * FRBT, 1024);
-      PC_FENCE();
-      acc = mma<0>(wf[ks], cur, acc);
-      hook(ks);
-      PC_FENCE();
-      if (ks < 7) cur = nxt;
-    }
-    return acc;
-  };
-  const int nsteps = nloc + 1;   // group A runs steps 0 .. nloc - 1, group B steps 1 .. nloc
-
-  if (grp == 0) {
-    // ---------------------------------------------------------------- group A: conv3 -> fold5 -> t image
-    auto stage_fold = [&](int p) {
-      if (tid < PC) {
-        fold[p & 1][0][tid] = a.sc1[(int64_t)p * a.sPb + tid];
-        fold[p & 1][1][tid] = a.sh1[(int64_t)p * a.sPb + tid];
-        fold[p & 1][2][tid] = a.sc5[(int64_t)p * a.sPb + tid];
-        fold[p & 1][3][tid] = a.sh5[(int64_t)p * a.sPb + tid];
-      }
-    };
-    const int xld4 = (int)a.xld * 4;
-    auto issue_x = [&](const Cur& c, float (&r)[16]) {   // rows 32w + 16t + 8h + i -> r[8t + i]
-      const int n = min(c.kc * CH + l32, N - 1);
-      const float* base = a.X + (int64_t)c.p * a.xps + (int64_t)(32 * w) * a.xld;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, 0x7fffffff, 0x00020000);
-      const int vo = 8 * h * xld4 + 4 * ((n >> 5) * (int)a.xcs + (n & 31));
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          r[8 * t + i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (16 * t + i) * xld4,
-                                                                                        PCONV_NTL));
-    };
-    auto split_half = [&](const Cur& c, const float (&r)[16], int slot, int t) {
-      const float* f = &fold[c.p & 1][0][32 * w + 16 * t + 8 * h];
-      const float4 sa = *reinterpret_cast<const float4*>(f), sb = *reinterpret_cast<const float4*>(f + 4);
-      const float4 ha = *reinterpret_cast<const float4*>(f + PC), hb = *reinterpret_cast<const float4*>(f + PC + 4);
-      const float s1[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
-      const float h1[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = fmaxf(fmaf(r[8 * t + i], s1[i], h1[i]), 0.f);
-      Frag fr;
-      split8(v, fr.h, fr.m, fr.l);
-      char* dst = xi[slot] + (2 * w + t) * FRBT + lane * 16;
-      *reinterpret_cast<bf16x8*>(dst) = fr.h;
-      *reinterpret_cast<bf16x8*>(dst + 1024) = fr.m;
-      *reinterpret_cast<bf16x8*>(dst + 2048) = fr.l;
-    };
-    // t of chunk c (accumulator acc) -> relu(fold5(t)) as k-steps 2w, 2w + 1 of t image slot
-    auto emit_t = [&](const Cur& c, const floatx16& acc, int slot) {
-      const float* f5 = &fold[c.p & 1][2][0];
-      float v[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = 32 * w + (q & 3) + 8 * (q >> 2) + 4 * h;
-        const float t = acc[q] + sb3[row];   // conv3's output value (its epilogue: 0 + (acc + bias))
-        v[q] = fmaxf(fmaf(t, f5[row], f5[PC + row]), 0.f);
-      }
-      // lanes 32-63 of rows (q & 3) + 4 <-> lanes 0-31 of rows 8 + (q & 3): each lane then holds k-step rows
-      // 16 s + 8h + 0..7 of its column in v[8s .. 8s + 7]
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[8 * s2 + i]),
-                                                          __float_as_uint(v[8 * s2 + 4 + i]), false, false);
-          v[8 * s2 + i] = __uint_as_float(r[0]);
-          v[8 * s2 + 4 + i] = __uint_as_float(r[1]);
-        }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        Frag fr;
-        split8(v + 8 * s2, fr.h, fr.m, fr.l);
-        char* dst = ti[slot] + (2 * w + s2) * FRBT + lane * 16;
-        *reinterpret_cast<bf16x8*>(dst) = fr.h;
-        *reinterpret_cast<bf16x8*>(dst + 1024) = fr.m;
-        *reinterpret_cast<bf16x8*>(dst + 2048) = fr.l;
-      }
-    };
-    float x0[16], x1[16], x2[16];   // chunk register sets: loads issued three steps ahead
-    Cur cc = cstart, cs = cstart, ci = cstart, cf = cstart;   // compute, split, issue, fold
-    stage_fold(cf.p);
-    adv(cf);
-    if (cf.p != cstart.p) stage_fold(cf.p);
-    issue_x(ci, x0);
-    adv(ci);
-    issue_x(ci, x1);
-    adv(ci);
-    issue_x(ci, x2);
-    adv(ci);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    split_half(cs, x0, 0, 0);
-    split_half(cs, x0, 0, 1);
-    adv(cs);
-    issue_x(ci, x0);
-    adv(ci);
-    {
-      const Cur prev = cf;
-      adv(cf);
-      if (cf.p != prev.p) stage_fold(cf.p);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    auto step = [&](int j, auto& xs) {
-      const floatx16 acc = mfma(xi[j & 1], [&](int ks) {
-        if ((ks & 1) && ks < 4) split_half(cs, xs, (j + 1) & 1, ks >> 1);
-        if (ks == 4) issue_x(ci, xs);
-      });
-      emit_t(cc, acc, j & 1);
-      adv(cc);
-      adv(cs);
-      adv(ci);
-      const Cur prev = cf;
-      adv(cf);
-      if (cf.p != prev.p) stage_fold(cf.p);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    int j = 0;
-    for (; j + 2 < nloc; j += 3) {
-      step(j, x1);
-      step(j + 1, x2);
-      step(j + 2, x0);
-    }
-    if (j < nloc) step(j, x1);
-    if (j + 1 < nloc) step(j + 1, x2);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // step nloc: group B's last chunk
-    (void)nsteps;
-  } else {
-    // ---------------------------------------------------------------- group B: conv7 + pconv's epilogue
-    const int erow = lane >> 3, ec0 = 4 * (lane & 7);
-    float* yb = ys[w];
-    // the residual of a chunk in registers, two sets used alternately by an unrolled loop (a loop-carried copy of
-    // registers with loads in flight would make every step wait for them, and for the stores issued before them)
-    float4 ra[4], rb[4];
-    auto load_r = [&](const Cur& c, float4 (&r)[4]) {
-      const int n = min(c.kc * CH + ec0, N4 - 4);
-      const float* src = a.X + (int64_t)c.p * a.xps + (int64_t)(32 * w + erow) * a.xld + (int64_t)(n >> 5) * a.xcs +
-                         (n & 31);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) r[q] = *reinterpret_cast<const float4*>(src + (int64_t)(8 * q) * a.xld);
-    };
-    int rn = 0;
-    float ls[4], lss[4];
-    auto epilogue = [&](const Cur& c, const floatx16& acc, const float4 (&rres)[4]) {
-      const int n0 = c.kc * CH;
-      float4 ev[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) ev[q] = rres[q];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) yb[((r & 3) + 8 * (r >> 2) + 4 * h) * YLD + l32] = acc[r];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(yb + (erow + 8 * q) * YLD + ec0);
-        const float bq = sb7[32 * w + erow + 8 * q];
-        ev[q].x += v.x + bq; ev[q].y += v.y + bq; ev[q].z += v.z + bq; ev[q].w += v.w + bq;
-      }
-      float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + (int64_t)c.kc * a.ycs + ec0;
-      const bool full = n0 + CH <= N;
-      if (HEAD != 2) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (full || n0 + ec0 < N4) {
-            if (PCONV_NTS) {
-              const u32x4 u = {__float_as_uint(ev[q].x), __float_as_uint(ev[q].y), __float_as_uint(ev[q].z),
-                               __float_as_uint(ev[q].w)};
-              __builtin_nontemporal_store(u, reinterpret_cast<u32x4*>(ydst + (int64_t)(8 * q) * a.yld));
-            } else {
-              *reinterpret_cast<float4*>(ydst + (int64_t)(8 * q) * a.yld) = ev[q];
-            }
-          }
-      }
-      if (HEAD) {
-        float hp[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float wq = shw[32 * w + erow + 8 * q];
-          hp[0] = fmaf(wq, ev[q].x, hp[0]); hp[1] = fmaf(wq, ev[q].y, hp[1]);
-          hp[2] = fmaf(wq, ev[q].z, hp[2]); hp[3] = fmaf(wq, ev[q].w, hp[3]);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          hp[e] += __shfl_xor(hp[e], 8, 64);
-          hp[e] += __shfl_xor(hp[e], 16, 64);
-          hp[e] += __shfl_xor(hp[e], 32, 64);
-        }
-        if (lane < 8) *reinterpret_cast<float4*>(&hpart[c.j & 1][w][ec0]) = make_float4(hp[0], hp[1], hp[2], hp[3]);
-      }
-      if (STATS) {
-        const int cnt = min(N - n0, CH);
-        const int nv = full ? 4 : min(max(N - n0 - ec0, 0), 4);
-        float sK[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sK[q] = sb7[32 * w + erow + 8 * q];
-        if (c.kc % GRP == 0) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) ls[q] = lss[q] = 0.f;
-          rn = 0;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float d0 = ev[q].x - sK[q], d1 = ev[q].y - sK[q], d2 = ev[q].z - sK[q], d3 = ev[q].w - sK[q];
-          if (!full) {
-            if (nv < 4) d3 = 0.f;
-            if (nv < 3) d2 = 0.f;
-            if (nv < 2) d1 = 0.f;
-            if (nv < 1) d0 = 0.f;
-          }
-          ls[q] += (d0 + d1) + (d2 + d3);
-          lss[q] = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, lss[q]))));
-        }
-        rn += cnt;
-        if ((c.kc % GRP) == GRP - 1 || c.kc == nch - 1) {
-          const float fn = (float)rn, rinv = __builtin_amdgcn_rcpf(fn);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float S = sum8(ls[q]), SS = sum8(lss[q]);
-            ls[q] = fmaf(fn, sK[q], S);
-            lss[q] = fmaxf(SS - S * S * rinv, 0.f);
-          }
-          if ((lane & 7) == 0) {
-            float2* st = a.stats + ((int64_t)c.p * a.ngrp + c.kc / GRP) * a.st_ld + a.st_off + 32 * w + erow;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) st[8 * q] = make_float2(ls[q], lss[q]);
-          }
-        }
-      }
-    };
-    auto head_finish = [&](const Cur& c) {   // wave w = 0 of the group: the logits of the chunk done one step ago
-      if (!HEAD || w != 0) return;
-      const int col = c.kc * CH + l32;
-      float lg = a.hb ? a.hb[0] : 0.f;
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww) lg += hpart[c.j & 1][ww][l32];
-      const float sc = fmaxf(tanhf(lg), 0.f);
-      const bool ok = lane < 32 && col < N;
-      if (ok) {
-        a.logits[(int64_t)c.p * N + col] = lg;
-        a.scores[(int64_t)c.p * N + col] = sc;
-      }
-      const int np = __popcll(__ballot(ok && sc > 0.f));
-      if (lane == 0 && np) atomicAdd(a.pos + c.p, np);
-    };
-    Cur cc = cstart, cr = cstart, ch = cstart;
-    load_r(cr, ra);
-    adv(cr);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // step 0: group A's first chunk
-    // step j: the next chunk's residual loads first (ahead of this step's stores), the MFMAs of chunk j - 1, its
-    // epilogue with the residual loaded one step ago
-    auto stepB = [&](int j, const float4 (&cur)[4], float4 (&nxt)[4]) {
-      load_r(cr, nxt);
-      adv(cr);
-      if (HEAD && j > 1) {
-        head_finish(ch);
-        adv(ch);
-      }
-      const floatx16 acc = mfma(ti[(j - 1) & 1], [&](int) {});
-      epilogue(cc, acc, cur);
-      adv(cc);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    for (int j = 1; j <= nloc; j += 2) {
-      stepB(j, ra, rb);
-      if (j + 1 <= nloc) stepB(j + 1, rb, ra);
-    }
-    if (HEAD) head_finish(ch);
-  }
-}
-
 }  // namespace
 
 // Dispatched by launch_gemm for the shapes it covers; the caller has checked the common contract.
@@ -1221,39 +864,6 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
 #undef MVR_PC16
 #undef MVR_PCL
   return MVR_EINVAL;
-}
-
-int launch_pcn_chain(const PcnChain& c, hipStream_t s) {
-  auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  auto lay_ok = [&](int64_t ld, int64_t cs) { return cs ? (ld == CH && cs % 4 == 0 && cs >= (int64_t)CH * PC) : ld >= round4(c.N); };
-  const int head = c.head_w ? (c.head_only ? 2 : 1) : 0;
-  if (c.P <= 0 || c.N <= CH || !c.X || !c.W3 || !c.W7 || !c.sc1 || !c.sh1 || !c.sc5 || !c.sh5 || c.sPb % 4) return MVR_EINVAL;
-  if (!al16(c.X) || !al16(c.W3) || !al16(c.W7) || !al16(c.sc1) || !al16(c.sh1) || !al16(c.sc5) || !al16(c.sh5) ||
-      c.xld % 4 || c.xps % 4 || !lay_ok(c.xld, c.xcs))
-    return MVR_EINVAL;
-  if (head != 2 && (!c.Y || !al16(c.Y) || c.yld % 4 || c.yps % 4 || !lay_ok(c.yld, c.ycs))) return MVR_EINVAL;
-  if (head ? (!c.logits || !c.scores || !c.pos) : (!c.stats || c.st_ld < PC + c.st_off)) return MVR_EINVAL;
-  if (c.Y && c.Y != c.X && ((c.Y < c.X + c.xps * c.P) && (c.X < c.Y + c.yps * c.P))) return MVR_EINVAL;   // disjoint or equal
-  ChArgs a{};
-  a.X = c.X; a.xps = c.xps; a.xld = c.xld; a.xcs = c.xcs ? c.xcs : CH;
-  a.Y = c.Y; a.yps = c.yps; a.yld = c.yld; a.ycs = c.ycs ? c.ycs : CH;
-  a.W3 = c.W3; a.b3 = c.b3; a.W7 = c.W7; a.b7 = c.b7;
-  a.sc1 = c.sc1; a.sh1 = c.sh1; a.sc5 = c.sc5; a.sh5 = c.sh5; a.sPb = c.sPb;
-  a.stats = c.stats; a.st_ld = c.st_ld; a.st_off = c.st_off;
-  a.N = c.N;
-  a.nch = (c.N + CH - 1) / CH;
-  a.ngrp = (a.nch + GRP - 1) / GRP;
-  a.groups = (int64_t)c.P * a.ngrp;
-  a.hw = c.head_w; a.hb = c.head_bp; a.logits = c.logits; a.scores = c.scores; a.pos = c.pos;
-  const int grid = (int)(a.groups < GPU_CUS ? a.groups : GPU_CUS);   // one persistent round, one workgroup per CU
-  // algorithmic work: two 128 x 128 convs per point; bytes: x read, y written (the residual is x again), weights
-  const double pts = (double)c.N * c.P;
-  ProfScope prof(PK_CONV_PTS, 2.0 * 2.0 * PC * PC * pts, 4.0 * (2.0 * PC * PC + PC * pts * (head == 2 ? 1 : 2)), s);
-  if (head == 0) hipLaunchKernelGGL(pcn_chain_kernel<0>, dim3(grid), dim3(512), 0, s, a);
-  else if (head == 1) hipLaunchKernelGGL(pcn_chain_kernel<1>, dim3(grid), dim3(512), 0, s, a);
-  else hipLaunchKernelGGL(pcn_chain_kernel<2>, dim3(grid), dim3(512), 0, s, a);
-  MVR_CHECK_LAUNCH();
-  return MVR_OK;
 }
 
 }  // namespace mvr

@@ -233,7 +233,7 @@ def prof_get(kind):
 MATH_KERNELS = "pconv_math,attn_math,spconv_math,gemm_f16,feat_nn"   # the kernels mvr_set_math(1) switches
 # mvr_debug_force paths (include/mvreg.h, csrc/knobs.hpp ForcePath)
 FORCE = {"feat_nn_online": 0, "generic_gemm": 1, "unfused_attn": 2, "no_conv1_fold": 3, "pool_nosplit": 4,
-         "unpool8": 5, "row_layout": 6, "no_chain": 7}
+         "unpool8": 5, "row_layout": 6}
 
 
 def math_state():

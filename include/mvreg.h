@@ -95,8 +95,7 @@ int mvr_ransac(const double* x1, const double* x2, int64_t x_pstride, const int3
  *   cover — 0 the feature NN's online softmax only, 1 point convs and OAFilter conv2 on the generic GEMM, 2 diff_pool
  *   / diff_unpool unfused (embedding GEMM + softmax + pooling GEMM), 3 the block's conv1 stored instead of folded
  *   into the first PointCN, 4 diff_pool without key splits, 5 the 8-wave diff_unpool at <= 512 clusters, 6 the
- *   OANet block's point activations row-major instead of chunk-major (bit-identical), 7 the PointCNs as a conv3 and a
- *   conv7 launch instead of a statistics-only conv3 pass + the chained kernel (bit-identical).  value 0 restores the
+ *   OANet block's point activations row-major instead of chunk-major (bit-identical).  value 0 restores the
  *   default.  Returns the previous value (MVR_EINVAL for an unknown path).
  * ---------------------------------------------------------------------- */
 int mvr_set_math(int mode);

@@ -427,40 +427,3 @@ def test_oanet_chunk_major_activations_bit_identical(gpu, npts, train, math):
             assert np.array_equal(u, v), (k, i, np.abs(u - v).max())
     u, v = a["latent features"].cpu().numpy(), b["latent features"].cpu().numpy()
     assert np.array_equal(u, v), np.abs(u - v).max()
-
-
-@pytest.mark.parametrize("npts,train,layout", [(2000, False, 0), (517, True, 0), (33, False, 1), (2000, True, 1)])
-def test_oanet_chained_pointcn_bit_identical(gpu, npts, train, layout):
-    """The PointCNs without a shortcut as a statistics-only conv3 pass + ONE chained launch (pconv.hip
-    pcn_chain_kernel: conv3 again, its fold + ReLU, conv7, residual, statistics / output head; conv3's output never
-    stored) vs the two-launch form (forced): bit-identical logits, scores, R, t, the returned latent activation and
-    every stage hash, in both point layouts, eval / train BatchNorm, ragged point counts (33 points: two chunks, one
-    of a single point)."""
-    import torch
-    from lib import _native as NV
-    from test_gpu_oanet import _oanet
-    from synth import synth_correspondences
-    xs, _, _ = synth_correspondences(5, npts, seed=37)
-    net = _oanet(128, 500, 13, gpu, train=train, which="full")
-    outs, hashes = [], []
-    L = NV.lib()
-    for no_chain in (0, 0, 1):   # (a first forward hashes never-written parts of shared statistics buffers)
-        buf = torch.zeros(4096, dtype=torch.int64, device=gpu)
-        L.mvr_debug_stage_hash(NV.ptr(buf), 4096)
-        try:
-            with NV.force("no_chain", no_chain), NV.force("row_layout", layout), torch.no_grad():
-                outs.append(net({"xs": torch.from_numpy(xs).unsqueeze(1)}))
-            torch.cuda.synchronize()
-        finally:
-            L.mvr_debug_stage_hash(None, 0)
-        hashes.append(buf.cpu().numpy())
-    a, b = outs[1:]
-    for k in ("logits", "scores", "rot_est", "trans_est"):
-        for i in range(2):
-            u, v = a[k][i].cpu().numpy(), b[k][i].cpu().numpy()
-            assert np.array_equal(u, v), (k, i, np.abs(u - v).max())
-    u, v = a["latent features"].cpu().numpy(), b["latent features"].cpu().numpy()
-    assert np.array_equal(u, v), np.abs(u - v).max()
-    assert np.count_nonzero(hashes[1]) > 50
-    bad = np.nonzero(hashes[1] != hashes[2])[0]
-    assert bad.size == 0, ("stages differ", bad.tolist(), np.count_nonzero(hashes[1]))
