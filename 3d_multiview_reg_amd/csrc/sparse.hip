@@ -280,6 +280,46 @@ __global__ void kernel_map_kernel(const int4* __restrict__ oc, int64_t Mo, HashV
   nbr[e] = (int32_t)hash_find(h, pack_key(c.x, qx, qy, qz), t);
 }
 
+// A 3^3 map of a set onto ITSELF (out set == the table's set, row o = table value o; FCGF's stride-1 convs at every
+// tensor stride) probes half the offsets: neighbour k of o is i exactly when neighbour 26 - k of i is o (offset 26 - k
+// is -offset k), so thread (o, k < 13) writes both entries and the centre is o itself.  Entries no probe reaches stay
+// -1 (the caller's fill).  Equal to kernel_map_kernel's map of the same table.
+__global__ void kernel_map_sym_kernel(const int4* __restrict__ oc, int64_t Mo, HashView h, int step,
+                                      int32_t* __restrict__ nbr) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= Mo * 14) return;
+  const int64_t o = e / 14;
+  const int k = (int)(e - o * 14);   // 0 .. 12 probed, 13 the centre
+  if (k == 13) {
+    nbr[o * 27 + 13] = (int32_t)o;
+    return;
+  }
+  const int t = h.hdr[0];
+  if (t < -1 || t > 15) return;   // not a table hash_build wrote: every entry stays -1
+  const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+  const int4 c = oc[o];
+  const int qx = c.y + dx * step, qy = c.z + dy * step, qz = c.w + dz * step;
+  if (t >= 0 && ((qx | qy | qz) & ((1 << t) - 1)) != 0) return;   // off the table's lattice: absent
+  const int64_t i = hash_find(h, pack_key(c.x, qx, qy, qz), t);
+  if (i < 0) return;
+  nbr[o * 27 + k] = (int32_t)i;
+  nbr[i * 27 + (26 - k)] = (int32_t)o;
+}
+
+// the transpose of a map: dst[i][k] = o exactly where src[o][k] = i (entries no source reaches stay -1, the caller's
+// fill).  A transposed stride-2 conv's map is the transpose of the strided conv's map between the same two sets:
+// out(i) - off_k s = out(o)  <=>  out(o) + off_k s = out(i).
+__global__ void kernel_map_transpose_kernel(const int32_t* __restrict__ src, int64_t Ms, int K, int32_t* __restrict__ dst,
+                                            int64_t Md) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= Ms * K) return;
+  const int32_t i = src[e];
+  if (i < 0 || i >= Md) return;
+  const int64_t o = e / K;
+  const int k = (int)(e - o * K);
+  dst[(int64_t)i * K + k] = (int32_t)o;
+}
+
 // ------------------------------------------------------------------ brick map
 // Coordinates grouped in 4x4x4 bricks: a hash (batch, x>>2, y>>2, z>>2) -> brick id and a pool
 // of 64 row indices per brick (-1 = empty cell).  A large stencil (FCGF conv1, 7^3) then costs
@@ -804,6 +844,33 @@ extern "C" int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const v
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)tot * 4.0, s);
   hipLaunchKernelGGL(kernel_map_kernel, dim3(nblk(tot)), dim3(256), 0, s, reinterpret_cast<const int4*>(out_coords),
                      Mout, h, ksize, step, transposed ? -1 : 1, nbr, row_order);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_kernel_map_sym(const int32_t* coords, int64_t M, const void* table, size_t table_bytes, int step,
+                                  int32_t* nbr, hipStream_t s) {
+  if (M < 0 || step <= 0) return MVR_EINVAL;
+  if (M == 0) return MVR_OK;
+  if (!coords || !table || !nbr) return MVR_EINVAL;
+  HashView h = hash_view(const_cast<void*>(table), table_bytes);
+  if (!h.cap) return MVR_EINVAL;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)M * 27 * 4.0, s);
+  if (hipMemsetAsync(nbr, 0xFF, sizeof(int32_t) * 27 * (size_t)M, s) != hipSuccess) return MVR_ELAUNCH;
+  hipLaunchKernelGGL(kernel_map_sym_kernel, dim3(nblk(M * 14)), dim3(256), 0, s, reinterpret_cast<const int4*>(coords), M,
+                     h, step, nbr);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
+}
+
+extern "C" int mvr_kernel_map_transpose(const int32_t* src, int64_t Ms, int K, int32_t* dst, int64_t Md, hipStream_t s) {
+  if (Ms < 0 || Md < 0 || K <= 0 || K > 343) return MVR_EINVAL;
+  if (Md == 0) return MVR_OK;
+  if (!dst || (Ms > 0 && !src)) return MVR_EINVAL;
+  ProfScope prof(PK_SPARSE_MISC, 0.0, (double)(Ms + Md) * K * 4.0, s);
+  if (hipMemsetAsync(dst, 0xFF, sizeof(int32_t) * (size_t)K * (size_t)Md, s) != hipSuccess) return MVR_ELAUNCH;
+  if (Ms > 0)
+    hipLaunchKernelGGL(kernel_map_transpose_kernel, dim3(nblk(Ms * K)), dim3(256), 0, s, src, Ms, K, dst, Md);
   MVR_CHECK_LAUNCH();
   return MVR_OK;
 }

@@ -110,6 +110,8 @@ _SIGS = {
     "mvr_hash_build_lattice": (c_int, [c_vp, c_i64, c_int, c_vp, c_size, c_vp]),
     "mvr_kernel_map": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp]),
     "mvr_kernel_map_x": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "mvr_kernel_map_sym": (c_int, [c_vp, c_i64, c_vp, c_size, c_int, c_vp, c_vp]),
+    "mvr_kernel_map_transpose": (c_int, [c_vp, c_i64, c_int, c_vp, c_i64, c_vp]),
     "mvr_kernel_map_order_bytes": (c_size, [c_i64]),
     "mvr_kernel_map_order": (c_int, [c_vp, c_vp, c_int, c_i64, c_int, c_vp, c_vp, c_size, c_vp]),
     "mvr_kernel_map_orders_bytes": (c_size, [c_i64]),

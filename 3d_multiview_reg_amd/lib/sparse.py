@@ -112,14 +112,25 @@ class CoordinateManager:
             else:
                 raise ValueError(kind)
             out_c = self.coords_at(out_s)
-            order = None
-            if ks == 3 and SPATIAL_MAPS:
-                self.spatial_orders()
-                order = self.spatial[out_s]
             K = ks ** 3
             nbr = torch.empty(out_c.shape[0], K, dtype=torch.int32, device=self.device)
-            N.check(N.lib().mvr_kernel_map_x(N.ptr(out_c), out_c.shape[0], N.ptr(tab), tab.numel(), ks, s, tr,
-                                             N.ptr(nbr), N.ptr(order), N.stream()), "mvr_kernel_map_x")
+            L = N.lib()
+            if ks == 3 and kind == "s1" and not SPATIAL_MAPS:
+                # a set onto itself: half the offsets probed, each hit writes its mirror entry too
+                N.check(L.mvr_kernel_map_sym(N.ptr(out_c), out_c.shape[0], N.ptr(tab), tab.numel(), s, N.ptr(nbr),
+                                             N.stream()), "mvr_kernel_map_sym")
+            elif ks == 3 and kind == "up" and not SPATIAL_MAPS:
+                # the transposed conv's map is the transpose of the strided conv's map between the same two sets
+                down = self.kernel_map("down", s, ks)
+                N.check(L.mvr_kernel_map_transpose(N.ptr(down), down.shape[0], K, N.ptr(nbr), out_c.shape[0],
+                                                   N.stream()), "mvr_kernel_map_transpose")
+            else:
+                order = None
+                if ks == 3 and SPATIAL_MAPS:
+                    self.spatial_orders()
+                    order = self.spatial[out_s]
+                N.check(L.mvr_kernel_map_x(N.ptr(out_c), out_c.shape[0], N.ptr(tab), tab.numel(), ks, s, tr,
+                                           N.ptr(nbr), N.ptr(order), N.stream()), "mvr_kernel_map_x")
             self.maps[key] = nbr
         return self.maps[key]
 

@@ -383,6 +383,15 @@ int mvr_kernel_map(const int32_t* out_coords, int64_t Mout, const void* in_table
  * neighbouring cells of the input table */
 int mvr_kernel_map_x(const int32_t* out_coords, int64_t Mout, const void* in_table, size_t in_table_bytes, int ksize,
                      int step, int transposed, int32_t* nbr, const int32_t* row_order, mvr_stream_t stream);
+/* 3^3 map of a set onto itself (out set == the table's set in row order: FCGF's stride-1 convs), equal to
+ * mvr_kernel_map(coords, M, table, ..., 3, step, 0, nbr): half the offsets are probed, each hit also writes its mirror
+ * entry (neighbour 26 - k of i is o when neighbour k of o is i), the centre is the row itself. */
+int mvr_kernel_map_sym(const int32_t* coords, int64_t M, const void* table, size_t table_bytes, int step, int32_t* nbr,
+                       mvr_stream_t stream);
+/* dst [Md][K] = the transpose of src [Ms][K]: dst[i][k] = o where src[o][k] = i, else -1.  The transposed stride-2
+ * conv's map between two sets (mvr_kernel_map(..., transposed = 1)) is the transpose of the strided conv's map between
+ * them (FCGF's up maps from its down maps). */
+int mvr_kernel_map_transpose(const int32_t* src, int64_t Ms, int K, int32_t* dst, int64_t Md, mvr_stream_t stream);
 /* Row order of a kernel map: output rows sorted by their active-offset mask (K <= 27), so that a
  * tile of consecutive rows shares its active offsets; with out_coords (int32 [Mout][4], the map's output
  * coordinates, multiples of step) rows of one mask are further ordered by fragment and Morton code of

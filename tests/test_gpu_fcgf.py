@@ -319,3 +319,54 @@ def test_empty_fragment_through_voxelize_and_orders(gpu, frags):
     for kind, s in FCGF_MAPS:
         assert z.kernel_map(kind, s).shape[0] == 0 and z.orders[(kind, s, 3)].numel() == 0
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("stride", [1, 2, 4])
+def test_symmetric_and_transposed_kernel_maps(gpu, stride):
+    """mvr_kernel_map_sym (a set onto itself: half the offsets probed, mirror entries written) equals mvr_kernel_map's
+    full probe over lattice and hashed tables (dense blocks whose buckets overflow, scattered voxels, two batches), and
+    mvr_kernel_map_transpose of the strided map fine -> coarse equals the transposed map coarse -> fine probed from
+    the coarse table (FCGF's up maps from its down maps)"""
+    import torch
+    from lib import _native as N
+    L = N.lib()
+    rng = np.random.default_rng(11 + stride)
+    pts = set()
+    for b in range(2):
+        g = np.arange(-5, 5) * stride
+        for x in g:
+            for y in g:
+                for z in g[:3]:
+                    pts.add((b, int(x), int(y), int(z)))
+        for _ in range(2500):
+            pts.add((b,) + tuple(int(v) * stride for v in rng.integers(-150, 150, 3)))
+    fine = np.array(sorted(pts, key=lambda p: rng.random()), dtype=np.int32)
+    coarse = np.unique(np.concatenate([fine[:, :1], (fine[:, 1:] // (2 * stride)) * (2 * stride)], 1), axis=0)
+    coarse = coarse[rng.permutation(len(coarse))].astype(np.int32)
+    Mf, Mc = len(fine), len(coarse)
+    fd, cd = torch.from_numpy(fine).to(gpu), torch.from_numpy(coarse).to(gpu)
+
+    def table(c, M, lat):
+        t = torch.empty(L.mvr_hash_table_bytes(M), dtype=torch.uint8, device=gpu)
+        if lat:
+            N.check(L.mvr_hash_build_lattice(N.ptr(c), M, lat, N.ptr(t), t.numel(), N.stream()), "lattice")
+        else:
+            N.check(L.mvr_hash_build(N.ptr(c), M, N.ptr(t), t.numel(), N.stream()), "hashed")
+        return t
+
+    def kmap(oc, Mo, t, tr):
+        nbr = torch.empty(Mo, 27, dtype=torch.int32, device=gpu)
+        N.check(L.mvr_kernel_map(N.ptr(oc), Mo, N.ptr(t), t.numel(), 3, stride, tr, N.ptr(nbr), N.stream()), "map")
+        return nbr
+    for lat in (stride, 0):
+        tf = table(fd, Mf, lat)
+        sym = torch.empty(Mf, 27, dtype=torch.int32, device=gpu)
+        N.check(L.mvr_kernel_map_sym(N.ptr(fd), Mf, N.ptr(tf), tf.numel(), stride, N.ptr(sym), N.stream()), "sym")
+        assert torch.equal(sym, kmap(fd, Mf, tf, 0)), lat
+    tf, tc = table(fd, Mf, stride), table(cd, Mc, 2 * stride)
+    down = kmap(cd, Mc, tf, 0)                     # coarse rows, neighbours in the fine set
+    up = kmap(fd, Mf, tc, 1)                       # fine rows, transposed neighbours in the coarse set
+    assert int((down >= 0).sum()) > Mc             # the test has teeth
+    upt = torch.empty(Mf, 27, dtype=torch.int32, device=gpu)
+    N.check(L.mvr_kernel_map_transpose(N.ptr(down), Mc, 27, N.ptr(upt), Mf, N.stream()), "transpose")
+    assert torch.equal(upt, up)

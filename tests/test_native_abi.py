@@ -59,6 +59,8 @@ _EMPTY_CALLS = {
     "mvr_radix_sort_pairs": lambda L: L.mvr_radix_sort_pairs(_Z, _Z, 0, 64, _Z, _Z, 0, _Z),
     "mvr_kernel_map_order": lambda L: L.mvr_kernel_map_order(_Z, _Z, 1, 0, 27, _Z, _Z, 0, _Z),
     "mvr_kernel_map_x": lambda L: L.mvr_kernel_map_x(_Z, 0, _Z, 0, 3, 1, 0, _Z, _Z, _Z),
+    "mvr_kernel_map_sym": lambda L: L.mvr_kernel_map_sym(_Z, 0, _Z, 0, 1, _Z, _Z),
+    "mvr_kernel_map_transpose": lambda L: L.mvr_kernel_map_transpose(_Z, 0, 27, _Z, 0, _Z),
     "mvr_kernel_map": lambda L: L.mvr_kernel_map(_Z, 0, _Z, 0, 3, 1, 1, _Z, _Z),
     "mvr_spconv_x": lambda L: L.mvr_spconv_x(_Z, 32, 32, _Z, _Z, 27, 0, _Z, 32, _Z, _bn0(), 1e-5, _Z, 0, 1, _Z, 32,
                                              _Z, _Z, _Z, _Z, _Z),
