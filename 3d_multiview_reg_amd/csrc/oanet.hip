@@ -87,11 +87,15 @@ __global__ void in_finalize_kernel(const float2* __restrict__ st, int64_t st_ld,
 // BatchNorm statistics per group of G consecutive pairs (the reference's forward batch: G = P, or one loader batch
 // of the benchmark each, mvr_oan_block_forward bn_train > 1): blockIdx.y = group
 __global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int G, int C, float eps_in, mvr_bn_p bn,
-                                   float* sc, float* sh, int64_t out_ld) {
+                                   float* __restrict__ sc, float* __restrict__ sh, int64_t out_ld) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const int p0 = blockIdx.y * G, p1 = min(P, p0 + G);
+  // (unrolled: the fp64 divisions and square roots of different pairs are independent — only the sum is a chain, kept
+  // in pair order — so eight of them overlap instead of each waiting for the last; a 1-2 workgroup launch per group
+  // spent ~16 us in those latencies)
   double bv = 0.0;
+#pragma unroll 8
   for (int p = p0; p < p1; ++p) {
     const double var = mv[(int64_t)p * C + c].y;
     bv += var / (var + eps_in);
@@ -99,6 +103,7 @@ __global__ void in_bn_train_kernel(const float2* __restrict__ mv, int P, int G, 
   bv /= (p1 - p0);
   const float g = bn.gamma ? bn.gamma[c] : 1.f, b = bn.gamma ? bn.beta[c] : 0.f;
   const float gs = g / sqrtf((float)bv + 1e-5f);
+#pragma unroll 8
   for (int p = p0; p < p1; ++p) {
     const float2 m = mv[(int64_t)p * C + c];
     const float rin = (float)(1.0 / sqrt((double)m.y + (double)eps_in));
