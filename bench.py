@@ -155,7 +155,7 @@ class SceneWorkload:
     name = "scene"
 
     def __init__(self, dev, rank, npts=5000, n_frag=30, voxel=0.025, samp="rand", shard="scenes", world=1,
-                 groups=None):
+                 groups=None, emulate=False):
         import lib.config
         from lib.sparse import fragment_views
         from synth import synth_scene_fragments
@@ -167,7 +167,7 @@ class SceneWorkload:
         self.model = lib.config.get_model(cfg)
         self.state = synth_module(self.model, seed=7)
         self.model = self.model.to(dev).eval()
-        self.shard, self.world, self.rank = shard, world, rank
+        self.shard, self.world, self.rank, self.emulate = shard, world, rank, emulate
         # scenes: every rank its own scene (weak scaling); pairs: ONE scene, its fragments and pairs split over the
         # ranks (strong scaling, north_star's pair-sharded batch)
         self.frags, self.poses = synth_scene_fragments(n_frag, seed=41 + (1000 * rank if shard == "scenes" else 0))
@@ -201,7 +201,10 @@ class SceneWorkload:
             cm.coords_at(s)
         d = {"pcd0": xyz_down, "sinput0_C": coords, "sinput0_F": torch.ones(coords.shape[0], 1, device=self.dev),
              "pts_list": torch.tensor(counts), "sinput0_coords_manager": cm}
-        if self.shard == "pairs":
+        if self.shard == "pairs" and self.emulate:   # rank 0 of `world`: every block sized like this rank's
+            mine = list(counts) + [counts[-1]] * (self.fper - len(counts))
+            d["pts_all"] = counts = (mine * self.world)[:self.n_frag]
+        elif self.shard == "pairs":
             import torch.distributed as dist
             mine = torch.full((self.fper,), -1, dtype=torch.int64)
             mine[:len(counts)] = torch.tensor(counts, dtype=torch.int64)
@@ -441,6 +444,19 @@ class SceneWorkload:
         return fl, by
 
 
+def emulate_collectives():
+    """--emulate-world: lib.distributed's collectives become local (rank 0 of N): an all-gather returns this rank's
+    block repeated N times (the same bytes land, from a device copy instead of xGMI), the guard's MAX all-reduce keeps
+    the local bit"""
+    from lib import distributed as D
+
+    def gather_rows(buf, world, pg=None):
+        return buf.repeat((world,) + (1,) * (buf.dim() - 1))
+
+    D.all_gather_rows = gather_rows
+    D.all_reduce_max = lambda t, pg=None: None
+
+
 def records_allgather(rec, world):
     import torch.distributed as dist
     from lib import distributed as D
@@ -626,6 +642,10 @@ def main():
                     help="scene workload at N > 1: scenes = one scene per rank (weak scaling); pairs = ONE scene per "
                     "step, its fragments (FCGF + sampling) and its pair batch (feature NN + OANet + Procrustes) split "
                     "over the ranks, with an RCCL all-gather of the samples and of the per-pair records (strong scaling)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="--shard pairs on ONE GPU: time rank 0 of an N-rank run (its fragments, its pair block; the "
+                         "all-gathers and the guard all-reduce replaced by local copies of the same sizes) -- the "
+                         "per-rank step of the N-GPU strong-scaling split, whose aggregate rate the line reports")
     ap.add_argument("--prof-seq", default=None, help="write the per-launch kernel-class sequence of the timed "
                     "steps (JSON) for PMC attribution (tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -666,13 +686,19 @@ def main():
     from lib import _native
     _native.lib()
     math_info = _native.set_math(args.math)
+    emulate = args.emulate_world > 1
+    if emulate:
+        if world > 1 or args.shard != "pairs":
+            raise SystemExit("--emulate-world runs one process with --shard pairs")
+        emulate_collectives()
+        world = args.emulate_world
     if args.workload == "scene":
-        if args.shard == "pairs" and not use_pg:
+        if args.shard == "pairs" and not use_pg and not emulate:
             raise SystemExit("--shard pairs needs a process group (torchrun, or MVR_BENCH_PG=1 at one rank)")
         if args.shard == "pairs" and world > args.frags:
             raise SystemExit("--shard pairs: at most one rank per fragment (%d)" % args.frags)
         wl = SceneWorkload(dev, rank, npts=args.npts, n_frag=args.frags, samp=args.samp, shard=args.shard,
-                           world=world, groups=groups)
+                           world=world, groups=groups or (None, None, None), emulate=emulate)
     else:
         wl = PrecomputedWorkload(dev, rank, args.pairs, args.npts, shard=args.shard, world=world)
     pipelined = args.workload == "scene" and not args.no_pipeline
@@ -803,6 +829,8 @@ def main():
             "config": dict(wl.config(), math=args.math,
                            oanet_point_layout={1: "chunk-major", 0: "row-major"}.get(
                                _native.lib().mvr_oan_last_layout(), "none"),
+                           emulated=("rank 0 of %d on ONE GPU: collectives replaced by local copies of the same "
+                                     "sizes; value = the whole job's pairs / rank 0's step" % world) if emulate else None,
                            spconv_presplit_planes=bool(_fcgf_mod().PRESPLIT), spatial_map_order=bool(
                                _sparse_mod().SPATIAL_MAPS), library=_native.source_hash(),
                            parallelism=(("pairs%d (one scene per step: fragments and pair batch sharded over %d "
