@@ -167,9 +167,11 @@ __device__ __forceinline__ int floor_div(int a, int s) { return (a >= 0) ? a / s
 // by the float64 voxel size, floored (scripts/utils.py:108-109, scripts/pairwise_demo.py:75-79); batch index from
 // the fragment offsets.  T = double: the caller's float64 points as they are (scripts/utils.py extract_features
 // floors Open3D's float64 array), no float32 rounding first.
+// vcoords may be null (the partitioned path decodes the coordinates from the keys); range_bad (optional) is set when
+// a coordinate falls outside the key's 17-bit field (keys would alias: the caller falls back to the global path).
 template <typename T>
 __global__ void vox_keys_kernel(const T* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
-                                double voxel, uint64_t* keys, int4* vcoords) {
+                                double voxel, uint64_t* keys, int4* vcoords, int* range_bad = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int lo = 0, hi = B - 1;
@@ -181,7 +183,10 @@ __global__ void vox_keys_kernel(const T* __restrict__ xyz, const int64_t* __rest
   const int y = (int)floor((double)xyz[3 * i + 1] / voxel);
   const int z = (int)floor((double)xyz[3 * i + 2] / voxel);
   keys[i] = pack_key(lo, x, y, z);
-  vcoords[i] = make_int4(lo, x, y, z);
+  if (vcoords) vcoords[i] = make_int4(lo, x, y, z);
+  if (range_bad && ((uint32_t)(x + KEY_BIAS) > KEY_MASK || (uint32_t)(y + KEY_BIAS) > KEY_MASK ||
+                    (uint32_t)(z + KEY_BIAS) > KEY_MASK))
+    atomicOr(range_bad, 1);
 }
 
 // coarse keys of a level: (b, floor(c/s)*s)
@@ -222,6 +227,144 @@ __global__ void compact_kernel(const int32_t* __restrict__ flags, const int32_t*
     coords_out[p] = cc[i];
     if (sel_out) sel_out[p] = i;
   }
+}
+
+// the same with the coordinates decoded from the packed keys (exact for in-range coordinates: vox_keys_kernel
+// flags the others)
+__global__ void compact_keys_kernel(const int32_t* __restrict__ flags, const int32_t* __restrict__ pos, int64_t n,
+                                    const uint64_t* __restrict__ keys, int4* coords_out, int64_t* sel_out,
+                                    int64_t* total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (total && i == n - 1) *total = (int64_t)pos[i] + flags[i];
+  if (i < n && flags[i]) {
+    const int p = pos[i];
+    const uint64_t k = keys[i];
+    coords_out[p] = make_int4((int)(k >> 51), (int)((k >> 34) & KEY_MASK) - KEY_BIAS,
+                              (int)((k >> 17) & KEY_MASK) - KEY_BIAS, (int)(k & KEY_MASK) - KEY_BIAS);
+    if (sel_out) sel_out[p] = i;
+  }
+}
+
+// Partitioned first occurrences of raw fragments (mvr_voxelize_hint).  Workgroup (fragment b, bucket q) scans the
+// fragment's keys, keeps the ones whose bucket hash is q in an LDS hash table (key -> smallest source row, LDS CAS +
+// min), then flags each kept key's smallest row: the global table's memory-side atomics and its clear / slot passes
+// are gone, and the ~12 raw points per voxel meet in LDS.  The P buckets of a fragment run on one XCD (dispatch is
+// round robin over the 8 XCDs: workgroups g, g + 8, ... share one), so its keys come from HBM once and from that
+// XCD's L2 P - 1 times.  A key that finds no slot within VP_MAXP probes (a fragment with more voxels than the hint
+// sized the buckets for) sets *overflow and the caller re-runs with the global table.  Same flags as insert_min +
+// slot_flag_kernel: the smallest row of each distinct key.
+#ifndef VP_LGTS
+#define VP_LGTS 13   // LDS slots per workgroup 2^13 (64 KB of keys, 32 KB of rows)
+#endif
+#ifndef VP_NT
+#define VP_NT 1024
+#endif
+#ifndef VP_UU
+#define VP_UU 8
+#endif
+#ifndef VP_MODE
+#define VP_MODE 0    // experiments: 1 scan + bucket test only (no inserts; results invalid)
+#endif
+constexpr int VP_TS = 1 << VP_LGTS;
+constexpr int VP_THREADS = VP_NT;
+constexpr int VP_MAXP = 64;
+constexpr int VP_U = VP_UU;      // keys per thread in flight
+constexpr int VP_Q = 128;        // per-wave member queue (entries)
+__device__ __forceinline__ uint32_t vp_bucket(uint64_t key, int lgP) {   // Fibonacci hash of the folded key
+  const uint32_t f = (uint32_t)key ^ (uint32_t)(key >> 32);
+  return lgP ? (f * 0x9E3779B1u) >> (32 - lgP) : 0u;
+}
+__global__ __launch_bounds__(VP_THREADS) void vox_part_kernel(const uint64_t* __restrict__ keys,
+                                                              const int64_t* __restrict__ off, int B, int lgP,
+                                                              int32_t* flags, int* overflow) {
+  __shared__ unsigned long long sk[VP_TS];
+  __shared__ int sv[VP_TS];
+  __shared__ int sovf;
+  __shared__ unsigned long long vq_key[VP_THREADS / 64][VP_Q];   // per-wave queues of member keys and their rows
+  __shared__ int vq_row[VP_THREADS / 64][VP_Q];
+  const int tid = threadIdx.x;
+  const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
+  const int b = xcd + 8 * (r >> lgP), q = r & ((1 << lgP) - 1);
+  if (b >= B) return;   // uniform
+  for (int s = tid; s < VP_TS; s += VP_THREADS) {
+    sk[s] = EMPTY_KEY;
+    sv[s] = 0x7fffffff;
+  }
+  if (tid == 0) sovf = 0;
+  __syncthreads();
+  const int64_t i1 = off[b + 1];
+  // VP_U keys per thread in flight, the next batch loaded while this one is inserted (the LDS round trips of the
+  // inserts would otherwise leave each wave one memory latency per batch)
+  const int64_t ib = off[b] + tid, ilast = i1 - 1;
+  constexpr int64_t VB = (int64_t)VP_U * VP_THREADS;   // rows per batch
+  uint64_t ka[VP_U], kb[VP_U];
+  auto load = [&](int64_t i0, uint64_t (&k)[VP_U]) {   // unconditional (clamped) loads: exact vmcnt waits
+#pragma unroll
+    for (int u = 0; u < VP_U; ++u) k[u] = keys[min(i0 + (int64_t)u * VP_THREADS, ilast)];
+  };
+  // Members (keys of this bucket, ~1 in P) go to a per-wave LDS queue, compacted by ballot; the queue is inserted 64
+  // entries per pass when the next key position could overflow it, so a wave runs ~1 insert pass per 64 members
+  // instead of one pass per key position with a few member lanes (the LDS atomics' latency is paid per pass):
+  // 82 us per scene at 30 fragments x 250 k points (96 with a plain read before each CAS), against 156 for the
+  // uncompacted loop and 520 for the global table's memory-side atomics (tools/vox_ab.sh).
+  const int lane = tid & 63, wv = tid >> 6;
+  unsigned long long* qk = vq_key[wv];
+  int* qr = vq_row[wv];
+  int qn = 0;   // wave-uniform queue fill
+  auto insert1 = [&](uint64_t key, int row) {
+    uint32_t s = (uint32_t)mix64(key) & (VP_TS - 1);
+    for (int p = 0; p < VP_MAXP; ++p) {   // in LDS the CAS itself is the probe (a plain read first measured slower)
+      const unsigned long long cur = atomicCAS(&sk[s], (unsigned long long)EMPTY_KEY, (unsigned long long)key);
+      if (cur == EMPTY_KEY || cur == key) {
+        atomicMin(&sv[s], row);
+        return;
+      }
+      s = (s + 1) & (VP_TS - 1);
+    }
+    sovf = 1;
+  };
+  auto flush = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the queue writes of every lane of the wave
+    if (VP_MODE != 1)
+      for (int e = lane; e < qn; e += 64) insert1(qk[e], qr[e]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // queue reads done before it is refilled
+    qn = 0;
+  };
+  auto enqueue = [&](int64_t i0, const uint64_t (&k)[VP_U]) {
+#pragma unroll
+    for (int u = 0; u < VP_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * VP_THREADS;
+      const bool m = i <= ilast && vp_bucket(k[u], lgP) == (uint32_t)q;
+      const uint64_t bal = __ballot(m);
+      const int cnt = __popcll(bal);
+      if (qn + cnt > VP_Q) flush();
+      if (m) {
+        const int pos = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+        qk[pos] = k[u];
+        qr[pos] = (int)i;
+      }
+      qn += cnt;
+    }
+  };
+  // batches in wave-uniform steps (every lane of a wave runs the same iterations: the ballots need them all; rows past
+  // the fragment are masked)
+  const int64_t wb = off[b] + (tid & ~63);   // the wave's first row
+  if (wb <= ilast) {
+    load(ib, ka);
+    for (int64_t w0 = wb; w0 <= ilast; w0 += 2 * VB) {
+      const int64_t i0 = w0 + lane;
+      load(i0 + VB, kb);
+      enqueue(i0, ka);
+      if (w0 + VB > ilast) break;
+      load(i0 + 2 * VB, ka);
+      enqueue(i0 + VB, kb);
+    }
+    flush();
+  }
+  __syncthreads();
+  for (int s = tid; s < VP_TS; s += VP_THREADS)
+    if (sk[s] != EMPTY_KEY) flags[sv[s]] = 1;
+  if (tid == 0 && sovf) atomicOr(overflow, 1);
 }
 
 // per-batch row counts of the compacted set: a block-private LDS histogram over a contiguous run of
@@ -789,10 +932,25 @@ extern "C" int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int 
   if (n == 0) return MVR_OK;
   ProfScope prof(PK_SPARSE_MISC, 0.0, (double)n * 40.0, s);
   DedupWs d = dedup_ws(ws, n, keys);
+  int* overflow = reinterpret_cast<int*>(counts_out + 1 + B);
+  // buckets per fragment: the mean fragment's hinted voxels over half an LDS table each
+  const int64_t per = (keys + B - 1) / B;
+  int lgP = 0;
+  while (lgP < 10 && ((int64_t)VP_TS / 2 << lgP) < per) ++lgP;
   hipLaunchKernelGGL(vox_keys_kernel<float>, dim3(nblk(n)), dim3(256), 0, s, xyz, frag_off, B, n, voxel,
-                     d.keys, d.cc);
-  return dedup_run(d, n, reinterpret_cast<int4*>(coords_out), sel_out, counts_out, B, s,
-                   reinterpret_cast<int*>(counts_out + 1 + B));
+                     d.keys, (int4*)nullptr, overflow);
+  if (hipMemsetAsync(d.flags, 0, sizeof(int32_t) * (size_t)n, s) != hipSuccess) return MVR_ELAUNCH;
+  const unsigned grid = 8u * (unsigned)((B + 7) / 8) << lgP;
+  hipLaunchKernelGGL(vox_part_kernel, dim3(grid), dim3(VP_THREADS), 0, s, d.keys, frag_off, B, lgP, d.flags, overflow);
+  const int rc = excl_scan_i32(d.flags, d.pos, n, d.bsum, dedup_scan_bytes(n), s);   // radix.hip
+  if (rc != MVR_OK) return rc;
+  hipLaunchKernelGGL(compact_keys_kernel, dim3(nblk(n)), dim3(256), 0, s, d.flags, d.pos, n, d.keys,
+                     reinterpret_cast<int4*>(coords_out), sel_out, counts_out);
+  const int cb = (int)std::min<int64_t>(nblk(n), 512);
+  hipLaunchKernelGGL(batch_count_kernel, dim3(cb), dim3(256), sizeof(int) * B, s, reinterpret_cast<int4*>(coords_out),
+                     B, counts_out);
+  MVR_CHECK_LAUNCH();
+  return MVR_OK;
 }
 
 extern "C" size_t mvr_coords_downsample_workspace_bytes(int64_t M) { return dedup_ws_bytes(M); }

@@ -356,9 +356,11 @@ int mvr_voxelize(const float* xyz, const int64_t* frag_off, int B, int64_t n, do
 int mvr_voxelize_f64(const double* xyz, const int64_t* frag_off, int B, int64_t n, double voxel, void* workspace,
                      size_t workspace_bytes, int32_t* coords_out, int64_t* sel_out, int64_t* counts_out,
                      mvr_stream_t stream);
-/* mvr_voxelize with the dedup hash table sized for distinct_hint voxels instead of n raw points (the raw
- * cloud holds ~12 points per voxel); inserts probe at most 64 slots and a key that finds none sets
- * counts_out[B + 1] (counts_out has B + 2 entries): the caller then re-runs mvr_voxelize. */
+/* mvr_voxelize for a hinted voxel count (distinct_hint: the expected voxels of the whole batch).  Each fragment's
+ * keys are split into hash buckets sized so that the mean fragment's share of the hint fills half of a workgroup's
+ * LDS table; a bucket with more voxels than its table takes, or a coordinate outside the keys' 17-bit range, sets
+ * counts_out[B + 1] (counts_out has B + 2 entries): the caller then re-runs mvr_voxelize.  Otherwise the same
+ * outputs as mvr_voxelize. */
 size_t mvr_voxelize_hint_workspace_bytes(int64_t n, int64_t distinct_hint);
 int mvr_voxelize_hint(const float* xyz, const int64_t* frag_off, int B, int64_t n, double voxel,
                       int64_t distinct_hint, void* ws, size_t ws_bytes, int32_t* coords_out, int64_t* sel_out,

@@ -73,6 +73,49 @@ def test_voxelize_hint_sized_table_matches_oracle(gpu, frags, hint):
     np.testing.assert_array_equal(sel2.cpu().numpy(), osel)
 
 
+def test_voxelize_partitioned_buckets(gpu):
+    """mvr_voxelize_hint's partitioned dedup (workgroup = fragment x hash bucket, LDS table, the buckets of a fragment
+    on one XCD): 11 fragments of unequal size (fragments past the first 8 take the second round of XCD slots) at
+    hints giving 1, 2, 8 and 64 buckets per fragment; a hint too small for one LDS table and a coordinate outside the
+    keys' 17-bit range both report overflow (counts_out[B + 1]) rather than wrong voxels"""
+    import torch
+    from lib import _native as N
+    from lib import sparse
+    from oracle.fcgf import voxelize as ovox
+    fr, _ = synth_scene_fragments(11, seed=9, n_pts=30000)
+    fr = [f[: 30000 - 2000 * i] for i, f in enumerate(fr)]
+    oc, osel, ocnt = ovox(fr, 0.025)
+    M = len(oc)
+    for h in (M // 11, 2 * M, 8 * 4096 * 11, 64 * 4096 * 11):
+        sparse._VOX_HINT.clear()
+        c, sel, counts, _ = sparse.voxelize(fr, 0.025, gpu, distinct_hint=h)
+        assert counts == list(ocnt), h
+        np.testing.assert_array_equal(c.cpu().numpy(), oc)
+        np.testing.assert_array_equal(sel.cpu().numpy(), osel)
+
+    L = N.lib()
+
+    def hint_call(pts, hint):
+        xyz = torch.from_numpy(np.concatenate(pts).astype(np.float32)).to(gpu)
+        off = torch.tensor(np.concatenate([[0], np.cumsum([len(p) for p in pts])]), dtype=torch.int64, device=gpu)
+        n, B = xyz.shape[0], len(pts)
+        ws = torch.empty(L.mvr_voxelize_hint_workspace_bytes(n, hint), dtype=torch.uint8, device=gpu)
+        coords = torch.empty(n, 4, dtype=torch.int32, device=gpu)
+        sel = torch.empty(n, dtype=torch.int64, device=gpu)
+        cnt = torch.empty(2 + B, dtype=torch.int64, device=gpu)
+        N.check(L.mvr_voxelize_hint(N.ptr(xyz), N.ptr(off), B, n, 0.025, hint, N.ptr(ws), ws.numel(), N.ptr(coords),
+                                    N.ptr(sel), N.ptr(cnt), N.stream()), "mvr_voxelize_hint")
+        return cnt.cpu().numpy()
+
+    big = synth_scene_fragments(1, seed=2, n_pts=250000)[0][0]   # ~20 k voxels: more than one 8192-slot table
+    assert hint_call([big], 1000)[2] != 0
+    far = fr[0].copy()
+    far[7] = (2000.0, 0.0, 0.0)                                   # 80 000 voxels from the origin
+    cnt = hint_call([far], 10 ** 5)
+    assert cnt[2] != 0
+    assert hint_call([fr[0]], 10 ** 5)[2] == 0
+
+
 def test_strided_sets_and_kernel_maps_match_oracle(gpu, frags):
     """every level's coordinate set and the 3^3 kernel maps equal the oracle's"""
     from lib.sparse import voxelize, CoordinateManager
