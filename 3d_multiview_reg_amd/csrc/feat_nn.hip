@@ -21,6 +21,7 @@
 // fragments (L2/MALL-resident across the pairs that share them).
 #include "common.hpp"
 #include "knobs.hpp"
+#include "mfma_bf16.hpp"
 #include "prof.hpp"
 
 namespace mvr {
@@ -114,11 +115,11 @@ __device__ __forceinline__ void nn_split8(const float4& a, const float4& b, u32x
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const unsigned hp = nn_cvt_pk(x[i]);
-    const f32x2 r = x[i] - nn_unpack(hp);
+    const f32x2 r = bx::sub2(x[i], nn_unpack(hp));
     const unsigned mp = nn_cvt_pk(r);
     H[i] = hp;
     Mm[i] = mp;
-    L[i] = nn_cvt_pk(r - nn_unpack(mp));
+    L[i] = nn_cvt_pk(bx::sub2(r, nn_unpack(mp)));
   }
 }
 // 8 fp32 -> two fp16x8 terms of 2^8 x (x 2^8 = h + l to 2^-22 relative, 2^-25 absolute), as u32x4; the

@@ -190,11 +190,11 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, u32x4& 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const unsigned hp = cvt_pk_bf16(x[i]);
-    const f32x2 r = x[i] - unpack_bf16(hp);
+    const f32x2 r = bx::sub2(x[i], unpack_bf16(hp));
     const unsigned mp = cvt_pk_bf16(r);
     H[i] = hp;
     Mm[i] = mp;
-    L[i] = cvt_pk_bf16(r - unpack_bf16(mp));
+    L[i] = cvt_pk_bf16(bx::sub2(r, unpack_bf16(mp)));
   }
 }
 __device__ __forceinline__ void split8(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
