@@ -46,6 +46,26 @@ namespace mvr {
 #define PCONV_NTL 2   // cache-policy bits of the activation buffer loads: nt (streamed once; -3 % per step's point convs)
 #endif
 
+#ifndef PCONV_TRACE
+#define PCONV_TRACE 0   // 1: per-phase cycle totals per wave (s_memtime) of the KS = 8 kernels, tools only (mvr_pconv_trace)
+#endif
+#if PCONV_TRACE
+__device__ unsigned long long g_pconv_trace[8];   // 0 MFMAs (+ splits, load issue), 1 epilogue, 2 step bookkeeping,
+                                                  // 3 step barrier, 4 prologue, 5 tail
+#define PCSTAMP(slot)                                                  \
+  do {                                                                 \
+    unsigned long long t_;                                             \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_));  \
+    __builtin_amdgcn_sched_barrier(0);                                 \
+    ptr_[pprev_] += t_ - plast_;                                       \
+    plast_ = t_;                                                       \
+    pprev_ = (slot);                                                   \
+  } while (0)
+#else
+#define PCSTAMP(slot) do {} while (0)
+#endif
+
 #ifndef PCONV_GRID
 #define PCONV_GRID 1   // workgroups per resident slot (1: one persistent round; >1 / <0: the round-4 grid experiments)
 #endif
@@ -252,6 +272,10 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   __shared__ __attribute__((aligned(16))) float4 xch[KW == 2 ? 2 : 1][KW == 2 ? 4 : 1][KW == 2 ? 4 : 1][KW == 2 ? 64 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+#if PCONV_TRACE
+  unsigned long long ptr_[8] = {0, 0, 0, 0, 0, 0, 0, 0}, plast_ = __builtin_amdgcn_s_memtime();
+  int pprev_ = 4;
+#endif
 #if PCONV_POISON   // debugging: NaN in every LDS array before use (finds reads of data never written)
   {
     auto poison = [&](void* p, size_t bytes) {
@@ -665,6 +689,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
   Cur cp = cstart;     // KW = 2: chunk whose epilogue is pending (lower half), one step behind
   floatx16 accp;       // ... and its lower-half accumulator
   auto step = [&](int j, auto& xs) {
+    PCSTAMP(0);
     if (HEAD && j > 0) {
       head_finish(ch);
       adv(ch);
@@ -673,6 +698,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       if ((ks & 1) && ks < 2 * NT) split_half(cs, xs, (j + 1) & 1, ks >> 1);
       if (ks == 2 * NT) issue_x(ci, xs);
     });
+    PCSTAMP(1);
     if constexpr (KW == 1) {
       epilogue(cc, acc);
     } else if (kh) {   // upper half: publish the partial sums (read by the lower half after the step barrier)
@@ -690,6 +716,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       }
       accp = acc;
     }
+    PCSTAMP(2);
     adv(cc);
     adv(cs);
     adv(ci);
@@ -698,6 +725,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     const Cur prev = cf;
     adv(cf);
     if (cf.p != prev.p) stage_fold(cf.p);
+    PCSTAMP(3);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
   int j = 0;
@@ -716,6 +744,7 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
     if (j < nloc) step(j, x1);
   }
+  PCSTAMP(5);
   if (HEAD) head_finish(ch);   // the last chunk (published by the last step's barrier)
   if constexpr (KW == 2) {
     if (!kh) {   // the last chunk's epilogue (its upper-half partials: published by the last step barrier)
@@ -729,6 +758,11 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
   }
   if (H && __any(xbad || (xmx > 0.f && xmx < 0.125f)) && lane == 0) atomicExch(a.range, a.epoch);
+#if PCONV_TRACE
+  PCSTAMP(5);
+  if (lane == 0 && KS == 8)
+    for (int q_ = 0; q_ < 8; ++q_) atomicAdd(&g_pconv_trace[q_], ptr_[q_]);
+#endif
   if constexpr (STATS && !H) {
     // Fused finalize (a.fcnt): publish this workgroup's statistics partials (every wave drains its stores, one
     // agent-scope release), add its tile count to each of its pairs' arrival counters; the workgroup completing
@@ -868,3 +902,14 @@ int launch_pconv(const GemmArgs& g, hipStream_t s) {
 
 }  // namespace mvr
 
+#if PCONV_TRACE
+// tools only (library built with -DPCONV_TRACE=1): the phase totals of every KS = 8 point-conv wave since the last reset
+extern "C" int mvr_pconv_trace(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mvr::g_pconv_trace), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mvr::g_pconv_trace), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

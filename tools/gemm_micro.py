@@ -27,6 +27,7 @@ CASES = {
 
 
 TRACE = False
+PTRACE = False
 PGRID = 1
 
 
@@ -85,6 +86,18 @@ def run(name, iters, math, pconv=1):
     by = 4.0 * P * (Kk * Nn + M * Nn * (2 if res else 1))
     print("P%-4d %-16s m%d%s %8.3f ms  %7.1f TF/s  %7.0f GB/s" % (P, name, math, " pconv" if pconv and M == C and Kk in (C, 2 * C) else "",
                                                           ms, fl / ms / 1e9, by / ms / 1e6), flush=True)
+    if PTRACE:
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        L.mvr_pconv_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.mvr_pconv_trace(buf, 1)
+        go()
+        torch.cuda.synchronize()
+        L.mvr_pconv_trace(buf, 1)
+        tot = sum(buf)
+        names = ["mfma+split", "epilogue", "bookkeeping", "step barrier", "prologue", "tail", "-", "-"]
+        print("   pconv phase shares (wave-cycles, one launch): " +
+              ", ".join("%s %.1f%%" % (names[q], 100.0 * buf[q] / max(tot, 1)) for q in range(6)), flush=True)
     if TRACE:
         import ctypes
         buf = (ctypes.c_ulonglong * 8)()
@@ -125,12 +138,14 @@ if __name__ == "__main__":
     ap.add_argument("--only", default=None)
     ap.add_argument("--math", default="01")
     ap.add_argument("--trace", action="store_true", help="library built with -DGEMM_TRACE=1 (MVR_LIB)")
+    ap.add_argument("--ptrace", action="store_true", help="library built with -DPCONV_TRACE=1 (MVR_LIB): point-conv phases")
     ap.add_argument("--pairs", type=int, default=P, help="pair batch (small batches stay in the Infinity Cache)")
     ap.add_argument("--pconv-grid", type=int, default=1, help="mvr_set_pconv_grid")
     a = ap.parse_args()
     P = a.pairs
     PGRID = a.pconv_grid
     TRACE = a.trace
+    PTRACE = a.ptrace
     if TRACE:
         import ctypes
         NV.lib().mvr_gemm_trace.argtypes = [ctypes.c_void_p, ctypes.c_int]
