@@ -169,15 +169,23 @@ __device__ __forceinline__ int floor_div(int a, int s) { return (a >= 0) ? a / s
 // floors Open3D's float64 array), no float32 rounding first.
 // vcoords may be null (the partitioned path decodes the coordinates from the keys); range_bad (optional) is set when
 // a coordinate falls outside the key's 17-bit field (keys would alias: the caller falls back to the global path).
+// The fragment offsets are staged in LDS first (B <= VK_MAXB; more: read from memory): the binary search's dependent
+// steps are then LDS round trips instead of memory ones.
+constexpr int VK_MAXB = 1024;
 template <typename T>
 __global__ void vox_keys_kernel(const T* __restrict__ xyz, const int64_t* __restrict__ off, int B, int64_t n,
                                 double voxel, uint64_t* keys, int4* vcoords, int* range_bad = nullptr) {
+  __shared__ int64_t soff[VK_MAXB];
+  const bool lds = B <= VK_MAXB;
+  if (lds)
+    for (int b = threadIdx.x; b < B; b += blockDim.x) soff[b] = off[b];
+  __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int lo = 0, hi = B - 1;
   while (lo < hi) {  // last fragment with off[b] <= i
     const int mid = (lo + hi + 1) >> 1;
-    if (off[mid] <= i) lo = mid; else hi = mid - 1;
+    if ((lds ? soff[mid] : off[mid]) <= i) lo = mid; else hi = mid - 1;
   }
   const int x = (int)floor((double)xyz[3 * i] / voxel);
   const int y = (int)floor((double)xyz[3 * i + 1] / voxel);
@@ -489,9 +497,12 @@ __global__ void brick_insert_kernel(const int4* __restrict__ c, int64_t M, HashV
   }
 }
 
-// representatives (the minimum row of each brick) draw brick ids; wave-aggregated counter
-__global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView h, int32_t* count,
-                                 int32_t* slot_of, int4* bcoord, int t) {
+// representatives (the minimum row of each brick) draw brick ids; workgroup-aggregated counter (one memory-side
+// atomic per 256 rows: the ~10 k per-wave atomics on one address serialised at the memory side)
+__global__ __launch_bounds__(256) void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView h,
+                                                        int32_t* count, int32_t* slot_of, int4* bcoord, int t) {
+  __shared__ int wcnt[4];
+  __shared__ int wbase;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t sl = -1;
   bool rep = false;
@@ -503,12 +514,21 @@ __global__ void brick_ids_kernel(const int4* __restrict__ c, int64_t M, HashView
     slot_of[i] = (int32_t)sl;
   }
   const unsigned long long m = __ballot(rep);
-  const int lane = threadIdx.x & 63;
-  int base = 0;
-  if (lane == 0 && m) base = atomicAdd(count, __popcll(m));
-  base = __shfl(base, 0, 64);
-  if (rep) h.vals[sl] = base + __popcll(m & ((1ULL << lane) - 1));
-  if (rep) bcoord[h.vals[sl]] = make_int4(v.x, v.y >> (t + 2), v.z >> (t + 2), v.w >> (t + 2));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) wcnt[wv] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    wbase = tot ? atomicAdd(count, tot) : 0;
+  }
+  __syncthreads();
+  int base = wbase;
+  for (int w = 0; w < wv; ++w) base += wcnt[w];
+  if (rep) {
+    const int id = base + __popcll(m & ((1ULL << lane) - 1));
+    h.vals[sl] = id;
+    bcoord[id] = make_int4(v.x, v.y >> (t + 2), v.z >> (t + 2), v.w >> (t + 2));
+  }
 }
 
 // the row slots of the bricks in use (count of them) to -1: the pool is sized for one brick per row, but a
