@@ -66,6 +66,12 @@ __device__ unsigned long long g_pconv_trace[8];   // 0 MFMAs (+ splits, load iss
 #define PCSTAMP(slot) do {} while (0)
 #endif
 
+#ifndef PCONV_BUF
+#define PCONV_BUF 1   // the residual loads and the output stores through a per-pair buffer resource with 32-bit lane offsets
+                      // (0: 64-bit per-lane addresses; conv7 then held 256 VGPRs with 2 spilled and 42 register copies
+                      // per step pair: bit-identical, -0.2 ms per step, profiles/r06/ab_r6s22_pconv_buffer.txt)
+#endif
+
 #ifndef PCONV_GRID
 #define PCONV_GRID 1   // workgroups per resident slot (1: one persistent round; >1 / <0: the round-4 grid experiments)
 #endif
@@ -456,6 +462,16 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
       rxi = *reinterpret_cast<const float4*>(a.R + (int64_t)c.p * a.rps + (int64_t)min(lane >> 3, a.xci - 1) * a.rld + n);
       return;
     }
+    if (PCONV_BUF) {   // the pair's residual as a buffer (wave-uniform base), 32-bit lane offsets
+      const __amdgpu_buffer_rsrc_t rr =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.R + (int64_t)c.p * a.rps), (short)0, 0x7fffffff, 0x00020000);
+      const int ro = 4 * ((32 * w + erow) * (int)a.rrs + (n >> 5) * (int)a.rcs + (n & 31));
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        rres[(RES && !(XI & 2)) ? q : 0] = __builtin_bit_cast(
+            float4, __builtin_amdgcn_raw_buffer_load_b128(rr, ro + 4 * 8 * q * (int)a.rrs, 0, 0));
+      return;
+    }
     const float* src = a.R + (int64_t)c.p * a.rps + (int64_t)(32 * w + erow) * a.rrs + (int64_t)(n >> 5) * a.rcs + (n & 31);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -542,7 +558,18 @@ __global__ __launch_bounds__(256 * KW, KS == 8 ? 2 : 1) void pconv_kernel(PcArgs
     }
     float* ydst = a.Y + (int64_t)c.p * a.yps + (int64_t)(32 * w + erow) * a.yld + (int64_t)c.kc * a.ycs + ec0;
     const bool full = n0 + CH <= N;   // uniform: every column of the chunk is valid
-    if (HEAD != 2 && a.Y) {   // (a.Y null: a statistics-only pass)
+    if (PCONV_BUF && HEAD != 2 && a.Y) {   // the pair's output as a buffer, 32-bit lane offsets
+      const __amdgpu_buffer_rsrc_t ry =
+          __builtin_amdgcn_make_buffer_rsrc(a.Y + (int64_t)c.p * a.yps, (short)0, 0x7fffffff, 0x00020000);
+      const int yo = 4 * ((32 * w + erow) * (int)a.yld + c.kc * (int)a.ycs + ec0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (full || n0 + ec0 < N4) {
+          const u32x4 u = {__float_as_uint(ev[q].x), __float_as_uint(ev[q].y), __float_as_uint(ev[q].z),
+                           __float_as_uint(ev[q].w)};
+          __builtin_amdgcn_raw_buffer_store_b128(u, ry, yo + 4 * 8 * q * (int)a.yld, 0, PCONV_NTS ? 2 : 0);
+        }
+    } else if (HEAD != 2 && a.Y) {   // (a.Y null: a statistics-only pass)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (full || n0 + ec0 < N4) {
