@@ -74,6 +74,11 @@ __device__ unsigned long long g_sp_trace[8];
 constexpr int SB_K = 32;     // input channels per step
 constexpr int SB_BST = 40;   // bf16 row stride of the weight image (80 B)
 constexpr int SB_CP = 128;   // output-channel padding of the weight image (largest TN)
+#ifndef SPBX_WBUF
+#define SPBX_WBUF 1   // the weight-stage loads through a buffer resource (wave-uniform base) with 32-bit lane offsets
+                      // (0: 64-bit per-lane addresses; spconv<128,3,0,0> then held 256 VGPRs with 4 spilled:
+                      // bit-identical, the FCGF convs -2 %, profiles/r06/ab_r6s24_spconv_wbuf.txt)
+#endif
 #ifndef SPBX_NS32   // gathered steps in flight per output-channel tile width (register budget)
 #define SPBX_NS32 3
 #endif
@@ -220,12 +225,25 @@ __global__ __launch_bounds__(256, 2) void spconv_bx_kernel(SpArgs a, const uint1
     }
     const int cb = s % nci;
     const char* wb = reinterpret_cast<const char*>(wimg) + ((int64_t)(k * nci + cb) * NPL * CoutP + c0) * SB_BST * 2;
+#if SPBX_WBUF
+    // the step's weight stage as a buffer (wave-uniform base), 32-bit lane offsets
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wb), (short)0, 0x7fffffff,
+                                                                        0x00020000);
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+      const int g = min(tid + 256 * i, BG - 1);
+      const int pl = g / (TN * 5), wi = g - pl * (TN * 5);
+      A.bq[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rw, pl * (int)CoutP * SB_BST * 2 + wi * 16, 0, 0));
+    }
+#else
 #pragma unroll
     for (int i = 0; i < GPT; ++i) {
       const int g = min(tid + 256 * i, BG - 1);
       const int pl = g / (TN * 5), wi = g - pl * (TN * 5);
       A.bq[i] = *reinterpret_cast<const f32x4*>(wb + (int64_t)pl * CoutP * SB_BST * 2 + wi * 16);
     }
+#endif
   };
   bool xbad = false;   // H = 1: a gathered value past the fp16 window
   float xmx = 0.f;     // H = 1: max |value| x XS of this lane's splits
